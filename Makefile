@@ -1,0 +1,124 @@
+# Native build for the MI355X bidirectional-BFS framework (gfx950 only).
+#
+#   make -j8            -> build/lib/libbibfs.so, build/lib/libbibfs_mpi.so,
+#                          build/bin/* CLI tools, bidirectional_bfs_amd/_native*.so
+#   make cpu            -> host-only pieces (no hipcc needed)
+#   make clean
+#
+# The reference builds each engine with its own Makefile (v1..v4/Makefile) and
+# ships two of them without optimisation (v1/Makefile:2,7 typo, v4/Makefile:27);
+# everything here is -O3.
+
+ROCM      ?= /opt/rocm
+MPI_HOME  ?= /opt/conda
+ARCH      ?= gfx950
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+PYTHON    ?= python3
+
+BUILD     := build
+OBJ       := $(BUILD)/obj
+LIB       := $(BUILD)/lib
+BIN       := $(BUILD)/bin
+PKG       := bidirectional_bfs_amd
+
+CXXSTD    := -std=c++17
+INC       := -Icsrc/include -Icsrc/hip
+CXXFLAGS  += -O3 -fPIC $(CXXSTD) -Wall -Wextra -Wno-unused-parameter $(INC) -pthread
+HIPFLAGS  := -O3 -fPIC $(CXXSTD) $(INC) --offload-arch=$(ARCH) -mcode-object-version=5 \
+             -Wno-unused-result -munsafe-fp-atomics
+MPI_INC   := -I$(MPI_HOME)/include
+# system libstdc++ first: conda ships an older one
+MPI_LD    := -L$(MPI_HOME)/lib -lmpi -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_HOME)/lib
+HIP_LD    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+RCCL_LD   := -L$(ROCM)/lib -lrccl
+
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include())")
+PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp
+HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/hip_engine.hip \
+             csrc/hip/capi.hip csrc/dist/dist_engine.hip
+MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp csrc/dist/mpi_bootstrap.cpp
+
+CORE_OBJ  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CORE_SRC))
+HIP_OBJ   := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRC))
+MPI_OBJ   := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(MPI_SRC))
+
+HEADERS   := $(wildcard csrc/include/bibfs/*.hpp csrc/include/bibfs/*.h csrc/hip/*.hpp)
+
+CPU_TOOLS := $(BIN)/bibfs_serial $(BIN)/show_matrix $(BIN)/bibfs_gen
+MPI_TOOLS := $(BIN)/second_try $(BIN)/mpi_queue_bibfs
+GPU_TOOLS := $(BIN)/bibfs_selftest $(BIN)/bibfs_hip $(BIN)/mpi_bibfs $(BIN)/bibfs_bench
+
+NATIVE_PY := $(PKG)/_native$(PY_EXT)
+
+.PHONY: all cpu gpu mpi python clean
+all: cpu mpi gpu python
+cpu: $(LIB)/libbibfs_core.so $(CPU_TOOLS)
+mpi: $(LIB)/libbibfs_mpi.so $(MPI_TOOLS)
+gpu: $(LIB)/libbibfs.so $(GPU_TOOLS) $(BIN)/bibfs_cuda_only
+python: $(NATIVE_PY)
+
+$(OBJ)/%.o: csrc/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(if $(findstring mpi,$<),$(MPI_INC)) -c $< -o $@
+
+$(OBJ)/%.o: csrc/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB)/libbibfs_core.so: $(CORE_OBJ)
+	@mkdir -p $(LIB)
+	$(CXX) -shared -o $@ $^ -pthread
+
+$(LIB)/libbibfs.so: $(CORE_OBJ) $(HIP_OBJ)
+	@mkdir -p $(LIB)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ $(HIP_LD) $(RCCL_LD) -pthread
+
+$(LIB)/libbibfs_mpi.so: $(MPI_OBJ) $(LIB)/libbibfs_core.so
+	@mkdir -p $(LIB)
+	$(CXX) -shared -o $@ $(MPI_OBJ) -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN' $(MPI_LD) -pthread
+
+# --- CLI tools ---------------------------------------------------------------
+TOOL_CXX = $(CXX) $(CXXFLAGS)
+$(BIN)/bibfs_serial: tools/bibfs_serial.cpp tools/cli_common.hpp $(LIB)/libbibfs_core.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib'
+$(BIN)/show_matrix: tools/show_matrix.cpp $(LIB)/libbibfs_core.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib'
+$(BIN)/bibfs_gen: tools/bibfs_gen.cpp tools/cli_common.hpp $(LIB)/libbibfs_core.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib'
+$(BIN)/second_try: tools/second_try.cpp tools/cli_common.hpp $(LIB)/libbibfs_mpi.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $(MPI_INC) $< -o $@ -L$(LIB) -lbibfs_mpi -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib' $(MPI_LD)
+$(BIN)/mpi_queue_bibfs: tools/mpi_queue_bibfs.cpp tools/cli_common.hpp $(LIB)/libbibfs_mpi.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $(MPI_INC) $< -o $@ -L$(LIB) -lbibfs_mpi -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib' $(MPI_LD)
+$(BIN)/bibfs_hip: tools/bibfs_hip.cpp tools/cli_common.hpp $(LIB)/libbibfs.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs -Wl,-rpath,'$$ORIGIN/../lib' $(HIP_LD)
+$(BIN)/bibfs_cuda_only: $(BIN)/bibfs_hip
+	ln -sf bibfs_hip $@
+$(BIN)/bibfs_bench: tools/bibfs_bench.cpp tools/cli_common.hpp $(LIB)/libbibfs.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs -Wl,-rpath,'$$ORIGIN/../lib' $(HIP_LD)
+$(BIN)/mpi_bibfs: tools/mpi_bibfs.cpp tools/cli_common.hpp $(LIB)/libbibfs.so $(LIB)/libbibfs_mpi.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $(MPI_INC) $< -o $@ -L$(LIB) -lbibfs_mpi -lbibfs \
+	  -Wl,-rpath,'$$ORIGIN/../lib' $(HIP_LD) $(RCCL_LD) $(MPI_LD)
+
+# --- Python extension (pybind11), in-tree next to the package --------------
+$(NATIVE_PY): csrc/python/bindings.cpp $(HEADERS) $(LIB)/libbibfs.so
+	$(CXX) $(CXXFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -shared $< -o $@ -L$(LIB) -lbibfs \
+	  -Wl,-rpath,'$$ORIGIN/../$(LIB)' $(HIP_LD)
+
+clean:
+	rm -rf $(BUILD) $(PKG)/_native*.so
+
+$(BIN)/bibfs_selftest: tools/bibfs_selftest.cpp tools/cli_common.hpp $(LIB)/libbibfs.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs -Wl,-rpath,'$$ORIGIN/../lib' $(HIP_LD)

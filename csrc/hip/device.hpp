@@ -1,0 +1,155 @@
+// Internal header shared by the HIP translation units of the engine.
+// gfx950 / CDNA4 only: wave64 everywhere, 64-bit ballots.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "bibfs/common.hpp"
+
+namespace bibfs {
+namespace dev {
+
+#define HIP_CHECK(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      throw ::bibfs::Error(std::string("HIP error ") + hipGetErrorString(_e) + " at " +   \
+                           __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);        \
+  } while (0)
+
+constexpr int kWave = 64;
+constexpr uint32_t kEmpty = 0xFFFFFFFFu;
+
+// Search status codes (DevState::status / HostResult::status)
+enum : uint32_t { kRunning = 0, kFound = 1, kNoPath = 2, kHandoff = 3, kError = 4 };
+
+// Search state shared by the LDS engine (on hand-off) and the grid engine.
+// Lives in device memory; the host mirrors it with one small async copy.
+struct DevState {
+  uint32_t status;
+  uint32_t meet;          // meet vertex (kEmpty = none yet)
+  uint32_t meet_side;     // side whose expansion found the meet
+  uint32_t levels;
+  int32_t depth[2];       // depth of each side's current frontier
+  uint32_t fbeg[2];       // current frontier = queue[s][fbeg, fend)
+  uint32_t fend[2];
+  uint32_t qtail[2];      // append cursor during a level (== fend between levels)
+  uint32_t hub_count;     // grid top-down: number of hub vertices deferred
+  uint32_t chunk;         // grid top-down: dynamic chunk counter
+  unsigned long long hub_edge_cursor;
+  unsigned long long fedges[2];   // sum of degrees of each current frontier
+  unsigned long long vedges[2];   // sum of degrees of every vertex claimed by the side
+  unsigned long long nedges;      // degrees of vertices claimed in the running level
+  unsigned long long einsp;       // edges inspected
+  uint32_t pad[4];
+};
+
+// Record the device writes straight into pinned host memory at the end of a
+// query (no hipMemcpy on the critical path; the host spins on `seq`).
+struct HostResult {
+  uint32_t seq;           // written LAST, system-scope release
+  uint32_t status;
+  int32_t hops;
+  uint32_t meet;
+  uint32_t levels;
+  uint32_t visited;
+  unsigned long long einsp;
+  int32_t depth[2];
+  uint32_t path_len;      // hops + 1 when found
+  uint32_t path_on_device;// 1 when the path did not fit the pinned buffer
+  uint32_t lds_levels;
+  uint32_t pad[3];
+};
+
+struct LevelTraceDev {
+  uint32_t side, depth, frontier, mode;
+  unsigned long long edges, discovered;
+};
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// exclusive prefix count of set bits below this lane
+__device__ __forceinline__ uint32_t mbcnt64(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+__device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace dev
+
+// ----------------------------------------------------------------------------
+// Host-side launchers (implemented in the .hip files)
+// ----------------------------------------------------------------------------
+namespace launch {
+
+struct GraphView {
+  uint32_t n;
+  uint64_t nnz;
+  const uint64_t* row_off;     // n + 1
+  const uint32_t* row_off32;   // n + 1 copy when nnz < 2^32 (else nullptr)
+  const uint32_t* col;
+};
+
+struct SearchBuffers {
+  uint32_t* vis[2];     // n/32 + 1 words each; all-zero between searches
+  uint32_t* fbits[2];   // frontier bitmaps (bottom-up)
+  uint32_t* nbits[2];   // next-frontier bitmaps (bottom-up)
+  uint32_t* parent[2];  // n each, valid only where visited
+  uint32_t* queue[2];   // n each, BFS order of claimed vertices
+  uint32_t* hub_list;   // n (grid top-down deferred hubs)
+  uint32_t* dpath;      // n + 1 (device path for long paths)
+  dev::DevState* st;
+  dev::LevelTraceDev* trace;
+  uint32_t trace_cap;
+  uint32_t words;       // n/32 + 1
+};
+
+struct HostSide {
+  dev::HostResult* res;  // pinned, device-visible
+  uint32_t* path;        // pinned
+  uint32_t path_cap;
+};
+
+// csr_device.hip
+void build_csr_from_edges(const uint32_t* d_uv, uint64_t m, uint32_t n, uint64_t* d_row_off,
+                          uint32_t** d_col_out, uint64_t* nnz_out, uint32_t* d_row_off32_or_null,
+                          hipStream_t s);
+uint64_t count_csr_entries(const uint32_t* d_uv, uint64_t m, uint32_t n, uint64_t* d_row_off,
+                           hipStream_t s);
+void fill_csr(const uint32_t* d_uv, uint64_t m, uint32_t n, const uint64_t* d_row_off,
+              uint64_t* d_cursor, uint32_t* d_col, hipStream_t s);
+void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s);
+uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);
+void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,
+                     uint32_t* d_uv, hipStream_t s);
+
+// engine_kernels.hip
+void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, uint32_t src,
+                uint32_t dst, uint32_t seq, int side_policy, int trace, hipStream_t s);
+int lds_threads();
+size_t lds_bytes(bool wide);
+void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
+                hipStream_t s);
+void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
+void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
+void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);
+void finish_level(const SearchBuffers& b, int side, int mode, int trace, hipStream_t s);
+void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
+void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
+               hipStream_t s);
+void cleanup(const SearchBuffers& b, uint32_t n, hipStream_t s);
+
+}  // namespace launch
+}  // namespace bibfs

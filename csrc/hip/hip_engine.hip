@@ -1,0 +1,553 @@
+// Host side of the single-GPU engine: graph residency, search dispatch
+// (LDS persistent engine -> optional hand-off to the grid engine), pinned
+// result delivery, and the step-wise C-API-style interface.
+//
+// Reference parity: v3/bibfs_cuda_only.cu:128-234 (allocation, per-level
+// host loop, cudaEvent timing) and v4/comp.cu:49-133 (device runtime API).
+// Differences by design: device state is allocated once per graph and kept
+// clean between queries, the per-level loop runs on the device, and the host
+// learns the result by polling a pinned word instead of a memcpy + sync chain.
+#include <immintrin.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "bibfs/hip_engine.hpp"
+#include "device.hpp"
+
+namespace bibfs {
+
+using namespace dev;
+
+struct HipBiBfs::Impl {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipDeviceProp_t prop{};
+  int cus = 256;
+
+  // graph
+  uint32_t n = 0;
+  uint64_t nnz = 0, m_input = 0;
+  uint64_t* d_row_off = nullptr;
+  uint32_t* d_row_off32 = nullptr;
+  uint32_t* d_col = nullptr;
+  uint32_t* d_uv = nullptr;  // last generated edge list (kept for small graphs / tests)
+  uint64_t uv_m = 0;
+  double build_ms = 0.0;
+
+  // search state
+  launch::SearchBuffers buf{};
+  void* state_block = nullptr;  // one allocation holding every per-search array
+  size_t state_bytes = 0;
+  uint32_t* d_flag = nullptr;
+
+  // pinned host memory
+  HostResult* h_res = nullptr;
+  uint32_t* h_path = nullptr;
+  uint32_t h_path_cap = 1u << 20;
+  DevState* h_state = nullptr;
+  uint32_t seq = 0;
+
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+  // step-wise API
+  int dir[2] = {1, 1};
+  bool fbits_valid[2] = {false, false};
+  vid_t step_src = 0, step_dst = 0;
+
+  launch::GraphView view() const {
+    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col};
+  }
+
+  void free_graph() {
+    if (d_row_off) HIP_CHECK(hipFree(d_row_off));
+    if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
+    if (d_col) HIP_CHECK(hipFree(d_col));
+    if (d_uv) HIP_CHECK(hipFree(d_uv));
+    if (state_block) HIP_CHECK(hipFree(state_block));
+    d_row_off = nullptr;
+    d_row_off32 = nullptr;
+    d_col = nullptr;
+    d_uv = nullptr;
+    state_block = nullptr;
+    n = 0;
+    nnz = m_input = uv_m = 0;
+  }
+
+  // One allocation for every per-search array, sized for the 288 GB HBM of
+  // the part: 3 bitmaps pairs (n/8 B each) + parent/queue (4n B each) per side.
+  void alloc_state() {
+    const uint64_t words = ((uint64_t)n + 63) / 64 * 2 + 2;
+    const uint64_t trace_cap = 4096;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+      size_t o = off;
+      off += (bytes + 255) & ~(size_t)255;
+      return o;
+    };
+    size_t o_vis[2], o_fb[2], o_nb[2], o_par[2], o_q[2];
+    for (int s = 0; s < 2; ++s) {
+      o_vis[s] = take(words * 4);
+      o_fb[s] = take(words * 4);
+      o_nb[s] = take(words * 4);
+    }
+    for (int s = 0; s < 2; ++s) {
+      o_par[s] = take((size_t)n * 4 + 4);
+      o_q[s] = take((size_t)n * 4 + 4);
+    }
+    size_t o_hub = take((size_t)n * 4 + 4);
+    size_t o_path = take((size_t)n * 4 + 8);
+    size_t o_st = take(sizeof(DevState));
+    size_t o_tr = take(trace_cap * sizeof(LevelTraceDev));
+    size_t o_flag = take(64);
+    state_bytes = off;
+    HIP_CHECK(hipMalloc(&state_block, state_bytes));
+    char* base = static_cast<char*>(state_block);
+    for (int s = 0; s < 2; ++s) {
+      buf.vis[s] = reinterpret_cast<uint32_t*>(base + o_vis[s]);
+      buf.fbits[s] = reinterpret_cast<uint32_t*>(base + o_fb[s]);
+      buf.nbits[s] = reinterpret_cast<uint32_t*>(base + o_nb[s]);
+      buf.parent[s] = reinterpret_cast<uint32_t*>(base + o_par[s]);
+      buf.queue[s] = reinterpret_cast<uint32_t*>(base + o_q[s]);
+    }
+    buf.hub_list = reinterpret_cast<uint32_t*>(base + o_hub);
+    buf.dpath = reinterpret_cast<uint32_t*>(base + o_path);
+    buf.st = reinterpret_cast<DevState*>(base + o_st);
+    buf.trace = reinterpret_cast<LevelTraceDev*>(base + o_tr);
+    buf.trace_cap = (uint32_t)trace_cap;
+    buf.words = (uint32_t)words;
+    d_flag = reinterpret_cast<uint32_t*>(base + o_flag);
+    // visited bitmaps must start (and stay) all-zero
+    for (int s = 0; s < 2; ++s) HIP_CHECK(hipMemsetAsync(buf.vis[s], 0, words * 4, stream));
+    HIP_CHECK(hipMemsetAsync(buf.st, 0, sizeof(DevState), stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+  }
+
+  void finish_graph(double ms) {
+    if (nnz < 0xFFFFFFFFULL) {
+      HIP_CHECK(hipMalloc(&d_row_off32, ((size_t)n + 1) * 4));
+      launch::make_row_off32(d_row_off, n, d_row_off32, stream);
+    }
+    alloc_state();
+    build_ms = ms;
+  }
+
+  void build_from_device_edges(const uint32_t* uv, uint64_t m) {
+    nnz = launch::count_csr_entries(uv, m, n, d_row_off, stream);
+    HIP_CHECK(hipMalloc(&d_col, std::max<uint64_t>(nnz, 1) * 4));
+    uint64_t* cursor = nullptr;
+    HIP_CHECK(hipMalloc(&cursor, ((size_t)n + 1) * 8));
+    launch::fill_csr(uv, m, n, d_row_off, cursor, d_col, stream);
+    HIP_CHECK(hipStreamSynchronize(stream));
+    HIP_CHECK(hipFree(cursor));
+  }
+
+  void wait_seq(uint32_t want) {
+    for (uint64_t it = 1;; ++it) {
+      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want) return;
+      if ((it & 4095) == 0) {
+        hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) {
+          if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want) return;
+          throw Error("bibfs: search kernel finished without publishing a result");
+        }
+        if (e != hipErrorNotReady)
+          throw Error(std::string("bibfs: search kernel failed: ") + hipGetErrorString(e));
+      } else {
+        _mm_pause();
+      }
+    }
+  }
+
+  void sync_state() {
+    HIP_CHECK(hipMemcpyAsync(h_state, buf.st, sizeof(DevState), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+  }
+
+  // one grid level of side s; mode 1 = top-down, 2 = bottom-up
+  void grid_level(int s, int mode, int trace) {
+    const auto g = view();
+    if (mode == 2) {
+      if (!fbits_valid[s]) launch::build_frontier_bits(g, buf, s, stream);
+      launch::grid_bottomup(g, buf, s, cus, stream);
+      std::swap(buf.fbits[s], buf.nbits[s]);
+      fbits_valid[s] = true;
+    } else {
+      launch::grid_topdown(g, buf, s, cus, stream);
+      fbits_valid[s] = false;
+    }
+    launch::finish_level(buf, s, mode, trace, stream);
+  }
+
+  int choose_mode(int s, const SearchOptions& opt) {
+    if (opt.direction == Direction::kTopDown) return 1;
+    if (opt.direction == Direction::kBottomUp) return 2;
+    const DevState& st = *h_state;
+    const double m_f = (double)st.fedges[s];
+    const double m_u = (double)nnz - (double)st.vedges[s];
+    const double n_f = (double)(st.fend[s] - st.fbeg[s]);
+    if (dir[s] == 1 && m_f > m_u / opt.alpha) dir[s] = 2;
+    else if (dir[s] == 2 && n_f < (double)n / opt.beta) dir[s] = 1;
+    return dir[s];
+  }
+
+  int choose_side(const SearchOptions& opt, int& turn) {
+    const DevState& st = *h_state;
+    if (opt.side == SidePolicy::kAlternate) {
+      int s = turn;
+      turn ^= 1;
+      return s;
+    }
+    if (opt.side == SidePolicy::kSmallerFrontier)
+      return (st.fend[0] - st.fbeg[0]) <= (st.fend[1] - st.fbeg[1]) ? 0 : 1;
+    return st.fedges[0] <= st.fedges[1] ? 0 : 1;
+  }
+
+  // Runs grid levels until the search ends; returns #grid levels and #bottom-up levels.
+  void grid_loop(const SearchOptions& opt, SearchStats& stats) {
+    dir[0] = dir[1] = 1;
+    fbits_valid[0] = fbits_valid[1] = false;
+    int turn = 0;
+    const int trace = opt.trace ? 1 : 0;
+    for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
+      sync_state();
+      if (h_state->status != kRunning || h_state->meet != kEmpty) break;
+      const int s = choose_side(opt, turn);
+      const int mode = choose_mode(s, opt);
+      grid_level(s, mode, trace);
+      stats.grid_levels++;
+      if (mode == 2) stats.bottomup_levels++;
+    }
+  }
+
+  SearchResult collect(uint32_t want_seq, const SearchOptions& opt, SearchStats stats) {
+    SearchResult r;
+    r.stats = std::move(stats);
+    const HostResult& R = *h_res;
+    r.found = R.status == kFound;
+    r.hops = r.found ? R.hops : -1;
+    r.meet = r.found ? R.meet : kNoVertex;
+    r.stats.levels = (int)R.levels;
+    r.stats.edges_inspected = R.einsp;
+    r.stats.visited = R.visited;
+    (void)want_seq;
+    if (r.found && opt.want_path) {
+      r.path.resize(R.path_len);
+      if (R.path_on_device) {
+        HIP_CHECK(hipMemcpyAsync(r.path.data(), buf.dpath, (size_t)R.path_len * 4,
+                                 hipMemcpyDeviceToHost, stream));
+        HIP_CHECK(hipStreamSynchronize(stream));
+      } else {
+        std::memcpy(r.path.data(), h_path, (size_t)R.path_len * 4);
+      }
+    }
+    return r;
+  }
+
+  void fetch_trace(SearchResult& r) {
+    const uint32_t L = std::min<uint32_t>((uint32_t)r.stats.levels, buf.trace_cap);
+    std::vector<LevelTraceDev> t(L);
+    if (L) {
+      HIP_CHECK(hipMemcpyAsync(t.data(), buf.trace, L * sizeof(LevelTraceDev), hipMemcpyDeviceToHost,
+                               stream));
+      HIP_CHECK(hipStreamSynchronize(stream));
+    }
+    r.stats.trace.clear();
+    for (auto& x : t) {
+      LevelTrace lt;
+      lt.side = (int)x.side;
+      lt.depth = (int)x.depth;
+      lt.frontier = x.frontier;
+      lt.edges = x.edges;
+      lt.discovered = x.discovered;
+      lt.mode = (int)x.mode;
+      r.stats.trace.push_back(lt);
+    }
+  }
+};
+
+HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
+  p_->device = device;
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipGetDeviceProperties(&p_->prop, device));
+  p_->cus = p_->prop.multiProcessorCount > 0 ? p_->prop.multiProcessorCount : 256;
+  HIP_CHECK(hipStreamCreateWithFlags(&p_->stream, hipStreamNonBlocking));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_res), sizeof(HostResult),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_path), (size_t)p_->h_path_cap * 4,
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_state), sizeof(DevState),
+                          hipHostMallocDefault));
+  std::memset(p_->h_res, 0, sizeof(HostResult));
+  HIP_CHECK(hipEventCreate(&p_->ev0));
+  HIP_CHECK(hipEventCreate(&p_->ev1));
+}
+
+HipBiBfs::~HipBiBfs() {
+  if (!p_) return;
+  try {
+    hipSetDevice(p_->device);
+    hipStreamSynchronize(p_->stream);
+    p_->free_graph();
+  } catch (...) {
+  }
+  hipHostFree(p_->h_res);
+  hipHostFree(p_->h_path);
+  hipHostFree(p_->h_state);
+  hipEventDestroy(p_->ev0);
+  hipEventDestroy(p_->ev1);
+  hipStreamDestroy(p_->stream);
+}
+
+void HipBiBfs::load_csr(const Csr& g) {
+  HIP_CHECK(hipSetDevice(p_->device));
+  p_->free_graph();
+  auto& I = *p_;
+  I.n = g.n;
+  I.nnz = g.nnz();
+  I.m_input = g.m_input;
+  HIP_CHECK(hipEventRecord(I.ev0, I.stream));
+  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)g.n + 1) * 8));
+  HIP_CHECK(hipMalloc(&I.d_col, std::max<size_t>(g.nnz(), 1) * 4));
+  HIP_CHECK(hipMemcpyAsync(I.d_row_off, g.row_off.data(), ((size_t)g.n + 1) * 8,
+                           hipMemcpyHostToDevice, I.stream));
+  if (g.nnz())
+    HIP_CHECK(hipMemcpyAsync(I.d_col, g.col.data(), g.nnz() * 4, hipMemcpyHostToDevice, I.stream));
+  HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  HIP_CHECK(hipEventSynchronize(I.ev1));
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
+  I.finish_graph(ms);
+}
+
+
+void HipBiBfs::load_edges(const EdgeList& el) {
+  HIP_CHECK(hipSetDevice(p_->device));
+  p_->free_graph();
+  auto& I = *p_;
+  I.n = el.n;
+  I.m_input = el.m();
+  HIP_CHECK(hipEventRecord(I.ev0, I.stream));
+  uint32_t* d_uv = nullptr;
+  HIP_CHECK(hipMalloc(&d_uv, std::max<size_t>(el.uv.size(), 2) * 4));
+  if (!el.uv.empty())
+    HIP_CHECK(hipMemcpyAsync(d_uv, el.uv.data(), el.uv.size() * 4, hipMemcpyHostToDevice, I.stream));
+  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)I.n + 1) * 8));
+  I.build_from_device_edges(d_uv, el.m());
+  HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  HIP_CHECK(hipEventSynchronize(I.ev1));
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
+  HIP_CHECK(hipFree(d_uv));
+  I.finish_graph(ms);
+}
+
+void HipBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
+  HIP_CHECK(hipSetDevice(p_->device));
+  p_->free_graph();
+  auto& I = *p_;
+  I.n = n;
+  HIP_CHECK(hipEventRecord(I.ev0, I.stream));
+  uint32_t* d_uv = nullptr;
+  const uint64_t m = launch::gen_gnp_device(n, p, seed, &d_uv, I.stream);
+  I.m_input = m;
+  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)n + 1) * 8));
+  I.build_from_device_edges(d_uv, m);
+  HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  HIP_CHECK(hipEventSynchronize(I.ev1));
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
+  I.d_uv = d_uv;
+  I.uv_m = m;
+  I.finish_graph(ms);
+}
+
+void HipBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c) {
+  HIP_CHECK(hipSetDevice(p_->device));
+  p_->free_graph();
+  auto& I = *p_;
+  BIBFS_REQUIRE(n >= 2, "R-MAT needs n >= 2");
+  I.n = n;
+  I.m_input = m;
+  HIP_CHECK(hipEventRecord(I.ev0, I.stream));
+  uint32_t* d_uv = nullptr;
+  HIP_CHECK(hipMalloc(&d_uv, std::max<uint64_t>(2 * m, 2) * 4));
+  launch::gen_rmat_device(n, m, seed, a, b, c, d_uv, I.stream);
+  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)n + 1) * 8));
+  I.build_from_device_edges(d_uv, m);
+  HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  HIP_CHECK(hipEventSynchronize(I.ev1));
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
+  I.d_uv = d_uv;
+  I.uv_m = m;
+  I.finish_graph(ms);
+}
+
+uint32_t HipBiBfs::n() const { return p_->n; }
+uint64_t HipBiBfs::nnz() const { return p_->nnz; }
+uint64_t HipBiBfs::m_input() const { return p_->m_input; }
+double HipBiBfs::last_build_ms() const { return p_->build_ms; }
+size_t HipBiBfs::device_bytes() const {
+  const auto& I = *p_;
+  return ((size_t)I.n + 1) * 8 + (I.d_row_off32 ? ((size_t)I.n + 1) * 4 : 0) + I.nnz * 4 +
+         (I.d_uv ? I.uv_m * 8 : 0) + I.state_bytes;
+}
+int HipBiBfs::device() const { return p_->device; }
+void* HipBiBfs::stream() const { return p_->stream; }
+void HipBiBfs::synchronize() const { HIP_CHECK(hipStreamSynchronize(p_->stream)); }
+
+DeviceInfo HipBiBfs::info() const {
+  DeviceInfo d;
+  d.name = p_->prop.name;
+  d.arch = p_->prop.gcnArchName;
+  d.cus = p_->prop.multiProcessorCount;
+  d.hbm_bytes = p_->prop.totalGlobalMem;
+  d.lds_bytes = (int)p_->prop.sharedMemPerBlock;
+  return d;
+}
+
+SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
+  auto& I = *p_;
+  const auto t0 = std::chrono::steady_clock::now();
+  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
+  BIBFS_REQUIRE(src < I.n && dst < I.n, "src/dst out of range");
+  if (src == dst) {
+    SearchResult r;
+    r.found = true;
+    r.hops = 0;
+    r.meet = src;
+    r.path = {src};
+    r.stats.visited = 1;
+    r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+  }
+  HIP_CHECK(hipSetDevice(I.device));
+  const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
+  const auto g = I.view();
+  launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap};
+  SearchStats stats;
+  bool grid = opt.force_grid;
+  HIP_CHECK(hipEventRecord(I.ev0, I.stream));
+  if (!grid) {
+    launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side,
+                       opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0, I.stream);
+    I.wait_seq(seq);
+    if (I.h_res->status == kHandoff) {
+      grid = true;
+      stats.handoff = true;
+    }
+  } else {
+    launch::seed_state(g, I.buf, src, dst, I.stream);
+  }
+  uint32_t pub_seq = seq;
+  if (grid) {
+    I.grid_loop(opt, stats);
+    pub_seq = ++I.seq == 0 ? ++I.seq : I.seq;
+    launch::walk_path(I.buf, hs, src, dst, pub_seq, I.stream);
+    I.wait_seq(pub_seq);
+  }
+  HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  SearchResult r = I.collect(pub_seq, opt, std::move(stats));
+  r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (grid) launch::cleanup(I.buf, I.n, I.stream);  // async: next query is stream-ordered behind it
+  HIP_CHECK(hipEventSynchronize(I.ev1));
+  float ms = 0;
+  HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
+  r.search_ms = ms;
+  if (opt.trace) I.fetch_trace(r);
+  return r;
+}
+
+// ---------------------------------------------------------------- step-wise API
+
+void HipBiBfs::begin(vid_t src, vid_t dst) {
+  auto& I = *p_;
+  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
+  BIBFS_REQUIRE(src < I.n && dst < I.n, "src/dst out of range");
+  HIP_CHECK(hipSetDevice(I.device));
+  I.step_src = src;
+  I.step_dst = dst;
+  I.fbits_valid[0] = I.fbits_valid[1] = false;
+  I.dir[0] = I.dir[1] = 1;
+  launch::seed_state(I.view(), I.buf, src, dst, I.stream);
+  I.sync_state();
+}
+
+uint64_t HipBiBfs::expand(int side, bool* met, Direction dir) {
+  auto& I = *p_;
+  BIBFS_REQUIRE(side == 0 || side == 1, "side must be 0 or 1");
+  const uint32_t before = I.h_state->qtail[side];
+  if (I.h_state->status != kRunning) {
+    if (met) *met = I.h_state->meet != kEmpty;
+    return 0;
+  }
+  I.grid_level(side, dir == Direction::kBottomUp ? 2 : 1, 0);
+  I.sync_state();
+  if (met) *met = I.h_state->meet != kEmpty;
+  return I.h_state->qtail[side] - before;
+}
+
+bool HipBiBfs::check_meet() {
+  auto& I = *p_;
+  launch::bitmap_meet(I.buf, I.d_flag, I.stream);
+  uint32_t f = 0;
+  HIP_CHECK(hipMemcpyAsync(&f, I.d_flag, 4, hipMemcpyDeviceToHost, I.stream));
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  return f != 0;
+}
+
+SearchResult HipBiBfs::finish() {
+  auto& I = *p_;
+  SearchResult r;
+  if (I.step_src == I.step_dst) {
+    r.found = true;
+    r.hops = 0;
+    r.meet = I.step_src;
+    r.path = {I.step_src};
+  } else {
+    const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
+    launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap};
+    launch::walk_path(I.buf, hs, I.step_src, I.step_dst, seq, I.stream);
+    I.wait_seq(seq);
+    SearchOptions opt;
+    r = I.collect(seq, opt, SearchStats{});
+  }
+  launch::cleanup(I.buf, I.n, I.stream);
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  return r;
+}
+
+// ---------------------------------------------------------------- test helpers
+
+Csr HipBiBfs::download_csr() const {
+  const auto& I = *p_;
+  Csr g;
+  g.n = I.n;
+  g.m_input = I.m_input;
+  g.row_off.resize((size_t)I.n + 1);
+  g.col.resize(I.nnz);
+  HIP_CHECK(hipMemcpyAsync(g.row_off.data(), I.d_row_off, ((size_t)I.n + 1) * 8, hipMemcpyDeviceToHost,
+                           I.stream));
+  if (I.nnz)
+    HIP_CHECK(hipMemcpyAsync(g.col.data(), I.d_col, I.nnz * 4, hipMemcpyDeviceToHost, I.stream));
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  return g;
+}
+
+EdgeList HipBiBfs::download_edges() const {
+  const auto& I = *p_;
+  EdgeList el;
+  el.n = I.n;
+  BIBFS_REQUIRE(I.d_uv != nullptr, "no device-generated edge list resident");
+  el.uv.resize(2 * I.uv_m);
+  if (I.uv_m)
+    HIP_CHECK(hipMemcpyAsync(el.uv.data(), I.d_uv, I.uv_m * 8, hipMemcpyDeviceToHost, I.stream));
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  return el;
+}
+
+}  // namespace bibfs

@@ -1,0 +1,77 @@
+// Single-GPU bidirectional BFS engine for MI355X (v3 capability, C7/K1/K2 in
+// SURVEY.md, re-designed for CDNA4; see docs/DESIGN.md).
+//
+// Two tiers, chosen per level on the device:
+//  * LDS engine: ONE persistent 1024-thread workgroup runs the whole search in
+//    a single launch.  Both visited sets live in LDS hash tables, both
+//    frontiers (with their CSR row offsets prefetched) live in LDS, the meet
+//    test is fused into the claim, and no global atomics are issued (a global
+//    atomic with return costs ~1,700 cycles on gfx950, an LDS CAS ~100).  On
+//    reference-shape graphs (G(n, 2.2/n)) the entire search runs here.
+//  * Grid engine: when a frontier outgrows LDS, state is handed off to
+//    device-wide top-down (load-balanced, wave-aggregated queue appends) and
+//    bottom-up (bitmap, early exit, ballot-built words) kernels with a Beamer
+//    direction switch.  This serves RMAT/Kronecker graphs.
+// Header is HIP-free (pimpl) so g++-built tools and bindings can include it.
+#pragma once
+
+#include <memory>
+
+#include "bibfs/graph.hpp"
+#include "bibfs/result.hpp"
+
+namespace bibfs {
+
+struct DeviceInfo {
+  std::string name;
+  std::string arch;
+  int cus = 0;
+  size_t hbm_bytes = 0;
+  int lds_bytes = 0;
+};
+
+class HipBiBfs {
+ public:
+  explicit HipBiBfs(int device = 0);
+  ~HipBiBfs();
+  HipBiBfs(const HipBiBfs&) = delete;
+  HipBiBfs& operator=(const HipBiBfs&) = delete;
+
+  // --- graph ingest -------------------------------------------------------
+  void load_csr(const Csr& g);                 // upload a host CSR
+  void load_edges(const EdgeList& el);         // upload edges, build CSR on device
+  void generate_gnp(uint32_t n, double p, uint64_t seed);                // on device
+  void generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a = 0.57, double b = 0.19,
+                     double c = 0.19);                                     // on device
+  uint32_t n() const;
+  uint64_t nnz() const;
+  uint64_t m_input() const;
+  double last_build_ms() const;                // device time of the last ingest
+  size_t device_bytes() const;                 // HBM held by graph + search state
+
+  // --- search ---------------------------------------------------------------
+  SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
+
+  // --- step-wise API (parity with the reference's per-level C API,
+  //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)
+  void begin(vid_t src, vid_t dst);
+  // Expands one level of `side` with the grid engine; returns number of newly
+  // claimed vertices (0 = frontier died).  *met set when the sides met.
+  uint64_t expand(int side, bool* met, Direction dir = Direction::kTopDown);
+  bool check_meet();                    // bitmap AND over all words (K2/K4 parity)
+  SearchResult finish();                // path reconstruction + cleanup
+
+  // --- introspection for tests --------------------------------------------
+  Csr download_csr() const;
+  EdgeList download_edges() const;      // edges of the last generate_* call
+  int device() const;
+  DeviceInfo info() const;
+  void* stream() const;                 // hipStream_t
+  void synchronize() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> p_;
+};
+
+}  // namespace bibfs

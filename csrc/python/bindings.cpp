@@ -1,0 +1,270 @@
+// pybind11 bindings: bidirectional_bfs_amd._native
+//
+// Exposes the native core (formats, generators, CSR, CPU engines, the HIP
+// single-GPU engine and the RCCL multi-GPU engine) to Python.  Every search
+// call releases the GIL.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "bibfs/cpu_engine.hpp"
+#include "bibfs/dist_engine.hpp"
+#include "bibfs/gen.hpp"
+#include "bibfs/hip_engine.hpp"
+#include "bibfs/io.hpp"
+
+namespace py = pybind11;
+using namespace bibfs;
+
+namespace {
+
+template <typename T>
+py::array_t<T> to_numpy(const std::vector<T>& v) {
+  py::array_t<T> a(v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+template <typename T>
+std::vector<T> from_numpy(const py::array_t<T, py::array::c_style | py::array::forcecast>& a) {
+  std::vector<T> v((size_t)a.size());
+  if (a.size()) std::memcpy(v.data(), a.data(), v.size() * sizeof(T));
+  return v;
+}
+
+py::dict stats_dict(const SearchStats& s) {
+  py::dict d;
+  d["levels"] = s.levels;
+  d["edges_inspected"] = s.edges_inspected;
+  d["visited"] = s.visited;
+  d["grid_levels"] = s.grid_levels;
+  d["bottomup_levels"] = s.bottomup_levels;
+  d["handoff"] = s.handoff;
+  py::list tr;
+  for (const auto& t : s.trace) {
+    py::dict x;
+    x["side"] = t.side;
+    x["depth"] = t.depth;
+    x["frontier"] = t.frontier;
+    x["edges"] = t.edges;
+    x["discovered"] = t.discovered;
+    x["mode"] = t.mode;
+    tr.append(x);
+  }
+  d["trace"] = tr;
+  return d;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "MI355X-native bidirectional BFS core (HIP/CDNA4 + RCCL)";
+
+  py::register_exception<Error>(m, "BibfsError", PyExc_RuntimeError);
+
+  // ---------------------------------------------------------------- graphs
+  py::class_<EdgeList>(m, "EdgeList")
+      .def(py::init<>())
+      .def_readwrite("n", &EdgeList::n)
+      .def_property_readonly("m", &EdgeList::m)
+      .def("edges",
+           [](const EdgeList& e) {
+             py::array_t<uint32_t> a({(py::ssize_t)e.m(), (py::ssize_t)2});
+             if (e.m()) std::memcpy(a.mutable_data(), e.uv.data(), e.uv.size() * 4);
+             return a;
+           })
+      .def_static(
+          "from_numpy",
+          [](uint32_t n, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> uv) {
+            EdgeList e;
+            e.n = n;
+            e.uv = from_numpy<uint32_t>(uv);
+            BIBFS_REQUIRE(e.uv.size() % 2 == 0, "edge array must have an even number of entries");
+            for (uint32_t x : e.uv) BIBFS_REQUIRE(x < n, "edge endpoint >= n");
+            return e;
+          },
+          py::arg("n"), py::arg("edges"));
+
+  py::class_<Csr>(m, "Csr")
+      .def(py::init<>())
+      .def_readonly("n", &Csr::n)
+      .def_readonly("m_input", &Csr::m_input)
+      .def_property_readonly("nnz", &Csr::nnz)
+      .def_property_readonly("row_off", [](const Csr& g) { return to_numpy(g.row_off); })
+      .def_property_readonly("col", [](const Csr& g) { return to_numpy(g.col); })
+      .def("degree", &Csr::degree);
+
+  m.def(
+      "build_csr",
+      [](const EdgeList& el, bool dedup, bool sort_rows, int threads) {
+        CsrOptions o;
+        o.dedup = dedup;
+        o.sort_rows = sort_rows;
+        o.threads = threads;
+        return build_csr(el, o);
+      },
+      py::arg("edges"), py::arg("dedup") = false, py::arg("sort_rows") = false, py::arg("threads") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "build_csr_rows",
+      [](const EdgeList& el, int rank, int size) {
+        return build_csr_rows(el, Partition::block(el.n, rank, size));
+      },
+      py::arg("edges"), py::arg("rank"), py::arg("size"));
+  m.def("csr_to_edges", &csr_to_edges);
+
+  m.def("read_bin", &read_bin, py::call_guard<py::gil_scoped_release>());
+  m.def("write_bin", &write_bin, py::call_guard<py::gil_scoped_release>());
+  m.def("read_bin_shard", &read_bin_shard);
+  m.def("read_csr_cache", &read_csr_cache);
+  m.def("write_csr_cache", &write_csr_cache);
+  m.def("sidecar_path", &sidecar_path);
+  m.def(
+      "read_dense",
+      [](const std::string& p) {
+        DenseMatrix d = read_dense(p);
+        py::array_t<uint8_t> a({(py::ssize_t)d.n, (py::ssize_t)d.n});
+        if (d.n) std::memcpy(a.mutable_data(), d.a.data(), d.a.size());
+        return a;
+      });
+  m.def("write_dense", [](const std::string& p, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> a) {
+    BIBFS_REQUIRE(a.ndim() == 2 && a.shape(0) == a.shape(1), "dense matrix must be square");
+    DenseMatrix d;
+    d.n = (uint32_t)a.shape(0);
+    d.a = from_numpy<uint8_t>(a);
+    write_dense(p, d);
+  });
+
+  m.def("gen_gnp", &gen_gnp, py::arg("n"), py::arg("p"), py::arg("seed") = 1, py::arg("threads") = 0,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gen_rmat", &gen_rmat, py::arg("n"), py::arg("m"), py::arg("seed") = 1, py::arg("a") = 0.57,
+        py::arg("b") = 0.19, py::arg("c") = 0.19, py::arg("threads") = 0,
+        py::call_guard<py::gil_scoped_release>());
+  m.def("gen_kronecker", &gen_kronecker, py::arg("scale"), py::arg("edgefactor") = 16,
+        py::arg("seed") = 1, py::arg("threads") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("reference_p", &reference_p);
+
+  // ---------------------------------------------------------------- search API
+  py::enum_<SidePolicy>(m, "SidePolicy")
+      .value("SMALLER_EDGES", SidePolicy::kSmallerEdges)
+      .value("SMALLER_FRONTIER", SidePolicy::kSmallerFrontier)
+      .value("ALTERNATE", SidePolicy::kAlternate);
+  py::enum_<Direction>(m, "Direction")
+      .value("AUTO", Direction::kAuto)
+      .value("TOPDOWN", Direction::kTopDown)
+      .value("BOTTOMUP", Direction::kBottomUp);
+
+  py::class_<SearchOptions>(m, "SearchOptions")
+      .def(py::init<>())
+      .def_readwrite("side", &SearchOptions::side)
+      .def_readwrite("direction", &SearchOptions::direction)
+      .def_readwrite("alpha", &SearchOptions::alpha)
+      .def_readwrite("beta", &SearchOptions::beta)
+      .def_readwrite("want_path", &SearchOptions::want_path)
+      .def_readwrite("force_grid", &SearchOptions::force_grid)
+      .def_readwrite("trace", &SearchOptions::trace);
+
+  py::class_<SearchResult>(m, "SearchResult")
+      .def_readonly("found", &SearchResult::found)
+      .def_readonly("hops", &SearchResult::hops)
+      .def_readonly("path", &SearchResult::path)
+      .def_readonly("meet", &SearchResult::meet)
+      .def_readonly("search_ms", &SearchResult::search_ms)
+      .def_readonly("total_ms", &SearchResult::total_ms)
+      .def_property_readonly("stats", [](const SearchResult& r) { return stats_dict(r.stats); })
+      .def("__repr__", [](const SearchResult& r) {
+        return "SearchResult(found=" + std::string(r.found ? "True" : "False") +
+               ", hops=" + std::to_string(r.hops) + ", search_ms=" + std::to_string(r.search_ms) + ")";
+      });
+
+  py::class_<SerialBiBfs>(m, "SerialBiBfs")
+      .def(py::init<const Csr&>(), py::keep_alive<1, 2>())
+      .def("search", &SerialBiBfs::search, py::arg("src"), py::arg("dst"),
+           py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>());
+  m.def("bfs_oracle", &bfs_oracle, py::call_guard<py::gil_scoped_release>());
+  m.def("bfs_distances", [](const Csr& g, vid_t src) { return to_numpy(bfs_distances(g, src)); });
+  m.def("validate_path", [](const Csr& g, vid_t src, vid_t dst, int64_t hops, const std::vector<vid_t>& path) {
+    std::string why;
+    bool ok = validate_path(g, src, dst, hops, path, &why);
+    return py::make_tuple(ok, why);
+  });
+
+  // ---------------------------------------------------------------- HIP engine
+  py::class_<DeviceInfo>(m, "DeviceInfo")
+      .def_readonly("name", &DeviceInfo::name)
+      .def_readonly("arch", &DeviceInfo::arch)
+      .def_readonly("cus", &DeviceInfo::cus)
+      .def_readonly("hbm_bytes", &DeviceInfo::hbm_bytes)
+      .def_readonly("lds_bytes", &DeviceInfo::lds_bytes);
+
+  py::class_<HipBiBfs>(m, "HipBiBfs")
+      .def(py::init<int>(), py::arg("device") = 0)
+      .def("load_csr", &HipBiBfs::load_csr, py::call_guard<py::gil_scoped_release>())
+      .def("load_edges", &HipBiBfs::load_edges, py::call_guard<py::gil_scoped_release>())
+      .def("generate_gnp", &HipBiBfs::generate_gnp, py::arg("n"), py::arg("p"), py::arg("seed") = 1,
+           py::call_guard<py::gil_scoped_release>())
+      .def("generate_rmat", &HipBiBfs::generate_rmat, py::arg("n"), py::arg("m"), py::arg("seed") = 1,
+           py::arg("a") = 0.57, py::arg("b") = 0.19, py::arg("c") = 0.19,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("n", &HipBiBfs::n)
+      .def_property_readonly("nnz", &HipBiBfs::nnz)
+      .def_property_readonly("m_input", &HipBiBfs::m_input)
+      .def_property_readonly("last_build_ms", &HipBiBfs::last_build_ms)
+      .def_property_readonly("device_bytes", &HipBiBfs::device_bytes)
+      .def_property_readonly("device", &HipBiBfs::device)
+      .def("search", &HipBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
+           py::call_guard<py::gil_scoped_release>())
+      .def("begin", &HipBiBfs::begin, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "expand",
+          [](HipBiBfs& e, int side, Direction dir) {
+            bool met = false;
+            uint64_t c;
+            {
+              py::gil_scoped_release rel;
+              c = e.expand(side, &met, dir);
+            }
+            return py::make_tuple(c, met);
+          },
+          py::arg("side"), py::arg("direction") = Direction::kTopDown)
+      .def("check_meet", &HipBiBfs::check_meet, py::call_guard<py::gil_scoped_release>())
+      .def("finish", &HipBiBfs::finish, py::call_guard<py::gil_scoped_release>())
+      .def("download_csr", &HipBiBfs::download_csr)
+      .def("download_edges", &HipBiBfs::download_edges)
+      .def("info", &HipBiBfs::info)
+      .def("synchronize", &HipBiBfs::synchronize, py::call_guard<py::gil_scoped_release>());
+
+  // ---------------------------------------------------------------- multi-GPU engine
+  m.def("rccl_unique_id", []() {
+    auto id = dist_unique_id();
+    return py::bytes(reinterpret_cast<const char*>(id.data()), id.size());
+  });
+  py::class_<DistBiBfs>(m, "DistBiBfs")
+      .def(py::init([](int rank, int size, int device, py::bytes uid) {
+             std::string s = uid;
+             std::vector<uint8_t> id(s.begin(), s.end());
+             py::gil_scoped_release rel;
+             return new DistBiBfs(rank, size, device, id);
+           }),
+           py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("unique_id"))
+      .def_property_readonly("rank", &DistBiBfs::rank)
+      .def_property_readonly("size", &DistBiBfs::size)
+      .def_property_readonly("n", &DistBiBfs::n)
+      .def_property_readonly("m_input", &DistBiBfs::m_input)
+      .def_property_readonly("local_nnz", &DistBiBfs::local_nnz)
+      .def_property_readonly("lo", &DistBiBfs::lo)
+      .def_property_readonly("hi", &DistBiBfs::hi)
+      .def("load_edges", &DistBiBfs::load_edges, py::call_guard<py::gil_scoped_release>())
+      .def("load_bin", &DistBiBfs::load_bin, py::call_guard<py::gil_scoped_release>())
+      .def("generate_gnp", &DistBiBfs::generate_gnp, py::arg("n"), py::arg("p"), py::arg("seed") = 1,
+           py::call_guard<py::gil_scoped_release>())
+      .def("generate_rmat", &DistBiBfs::generate_rmat, py::arg("n"), py::arg("m"), py::arg("seed") = 1,
+           py::arg("a") = 0.57, py::arg("b") = 0.19, py::arg("c") = 0.19,
+           py::call_guard<py::gil_scoped_release>())
+      .def("search", &DistBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
+           py::call_guard<py::gil_scoped_release>())
+      .def("barrier", &DistBiBfs::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>());
+}
