@@ -29,7 +29,7 @@ HIPFLAGS  := -O3 -fPIC $(CXXSTD) $(INC) --offload-arch=$(ARCH) -mcode-object-ver
              -Wno-unused-result -munsafe-fp-atomics
 MPI_INC   := -I$(MPI_HOME)/include
 # system libstdc++ first: conda ships an older one
-MPI_LD    := -L$(MPI_HOME)/lib -lmpi -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_HOME)/lib
+MPI_LD    := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_HOME)/lib
 HIP_LD    := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
 RCCL_LD   := -L$(ROCM)/lib -lrccl
 
@@ -40,7 +40,7 @@ PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_
 CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp
 HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/hip_engine.hip \
              csrc/hip/capi.hip csrc/dist/dist_engine.hip
-MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp csrc/dist/mpi_bootstrap.cpp
+MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp
 
 CORE_OBJ  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CORE_SRC))
 HIP_OBJ   := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRC))

@@ -1,0 +1,120 @@
+"""MI355X compute path: the hand-written HIP/CDNA4 kernels behind a Python API.
+
+``HipEngine`` owns one GPU's copy of a graph (CSR in HBM, built on the device)
+and answers shortest-path queries with the single-workgroup LDS engine,
+handing large frontiers to the grid engine (top-down / bottom-up with a
+Beamer switch).  No CPU fallback: constructing it without a GPU raises.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+from .._lib import native
+from ..models import Graph
+
+SearchOptions = native.SearchOptions
+SidePolicy = native.SidePolicy
+Direction = native.Direction
+
+
+def make_options(
+    side: str = "edges",
+    direction: str = "auto",
+    alpha: float = 14.0,
+    beta: float = 24.0,
+    want_path: bool = True,
+    force_grid: bool = False,
+    trace: bool = False,
+) -> "native.SearchOptions":
+    o = native.SearchOptions()
+    o.side = {"edges": SidePolicy.SMALLER_EDGES, "frontier": SidePolicy.SMALLER_FRONTIER,
+              "alternate": SidePolicy.ALTERNATE}[side]
+    o.direction = {"auto": Direction.AUTO, "topdown": Direction.TOPDOWN, "bottomup": Direction.BOTTOMUP}[direction]
+    o.alpha, o.beta = float(alpha), float(beta)
+    o.want_path, o.force_grid, o.trace = bool(want_path), bool(force_grid), bool(trace)
+    return o
+
+
+class HipEngine:
+    """Single-GPU bidirectional BFS (v3 capability)."""
+
+    def __init__(self, device: int = 0):
+        self._e = native.HipBiBfs(int(device))
+
+    # ---- ingest
+    def load(self, graph: Graph, build_on_device: bool = True) -> "HipEngine":
+        if build_on_device:
+            self._e.load_edges(graph.edges)
+        else:
+            self._e.load_csr(graph.csr)
+        return self
+
+    def load_csr(self, csr) -> "HipEngine":
+        self._e.load_csr(csr)
+        return self
+
+    def generate_gnp(self, n: int, p: Optional[float] = None, seed: int = 1) -> "HipEngine":
+        self._e.generate_gnp(int(n), native.reference_p(int(n)) if p is None else float(p), int(seed))
+        return self
+
+    def generate_rmat(self, n: int, m: int, seed: int = 1, a=0.57, b=0.19, c=0.19) -> "HipEngine":
+        self._e.generate_rmat(int(n), int(m), int(seed), a, b, c)
+        return self
+
+    # ---- queries
+    def search(self, src: int, dst: int, options: Optional["native.SearchOptions"] = None, **kw):
+        return self._e.search(int(src), int(dst), options if options is not None else make_options(**kw))
+
+    # step-wise API (reference v4/comp.h parity)
+    def begin(self, src: int, dst: int) -> None:
+        self._e.begin(int(src), int(dst))
+
+    def expand(self, side: int, direction: str = "topdown"):
+        d = Direction.BOTTOMUP if direction == "bottomup" else Direction.TOPDOWN
+        return self._e.expand(int(side), d)
+
+    def check_meet(self) -> bool:
+        return self._e.check_meet()
+
+    def finish(self):
+        return self._e.finish()
+
+    # ---- introspection
+    @property
+    def n(self) -> int:
+        return self._e.n
+
+    @property
+    def m(self) -> int:
+        return self._e.m_input
+
+    @property
+    def nnz(self) -> int:
+        return self._e.nnz
+
+    @property
+    def build_ms(self) -> float:
+        return self._e.last_build_ms
+
+    @property
+    def device_bytes(self) -> int:
+        return self._e.device_bytes
+
+    def info(self):
+        return self._e.info()
+
+    def download_csr(self):
+        return self._e.download_csr()
+
+    def download_edges(self):
+        return self._e.download_edges()
+
+    def synchronize(self) -> None:
+        self._e.synchronize()
+
+    @property
+    def native(self):
+        return self._e
+
+
+__all__ = ["HipEngine", "make_options", "SearchOptions", "SidePolicy", "Direction"]

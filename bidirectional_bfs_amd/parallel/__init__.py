@@ -1,0 +1,122 @@
+"""Multi-GPU and multi-process execution (v2 / v4 capabilities).
+
+* ``DistEngine``: one process per GPU, graph 1-D partitioned, every per-level
+  exchange an RCCL collective over xGMI (native ``DistBiBfs``).  The RCCL
+  communicator is bootstrapped from a unique id broadcast over
+  ``torch.distributed`` (``from_torch_distributed``) or over MPI by the
+  ``mpi_bibfs`` CLI.
+* ``ReplicatedServer``: query-parallel serving -- every GPU holds the whole
+  graph (a 10M-vertex graph is ~0.2 GB of a 288 GB HBM3E part) and answers its
+  own share of queries; throughput scales with the number of GPUs.
+* ``run_mpi``: launch the CPU MPI engines (``second_try`` = C3,
+  ``mpi_queue_bibfs`` = C4) or ``mpi_bibfs`` under ``mpiexec``.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+from typing import List, Optional, Sequence
+
+from .._lib import native, tool_path
+from ..models import Graph
+from ..ops import HipEngine, make_options
+
+MPIEXEC = os.environ.get("BIBFS_MPIEXEC", "/opt/conda/bin/mpiexec")
+
+
+class DistEngine:
+    """Partitioned multi-GPU bidirectional BFS (collective API: call on every rank)."""
+
+    def __init__(self, rank: int, world: int, device: int, unique_id: bytes):
+        self._e = native.DistBiBfs(int(rank), int(world), int(device), unique_id)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        return native.rccl_unique_id()
+
+    @classmethod
+    def from_torch_distributed(cls, device: Optional[int] = None) -> "DistEngine":
+        """Bootstrap from an initialised torch.distributed process group."""
+        import torch.distributed as dist
+
+        rank, world = dist.get_rank(), dist.get_world_size()
+        obj = [native.rccl_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        if device is None:
+            device = int(os.environ.get("LOCAL_RANK", rank))
+        return cls(rank, world, device, obj[0])
+
+    def load(self, graph: Graph) -> "DistEngine":
+        self._e.load_edges(graph.edges)
+        return self
+
+    def load_bin(self, path: str) -> "DistEngine":
+        self._e.load_bin(path)
+        return self
+
+    def generate_gnp(self, n: int, p: Optional[float] = None, seed: int = 1) -> "DistEngine":
+        self._e.generate_gnp(int(n), native.reference_p(int(n)) if p is None else float(p), int(seed))
+        return self
+
+    def generate_rmat(self, n: int, m: int, seed: int = 1) -> "DistEngine":
+        self._e.generate_rmat(int(n), int(m), int(seed))
+        return self
+
+    def search(self, src: int, dst: int, options=None, **kw):
+        return self._e.search(int(src), int(dst), options if options is not None else make_options(**kw))
+
+    def barrier(self) -> None:
+        self._e.barrier()
+
+    def allreduce_max(self, x: float) -> float:
+        return self._e.allreduce_max(float(x))
+
+    @property
+    def rank(self) -> int:
+        return self._e.rank
+
+    @property
+    def world(self) -> int:
+        return self._e.size
+
+    @property
+    def n(self) -> int:
+        return self._e.n
+
+    @property
+    def m(self) -> int:
+        return self._e.m_input
+
+    @property
+    def owned(self):
+        return self._e.lo, self._e.hi
+
+
+class ReplicatedServer:
+    """Query-parallel serving: rank r answers queries r, r+W, r+2W, ... on its own GPU."""
+
+    def __init__(self, rank: int, world: int, device: int):
+        self.rank, self.world = int(rank), int(world)
+        self.engine = HipEngine(device)
+
+    def load(self, graph: Graph) -> "ReplicatedServer":
+        self.engine.load(graph)
+        return self
+
+    def my_queries(self, pairs: Sequence) -> List:
+        return list(pairs[self.rank :: self.world])
+
+    def serve(self, pairs: Sequence, options=None) -> List:
+        return [self.engine.search(s, d, options) for s, d in self.my_queries(pairs)]
+
+
+def run_mpi(tool: str, args: Sequence[str], np: int = 2, timeout: float = 300.0, env=None) -> subprocess.CompletedProcess:
+    """Run a native MPI tool (second_try, mpi_queue_bibfs, mpi_bibfs) under mpiexec."""
+    cmd = [MPIEXEC, "-n", str(int(np)), tool_path(tool)] + [str(a) for a in args]
+    e = dict(os.environ)
+    if env:
+        e.update(env)
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
+
+
+__all__ = ["DistEngine", "ReplicatedServer", "run_mpi", "MPIEXEC"]

@@ -19,13 +19,16 @@ constexpr int kScanThreads = 1024;
 constexpr int kScanItems = 8;
 constexpr uint64_t kScanTile = (uint64_t)kScanThreads * kScanItems;
 
-__global__ void k_degree(const uint32_t* __restrict__ uv, uint64_t m, uint64_t* __restrict__ deg) {
+// Rows [lo, hi) only (full graph: lo = 0, hi = n): the partitioned engine
+// builds just its owned rows from the same edge stream.
+__global__ void k_degree(const uint32_t* __restrict__ uv, uint64_t m, uint32_t lo, uint32_t hi,
+                         uint64_t* __restrict__ deg) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint2 e = reinterpret_cast<const uint2*>(uv)[i];
     if (e.x == e.y) continue;  // self loops carry no BFS information
-    atomicAdd(reinterpret_cast<unsigned long long*>(&deg[e.x]), 1ULL);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&deg[e.y]), 1ULL);
+    if (e.x >= lo && e.x < hi) atomicAdd(reinterpret_cast<unsigned long long*>(&deg[e.x - lo]), 1ULL);
+    if (e.y >= lo && e.y < hi) atomicAdd(reinterpret_cast<unsigned long long*>(&deg[e.y - lo]), 1ULL);
   }
 }
 
@@ -118,14 +121,14 @@ void exclusive_scan_u64(uint64_t* d, uint64_t count, hipStream_t s) {
   HIP_CHECK(hipFree(bsum));
 }
 
-__global__ void k_scatter(const uint32_t* __restrict__ uv, uint64_t m,
+__global__ void k_scatter(const uint32_t* __restrict__ uv, uint64_t m, uint32_t lo, uint32_t hi,
                           unsigned long long* __restrict__ cursor, uint32_t* __restrict__ col) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < m;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint2 e = reinterpret_cast<const uint2*>(uv)[i];
     if (e.x == e.y) continue;
-    col[atomicAdd(&cursor[e.x], 1ULL)] = e.y;
-    col[atomicAdd(&cursor[e.y], 1ULL)] = e.x;
+    if (e.x >= lo && e.x < hi) col[atomicAdd(&cursor[e.x - lo], 1ULL)] = e.y;
+    if (e.y >= lo && e.y < hi) col[atomicAdd(&cursor[e.y - lo], 1ULL)] = e.x;
   }
 }
 
@@ -183,10 +186,11 @@ __global__ void k_rmat(RmatParams P, uint64_t m, uint32_t* __restrict__ uv) {
 
 namespace launch {
 
-uint64_t count_csr_entries(const uint32_t* d_uv, uint64_t m, uint32_t n, uint64_t* d_row_off,
-                           hipStream_t s) {
+uint64_t count_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, uint64_t* d_row_off,
+                        hipStream_t s) {
+  const uint32_t n = hi - lo;
   HIP_CHECK(hipMemsetAsync(d_row_off, 0, (n + 1ULL) * sizeof(uint64_t), s));
-  if (m) k_degree<<<grid_for(m, 256), 256, 0, s>>>(d_uv, m, d_row_off);
+  if (m) k_degree<<<grid_for(m, 256), 256, 0, s>>>(d_uv, m, lo, hi, d_row_off);
   HIP_CHECK(hipGetLastError());
   exclusive_scan_u64(d_row_off, n + 1ULL, s);
   uint64_t nnz = 0;
@@ -195,13 +199,24 @@ uint64_t count_csr_entries(const uint32_t* d_uv, uint64_t m, uint32_t n, uint64_
   return nnz;
 }
 
-void fill_csr(const uint32_t* d_uv, uint64_t m, uint32_t n, const uint64_t* d_row_off,
-              uint64_t* d_cursor, uint32_t* d_col, hipStream_t s) {
+uint64_t count_csr_entries(const uint32_t* d_uv, uint64_t m, uint32_t n, uint64_t* d_row_off,
+                           hipStream_t s) {
+  return count_csr_rows(d_uv, m, 0, n, d_row_off, s);
+}
+
+void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, const uint64_t* d_row_off,
+                   uint64_t* d_cursor, uint32_t* d_col, hipStream_t s) {
+  const uint32_t n = hi - lo;
   k_copy_u64<<<grid_for(n + 1ULL, 256), 256, 0, s>>>(d_row_off, n + 1ULL, d_cursor);
   if (m)
-    k_scatter<<<grid_for(m, 256), 256, 0, s>>>(d_uv, m,
+    k_scatter<<<grid_for(m, 256), 256, 0, s>>>(d_uv, m, lo, hi,
                                                reinterpret_cast<unsigned long long*>(d_cursor), d_col);
   HIP_CHECK(hipGetLastError());
+}
+
+void fill_csr(const uint32_t* d_uv, uint64_t m, uint32_t n, const uint64_t* d_row_off,
+              uint64_t* d_cursor, uint32_t* d_col, hipStream_t s) {
+  fill_csr_rows(d_uv, m, 0, n, d_row_off, d_cursor, d_col, s);
 }
 
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s) {

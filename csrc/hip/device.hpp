@@ -130,6 +130,10 @@ uint64_t count_csr_entries(const uint32_t* d_uv, uint64_t m, uint32_t n, uint64_
                            hipStream_t s);
 void fill_csr(const uint32_t* d_uv, uint64_t m, uint32_t n, const uint64_t* d_row_off,
               uint64_t* d_cursor, uint32_t* d_col, hipStream_t s);
+uint64_t count_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, uint64_t* d_row_off,
+                        hipStream_t s);
+void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, const uint64_t* d_row_off,
+                   uint64_t* d_cursor, uint32_t* d_col, hipStream_t s);
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s);
 uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);
 void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,

@@ -289,17 +289,17 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
 HipBiBfs::~HipBiBfs() {
   if (!p_) return;
   try {
-    hipSetDevice(p_->device);
-    hipStreamSynchronize(p_->stream);
+    (void)hipSetDevice(p_->device);
+    (void)hipStreamSynchronize(p_->stream);
     p_->free_graph();
   } catch (...) {
   }
-  hipHostFree(p_->h_res);
-  hipHostFree(p_->h_path);
-  hipHostFree(p_->h_state);
-  hipEventDestroy(p_->ev0);
-  hipEventDestroy(p_->ev1);
-  hipStreamDestroy(p_->stream);
+  (void)hipHostFree(p_->h_res);
+  (void)hipHostFree(p_->h_path);
+  (void)hipHostFree(p_->h_state);
+  (void)hipEventDestroy(p_->ev0);
+  (void)hipEventDestroy(p_->ev1);
+  (void)hipStreamDestroy(p_->stream);
 }
 
 void HipBiBfs::load_csr(const Csr& g) {

@@ -1,0 +1,76 @@
+"""Multi-GPU engine (world size 1 on the single-GPU box: RCCL communicator of
+one rank), the GPU CLI tools and the bench.py contract."""
+import json
+import os
+import random
+import subprocess
+import sys
+
+import pytest
+
+import bidirectional_bfs_amd as bb
+from bidirectional_bfs_amd import native
+from bidirectional_bfs_amd._lib import tool_path
+from bidirectional_bfs_amd.parallel import MPIEXEC, run_mpi
+from bidirectional_bfs_amd.utils.oracle import check_result
+
+pytestmark = pytest.mark.gpu
+
+
+def test_dist_engine_world1():
+    import torch  # noqa: F401
+
+    from bidirectional_bfs_amd.parallel import DistEngine
+
+    eng = DistEngine(0, 1, 0, DistEngine.unique_id())
+    for spec in ["gnp:100000::6", "rmat:65536:1048576:3"]:
+        g = bb.from_spec(spec)
+        eng.load(g)
+        rnd = random.Random(3)
+        for s, d in [(0, g.n - 1)] + [(rnd.randrange(g.n), rnd.randrange(g.n)) for _ in range(10)]:
+            for direction in ("auto", "topdown", "bottomup"):
+                r = eng.search(s, d, direction=direction)
+                check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+    eng.generate_gnp(1_000_000, None, 2)
+    r = eng.search(0, 999_999)
+    assert r.hops == 19 and len(r.path) == 20
+
+
+def test_bibfs_hip_cli():
+    out = subprocess.run([tool_path("bibfs_hip"), "gnp:100000::6", "0", "99999", "--verify", "--repeat", "3"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    assert lines[0] == "Shortest path length = 17"
+    assert lines[2].startswith("[Time] HIP bi-BFS query = ") and lines[2].endswith(" s")
+    assert "GPU BFS: PATH FOUND" in out.stdout and "Verify: OK" in out.stdout
+    js = subprocess.run([tool_path("bibfs_cuda_only"), "gnp:100000::6", "0", "99999", "--json"],
+                        capture_output=True, text=True, timeout=120)
+    d = json.loads(js.stdout)
+    assert d["hops"] == 17 and d["gteps"] > 0.952  # beats the best published 100k number
+
+
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="MPICH not installed")
+def test_mpi_bibfs_one_rank():
+    r = run_mpi("mpi_bibfs", ["gnp:100000::6", 0, 99999, "--verify"], np=1, timeout=180)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Shortest path length = 17" in r.stdout and "Verify: OK" in r.stdout
+
+
+def test_bibfs_bench_tool():
+    out = subprocess.run([tool_path("bibfs_bench"), "gnp:100000::6", "--queries", "30", "--warmup", "5"],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout)
+    assert d["queries"] == 30 and d["median_query_ms"] > 0
+
+
+def test_bench_py_contract(repo_root):
+    out = subprocess.run([sys.executable, os.path.join(repo_root, "bench.py"), "--steps", "20", "--warmup", "5",
+                          "--extra-graph", ""], capture_output=True, text=True, timeout=300, cwd=repo_root)
+    assert out.returncode == 0, out.stderr
+    d = json.loads(out.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in d
+    assert d["n_gpus"] == 1 and d["steps"] == 20 and d["value"] > 0

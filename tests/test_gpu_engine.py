@@ -1,0 +1,153 @@
+"""Single-GPU HIP engine (v3 capability) on a real MI355X, against the CPU oracle."""
+import ctypes
+import random
+
+import numpy as np
+import pytest
+
+import bidirectional_bfs_amd as bb
+from bidirectional_bfs_amd import native
+from bidirectional_bfs_amd.models import Graph, gnp, kronecker, rmat
+from bidirectional_bfs_amd.ops import make_options
+from bidirectional_bfs_amd.utils.oracle import check_result
+
+pytestmark = pytest.mark.gpu
+
+
+def pairs_for(n, k, seed):
+    rnd = random.Random(seed)
+    return [(0, n - 1)] + [(rnd.randrange(n), rnd.randrange(n)) for _ in range(k)]
+
+
+def assert_engine(eng, g, pairs, **opt):
+    o = make_options(**opt)
+    for s, d in pairs:
+        r = eng.search(s, d, o)
+        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+
+
+@pytest.mark.parametrize("spec", ["gnp:1000::1", "gnp:100000::6", "gnp:1000000::2", "rmat:65536:1048576:3",
+                                  "kron:16:16:2"])
+def test_lds_and_grid_vs_oracle(gpu_engine, spec):
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 25, 7)
+    assert_engine(gpu_engine, g, pairs)
+    assert_engine(gpu_engine, g, pairs[:8], force_grid=True)
+    assert_engine(gpu_engine, g, pairs[:5], force_grid=True, direction="topdown")
+    assert_engine(gpu_engine, g, pairs[:5], force_grid=True, direction="bottomup")
+    assert_engine(gpu_engine, g, pairs[:5], side="frontier")
+    assert_engine(gpu_engine, g, pairs[:5], side="alternate")
+
+
+def test_device_csr_equals_host(gpu_engine):
+    g = gnp(50000, seed=3)
+    gpu_engine.load(g)
+    d = gpu_engine.download_csr()
+    h = g.csr
+    assert np.array_equal(d.row_off, h.row_off)
+    for v in range(0, g.n, 97):
+        a, b = slice(h.row_off[v], h.row_off[v + 1]), slice(d.row_off[v], d.row_off[v + 1])
+        assert sorted(h.col[a]) == sorted(d.col[b])
+
+
+def test_device_generators_match_host(gpu_engine):
+    gpu_engine.generate_gnp(30000, 3.0 / 30000, 9)
+    assert np.array_equal(gpu_engine.download_edges().edges(), native.gen_gnp(30000, 3.0 / 30000, 9).edges())
+    gpu_engine.generate_rmat(20000, 150000, 5)
+    assert np.array_equal(gpu_engine.download_edges().edges(), native.gen_rmat(20000, 150000, 5).edges())
+
+
+def test_handoff_to_grid_on_10m(gpu_engine):
+    gpu_engine.generate_gnp(10_000_000, 2.2000000001 / 10_000_000, 1)
+    r = gpu_engine.search(0, 9_999_999)
+    assert r.found and r.hops == 19 and len(r.path) == 20
+    el = gpu_engine.download_edges()
+    g = Graph(el)
+    check_result(g.csr, 0, 9_999_999, r.hops, r.path, 19)
+
+
+def test_edge_cases(gpu_engine):
+    g = Graph.from_edges(8, [[0, 1], [1, 2], [3, 4], [4, 5]])
+    gpu_engine.load(g)
+    assert gpu_engine.search(1, 1).hops == 0
+    assert not gpu_engine.search(0, 5).found
+    assert not gpu_engine.search(7, 0).found  # isolated source
+    assert gpu_engine.search(0, 2).hops == 2
+    # hub source (degree > LDS capacity => immediate hand-off)
+    star = Graph.from_edges(20001, [[0, i] for i in range(1, 20001)] + [[5, 20000 - 1]])
+    gpu_engine.load(star)
+    r = gpu_engine.search(0, 7)
+    check_result(star.csr, 0, 7, r.hops, r.path, 1)
+    r = gpu_engine.search(3, 7)
+    check_result(star.csr, 3, 7, r.hops, r.path, 2)
+
+
+def test_long_path_goes_to_device_buffer(gpu_engine):
+    n = (1 << 20) + 500  # hops + 1 > pinned path capacity (2^20)
+    g = Graph.from_edges(n, np.stack([np.arange(n - 1), np.arange(1, n)], 1).astype(np.uint32))
+    gpu_engine.load(g)
+    r = gpu_engine.search(0, n - 1)
+    assert r.hops == n - 1 and r.path[0] == 0 and r.path[-1] == n - 1
+    assert np.array_equal(np.asarray(r.path), np.arange(n))
+
+
+def test_stepwise_api(gpu_engine):
+    g = gnp(100000, seed=6)
+    gpu_engine.load(g)
+    gpu_engine.begin(0, 99999)
+    met, side, levels = False, 0, 0
+    while not met and levels < 100:
+        claimed, met = gpu_engine.expand(side)
+        levels += 1
+        if claimed == 0 and not met:
+            break
+        side ^= 1
+    assert met and gpu_engine.check_meet()
+    r = gpu_engine.finish()
+    check_result(g.csr, 0, 99999, r.hops, r.path, 17)
+    assert gpu_engine.search(0, 99999).hops == 17  # state fully reset
+
+
+def test_c_api(repo_root):
+    lib = ctypes.CDLL(f"{repo_root}/build/lib/libbibfs.so")
+
+    class Res(ctypes.Structure):
+        _fields_ = [("found", ctypes.c_int32), ("hops", ctypes.c_int64), ("meet", ctypes.c_uint32),
+                    ("levels", ctypes.c_int32), ("edges_inspected", ctypes.c_uint64), ("search_ms", ctypes.c_double),
+                    ("total_ms", ctypes.c_double), ("path_len", ctypes.c_size_t)]
+
+    lib.bibfs_create.restype = ctypes.c_void_p
+    lib.bibfs_last_error.restype = ctypes.c_char_p
+    ctx = ctypes.c_void_p(lib.bibfs_create(0))
+    assert ctx.value, lib.bibfs_last_error()
+    el = native.gen_gnp(10000, native.reference_p(10000), 1)
+    uv = np.ascontiguousarray(el.edges().ravel())
+    assert lib.bibfs_init_graph_edges(ctx, ctypes.c_uint32(10000), ctypes.c_uint64(el.m),
+                                      uv.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32))) == 0
+    res = Res()
+    path = (ctypes.c_uint32 * 64)()
+    assert lib.bibfs_search(ctx, ctypes.c_uint32(0), ctypes.c_uint32(9999), ctypes.byref(res), path, 64) == 0
+    assert res.found == 1 and res.hops == 12 and res.path_len == 13 and path[0] == 0 and path[12] == 9999
+    # step-wise entry points
+    assert lib.bibfs_init_frontiers(ctx, ctypes.c_uint32(0), ctypes.c_uint32(9999)) == 0
+    met, claimed, side = ctypes.c_int(0), ctypes.c_uint64(0), 0
+    for _ in range(64):
+        assert lib.bibfs_expand_frontier(ctx, side, ctypes.byref(claimed), ctypes.byref(met)) == 0
+        if met.value:
+            break
+        side ^= 1
+    found = ctypes.c_int(0)
+    assert lib.bibfs_check_intersect(ctx, ctypes.byref(found)) == 0 and found.value == 1
+    assert lib.bibfs_finish(ctx, ctypes.byref(res), path, 64) == 0 and res.hops == 12
+    lib.bibfs_destroy(ctx)
+
+
+def test_trace_and_stats(gpu_engine):
+    g = gnp(100000, seed=6)
+    gpu_engine.load(g)
+    r = gpu_engine.search(0, 99999, make_options(trace=True))
+    tr = r.stats["trace"]
+    assert len(tr) == r.stats["levels"] == 17
+    assert all(t["mode"] == 0 for t in tr)
+    assert sum(t["edges"] for t in tr) == r.stats["edges_inspected"]

@@ -106,6 +106,17 @@ inline void print_result(const bibfs::SearchResult& r, bibfs::vid_t src, bibfs::
   }
 }
 
+inline void print_path(const bibfs::SearchResult& r) {
+  if (!r.found || r.path.empty()) return;
+  std::string line = "Path:";
+  char buf[16];
+  for (auto v : r.path) {
+    std::snprintf(buf, sizeof buf, " %u", v);
+    line += buf;
+  }
+  std::printf("%s\n", line.c_str());
+}
+
 inline void print_json(const bibfs::SearchResult& r, const std::string& engine, const std::string& graph,
                        uint32_t n, uint64_t m, bibfs::vid_t src, bibfs::vid_t dst, double load_ms,
                        double build_ms, double median_search_ms, double median_total_ms, int repeat,
