@@ -25,6 +25,7 @@ def make_options(
     want_path: bool = True,
     force_grid: bool = False,
     trace: bool = False,
+    lockstep: bool = True,
 ) -> "native.SearchOptions":
     o = native.SearchOptions()
     o.side = {"edges": SidePolicy.SMALLER_EDGES, "frontier": SidePolicy.SMALLER_FRONTIER,
@@ -32,6 +33,7 @@ def make_options(
     o.direction = {"auto": Direction.AUTO, "topdown": Direction.TOPDOWN, "bottomup": Direction.BOTTOMUP}[direction]
     o.alpha, o.beta = float(alpha), float(beta)
     o.want_path, o.force_grid, o.trace = bool(want_path), bool(force_grid), bool(trace)
+    o.lockstep = bool(lockstep)
     return o
 
 

@@ -68,7 +68,7 @@ SearchResult SerialBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt)
     lt.side = s;
     lt.depth = depth[s];
     lt.frontier = fe[s] - fb[s];
-    lt.mode = 3;
+    lt.mode = 0;
     const size_t e = fe[s];
     for (size_t i = fb[s]; i < e && meet == kNoVertex; ++i) {
       const vid_t u = q[i];

@@ -141,7 +141,8 @@ void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, 
 
 // engine_kernels.hip
 void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, uint32_t src,
-                uint32_t dst, uint32_t seq, int side_policy, int trace, hipStream_t s);
+                uint32_t dst, uint32_t seq, int side_policy, int trace, int pin_xcc, uint32_t* ticket,
+                int lockstep, hipStream_t s);
 int lds_threads();
 size_t lds_bytes(bool wide);
 void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
@@ -152,7 +153,7 @@ void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, h
 void finish_level(const SearchBuffers& b, int side, int mode, int trace, hipStream_t s);
 void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
-               hipStream_t s);
+               uint32_t n, hipStream_t s);
 void cleanup(const SearchBuffers& b, uint32_t n, hipStream_t s);
 
 }  // namespace launch

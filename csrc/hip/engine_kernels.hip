@@ -34,38 +34,55 @@ using namespace dev;
 // ============================================================================
 // LDS engine
 // ============================================================================
-// One 1024-thread workgroup runs the whole search.  LDS holds
-//   * H[2][8192]: open-addressing hash sets of every vertex each side claimed,
-//   * R[3][kRecCap]: per-edge work records {parent u, CSR index k} of the two
-//     current frontiers and the frontier being built.  A record is written at
-//     claim time for every edge of the new vertex (its row offsets are
-//     prefetched speculatively the moment its id arrives), so the next level
-//     needs neither a degree scan nor an edge->vertex search: lane e reads
-//     record e and issues the column load.
-// Per level: record (LDS) -> column id (global) -> {row offsets (global),
-// claim CAS + meet lookup (LDS)} -> one packed LDS atomic for (index, edge
-// base) -> record writes -> barrier.  All bookkeeping is replicated in every
-// thread's registers from two LDS words; the counters are triple-buffered so
-// one barrier per level suffices.
+// One persistent 1024-thread workgroup runs the whole search; no global
+// atomics, no per-level host round trip.  LDS holds
+//   * H[2][8192]  open-addressing hash sets of every vertex each side claimed.
+//                 Keys carry the parity of the claim depth in bit 31, which is
+//                 all the meet rule needs (below).
+//   * R[4][CAP]   per-edge work records {parent u, CSR index k} of the two
+//                 current frontiers and two frontiers being built.  Records are
+//                 written at claim time for every edge of the new vertex (its
+//                 row offsets are prefetched the moment its id arrives), so a
+//                 level needs no degree scan and no edge->vertex search.
+// A level costs two dependent global loads (column id, then row offsets of
+// the new vertex) plus LDS work.  Two schedules hide that chain:
+//   * lockstep rounds -- while both frontiers are small, wave 0 expands the
+//     source side and wave 1 the target side CONCURRENTLY (one round = two
+//     levels in the time of one); they sync through an LDS counter.
+//   * big levels -- a frontier above kSmallEdges edges is expanded by all 16
+//     waves (one edge per lane, 4 in flight), appends placed by one packed LDS
+//     atomic per wave + a DPP prefix sum; waves 2-15 are parked at the
+//     workgroup barrier otherwise.
+// Meet rule.  At the first round in which any vertex becomes visited by both
+// sides (S expanding depth a -> a+1, T expanding b -> b+1 or idle), every hit
+// of a newly claimed vertex in the other side's set has the other depth in
+// {b, b+1} (a shallower one would have met a round earlier), so the stored
+// depth parity identifies it and each candidate's exact length is known; the
+// answer is the minimum candidate of that round.  Two concurrent claims of the
+// same vertex are always seen by at least one side: each side completes its
+// own insert (LDS CAS) before reading the other set.
 constexpr int kLdsThreads = 1024;
 constexpr int kHashBits = 13;
 constexpr uint32_t kHashSize = 1u << kHashBits;  // slots per side
 constexpr uint32_t kHashMask = kHashSize - 1;
 constexpr uint32_t kHashLimit = kHashSize * 3 / 4;  // max visited per side in LDS
-constexpr int kBatch = 4;                           // edges per thread per round
+constexpr int kBatch = 4;                           // edges per thread per round (big levels)
+constexpr uint32_t kSmallEdges = 256;               // a level this small runs on one wave
 constexpr uint32_t kDegClamp = 65535;               // per-lane edge contribution to the packed counter
+constexpr uint32_t kParity = 0x80000000u;           // depth-parity bit of a hash key
+constexpr uint32_t kIdMask = 0x7fffffffu;
 
 template <typename OffT>
 struct LdsRec;
 template <>
 struct LdsRec<uint32_t> {
   using type = uint2;  // {parent, k}
-  static constexpr uint32_t cap = 3968;
+  static constexpr uint32_t cap = 2976;
 };
 template <>
 struct LdsRec<uint64_t> {
   using type = uint4;  // {parent, k_lo, k_hi, pad}
-  static constexpr uint32_t cap = 1984;
+  static constexpr uint32_t cap = 1488;
 };
 
 __device__ __forceinline__ void rec_set(uint2& r, uint32_t u, uint32_t k) { r = make_uint2(u, k); }
@@ -83,52 +100,60 @@ struct LdsParams {
   uint32_t src, dst, seq;
   int side_policy;
   int trace;
+  int pin_xcc;        // >= 0: only a block on this XCD may run the search
+  uint32_t* ticket;   // monotonic election word (atomicMax with seq)
+  int lockstep;       // allow concurrent two-sided rounds
+  OffT nnz_m1;        // last valid CSR index (clamp for record-driven loads)
   launch::SearchBuffers b;
   launch::HostSide h;
 };
+
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 0xf;
+}
 
 __device__ __forceinline__ uint32_t hslot(uint32_t v) {
   return (v * 0x9E3779B1u) >> (32 - kHashBits);
 }
 
-// Insert v; true when v was absent (this lane claimed it).
-__device__ __forceinline__ bool hash_insert(uint32_t* H, uint32_t v) {
+// Insert vertex v with the given key (v | parity); true when v was absent.
+__device__ __forceinline__ bool hash_insert(uint32_t* H, uint32_t v, uint32_t key) {
   uint32_t h = hslot(v);
-  for (;;) {
-    const uint32_t old = atomicCAS(&H[h], kEmpty, v);
+  for (uint32_t probe = 0; probe < kHashSize; ++probe) {  // bounded: the load limit keeps it short
+    const uint32_t old = atomicCAS(&H[h], kEmpty, key);
     if (old == kEmpty) return true;
-    if (old == v) return false;
+    if ((old & kIdMask) == v) return false;
     h = (h + 1) & kHashMask;
   }
+  return false;
 }
 
-__device__ __forceinline__ bool hash_contains(const uint32_t* H, uint32_t v) {
+// Stored key of v (kEmpty when absent).
+__device__ __forceinline__ uint32_t hash_find(const uint32_t* H, uint32_t v) {
   uint32_t h = hslot(v);
-  for (;;) {
+  for (uint32_t probe = 0; probe < kHashSize; ++probe) {
     const uint32_t k = H[h];
-    if (k == v) return true;
-    if (k == kEmpty) return false;
+    if (k == kEmpty || (k & kIdMask) == v) return k;
     h = (h + 1) & kHashMask;
   }
+  return kEmpty;
 }
 
-// Walk one side's parent chain from the meet vertex, writing positions
-// [depth .. 0] (side 0) or [d0 .. d0+d1] (side 1) of the path.
-__device__ void walk_side(const uint32_t* parent, uint32_t meet, int side, int d0, int d1,
+// Walk one side's parent chain from the meet vertex: side 0 writes path
+// positions d0 .. 0, side 1 writes d0 .. d0 + d1.  One loop shape for both
+// sides so two lanes of one wave walk the two chains concurrently.
+__device__ void walk_side(const uint32_t* parent, uint32_t n, uint32_t meet, int side, int d0, int d1,
                           uint32_t* out) {
   uint32_t v = meet;
-  if (side == 0) {
-    for (int pos = d0;; --pos) {
-      out[pos] = v;
-      if (pos == 0) break;
-      v = load_agent(&parent[v]);
-    }
-  } else {
-    for (int pos = d0;; ++pos) {
-      out[pos] = v;
-      if (pos == d0 + d1) break;
-      v = load_agent(&parent[v]);
-    }
+  int pos = d0;
+  const int step = side ? 1 : -1;
+  for (int remain = side ? d1 : d0;; --remain) {
+    out[pos] = v;
+    if (remain == 0 || v >= n) break;  // v >= n only if the chain were inconsistent: never read past it
+    v = load_agent(&parent[v]);
+    pos += step;
   }
 }
 
@@ -153,35 +178,62 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
+// Result of one level expanded by one wave (lockstep / single rounds).
+struct WaveLevel {
+  uint32_t ncnt, necl;               // claims, clamped degree sum of the claims
+  uint32_t mlen, mv, md_self, md_other;  // best meet candidate (mlen = ~0 when none)
+  uint32_t pad[2];
+};
+
+// Published by wave 0 for the parked waves: the big level to run (or the end).
+struct LevelPlan {
+  uint32_t status, side, E, cur, nxt, qbase, depth_self, depth_other;
+};
+
 template <typename OffT, bool kStamp>
 __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P) {
   using Rec = typename LdsRec<OffT>::type;
   constexpr uint32_t CAP = LdsRec<OffT>::cap;
   __shared__ uint32_t H[2][kHashSize];
-  __shared__ Rec R[3][CAP];
-  __shared__ unsigned long long ctr[3];   // (count << 32) | clamped edge sum of claims
-  __shared__ unsigned long long vsum[3];  // exact degree sum of claims
-  __shared__ uint32_t meetv[3];
+  __shared__ Rec R[4][CAP];
+  __shared__ unsigned long long ctr[2];  // big levels: (count << 32) | clamped edge sum
+  __shared__ uint32_t meetv[2];          // big levels: a meet vertex of the level
+  __shared__ WaveLevel res[2][2];        // [round parity][worker wave]: a wave rewrites a slot only
+                                         // two rounds later, after the other wave has read it
+  __shared__ LevelPlan plan;
+  __shared__ uint32_t rsync;             // two-wave round counter
+  __shared__ uint32_t won;
 
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, wid = tid >> 6;
+  const uint32_t lane = __lane_id();
+  // XCD affinity: the search is latency-bound on dependent CSR loads, so it
+  // always runs on the same XCD, whose L2 keeps the graph's hot lines across
+  // queries.  Several blocks are launched; the first one on the chosen XCD
+  // wins the ticket and every other block exits at once (the host relaunches
+  // with pin_xcc = -1 if no block reached that XCD).
+  if (tid == 0) {
+    const bool cand = P.pin_xcc < 0 ? blockIdx.x == 0 : xcc_id() == (uint32_t)P.pin_xcc;
+    won = cand && atomicMax(P.ticket, P.seq) < P.seq;
+  }
+  __syncthreads();
+  if (!won) return;
+
   uint32_t* Hflat = &H[0][0];
   for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) Hflat[i] = kEmpty;
-  if (tid < 3) {
+  if (tid < 2) {
     ctr[tid] = 0;
-    vsum[tid] = 0;
     meetv[tid] = kEmpty;
   }
-  // ---- replicated search state (identical in every thread).  Kept as two
-  // structs selected by value (never indexed by the runtime side, which would
-  // put it in scratch).
+  if (tid == 0) rsync = 0;
+
+  // ---- replicated search state: identical in waves 0 and 1 (the workers);
+  // two structs selected field-wise (a struct-level `?:` or an array indexed
+  // by the runtime side is lowered through scratch memory).
   struct SideState {
-    int cur;
-    uint32_t cnt, hcnt, qend, fbeg;
+    uint32_t cur, cnt, hcnt, qend, fbeg, ovf;
     int depth;
-    uint32_t ovf;
     unsigned long long fed, ved;
   };
-  // field-wise select: a struct-level `?:` is lowered through scratch memory
   auto sel = [](bool one, const SideState& a, const SideState& b) {
     SideState x;
     x.cur = one ? b.cur : a.cur;
@@ -189,8 +241,8 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
     x.hcnt = one ? b.hcnt : a.hcnt;
     x.qend = one ? b.qend : a.qend;
     x.fbeg = one ? b.fbeg : a.fbeg;
-    x.depth = one ? b.depth : a.depth;
     x.ovf = one ? b.ovf : a.ovf;
+    x.depth = one ? b.depth : a.depth;
     x.fed = one ? b.fed : a.fed;
     x.ved = one ? b.ved : a.ved;
     return x;
@@ -199,7 +251,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
     SideState x;
     const uint32_t r = q ? P.dst : P.src;
     const OffT b = P.row_off[r], e = P.row_off[r + 1];
-    x.cur = q;
+    x.cur = (uint32_t)q;
     x.cnt = 1;
     x.hcnt = 1;
     x.qend = 1;
@@ -217,55 +269,268 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
     return x;
   };
   SideState s0 = init_side(0), s1 = init_side(1);
-  int spare = 2;
-  uint32_t levels = 0, status = kRunning, meet = kEmpty;
+  uint32_t free0 = 2, free1 = 3;  // record buffers not holding a current frontier
+  uint32_t levels = 0, status = kRunning, meet = kEmpty, md0 = 0, md1 = 0, rounds = 0, bigs = 0;
   unsigned long long einsp = 0;
   int turn = 0;
   __syncthreads();
-  if (tid < 2) hash_insert(H[tid], tid ? P.dst : P.src);
-  // pick(): side choice + LDS feasibility (worst case every inspected edge claims a new vertex)
-#define BIBFS_PICK(q)                                                              \
-  do {                                                                             \
-    if (P.side_policy == 2) {                                                      \
-      q = turn;                                                                    \
-      turn ^= 1;                                                                   \
-    } else if (P.side_policy == 1) {                                               \
-      q = s0.cnt <= s1.cnt ? 0 : 1;                                                \
-    } else {                                                                       \
-      q = s0.fed <= s1.fed ? 0 : 1;                                                \
-    }                                                                              \
-    const SideState x_ = sel(q, s0, s1);                                           \
-    if (x_.ovf || (unsigned long long)x_.hcnt + x_.fed > kHashLimit) status = kHandoff; \
-  } while (0)
-  int s;
-  BIBFS_PICK(s);
+  if (tid < 2) hash_insert(H[tid], tid ? P.dst : P.src, tid ? P.dst : P.src);  // depth 0: parity 0
   __syncthreads();
 
-  unsigned long long ts0 = 0, ts1 = 0, ts2 = 0, ts3 = 0;
-  while (status == kRunning) {
-    if (kStamp && tid == 0) ts0 = stamp();
-    SideState me = sel(s, s0, s1);
-    const int o = s ^ 1;
-    const int c = me.cur, nx = spare;
-    const uint32_t E = (uint32_t)me.fed;
-    const uint32_t L3 = levels % 3, N3 = (levels + 1) % 3;
-    if (tid == 0) {  // counters of the NEXT level: last read before the previous barrier
-      ctr[N3] = 0;
-      vsum[N3] = 0;
-      meetv[N3] = kEmpty;
+  auto fits = [&](const SideState& x) {
+    return !x.ovf && (unsigned long long)x.hcnt + x.fed <= kHashLimit;
+  };
+  auto record_trace = [&](int q, const SideState& x, uint32_t E, uint32_t ncnt, uint32_t mode) {
+    if (lane == 0 && wid == 0 && P.trace && levels < P.b.trace_cap) {
+      LevelTraceDev& t = P.b.trace[levels];
+      t.side = (uint32_t)q;
+      t.depth = (uint32_t)x.depth;
+      t.frontier = x.cnt;
+      t.mode = mode;
+      t.edges = E;
+      t.discovered = ncnt;
     }
-    const uint32_t qbase = me.qend;
-    uint32_t* __restrict__ par = s ? P.b.parent[1] : P.b.parent[0];
-    uint32_t* __restrict__ que = s ? P.b.queue[1] : P.b.queue[0];
-    uint32_t* Hs = H[s];
-    const uint32_t* Ho = H[o];
-    const Rec* Rc = R[c];
-    Rec* Rn = R[nx];
+  };
+  // apply a finished level of side q to the replicated state
+  auto apply = [&](int q, uint32_t E, uint32_t nxt, uint32_t ncnt, uint32_t necl, uint32_t mode) {
+    SideState x = sel(q, s0, s1);
+    record_trace(q, x, E, ncnt, mode);
+    ++levels;
+    einsp += E;
+    const uint32_t qbase = x.qend;
+    ++x.depth;
+    x.hcnt += ncnt;
+    x.qend += ncnt;
+    if (ncnt) {
+      x.fbeg = qbase;
+      const uint32_t old = x.cur;
+      x.cur = nxt;
+      // the consumed buffer replaces the one just filled in the free pair
+      if (free0 == nxt) free0 = old;
+      else free1 = old;
+    }
+    x.cnt = ncnt;
+    x.fed = necl;
+    x.ved += necl;
+    x.ovf = necl > CAP ? 1u : 0u;
+    s0 = sel(q, x, s0);
+    s1 = sel(q, s1, x);
+  };
 
-    // Branch-free batches: invalid lanes re-read record 0 (E > 0 here), so
-    // every global load of a batch is issued back to back and the compiler's
-    // in-order vmcnt waits stay exact (a guarded load per slot made hipcc
-    // drain vmcnt(0) between slots).
+  // One wave expands one level of side q (depth a -> a+1) while the other side
+  // sits at depth b (or concurrently goes b -> b+1 when `both`).
+  auto wave_level = [&](int q, uint32_t nxt) -> WaveLevel {
+    const SideState me = sel(q, s0, s1);
+    const SideState ot = sel(q, s1, s0);
+    const uint32_t E = (uint32_t)me.fed;
+    const uint32_t a1 = (uint32_t)me.depth + 1, b = (uint32_t)ot.depth;
+    const uint32_t keybit = (a1 & 1) ? kParity : 0u;
+    const Rec* Rc = R[me.cur];
+    Rec* Rn = R[nxt];
+    uint32_t* __restrict__ par = q ? P.b.parent[1] : P.b.parent[0];
+    uint32_t* __restrict__ que = q ? P.b.queue[1] : P.b.queue[0];
+    uint32_t* Hs = H[q];
+    const uint32_t* Ho = H[q ^ 1];
+    WaveLevel w;
+    w.ncnt = 0;
+    w.necl = 0;
+    w.mlen = kEmpty;
+    w.mv = kEmpty;
+    w.md_self = a1;
+    w.md_other = b;
+    if (E == 0) return w;  // isolated frontier: the side is exhausted
+    auto run = [&](auto bc) {
+      constexpr int B = decltype(bc)::value;
+      uint32_t vv[B], uu[B];
+      OffT ob[B], oe[B];
+      bool ok[B], isnew[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const uint32_t e = k * kWave + lane;
+        ok[k] = e < E;
+        const Rec r = Rc[ok[k] ? e : 0u];  // invalid lanes re-read record 0: loads stay branch-free
+        uu[k] = r.x;
+        vv[k] = P.col[min(rec_k(r), P.nnz_m1)];  // clamp: a bad record can never fault
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) {  // speculative row-offset prefetch, in flight during the claims
+        ob[k] = P.row_off[vv[k]];
+        oe[k] = P.row_off[vv[k] + 1];
+      }
+      uint32_t hl = kEmpty, hv = 0, hdo = 0;  // this lane's best meet candidate
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
+        if (isnew[k]) {
+          const uint32_t f = hash_find(Ho, vv[k]);
+          if (f != kEmpty) {
+            const uint32_t dob = ((f >> 31) == (b & 1)) ? b : b + 1;
+            if (a1 + dob < hl) {
+              hl = a1 + dob;
+              hv = vv[k];
+              hdo = dob;
+            }
+          }
+        }
+      }
+      unsigned long long hm = __ballot(hl != kEmpty);
+      while (hm) {  // rare: only in the meeting round
+        const int l = __ffsll((long long)hm) - 1;
+        hm &= hm - 1;
+        const uint32_t len = __builtin_amdgcn_readlane(hl, l);
+        if (len < w.mlen) {
+          w.mlen = len;
+          w.mv = __builtin_amdgcn_readlane(hv, l);
+          w.md_other = __builtin_amdgcn_readlane(hdo, l);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const unsigned long long mask = __ballot(isnew[k]);
+        if (!mask) continue;
+        const OffT d = isnew[k] ? oe[k] - ob[k] : (OffT)0;
+        const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
+        const uint32_t incl = wave_incl_scan(dc);
+        if (isnew[k]) {
+          const uint32_t idx = w.ncnt + mbcnt64(mask);
+          const uint32_t eb = w.necl + incl - dc;
+          const uint32_t v = vv[k];
+          par[v] = uu[k];
+          if (me.qend + idx < P.n) que[me.qend + idx] = v;
+          if ((OffT)eb + d <= (OffT)CAP)
+            for (uint32_t j = 0; j < (uint32_t)d; ++j) rec_set(Rn[eb + j], v, ob[k] + j);
+        }
+        w.ncnt += (uint32_t)__popcll(mask);
+        w.necl += __builtin_amdgcn_readlane(incl, 63);
+      }
+    };
+    if (E <= (uint32_t)kWave) run(std::integral_constant<int, 1>{});
+    else run(std::integral_constant<int, kSmallEdges / kWave>{});
+    return w;
+  };
+
+  // fold a round's candidates into the result (identical in both workers)
+  auto take_meet = [&](int q, const WaveLevel& w) {
+    if (w.mlen == kEmpty) return;
+    if (meet == kEmpty || w.mlen < md0 + md1) {
+      meet = w.mv;
+      md0 = q ? w.md_other : w.md_self;
+      md1 = q ? w.md_self : w.md_other;
+    }
+  };
+
+  unsigned long long clk0 = 0, rt0 = 0;
+  if (kStamp && tid == 0) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
+  uint32_t fstatus = kRunning;
+  for (;;) {
+    if (wid < 2) {
+      // ---- worker waves: lockstep and single-wave rounds
+      for (;;) {
+        if (status != kRunning) break;
+        const bool f0 = fits(s0), f1 = fits(s1);
+        const bool small0 = s0.fed <= kSmallEdges, small1 = s1.fed <= kSmallEdges;
+        int q;
+        if (P.side_policy == 2) {
+          q = turn;
+        } else if (P.side_policy == 1) {
+          q = s0.cnt <= s1.cnt ? 0 : 1;
+        } else {
+          q = s0.fed <= s1.fed ? 0 : 1;
+        }
+        const bool lock = P.lockstep && small0 && small1 && f0 && f1;
+        const bool fq = q ? f1 : f0;
+        const bool smallq = q ? small1 : small0;
+        if (!lock && (!fq || !smallq)) {
+          if (!fq) status = kHandoff;
+          break;  // big level (all waves) or hand-off
+        }
+        unsigned long long ts0 = 0;
+        if (kStamp && tid == 0) ts0 = stamp();
+        // expand: both sides (lockstep) or side q only
+        const int mine = wid;  // wave w owns side w
+        const bool work = lock || mine == q;
+        if (work) {
+          const uint32_t nxt = (lock && mine == 1) ? free1 : free0;
+          const WaveLevel w = wave_level(mine, nxt);
+          if (lane == 0) res[rounds & 1][mine] = w;
+        }
+        // two-wave round barrier through LDS (the hardware barrier would also
+        // release the parked waves)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) atomicAdd(&rsync, 1u);
+        const uint32_t target = 2 * (rounds + 1);
+        while (__hip_atomic_load(&rsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
+          __builtin_amdgcn_s_sleep(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const uint32_t rp = rounds & 1;
+        ++rounds;
+        const uint32_t fz0 = free0, fz1 = free1;
+        if (lock) {
+          WaveLevel w0, w1;
+          w0 = res[rp][0];
+          w1 = res[rp][1];
+          take_meet(0, w0);
+          take_meet(1, w1);
+          apply(0, (uint32_t)s0.fed, fz0, uni(w0.ncnt), uni(w0.necl), 1);
+          apply(1, (uint32_t)s1.fed, fz1, uni(w1.ncnt), uni(w1.necl), 1);
+          if (meet != kEmpty) status = kFound;
+          else if (s0.cnt == 0 || s1.cnt == 0) status = kNoPath;
+        } else {
+          WaveLevel w = res[rp][q];
+          take_meet(q, w);
+          apply(q, (uint32_t)(q ? s1.fed : s0.fed), fz0, uni(w.ncnt), uni(w.necl), 2);
+          if (P.side_policy == 2) turn ^= 1;
+          if (meet != kEmpty) status = kFound;
+          else if ((q ? s1.cnt : s0.cnt) == 0) status = kNoPath;
+        }
+        if (kStamp && tid == 0 && levels - 1 < P.b.trace_cap) {
+          LevelTraceDev& t = P.b.trace[levels - 1];
+          t.side = (uint32_t)(stamp() - ts0);
+          t.depth = t.frontier = 0;
+          t.mode = lock ? 1 : 2;
+        }
+      }
+      // publish the plan for a big level (or the end)
+      if (wid == 0 && lane == 0) {
+        int q;
+        if (P.side_policy == 2) q = turn;
+        else if (P.side_policy == 1) q = s0.cnt <= s1.cnt ? 0 : 1;
+        else q = s0.fed <= s1.fed ? 0 : 1;
+        const SideState x = sel(q, s0, s1), y = sel(q, s1, s0);
+        LevelPlan p;
+        p.status = status;
+        p.side = (uint32_t)q;
+        p.E = (uint32_t)x.fed;
+        p.cur = x.cur;
+        p.nxt = free0;
+        p.qbase = x.qend;
+        p.depth_self = (uint32_t)x.depth;
+        p.depth_other = (uint32_t)y.depth;
+        plan = p;
+      }
+    }
+    __syncthreads();  // B1: parked waves released for a big level, or for the exit
+    unsigned long long ts0 = 0, ts1 = 0, ts2 = 0;
+    if (kStamp && tid == 0) ts0 = stamp();
+    fstatus = uni(plan.status);
+    if (fstatus != kRunning) break;
+    // ---- big level: every wave, one edge per lane, LDS counters for the appends
+    const int so = (int)uni(plan.side), o = so ^ 1;
+    const uint32_t E = uni(plan.E);
+    const uint32_t qbase = uni(plan.qbase);
+    const uint32_t nxt = uni(plan.nxt);
+    const uint32_t a1 = uni(plan.depth_self) + 1;
+    const uint32_t keybit = (a1 & 1) ? kParity : 0u;
+    const Rec* Rc = R[uni(plan.cur)];
+    Rec* Rn = R[nxt];
+    uint32_t* __restrict__ par = so ? P.b.parent[1] : P.b.parent[0];
+    uint32_t* __restrict__ que = so ? P.b.queue[1] : P.b.queue[0];
+    uint32_t* Hs = H[so];
+    const uint32_t* Ho = H[o];
+    const uint32_t slot = bigs & 1;  // double-buffered: both workers read it after B2
     auto batch = [&](auto bc, uint32_t base) {
       constexpr int B = decltype(bc)::value;
       uint32_t vv[B], uu[B];
@@ -277,14 +542,8 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         ok[k] = e < E;
         const Rec r = Rc[ok[k] ? e : 0u];
         uu[k] = r.x;
-        vv[k] = P.col[rec_k(r)];
+        vv[k] = P.col[min(rec_k(r), P.nnz_m1)];
       }
-      if (kStamp && tid == 0) {
-        uint32_t x = vv[0];
-        asm volatile("" ::"v"(x));
-        ts1 = stamp();
-      }
-      // speculative row-offset prefetch: in flight while the LDS claim runs
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         ob[k] = P.row_off[vv[k]];
@@ -293,11 +552,10 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
       bool isnew[B];
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        isnew[k] = ok[k] && hash_insert(Hs, vv[k]);
-        if (isnew[k] && hash_contains(Ho, vv[k])) meetv[L3] = vv[k];  // any meet of this level is shortest
+        isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
+        // the other side is idle during a big level: any hit has its current depth
+        if (isnew[k] && hash_find(Ho, vv[k]) != kEmpty) meetv[slot] = vv[k];
       }
-      // wave-aggregated append: ONE packed LDS atomic (count << 32 | edge sum)
-      // per wave per batch slot; lane offsets from a DPP prefix sum.
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         const unsigned long long mask = __ballot(isnew[k]);
@@ -308,8 +566,8 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         const uint32_t wtot = __builtin_amdgcn_readlane(incl, 63);
         const int leader = __ffsll((long long)mask) - 1;
         unsigned long long old = 0;
-        if (__lane_id() == (uint32_t)leader)
-          old = atomicAdd(&ctr[L3], ((unsigned long long)__popcll(mask) << 32) | wtot);
+        if (lane == (uint32_t)leader)
+          old = atomicAdd(&ctr[slot], ((unsigned long long)__popcll(mask) << 32) | wtot);
         const uint32_t olo = __builtin_amdgcn_readlane((uint32_t)old, leader);
         const uint32_t ohi = __builtin_amdgcn_readlane((uint32_t)(old >> 32), leader);
         if (isnew[k]) {
@@ -317,88 +575,74 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
           const uint32_t eb = olo + incl - dc;
           const uint32_t v = vv[k];
           par[v] = uu[k];
-          que[qbase + idx] = v;
+          if (qbase + idx < P.n) que[qbase + idx] = v;
           if ((OffT)eb + d <= (OffT)CAP)
             for (uint32_t j = 0; j < (uint32_t)d; ++j) rec_set(Rn[eb + j], v, ob[k] + j);
         }
       }
     };
     if (E <= (uint32_t)kLdsThreads) {
-      if (E) batch(std::integral_constant<int, 1>{}, 0u);
+      if ((uint32_t)wid * kWave < E) batch(std::integral_constant<int, 1>{}, 0u);
     } else {
       for (uint32_t base = 0; base < E; base += kLdsThreads * kBatch)
-        batch(std::integral_constant<int, kBatch>{}, base);
+        if (base + (uint32_t)wid * kWave < E) batch(std::integral_constant<int, kBatch>{}, base);
     }
+    if (kStamp && tid == 0) ts1 = stamp();
+    __syncthreads();  // B2: every claim of the big level is in LDS
     if (kStamp && tid == 0) ts2 = stamp();
-    __syncthreads();
-    if (kStamp && tid == 0) ts3 = stamp();
-    // ---- replicated bookkeeping
-    const unsigned long long pk = ctr[L3];
-    const uint32_t ncnt = uni((uint32_t)(pk >> 32));
-    const uint32_t necl = uni((uint32_t)pk);
-    const unsigned long long nved = necl;
-    const uint32_t mv = uni(meetv[L3]);
-    if (tid == 0 && P.trace && levels < P.b.trace_cap) {
-      LevelTraceDev& t = P.b.trace[levels];
-      if (kStamp) {  // diagnostic build: cycles of record+col load | claim+append | barrier wait
+    if (wid < 2) {
+      const unsigned long long pk = ctr[slot];
+      const uint32_t ncnt = uni((uint32_t)(pk >> 32));
+      const uint32_t necl = uni((uint32_t)pk);
+      const uint32_t mv = uni(meetv[slot]);
+      ++bigs;
+      // slot bigs&1 (the other one) is next used by the following big level;
+      // both workers have read it before this point
+      if (wid == 0 && lane == 0) {
+        ctr[bigs & 1] = 0;
+        meetv[bigs & 1] = kEmpty;
+      }
+      const SideState x = sel(so, s0, s1), y = sel(so, s1, s0);
+      if (mv != kEmpty) {
+        meet = mv;
+        md0 = so ? (uint32_t)y.depth : (uint32_t)x.depth + 1;
+        md1 = so ? (uint32_t)x.depth + 1 : (uint32_t)y.depth;
+      }
+      apply(so, E, nxt, ncnt, necl, 3);
+      if (P.side_policy == 2) turn ^= 1;
+      if (meet != kEmpty) status = kFound;
+      else if (ncnt == 0) status = kNoPath;
+      if (kStamp && tid == 0 && levels - 1 < P.b.trace_cap) {
+        LevelTraceDev& t = P.b.trace[levels - 1];
         t.side = (uint32_t)(ts1 - ts0);
         t.depth = (uint32_t)(ts2 - ts1);
-        t.frontier = (uint32_t)(ts3 - ts2);
-      } else {
-        t.side = s;
-        t.depth = me.depth;
-        t.frontier = me.cnt;
+        t.frontier = (uint32_t)(stamp() - ts2);
+        t.mode = 3;
       }
-      t.mode = 0;
-      t.edges = E;
-      t.discovered = ncnt;
     }
-    ++levels;
-    einsp += E;
-    ++me.depth;
-    me.hcnt += ncnt;
-    me.qend += ncnt;
-    if (mv != kEmpty) {
-      status = kFound;
-      meet = mv;
-    } else if (ncnt == 0) {
-      status = kNoPath;
-    } else {
-      me.fbeg = qbase;
-      spare = c;
-      me.cur = nx;
-      me.cnt = ncnt;
-      me.fed = nved;
-      me.ved += nved;
-      me.ovf = (necl > CAP || nved > CAP) ? 1u : 0u;
-    }
-    s0 = sel(s, me, s0);
-    s1 = sel(s, s1, me);
-    if (status == kRunning) BIBFS_PICK(s);
   }
-#undef BIBFS_PICK
-  const int depth0 = s0.depth, depth1 = s1.depth;
+  if (kStamp && tid == 0 && P.b.trace_cap > 1) {
+    LevelTraceDev& t = P.b.trace[P.b.trace_cap - 1];
+    t.edges = __builtin_amdgcn_s_memtime() - clk0;
+    t.discovered = __builtin_amdgcn_s_memrealtime() - rt0;
+  }
 
+  // state is valid in waves 0/1; fstatus (from the final plan) in every wave
   HostResult* Rr = P.h.res;
   // Parent stores of every wave must have reached L2 before the walkers'
   // L1-bypassing loads read them.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  const uint32_t path_len = status == kFound ? (uint32_t)(depth0 + depth1 + 1) : 0u;
-  const bool path_dev = status == kFound && path_len > P.h.path_cap;
-  if (status == kFound) {
-    uint32_t* out = path_dev ? P.b.dpath : P.h.path;
-    if (tid == 0 || tid == kWave) {
-      walk_side(tid ? P.b.parent[1] : P.b.parent[0], meet, tid ? 1 : 0, depth0, depth1, out);
+  if (wid == 0) {
+    const uint32_t hops = md0 + md1;
+    const uint32_t path_len = status == kFound ? hops + 1 : 0u;
+    const bool path_dev = status == kFound && path_len > P.h.path_cap;
+    if (status == kFound && tid < 2) {  // two lanes walk the two parent chains side by side
+      uint32_t* out = path_dev ? P.b.dpath : P.h.path;
+      walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1, out);
       __threadfence_system();
     }
-  } else if (status == kHandoff) {
-    // Materialise the LDS visited sets as global bitmaps for the grid engine.
-    for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) {
-      const uint32_t v = Hflat[i];
-      if (v != kEmpty) atomicOr(&((i >> kHashBits) ? P.b.vis[1] : P.b.vis[0])[v >> 5], 1u << (v & 31));
-    }
-    if (tid == 0) {
+    if (status == kHandoff && tid == 0) {
       DevState* st = P.b.st;
       st->status = kRunning;
       st->meet = kEmpty;
@@ -419,20 +663,33 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         st->vedges[q] = x.ved;
       }
     }
+    if (tid == 0) {
+      Rr->status = status;
+      Rr->hops = status == kFound ? (int32_t)hops : -1;
+      Rr->meet = meet;
+      Rr->levels = levels;
+      Rr->lds_levels = levels;
+      Rr->visited = s0.hcnt + s1.hcnt;
+      Rr->einsp = einsp;
+      Rr->depth[0] = status == kFound ? (int32_t)md0 : s0.depth;
+      Rr->depth[1] = status == kFound ? (int32_t)md1 : s1.depth;
+      Rr->path_len = path_len;
+      Rr->path_on_device = path_dev ? 1u : 0u;
+    }
   }
-  __syncthreads();  // every wave's path / state stores drained (vmcnt(0)) before publishing
+  if (fstatus == kHandoff) {
+    // Materialise the LDS visited sets as global bitmaps for the grid engine.
+    for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) {
+      const uint32_t k = Hflat[i];
+      if (k != kEmpty) {
+        const uint32_t v = k & kIdMask;
+        atomicOr(&((i >> kHashBits) ? P.b.vis[1] : P.b.vis[0])[v >> 5], 1u << (v & 31));
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave's path / state / bitmap stores drained before publishing
   if (tid == 0) {
-    Rr->status = status;
-    Rr->hops = status == kFound ? depth0 + depth1 : -1;
-    Rr->meet = meet;
-    Rr->levels = levels;
-    Rr->lds_levels = levels;
-    Rr->visited = s0.hcnt + s1.hcnt;
-    Rr->einsp = einsp;
-    Rr->depth[0] = depth0;
-    Rr->depth[1] = depth1;
-    Rr->path_len = path_len;
-    Rr->path_on_device = path_dev ? 1u : 0u;
     __threadfence_system();
     __hip_atomic_store(&Rr->seq, P.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -682,7 +939,7 @@ __global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int tra
     t.side = s;
     t.depth = st->depth[s];
     t.frontier = st->fend[s] - st->fbeg[s];
-    t.mode = mode;
+    t.mode = (uint32_t)mode + 3;  // 4 = grid top-down, 5 = grid bottom-up
     t.edges = mode == 1 ? st->fedges[s] : 0;
     t.discovered = ncnt;
   }
@@ -736,7 +993,7 @@ __global__ void k_seed(const OffT* row_off, launch::SearchBuffers b, uint32_t sr
 
 // Publish a finished grid search: walk both parent chains (two waves in
 // parallel) into pinned host memory, then release the result record.
-__global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t seq) {
+__global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t seq, uint32_t n) {
   const DevState* st = b.st;
   const int tid = threadIdx.x;
   const uint32_t status = st->status == kFound ? kFound : kNoPath;
@@ -744,7 +1001,7 @@ __global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t 
   const uint32_t hops = (uint32_t)(d0 + d1);
   uint32_t* out = (hops + 1 <= h.path_cap) ? h.path : b.dpath;
   if (status == kFound && (tid == 0 || tid == kWave)) {
-    walk_side(b.parent[tid ? 1 : 0], st->meet, tid ? 1 : 0, d0, d1, out);
+    walk_side(b.parent[tid ? 1 : 0], n, st->meet, tid ? 1 : 0, d0, d1, out);
     __threadfence_system();
   }
   __syncthreads();
@@ -805,23 +1062,28 @@ namespace launch {
 int lds_threads() { return kLdsThreads; }
 
 size_t lds_bytes(bool wide) {
-  return 2 * kHashSize * 4 + 3 * (wide ? LdsRec<uint64_t>::cap * 16 : LdsRec<uint32_t>::cap * 8) + 3 * 20;
+  return 2 * kHashSize * 4 + 4 * (wide ? LdsRec<uint64_t>::cap * 16 : LdsRec<uint32_t>::cap * 8) + 128;
 }
 
 void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, uint32_t src,
-                uint32_t dst, uint32_t seq, int side_policy, int trace, hipStream_t s) {
+                uint32_t dst, uint32_t seq, int side_policy, int trace, int pin_xcc, uint32_t* ticket,
+                int lockstep, hipStream_t s) {
+  // 16 blocks = 2 per XCD under round-robin dispatch; only the elected one works
+  const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   if (g.row_off32) {
-    LdsParams<uint32_t> P{g.row_off32, g.col, g.n, src, dst, seq, side_policy, trace, b, h};
+    LdsParams<uint32_t> P{g.row_off32, g.col, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
+                           lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), b, h};
     if (trace == 2)
-      k_lds_bibfs<uint32_t, true><<<1, kLdsThreads, 0, s>>>(P);
+      k_lds_bibfs<uint32_t, true><<<blocks, kLdsThreads, 0, s>>>(P);
     else
-      k_lds_bibfs<uint32_t, false><<<1, kLdsThreads, 0, s>>>(P);
+      k_lds_bibfs<uint32_t, false><<<blocks, kLdsThreads, 0, s>>>(P);
   } else {
-    LdsParams<uint64_t> P{g.row_off, g.col, g.n, src, dst, seq, side_policy, trace, b, h};
+    LdsParams<uint64_t> P{g.row_off, g.col, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
+                           lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), b, h};
     if (trace == 2)
-      k_lds_bibfs<uint64_t, true><<<1, kLdsThreads, 0, s>>>(P);
+      k_lds_bibfs<uint64_t, true><<<blocks, kLdsThreads, 0, s>>>(P);
     else
-      k_lds_bibfs<uint64_t, false><<<1, kLdsThreads, 0, s>>>(P);
+      k_lds_bibfs<uint64_t, false><<<blocks, kLdsThreads, 0, s>>>(P);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -884,10 +1146,10 @@ void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s) {
 }
 
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
-               hipStream_t s) {
+               uint32_t n, hipStream_t s) {
   (void)src;
   (void)dst;
-  k_publish<<<1, 128, 0, s>>>(b, h, seq);
+  k_publish<<<1, 128, 0, s>>>(b, h, seq, n);
   HIP_CHECK(hipGetLastError());
 }
 

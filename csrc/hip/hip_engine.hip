@@ -50,6 +50,7 @@ struct HipBiBfs::Impl {
   uint32_t h_path_cap = 1u << 20;
   DevState* h_state = nullptr;
   uint32_t seq = 0;
+  int pin_xcc = 0;  // XCD that runs the LDS engine (-1 = wherever block 0 lands)
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
@@ -123,6 +124,7 @@ struct HipBiBfs::Impl {
     // visited bitmaps must start (and stay) all-zero
     for (int s = 0; s < 2; ++s) HIP_CHECK(hipMemsetAsync(buf.vis[s], 0, words * 4, stream));
     HIP_CHECK(hipMemsetAsync(buf.st, 0, sizeof(DevState), stream));
+    HIP_CHECK(hipMemsetAsync(d_flag, 0, 64, stream));  // bitmap-meet flag + LDS-engine election ticket
     HIP_CHECK(hipStreamSynchronize(stream));
   }
 
@@ -154,6 +156,21 @@ struct HipBiBfs::Impl {
           if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want) return;
           throw Error("bibfs: search kernel finished without publishing a result");
         }
+        if (e != hipErrorNotReady)
+          throw Error(std::string("bibfs: search kernel failed: ") + hipGetErrorString(e));
+      } else {
+        _mm_pause();
+      }
+    }
+  }
+
+  // like wait_seq, but returns false when the kernel completed without publishing
+  bool wait_seq_or_done(uint32_t want) {
+    for (uint64_t it = 1;; ++it) {
+      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want) return true;
+      if ((it & 4095) == 0) {
+        hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) return __atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want;
         if (e != hipErrorNotReady)
           throw Error(std::string("bibfs: search kernel failed: ") + hipGetErrorString(e));
       } else {
@@ -245,6 +262,15 @@ struct HipBiBfs::Impl {
       }
     }
     return r;
+  }
+
+  void fetch_clock(SearchResult& r) {
+    LevelTraceDev t{};
+    HIP_CHECK(hipMemcpyAsync(&t, buf.trace + buf.trace_cap - 1, sizeof t, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    if (t.discovered)
+      std::fprintf(stderr, "[stamp] shader clock %.0f MHz over %.2f us\n", (double)t.edges / (double)t.discovered * 100.0,
+                   (double)t.discovered / 100.0);
   }
 
   void fetch_trace(SearchResult& r) {
@@ -432,10 +458,17 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   SearchStats stats;
   bool grid = opt.force_grid;
   HIP_CHECK(hipEventRecord(I.ev0, I.stream));
+  grid = grid || I.n > 0x7fffffffu;  // LDS hash keys carry a parity bit: ids < 2^31
   if (!grid) {
-    launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side,
-                       opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0, I.stream);
-    I.wait_seq(seq);
+    const int tr = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
+    const int lock = (opt.lockstep && I.n <= 0x7fffffffu) ? 1 : 0;
+    launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, I.pin_xcc, I.d_flag + 4, lock, I.stream);
+    if (!I.wait_seq_or_done(seq)) {
+      // no block reached the pinned XCD: relaunch unpinned, and stop pinning
+      I.pin_xcc = -1;
+      launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, -1, I.d_flag + 4, lock, I.stream);
+      I.wait_seq(seq);
+    }
     if (I.h_res->status == kHandoff) {
       grid = true;
       stats.handoff = true;
@@ -447,7 +480,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   if (grid) {
     I.grid_loop(opt, stats);
     pub_seq = ++I.seq == 0 ? ++I.seq : I.seq;
-    launch::walk_path(I.buf, hs, src, dst, pub_seq, I.stream);
+    launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
     I.wait_seq(pub_seq);
   }
   HIP_CHECK(hipEventRecord(I.ev1, I.stream));
@@ -459,6 +492,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
   r.search_ms = ms;
   if (opt.trace) I.fetch_trace(r);
+  if (opt.trace && std::getenv("BIBFS_STAMP")) I.fetch_clock(r);
   return r;
 }
 
@@ -511,7 +545,7 @@ SearchResult HipBiBfs::finish() {
   } else {
     const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
     launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap};
-    launch::walk_path(I.buf, hs, I.step_src, I.step_dst, seq, I.stream);
+    launch::walk_path(I.buf, hs, I.step_src, I.step_dst, seq, I.n, I.stream);
     I.wait_seq(seq);
     SearchOptions opt;
     r = I.collect(seq, opt, SearchStats{});

@@ -26,6 +26,7 @@ struct SearchOptions {
   double beta = 24.0;    // bottom-up -> top-down switch: n_f < n / beta
   bool want_path = true;
   bool force_grid = false;     // GPU: skip the single-workgroup LDS engine
+  bool lockstep = true;        // GPU LDS engine: expand both small frontiers concurrently
   bool trace = false;          // record per-level trace
 };
 
@@ -35,7 +36,7 @@ struct LevelTrace {
   uint64_t frontier = 0;    // vertices expanded
   uint64_t edges = 0;       // edges inspected
   uint64_t discovered = 0;  // newly claimed vertices
-  int mode = 0;             // 0 = LDS persistent, 1 = grid top-down, 2 = grid bottom-up, 3 = CPU
+  int mode = 0;  // 0 CPU, 1 LDS lockstep round, 2 LDS single wave, 3 LDS all waves, 4 grid top-down, 5 grid bottom-up
 };
 
 struct SearchStats {

@@ -164,6 +164,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("beta", &SearchOptions::beta)
       .def_readwrite("want_path", &SearchOptions::want_path)
       .def_readwrite("force_grid", &SearchOptions::force_grid)
+      .def_readwrite("lockstep", &SearchOptions::lockstep)
       .def_readwrite("trace", &SearchOptions::trace);
 
   py::class_<SearchResult>(m, "SearchResult")

@@ -8,6 +8,17 @@
 // "PATH FOUND", :224), reports seconds on the harness-parsed line, and warms
 // up before timing (v3 timed the first launch).
 #include "bibfs/hip_engine.hpp"
+
+static const char* bibfs_mode_name(int m) {
+  switch (m) {
+    case 1: return "lds-lockstep";
+    case 2: return "lds-wave";
+    case 3: return "lds-all-waves";
+    case 4: return "grid-topdown";
+    case 5: return "grid-bottomup";
+    default: return "cpu";
+  }
+}
 #include "cli_common.hpp"
 
 int main(int argc, char** argv) {
@@ -71,14 +82,14 @@ int main(int argc, char** argv) {
       std::printf("GPU BFS: %s\n", r.found ? "PATH FOUND" : "NO PATH");
       if (opt.trace && std::getenv("BIBFS_STAMP")) {
         for (auto& t : r.stats.trace)
-          std::printf("Stamp cycles: scan=%d colload=%d claim=%llu barrier=%d\n", t.side, t.depth,
-                      (unsigned long long)t.frontier, t.mode);
+          std::printf("Stamp cycles: %s level=%d barrier=%d book=%llu\n", bibfs_mode_name(t.mode), t.side,
+                      t.depth, (unsigned long long)t.frontier);
       } else if (opt.trace) {
         for (auto& t : r.stats.trace)
           std::printf("Level side=%d depth=%d frontier=%llu edges=%llu new=%llu mode=%s\n", t.side, t.depth,
                       (unsigned long long)t.frontier, (unsigned long long)t.edges,
                       (unsigned long long)t.discovered,
-                      t.mode == 0 ? "lds" : (t.mode == 1 ? "grid-td" : "grid-bu"));
+                      bibfs_mode_name(t.mode));
       }
     }
     if (a.has("verify")) {

@@ -97,6 +97,12 @@ int main(int argc, char** argv) {
       if (failures) { std::printf("stopping before searches\n"); return 1; }
       SearchOptions o;
       check_searches(eng, host, 40, 11, o, "lds");
+      SearchOptions nl;
+      nl.lockstep = false;
+      check_searches(eng, host, 20, 16, nl, "lds-nolock");
+      SearchOptions al;
+      al.side = SidePolicy::kAlternate;
+      check_searches(eng, host, 10, 17, al, "lds-alt");
       SearchOptions g;
       g.force_grid = true;
       check_searches(eng, host, 20, 12, g, "grid-auto");

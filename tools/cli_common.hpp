@@ -84,6 +84,7 @@ inline bibfs::SearchOptions options_from(const Args& a) {
   o.beta = a.getd("beta", o.beta);
   o.force_grid = a.has("force-grid");
   o.trace = a.has("trace");
+  o.lockstep = !a.has("no-lockstep");
   return o;
 }
 
