@@ -37,6 +37,9 @@ def make_options(
     return o
 
 
+_DEFAULT_OPTIONS = make_options()
+
+
 class HipEngine:
     """Single-GPU bidirectional BFS (v3 capability)."""
 
@@ -65,7 +68,9 @@ class HipEngine:
 
     # ---- queries
     def search(self, src: int, dst: int, options: Optional["native.SearchOptions"] = None, **kw):
-        return self._e.search(int(src), int(dst), options if options is not None else make_options(**kw))
+        if options is None:
+            options = make_options(**kw) if kw else _DEFAULT_OPTIONS
+        return self._e.search(int(src), int(dst), options)
 
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:

@@ -19,7 +19,7 @@ from typing import List, Optional, Sequence
 
 from .._lib import native, tool_path
 from ..models import Graph
-from ..ops import HipEngine, make_options
+from ..ops import _DEFAULT_OPTIONS, HipEngine, make_options
 
 MPIEXEC = os.environ.get("BIBFS_MPIEXEC", "/opt/conda/bin/mpiexec")
 
@@ -63,7 +63,9 @@ class DistEngine:
         return self
 
     def search(self, src: int, dst: int, options=None, **kw):
-        return self._e.search(int(src), int(dst), options if options is not None else make_options(**kw))
+        if options is None:
+            options = make_options(**kw) if kw else _DEFAULT_OPTIONS
+        return self._e.search(int(src), int(dst), options)
 
     def barrier(self) -> None:
         self._e.barrier()

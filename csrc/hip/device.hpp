@@ -61,7 +61,8 @@ struct HostResult {
   uint32_t path_len;      // hops + 1 when found
   uint32_t path_on_device;// 1 when the path did not fit the pinned buffer
   uint32_t lds_levels;
-  uint32_t pad[3];
+  uint32_t pad;
+  unsigned long long rt_begin, rt_end;  // s_memrealtime (100 MHz) around the LDS search
 };
 
 struct LevelTraceDev {

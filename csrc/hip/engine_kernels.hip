@@ -419,11 +419,9 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
     }
   };
 
-  unsigned long long clk0 = 0, rt0 = 0;
-  if (kStamp && tid == 0) {
-    clk0 = __builtin_amdgcn_s_memtime();
-    rt0 = __builtin_amdgcn_s_memrealtime();
-  }
+  unsigned long long clk0 = 0;
+  const unsigned long long rt0 = tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
   uint32_t fstatus = kRunning;
   for (;;) {
     if (wid < 2) {
@@ -595,12 +593,11 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
       const uint32_t ncnt = uni((uint32_t)(pk >> 32));
       const uint32_t necl = uni((uint32_t)pk);
       const uint32_t mv = uni(meetv[slot]);
-      ++bigs;
-      // slot bigs&1 (the other one) is next used by the following big level;
-      // both workers have read it before this point
+      // the other slot is used by the next big level; both workers read it
+      // (one big level ago) before this point
       if (wid == 0 && lane == 0) {
-        ctr[bigs & 1] = 0;
-        meetv[bigs & 1] = kEmpty;
+        ctr[slot ^ 1] = 0;
+        meetv[slot ^ 1] = kEmpty;
       }
       const SideState x = sel(so, s0, s1), y = sel(so, s1, s0);
       if (mv != kEmpty) {
@@ -620,6 +617,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         t.mode = 3;
       }
     }
+    ++bigs;  // every wave: the slot parity must agree across the workgroup
   }
   if (kStamp && tid == 0 && P.b.trace_cap > 1) {
     LevelTraceDev& t = P.b.trace[P.b.trace_cap - 1];
@@ -675,6 +673,8 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
       Rr->depth[1] = status == kFound ? (int32_t)md1 : s1.depth;
       Rr->path_len = path_len;
       Rr->path_on_device = path_dev ? 1u : 0u;
+      Rr->rt_begin = rt0;
+      Rr->rt_end = __builtin_amdgcn_s_memrealtime();
     }
   }
   if (fstatus == kHandoff) {

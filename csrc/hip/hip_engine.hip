@@ -457,8 +457,11 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap};
   SearchStats stats;
   bool grid = opt.force_grid;
-  HIP_CHECK(hipEventRecord(I.ev0, I.stream));
-  grid = grid || I.n > 0x7fffffffu;  // LDS hash keys carry a parity bit: ids < 2^31
+  double lds_ms = 0.0;
+  grid = grid || I.n > 0x7fffffffu;
+  // device time: the LDS kernel stamps itself (s_memrealtime); events only
+  // around grid levels, where their ~µs cost is noise
+  if (grid) HIP_CHECK(hipEventRecord(I.ev0, I.stream));  // LDS hash keys carry a parity bit: ids < 2^31
   if (!grid) {
     const int tr = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
     const int lock = (opt.lockstep && I.n <= 0x7fffffffu) ? 1 : 0;
@@ -469,9 +472,11 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
       launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, -1, I.d_flag + 4, lock, I.stream);
       I.wait_seq(seq);
     }
+    lds_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;  // 100 MHz
     if (I.h_res->status == kHandoff) {
       grid = true;
       stats.handoff = true;
+      HIP_CHECK(hipEventRecord(I.ev0, I.stream));
     }
   } else {
     launch::seed_state(g, I.buf, src, dst, I.stream);
@@ -483,14 +488,17 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
     I.wait_seq(pub_seq);
   }
-  HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  if (grid) HIP_CHECK(hipEventRecord(I.ev1, I.stream));
   SearchResult r = I.collect(pub_seq, opt, std::move(stats));
   r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  if (grid) launch::cleanup(I.buf, I.n, I.stream);  // async: next query is stream-ordered behind it
-  HIP_CHECK(hipEventSynchronize(I.ev1));
-  float ms = 0;
-  HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
-  r.search_ms = ms;
+  r.search_ms = lds_ms;
+  if (grid) {
+    launch::cleanup(I.buf, I.n, I.stream);  // async: next query is stream-ordered behind it
+    HIP_CHECK(hipEventSynchronize(I.ev1));
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
+    r.search_ms += ms;
+  }
   if (opt.trace) I.fetch_trace(r);
   if (opt.trace && std::getenv("BIBFS_STAMP")) I.fetch_clock(r);
   return r;

@@ -175,6 +175,11 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("search_ms", &SearchResult::search_ms)
       .def_readonly("total_ms", &SearchResult::total_ms)
       .def_property_readonly("stats", [](const SearchResult& r) { return stats_dict(r.stats); })
+      // cheap scalar views (the stats dict is rebuilt on every access)
+      .def_property_readonly("levels", [](const SearchResult& r) { return r.stats.levels; })
+      .def_property_readonly("edges_inspected", [](const SearchResult& r) { return r.stats.edges_inspected; })
+      .def_property_readonly("visited", [](const SearchResult& r) { return r.stats.visited; })
+      .def_property_readonly("handoff", [](const SearchResult& r) { return r.stats.handoff; })
       .def("__repr__", [](const SearchResult& r) {
         return "SearchResult(found=" + std::string(r.found ? "True" : "False") +
                ", hops=" + std::to_string(r.hops) + ", search_ms=" + std::to_string(r.search_ms) + ")";

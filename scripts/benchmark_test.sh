@@ -1,0 +1,103 @@
+#!/usr/bin/env bash
+# Benchmark harness (reference benchmark_test.sh:1-124 / single_machine_bench.sh,
+# SURVEY.md C20/C21).
+#
+# For every engine tier and every graph of the suite (scripts/make_graphs):
+# run <tool> <graph.bin> 0 N-1, log to logs/<tier>/<graph>.log, take the
+# first number on the first line matching the reference's regex
+# (/search time|^\[time\]|took[[:space:]]+[0-9]|gpu bfs time/, case-
+# insensitive like its awk) and append  version,graph,time_sec,logfile  to
+# benchmark_results.csv; then print the boxed table.
+#
+# Differences from the reference, on purpose:
+#   * every tool runs REPEAT timed queries after WARMUP untimed ones and prints
+#     the median (the reference ran once, cold);
+#   * all times are seconds (the reference's v3 printed ms in a seconds column);
+#   * the hop count printed by each tool is checked against the .json ground
+#     truth (column `hops_ok`), and GTEPS(M/t) is reported next to the time.
+#
+#   scripts/benchmark_test.sh [GRAPH_DIR]            (default graphs/)
+#   TIERS="v1 v3" REPEAT=20 NP=4 NGPU=1 scripts/benchmark_test.sh
+set -uo pipefail
+
+ROOT="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
+GDIR="${1:-$ROOT/graphs}"
+BIN="$ROOT/build/bin"
+TIERS="${TIERS:-v1 v2 v3 v4}"
+GRAPHS="${GRAPHS:-1k 10k 50k 100k}"
+REPEAT="${REPEAT:-10}"
+WARMUP="${WARMUP:-2}"
+NP="${NP:-4}"          # MPI ranks for the CPU tier (benchmark_test.sh:47-51 used 4)
+NGPU="${NGPU:-1}"      # ranks (one per GPU) for the multi-GPU tier
+MPIEXEC="${MPIEXEC:-$(command -v mpiexec || echo /opt/conda/bin/mpiexec)}"
+LOGDIR="${LOGDIR:-$ROOT/logs}"
+CSV="${CSV:-$ROOT/benchmark_results.csv}"
+PER_RUN_TIMEOUT="${PER_RUN_TIMEOUT:-300}"
+
+if [[ ! -x "$BIN/bibfs_serial" ]]; then
+  echo "building native tools..."
+  make -C "$ROOT" -j"$(( $(nproc) < 16 ? $(nproc) : 16 ))" cpu mpi gpu >/dev/null || exit 1
+fi
+
+tool_cmd() {  # tier graph.bin src dst -> command line
+  local tier=$1 g=$2 s=$3 d=$4
+  case $tier in
+    v1) echo "$BIN/bibfs_serial $g $s $d --repeat $REPEAT" ;;
+    v2) echo "$MPIEXEC -n $NP $BIN/second_try $g $s $d --repeat $REPEAT" ;;
+    v3) echo "$BIN/bibfs_hip $g $s $d --repeat $REPEAT --warmup $WARMUP" ;;
+    v4) echo "$MPIEXEC -n $NGPU $BIN/mpi_bibfs $g $s $d --repeat $REPEAT --warmup $WARMUP" ;;
+    *) return 1 ;;
+  esac
+}
+
+echo "version,graph,time_sec,logfile,hops,hops_expected,hops_ok,gteps" > "$CSV"
+for tier in $TIERS; do
+  mkdir -p "$LOGDIR/$tier"
+  for gname in $GRAPHS; do
+    g="$GDIR/$gname.bin"
+    js="$GDIR/$gname.json"
+    if [[ ! -f "$g" ]]; then
+      echo "skip $tier/$gname: $g missing (run scripts/make_graphs)"
+      continue
+    fi
+    read -r N M < <(python3 - "$g" <<'EOF'
+import struct, sys
+with open(sys.argv[1], "rb") as f:
+    n, m = struct.unpack("<II", f.read(8))
+print(n, m)
+EOF
+)
+    src=0
+    dst=$((N - 1))
+    log="$LOGDIR/$tier/$gname.log"
+    cmd=$(tool_cmd "$tier" "$g" "$src" "$dst")
+    echo "==> [$tier] $gname: $cmd"
+    timeout -k 10 "$PER_RUN_TIMEOUT" $cmd > "$log" 2>&1
+    rc=$?
+    t=$(awk 'tolower($0) ~ /search time|^\[time\]|took[[:space:]]+[0-9]|gpu bfs time/ {
+               for (i = 1; i <= NF; i++) if ($i ~ /^[0-9.]+(e[-+]?[0-9]+)?$/) { print $i; exit } }' "$log")
+    [[ $rc -ne 0 || -z "$t" ]] && t="ERROR"
+    hops=$(awk '/Shortest path length/ {print $NF; exit} /No path found/ {print "none"; exit}' "$log")
+    exp=$(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('none' if d.get('hop_count') is None else d['hop_count'])" "$js" 2>/dev/null || echo "?")
+    ok=$([[ "$hops" == "$exp" ]] && echo yes || echo no)
+    gteps=$(python3 -c "import sys; t=sys.argv[1]; print('%.4f' % (int(sys.argv[2]) / float(t) / 1e9) if t not in ('ERROR','0') and float(t) > 0 else '')" "$t" "$M" 2>/dev/null)
+    echo "$tier,$gname,$t,$log,$hops,$exp,$ok,$gteps" >> "$CSV"
+  done
+done
+
+python3 - "$CSV" <<'EOF'
+import csv, sys
+rows = list(csv.DictReader(open(sys.argv[1])))
+if not rows:
+    sys.exit(0)
+cols = ["version", "graph", "time_sec", "hops", "hops_ok", "gteps"]
+w = {c: max(len(c), *(len(r[c]) for r in rows)) for c in cols}
+bar = "+" + "+".join("-" * (w[c] + 2) for c in cols) + "+"
+print(bar)
+print("| " + " | ".join(c.ljust(w[c]) for c in cols) + " |")
+print(bar)
+for r in rows:
+    print("| " + " | ".join(r[c].ljust(w[c]) for c in cols) + " |")
+print(bar)
+EOF
+echo "results: $CSV"

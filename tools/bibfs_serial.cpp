@@ -40,6 +40,10 @@ int main(int argc, char** argv) {
       return 0;
     }
     cli::print_result(r, src, dst);
+    for (auto& t : r.stats.trace)
+      std::printf("Level side=%d depth=%d frontier=%llu edges=%llu new=%llu mode=cpu\n", t.side, t.depth,
+                  (unsigned long long)t.frontier, (unsigned long long)t.edges,
+                  (unsigned long long)t.discovered);
     std::printf("Serial bidirectional BFS took %.9g seconds\n", med * 1e-3);
     if (a.has("verify")) {
       auto o = bibfs::bfs_oracle(g, src, dst);
