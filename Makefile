@@ -54,12 +54,21 @@ GPU_TOOLS := $(BIN)/bibfs_selftest $(BIN)/bibfs_hip $(BIN)/mpi_bibfs $(BIN)/bibf
 
 NATIVE_PY := $(PKG)/_native$(PY_EXT)
 
-.PHONY: all cpu gpu mpi python clean
-all: cpu mpi gpu python
+.PHONY: all cpu gpu mpi python micro clean
+all: cpu mpi gpu python micro
 cpu: $(LIB)/libbibfs_core.so $(CPU_TOOLS)
 mpi: $(LIB)/libbibfs_mpi.so $(MPI_TOOLS)
 gpu: $(LIB)/libbibfs.so $(GPU_TOOLS) $(BIN)/bibfs_cuda_only
 python: $(NATIVE_PY)
+micro: $(BIN)/lat_probe $(BIN)/mailbox_rtt
+
+$(BIN)/mailbox_rtt: benchmarks/micro/mailbox_rtt.hip
+	@mkdir -p $(BIN)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 $< -o $@
+
+$(BIN)/lat_probe: benchmarks/micro/lat_probe.hip
+	@mkdir -p $(BIN)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 $< -o $@
 
 $(OBJ)/%.o: csrc/%.cpp $(HEADERS)
 	@mkdir -p $(dir $@)

@@ -1,0 +1,124 @@
+// Host <-> resident-kernel mailbox round trip, for the resident query server
+// (csrc/hip/engine_kernels.hip, k_lds_server).  A one-wave kernel polls a
+// request word; the host writes seq, the kernel echoes it into a pinned host
+// word, the host spins on the echo.  Prints the median round trip per
+// mailbox placement:
+//   host     : request word in pinned host memory (GPU polls over PCIe)
+//   devfine  : request word in fine-grained device memory written by the CPU
+//              through the BAR (GPU polls its own HBM, bypassing L2)
+// plus the kernel-launch round trip (empty kernel + host spin on a flag) for
+// reference.  Build: make micro.
+#include <hip/hip_runtime.h>
+#include <x86intrin.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      std::exit(1);                                                                  \
+    }                                                                                \
+  } while (0)
+
+// pipelined: keep several poll loads in flight (window 4) spaced by s_sleep
+__global__ void k_echo(const uint32_t* req, uint32_t* resp, uint32_t n, int pipelined) {
+  uint32_t last = 0;
+  const unsigned long long t_end = __builtin_amdgcn_s_memrealtime() + 100000000ull;  // 1 s cap
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s = last;
+    while (s == last) {
+      if (pipelined) {
+        const uint32_t a = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_sleep(16);
+        const uint32_t b = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_sleep(16);
+        const uint32_t c = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_sleep(16);
+        const uint32_t d = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s = a != last ? a : b != last ? b : c != last ? c : d;
+      } else {
+        s = __hip_atomic_load(req, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (__builtin_amdgcn_s_memrealtime() > t_end) return;
+    }
+    last = s;
+    __hip_atomic_store(resp, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void k_flag(uint32_t* resp, uint32_t v) {
+  __hip_atomic_store(resp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static double median(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v[v.size() / 2];
+}
+
+static double run_echo(uint32_t* req_host_view, const uint32_t* req_dev_view, uint32_t* resp, int pipelined) {
+  const uint32_t n = 2000;
+  *(volatile uint32_t*)req_host_view = 0;
+  *(volatile uint32_t*)resp = 0;
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  k_echo<<<1, 64, 0, st>>>(req_dev_view, resp, n, pipelined);
+  CK(hipGetLastError());
+  std::vector<double> rt;
+  for (uint32_t i = 1; i <= n; ++i) {
+    const auto t0 = std::chrono::steady_clock::now();
+    __atomic_store_n(req_host_view, i, __ATOMIC_RELEASE);
+    const auto tmax = t0 + std::chrono::milliseconds(200);
+    while (__atomic_load_n(resp, __ATOMIC_ACQUIRE) != i) {
+      _mm_pause();
+      if (std::chrono::steady_clock::now() > tmax) {
+        std::printf("  timeout at %u\n", i);
+        CK(hipStreamSynchronize(st));
+        return -1;
+      }
+    }
+    rt.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+  CK(hipStreamSynchronize(st));
+  CK(hipStreamDestroy(st));
+  return median(rt);
+}
+
+int main() {
+  uint32_t *hreq, *resp;
+  CK(hipHostMalloc(reinterpret_cast<void**>(&hreq), 4096, hipHostMallocMapped | hipHostMallocCoherent));
+  CK(hipHostMalloc(reinterpret_cast<void**>(&resp), 4096, hipHostMallocMapped | hipHostMallocCoherent));
+  std::printf("host-pinned mailbox, serial polls    : %.2f us\n", run_echo(hreq, hreq, resp, 0));
+  std::printf("host-pinned mailbox, pipelined polls : %.2f us\n", run_echo(hreq, hreq, resp, 1));
+
+  uint32_t* dfine = nullptr;
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&dfine), 4096, hipDeviceMallocFinegrained) == hipSuccess) {
+    hipPointerAttribute_t at{};
+    CK(hipPointerGetAttributes(&at, dfine));
+    std::printf("fine-grained device buffer: device ptr %p host ptr %p\n", at.devicePointer, at.hostPointer);
+    if (at.hostPointer) {
+      std::printf("device-fine mailbox, serial polls    : %.2f us\n",
+                  run_echo(static_cast<uint32_t*>(at.hostPointer), dfine, resp, 0));
+    } else {
+      std::printf("device-fine mailbox: not host-mapped\n");
+    }
+  }
+  // launch round trip
+  hipStream_t st;
+  CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  std::vector<double> rt;
+  for (uint32_t i = 1; i <= 2000; ++i) {
+    const auto t0 = std::chrono::steady_clock::now();
+    k_flag<<<1, 64, 0, st>>>(resp, 100000 + i);
+    while (__atomic_load_n(resp, __ATOMIC_ACQUIRE) != 100000 + i) _mm_pause();
+    rt.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+  }
+  CK(hipStreamSynchronize(st));
+  std::printf("kernel launch -> flag round trip     : %.2f us\n", median(rt));
+  return 0;
+}

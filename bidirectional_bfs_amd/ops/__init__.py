@@ -72,6 +72,15 @@ class HipEngine:
             options = make_options(**kw) if kw else _DEFAULT_OPTIONS
         return self._e.search(int(src), int(dst), options)
 
+    # resident query server (no kernel launch per query; see docs/DESIGN.md)
+    def set_resident(self, on: bool = True, idle_ms: float = 200.0) -> "HipEngine":
+        self._e.set_resident(bool(on), float(idle_ms))
+        return self
+
+    @property
+    def resident(self) -> bool:
+        return self._e.resident
+
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:
         self._e.begin(int(src), int(dst))

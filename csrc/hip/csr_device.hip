@@ -144,6 +144,21 @@ __global__ void k_row32(const uint64_t* __restrict__ r, uint32_t n1, uint32_t* _
     r32[i] = (uint32_t)r[i];
 }
 
+// Packed adjacency for the latency-bound search: entry k carries everything
+// the expansion of edge k needs -- the neighbour id, its degree and its row
+// base -- so a BFS level costs ONE dependent global load per edge instead of
+// col[k] followed by row_off[col[k]].
+__global__ void k_padj(const uint64_t* __restrict__ r, const uint32_t* __restrict__ col, uint64_t nnz,
+                       uint4* __restrict__ pa) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nnz;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = col[k];
+    const uint64_t b = r[v], e = r[v + 1];
+    const uint64_t d = e - b;
+    pa[k] = make_uint4(v, d > 0xffffffffull ? 0xffffffffu : (uint32_t)d, (uint32_t)b, (uint32_t)(b >> 32));
+  }
+}
+
 unsigned grid_for(uint64_t work, int threads) {
   uint64_t b = (work + threads - 1) / threads;
   if (b > 8192) b = 8192;  // 32 blocks per CU on 256 CUs, grid-stride beyond
@@ -217,6 +232,11 @@ void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, c
 void fill_csr(const uint32_t* d_uv, uint64_t m, uint32_t n, const uint64_t* d_row_off,
               uint64_t* d_cursor, uint32_t* d_col, hipStream_t s) {
   fill_csr_rows(d_uv, m, 0, n, d_row_off, d_cursor, d_col, s);
+}
+
+void build_padj(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, uint4* padj, hipStream_t s) {
+  if (nnz) k_padj<<<grid_for(nnz, 256), 256, 0, s>>>(row_off, col, nnz, padj);
+  HIP_CHECK(hipGetLastError());
 }
 
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s) {

@@ -65,6 +65,22 @@ struct HostResult {
   unsigned long long rt_begin, rt_end;  // s_memrealtime (100 MHz) around the LDS search
 };
 
+// Pinned mailbox of the resident query server (k_lds_server).  The host
+// writes src/dst/options, then `seq` (release); the server answers through
+// HostResult with the same seq.
+// The request is ONE 16-byte word, read by the server with a single PCIe
+// load per poll (a poll of pinned host memory costs ~1 us): {seq, src, dst,
+// tag} with tag = flags | (seq & 0xffffff) << 8, so a torn read is detected.
+struct alignas(16) ServerBox {
+  uint32_t seq, src, dst, tag;  // host -> server
+  uint32_t alive;  // server -> host: its launch seq while running, ~launch seq after exit
+  uint32_t stage;  // server -> host (diagnostics): 1 polling, 2 request taken, 3 answered
+  uint32_t seen;   // last request seq the server took
+  uint32_t pad[9];
+};
+constexpr uint32_t kReqStop = 1u, kReqLockstep = 2u;  // tag flags; side policy in bits 2..3
+__host__ __device__ inline uint32_t req_tag(uint32_t seq, uint32_t flags) { return (flags & 0xffu) | (seq << 8); }
+
 struct LevelTraceDev {
   uint32_t side, depth, frontier, mode;
   unsigned long long edges, discovered;
@@ -101,6 +117,7 @@ struct GraphView {
   const uint64_t* row_off;     // n + 1
   const uint32_t* row_off32;   // n + 1 copy when nnz < 2^32 (else nullptr)
   const uint32_t* col;
+  const uint4* padj;           // nnz packed {v, deg(v), row_off[v] lo, hi}, or nullptr
 };
 
 struct SearchBuffers {
@@ -135,6 +152,7 @@ uint64_t count_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t 
                         hipStream_t s);
 void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, const uint64_t* d_row_off,
                    uint64_t* d_cursor, uint32_t* d_col, hipStream_t s);
+void build_padj(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, uint4* padj, hipStream_t s);
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s);
 uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);
 void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,
@@ -146,6 +164,9 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
                 int lockstep, hipStream_t s);
 int lds_threads();
 size_t lds_bytes(bool wide);
+void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, dev::ServerBox* box,
+                uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
+                unsigned long long idle_ticks, hipStream_t s);
 void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
                 hipStream_t s);
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);

@@ -61,6 +61,16 @@ using namespace dev;
 // answer is the minimum candidate of that round.  Two concurrent claims of the
 // same vertex are always seen by at least one side: each side completes its
 // own insert (LDS CAS) before reading the other set.
+// Tuning knobs (compile-time; scripts/build_variants.sh builds A/B libraries).
+#ifndef BIBFS_KNOB_WID_UNIFORM
+#define BIBFS_KNOB_WID_UNIFORM 0
+#endif
+#ifndef BIBFS_KNOB_APPEND_BALLOT
+#define BIBFS_KNOB_APPEND_BALLOT 0
+#endif
+constexpr bool kWidUniform = BIBFS_KNOB_WID_UNIFORM;
+constexpr bool kAppendBallot = BIBFS_KNOB_APPEND_BALLOT;
+
 constexpr int kLdsThreads = 1024;
 constexpr int kHashBits = 13;
 constexpr uint32_t kHashSize = 1u << kHashBits;  // slots per side
@@ -96,6 +106,7 @@ template <typename OffT>
 struct LdsParams {
   const OffT* row_off;
   const uint32_t* col;
+  const uint4* padj;  // packed {v, deg, base lo, base hi} per edge, or nullptr
   uint32_t n;
   uint32_t src, dst, seq;
   int side_policy;
@@ -139,6 +150,28 @@ __device__ __forceinline__ uint32_t hash_find(const uint32_t* H, uint32_t v) {
     h = (h + 1) & kHashMask;
   }
   return kEmpty;
+}
+
+// ---- bitmap visited sets (graphs with n <= kBmMaxN): the hash area holds,
+// per side, one u64 per 32 vertices -- low half = claimed at an even depth,
+// high half = claimed at an odd depth.  A claim is one ds_or_rtn_b64: the
+// returned word says whether the vertex was already held at either parity.
+// A losing claim still sets its parity bit ("pollution"); a vertex with both
+// bits therefore has the OLDER depth, which for a first meet is b (see the
+// lockstep rule above), so the readers below map both-bits to b.
+constexpr uint32_t kBmMaxN = kHashSize * 16;  // 4096 u64 words per side = 131072 vertices
+
+__device__ __forceinline__ bool bm_claim(unsigned long long* W, uint32_t v, uint32_t parity) {
+  const uint32_t b = v & 31;
+  const unsigned long long old = atomicOr(&W[v >> 5], 1ull << (b + 32 * parity));
+  return ((old >> b) & 1ull) == 0 && ((old >> (32 + b)) & 1ull) == 0;
+}
+
+// 0 = absent, 1 = even depth, 2 = odd depth, 3 = both (the older claim)
+__device__ __forceinline__ uint32_t bm_state(const unsigned long long* W, uint32_t v) {
+  const uint32_t b = v & 31;
+  const unsigned long long w = W[v >> 5];
+  return (uint32_t)((w >> b) & 1ull) | ((uint32_t)((w >> (32 + b)) & 1ull) << 1);
 }
 
 // Walk one side's parent chain from the meet vertex: side 0 writes path
@@ -190,8 +223,10 @@ struct LevelPlan {
   uint32_t status, side, E, cur, nxt, qbase, depth_self, depth_other;
 };
 
-template <typename OffT, bool kStamp>
-__global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P) {
+// One whole search by one workgroup.  `elected`: the caller already owns the
+// search (the resident server); otherwise the block runs the XCD election.
+template <typename OffT, bool kStamp, bool kBm>
+__device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool elected) {
   using Rec = typename LdsRec<OffT>::type;
   constexpr uint32_t CAP = LdsRec<OffT>::cap;
   __shared__ uint32_t H[2][kHashSize];
@@ -203,23 +238,62 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
   __shared__ LevelPlan plan;
   __shared__ uint32_t rsync;             // two-wave round counter
   __shared__ uint32_t won;
+  __shared__ Rec junk[kWave];            // record writes of finished lanes land here (no divergence)
 
-  const int tid = threadIdx.x, wid = tid >> 6;
+  const int tid = threadIdx.x;
+  const int wid = kWidUniform ? (int)__builtin_amdgcn_readfirstlane((uint32_t)tid >> 6) : tid >> 6;
   const uint32_t lane = __lane_id();
   // XCD affinity: the search is latency-bound on dependent CSR loads, so it
   // always runs on the same XCD, whose L2 keeps the graph's hot lines across
   // queries.  Several blocks are launched; the first one on the chosen XCD
   // wins the ticket and every other block exits at once (the host relaunches
-  // with pin_xcc = -1 if no block reached that XCD).
-  if (tid == 0) {
-    const bool cand = P.pin_xcc < 0 ? blockIdx.x == 0 : xcc_id() == (uint32_t)P.pin_xcc;
-    won = cand && atomicMax(P.ticket, P.seq) < P.seq;
-  }
-  __syncthreads();
-  if (!won) return;
+  // with pin_xcc = -1 if no block reached that XCD).  The ticket atomic
+  // (~1.6k cycles) is only resolved after the block-private initialisation
+  // below; a losing candidate's few global writes there are idempotent.
+  unsigned long long e0 = 0, e1 = 0, e3 = 0, e4 = 0;  // kStamp: entry / elected / loop end / walked
+  if (kStamp && tid == 0) e0 = __builtin_amdgcn_s_memtime();
+  const bool cand = elected || (P.pin_xcc < 0 ? blockIdx.x == 0 : xcc_id() == (uint32_t)P.pin_xcc);
+  if (!cand) return;  // block-uniform
+  uint32_t ticket_old = 0;
+  if (tid == 0 && !elected) ticket_old = atomicMax(P.ticket, P.seq);
 
+  // Lane writes its vertex's dl edge records Rn[eb .. eb+dl).  The trip count
+  // is the wave's max dl (ballot-driven, scalar loop); lanes already done
+  // write their own junk slot instead of masking, so the body never diverges.
+  auto append_records = [&](Rec* Rn, uint32_t dl, uint32_t eb, uint32_t v, OffT base) {
+    if constexpr (kAppendBallot) {
+      for (uint32_t j = 0; __ballot(j < dl); ++j) rec_set(j < dl ? Rn[eb + j] : junk[lane], v, base + j);
+    } else {
+      for (uint32_t j = 0; j < dl; ++j) rec_set(Rn[eb + j], v, base + j);
+    }
+  };
+  // Edge k -> (neighbour v, its row [ob, oe)): one packed load, or col[k] then
+  // the row offsets (a second dependent load) when no packed adjacency exists.
+  // The branch is on a kernel argument: wave-uniform.
+  auto fetch_edges = [&](auto bc, const OffT* kk, uint32_t* vv, OffT* ob, OffT* oe) {
+    constexpr int B = decltype(bc)::value;
+    if (P.padj) {
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const uint4 q = P.padj[kk[k]];
+        vv[k] = q.x;
+        ob[k] = (OffT)((uint64_t)q.z | ((uint64_t)q.w << 32));
+        oe[k] = ob[k] + (OffT)q.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < B; ++k) vv[k] = P.col[kk[k]];
+#pragma unroll
+      for (int k = 0; k < B; ++k) {  // row offsets, in flight during the claims
+        ob[k] = P.row_off[vv[k]];
+        oe[k] = P.row_off[vv[k] + 1];
+      }
+    }
+  };
   uint32_t* Hflat = &H[0][0];
-  for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) Hflat[i] = kEmpty;
+  for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) Hflat[i] = kBm ? 0u : kEmpty;
+  // side q's bitmap view of the same LDS (kBm)
+  auto W = [&](int q) { return reinterpret_cast<unsigned long long*>(q ? H[1] : H[0]); };
   if (tid < 2) {
     ctr[tid] = 0;
     meetv[tid] = kEmpty;
@@ -273,12 +347,18 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
   uint32_t levels = 0, status = kRunning, meet = kEmpty, md0 = 0, md1 = 0, rounds = 0, bigs = 0;
   unsigned long long einsp = 0;
   int turn = 0;
+  if (tid == 0) won = elected || ticket_old < P.seq;
   __syncthreads();
-  if (tid < 2) hash_insert(H[tid], tid ? P.dst : P.src, tid ? P.dst : P.src);  // depth 0: parity 0
+  if (!uni(won)) return;  // uniform: a divergent-looking exit around barriers can be mis-structurized
+  if (kStamp && tid == 0) e1 = __builtin_amdgcn_s_memtime();
+  if (tid < 2) {  // depth 0: parity 0
+    if constexpr (kBm) bm_claim(W(tid), tid ? P.dst : P.src, 0);
+    else hash_insert(H[tid], tid ? P.dst : P.src, tid ? P.dst : P.src);
+  }
   __syncthreads();
 
   auto fits = [&](const SideState& x) {
-    return !x.ovf && (unsigned long long)x.hcnt + x.fed <= kHashLimit;
+    return !x.ovf && (kBm || (unsigned long long)x.hcnt + x.fed <= kHashLimit);
   };
   auto record_trace = [&](int q, const SideState& x, uint32_t E, uint32_t ncnt, uint32_t mode) {
     if (lane == 0 && wid == 0 && P.trace && levels < P.b.trace_cap) {
@@ -338,33 +418,49 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
     w.mv = kEmpty;
     w.md_self = a1;
     w.md_other = b;
+    w.pad[0] = w.pad[1] = 0;
     if (E == 0) return w;  // isolated frontier: the side is exhausted
     auto run = [&](auto bc) {
       constexpr int B = decltype(bc)::value;
       uint32_t vv[B], uu[B];
       OffT ob[B], oe[B];
       bool ok[B], isnew[B];
+      // kStamp: per-phase cycle split (explicit waits serialise the phases)
+      unsigned long long sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+      if constexpr (kStamp) sp0 = stamp();
+      OffT kk[B];
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         const uint32_t e = k * kWave + lane;
         ok[k] = e < E;
         const Rec r = Rc[ok[k] ? e : 0u];  // invalid lanes re-read record 0: loads stay branch-free
         uu[k] = r.x;
-        vv[k] = P.col[min(rec_k(r), P.nnz_m1)];  // clamp: a bad record can never fault
+        kk[k] = min(rec_k(r), P.nnz_m1);  // clamp: a bad record can never fault
       }
-#pragma unroll
-      for (int k = 0; k < B; ++k) {  // speculative row-offset prefetch, in flight during the claims
-        ob[k] = P.row_off[vv[k]];
-        oe[k] = P.row_off[vv[k] + 1];
+      fetch_edges(bc, kk, vv, ob, oe);
+      if constexpr (kStamp) {
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        sp1 = stamp();
+      }
+      if constexpr (kStamp) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        sp2 = stamp();
       }
       uint32_t hl = kEmpty, hv = 0, hdo = 0;  // this lane's best meet candidate
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
+        uint32_t f;  // other side's state of vv[k]: 0 = absent, else 1 + parity (3 = older claim)
+        if constexpr (kBm) {
+          isnew[k] = ok[k] && bm_claim(W(q), vv[k], a1 & 1);
+          f = isnew[k] ? bm_state(W(q ^ 1), vv[k]) : 0u;
+        } else {
+          isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
+          const uint32_t key = isnew[k] ? hash_find(Ho, vv[k]) : kEmpty;
+          f = key == kEmpty ? 0u : 1u + (key >> 31);
+        }
         if (isnew[k]) {
-          const uint32_t f = hash_find(Ho, vv[k]);
-          if (f != kEmpty) {
-            const uint32_t dob = ((f >> 31) == (b & 1)) ? b : b + 1;
+          if (f != 0) {
+            const uint32_t dob = (f == 3 || (f - 1) == (b & 1)) ? b : b + 1;
             if (a1 + dob < hl) {
               hl = a1 + dob;
               hv = vv[k];
@@ -372,6 +468,10 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
             }
           }
         }
+      }
+      if constexpr (kStamp) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        sp3 = stamp();
       }
       unsigned long long hm = __ballot(hl != kEmpty);
       while (hm) {  // rare: only in the meeting round
@@ -391,17 +491,22 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         const OffT d = isnew[k] ? oe[k] - ob[k] : (OffT)0;
         const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
         const uint32_t incl = wave_incl_scan(dc);
+        const uint32_t eb = w.necl + incl - dc;
         if (isnew[k]) {
           const uint32_t idx = w.ncnt + mbcnt64(mask);
-          const uint32_t eb = w.necl + incl - dc;
-          const uint32_t v = vv[k];
-          par[v] = uu[k];
-          if (me.qend + idx < P.n) que[me.qend + idx] = v;
-          if ((OffT)eb + d <= (OffT)CAP)
-            for (uint32_t j = 0; j < (uint32_t)d; ++j) rec_set(Rn[eb + j], v, ob[k] + j);
+          par[vv[k]] = uu[k];
+          if (me.qend + idx < P.n) que[me.qend + idx] = vv[k];
         }
+        append_records(Rn, isnew[k] && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, vv[k], ob[k]);
         w.ncnt += (uint32_t)__popcll(mask);
         w.necl += __builtin_amdgcn_readlane(incl, 63);
+      }
+      if constexpr (kStamp) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const unsigned long long sp4 = stamp();
+        auto c16 = [](unsigned long long d) { return (uint32_t)(d > 0xffff ? 0xffff : d); };
+        w.pad[0] = c16(sp1 - sp0) | (c16(sp2 - sp1) << 16);
+        w.pad[1] = c16(sp3 - sp2) | (c16(sp4 - sp3) << 16);
       }
     };
     if (E <= (uint32_t)kWave) run(std::integral_constant<int, 1>{});
@@ -457,12 +562,19 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         }
         // two-wave round barrier through LDS (the hardware barrier would also
         // release the parked waves)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        // Only LDS data (records, hash, res) crosses between the two waves, so
+        // the round barrier orders LDS only: a workgroup-scope fence would also
+        // wait for this wave's global parent/queue stores (~1k cycles), which
+        // nobody reads before the final vmcnt(0) + s_barrier.
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        unsigned long long ts_pre = 0, ts_bar = 0;
+        if (kStamp && tid == 0) ts_pre = stamp();
         if (lane == 0) atomicAdd(&rsync, 1u);
         const uint32_t target = 2 * (rounds + 1);
         while (__hip_atomic_load(&rsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
           __builtin_amdgcn_s_sleep(0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        asm volatile("" ::: "memory");
+        if (kStamp && tid == 0) ts_bar = stamp();
         const uint32_t rp = rounds & 1;
         ++rounds;
         const uint32_t fz0 = free0, fz1 = free1;
@@ -487,8 +599,11 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         if (kStamp && tid == 0 && levels - 1 < P.b.trace_cap) {
           LevelTraceDev& t = P.b.trace[levels - 1];
           t.side = (uint32_t)(stamp() - ts0);
-          t.depth = t.frontier = 0;
+          t.depth = (uint32_t)(ts_bar - ts_pre);  // wave 0's wait in the round barrier
+          t.frontier = 0;
           t.mode = lock ? 1 : 2;
+          const WaveLevel& wl = res[rp][lock ? 0 : q];
+          t.edges = (unsigned long long)wl.pad[0] | ((unsigned long long)wl.pad[1] << 32);
         }
       }
       // publish the plan for a big level (or the end)
@@ -534,25 +649,27 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
       uint32_t vv[B], uu[B];
       OffT ob[B], oe[B];
       bool ok[B];
+      OffT kk[B];
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         const uint32_t e = base + k * kLdsThreads + tid;
         ok[k] = e < E;
         const Rec r = Rc[ok[k] ? e : 0u];
         uu[k] = r.x;
-        vv[k] = P.col[min(rec_k(r), P.nnz_m1)];
+        kk[k] = min(rec_k(r), P.nnz_m1);
       }
-#pragma unroll
-      for (int k = 0; k < B; ++k) {
-        ob[k] = P.row_off[vv[k]];
-        oe[k] = P.row_off[vv[k] + 1];
-      }
+      fetch_edges(bc, kk, vv, ob, oe);
       bool isnew[B];
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
         // the other side is idle during a big level: any hit has its current depth
-        if (isnew[k] && hash_find(Ho, vv[k]) != kEmpty) meetv[slot] = vv[k];
+        if constexpr (kBm) {
+          isnew[k] = ok[k] && bm_claim(W(so), vv[k], a1 & 1);
+          if (isnew[k] && bm_state(W(o), vv[k]) != 0) meetv[slot] = vv[k];
+        } else {
+          isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
+          if (isnew[k] && hash_find(Ho, vv[k]) != kEmpty) meetv[slot] = vv[k];
+        }
       }
 #pragma unroll
       for (int k = 0; k < B; ++k) {
@@ -568,15 +685,13 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
           old = atomicAdd(&ctr[slot], ((unsigned long long)__popcll(mask) << 32) | wtot);
         const uint32_t olo = __builtin_amdgcn_readlane((uint32_t)old, leader);
         const uint32_t ohi = __builtin_amdgcn_readlane((uint32_t)(old >> 32), leader);
+        const uint32_t eb = olo + incl - dc;
         if (isnew[k]) {
           const uint32_t idx = ohi + mbcnt64(mask);
-          const uint32_t eb = olo + incl - dc;
-          const uint32_t v = vv[k];
-          par[v] = uu[k];
-          if (qbase + idx < P.n) que[qbase + idx] = v;
-          if ((OffT)eb + d <= (OffT)CAP)
-            for (uint32_t j = 0; j < (uint32_t)d; ++j) rec_set(Rn[eb + j], v, ob[k] + j);
+          par[vv[k]] = uu[k];
+          if (qbase + idx < P.n) que[qbase + idx] = vv[k];
         }
+        append_records(Rn, isnew[k] && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, vv[k], ob[k]);
       }
     };
     if (E <= (uint32_t)kLdsThreads) {
@@ -621,7 +736,8 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
   }
   if (kStamp && tid == 0 && P.b.trace_cap > 1) {
     LevelTraceDev& t = P.b.trace[P.b.trace_cap - 1];
-    t.edges = __builtin_amdgcn_s_memtime() - clk0;
+    e3 = __builtin_amdgcn_s_memtime();
+    t.edges = e3 - clk0;
     t.discovered = __builtin_amdgcn_s_memrealtime() - rt0;
   }
 
@@ -635,11 +751,21 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
     const uint32_t hops = md0 + md1;
     const uint32_t path_len = status == kFound ? hops + 1 : 0u;
     const bool path_dev = status == kFound && path_len > P.h.path_cap;
-    if (status == kFound && tid < 2) {  // two lanes walk the two parent chains side by side
-      uint32_t* out = path_dev ? P.b.dpath : P.h.path;
-      walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1, out);
-      __threadfence_system();
+    // Two lanes walk the two parent chains side by side into LDS (the record
+    // buffers are free now); then the whole wave streams the path to the
+    // pinned host buffer with write-through stores, 64 entries per instruction.
+    uint32_t* pbuf = reinterpret_cast<uint32_t*>(&R[0][0]);
+    constexpr uint32_t kPbufCap = sizeof(R) / sizeof(uint32_t);
+    const bool staged = !path_dev && path_len <= kPbufCap;
+    if (status == kFound && tid < 2)
+      walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1,
+                staged ? pbuf : (path_dev ? P.b.dpath : P.h.path));
+    if (staged) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (uint32_t i = lane; i < path_len; i += kWave)
+        __hip_atomic_store(&P.h.path[i], pbuf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (kStamp && tid == 0) e4 = __builtin_amdgcn_s_memtime();
     if (status == kHandoff && tid == 0) {
       DevState* st = P.b.st;
       st->status = kRunning;
@@ -661,37 +787,157 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P)
         st->vedges[q] = x.ved;
       }
     }
-    if (tid == 0) {
-      Rr->status = status;
-      Rr->hops = status == kFound ? (int32_t)hops : -1;
-      Rr->meet = meet;
-      Rr->levels = levels;
-      Rr->lds_levels = levels;
-      Rr->visited = s0.hcnt + s1.hcnt;
-      Rr->einsp = einsp;
-      Rr->depth[0] = status == kFound ? (int32_t)md0 : s0.depth;
-      Rr->depth[1] = status == kFound ? (int32_t)md1 : s1.depth;
-      Rr->path_len = path_len;
-      Rr->path_on_device = path_dev ? 1u : 0u;
-      Rr->rt_begin = rt0;
-      Rr->rt_end = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {  // write-through (system-scope) stores: no L2 writeback needed for the host
+      auto put = [](auto* p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+      put(&Rr->status, status);
+      put(&Rr->hops, status == kFound ? (int32_t)hops : -1);
+      put(&Rr->meet, meet);
+      put(&Rr->levels, levels);
+      put(&Rr->lds_levels, levels);
+      put(&Rr->visited, s0.hcnt + s1.hcnt);
+      put(&Rr->einsp, einsp);
+      put(&Rr->depth[0], status == kFound ? (int32_t)md0 : s0.depth);
+      put(&Rr->depth[1], status == kFound ? (int32_t)md1 : s1.depth);
+      put(&Rr->path_len, path_len);
+      put(&Rr->path_on_device, path_dev ? 1u : 0u);
+      put(&Rr->rt_begin, rt0);
+      put(&Rr->rt_end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
   }
   if (fstatus == kHandoff) {
     // Materialise the LDS visited sets as global bitmaps for the grid engine.
-    for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) {
-      const uint32_t k = Hflat[i];
-      if (k != kEmpty) {
-        const uint32_t v = k & kIdMask;
-        atomicOr(&((i >> kHashBits) ? P.b.vis[1] : P.b.vis[0])[v >> 5], 1u << (v & 31));
+    if constexpr (kBm) {
+      const uint32_t words = (P.n + 31) >> 5;  // <= kHashSize / 2 per side
+      for (uint32_t i = tid; i < 2 * words; i += kLdsThreads) {
+        const int q = i >= words;
+        const uint32_t wi = q ? i - words : i;
+        const unsigned long long w = W(q)[wi];
+        (q ? P.b.vis[1] : P.b.vis[0])[wi] = (uint32_t)w | (uint32_t)(w >> 32);
+      }
+    } else {
+      for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) {
+        const uint32_t k = Hflat[i];
+        if (k != kEmpty) {
+          const uint32_t v = k & kIdMask;
+          atomicOr(&((i >> kHashBits) ? P.b.vis[1] : P.b.vis[0])[v >> 5], 1u << (v & 31));
+        }
       }
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave's path / state / bitmap stores drained before publishing
   if (tid == 0) {
+    // Device-memory results (hand-off state and bitmaps, an over-long path)
+    // are read next by kernels / copies that may run on other XCDs: write
+    // this XCD's L2 back first.  The host-visible fields went write-through.
+    // (an unstaged path written with plain stores to host memory also needs the
+    // system-scope release)
+    if (status == kFound && md0 + md1 + 1 > sizeof(R) / sizeof(uint32_t)) __threadfence_system();
+    else if (fstatus == kHandoff) __threadfence();
+    if (kStamp && P.b.trace_cap > 2) {  // phase split: election / init / (loop) / walk / publish
+      LevelTraceDev& t = P.b.trace[P.b.trace_cap - 2];
+      t.side = (uint32_t)(e1 - e0);  // entry -> election resolved (init overlapped)
+      t.depth = (uint32_t)(clk0 - e1);
+      t.frontier = (uint32_t)(e4 - e3);
+      t.mode = (uint32_t)(__builtin_amdgcn_s_memtime() - e4);
+    }
+    __hip_atomic_store(&Rr->seq, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+template <typename OffT, bool kStamp, bool kBm>
+__global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P) {
+  lds_search_body<OffT, kStamp, kBm>(P, false);
+}
+
+// ---- resident query server -------------------------------------------------
+// One elected workgroup stays on the GPU and serves queries posted by the
+// host in a pinned mailbox: no kernel launch per query (~5 us saved of a
+// ~30 us query).  Thread 0 polls the mailbox over PCIe with system-scope
+// loads; the search itself is the same body as the one-shot kernel, and the
+// result is published through the same pinned HostResult.  Exit: the host's
+// stop word, or `idle_ticks` of s_memrealtime (100 MHz) without a request --
+// every wave reaches the exit through the same barrier, so the grid drains
+// even if the host process is gone.
+template <typename OffT, bool kBm>
+__global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P, ServerBox* box,
+                                                              uint32_t last_seq, unsigned long long idle_ticks) {
+  // Every branch that encloses a barrier is made provably wave-uniform
+  // (readfirstlane): with a lane-divergent-looking loop exit the structurizer
+  // may keep lanes 1..63 of wave 0 looping over the barriers while lane 0
+  // waits to poll -- a deadlock.  So the whole of wave 0 polls, uniformly.
+  __shared__ uint32_t cmd[6];  // stop, seq, src, dst, side_policy, lockstep
+  __shared__ uint32_t srv_won;
+  const int tid = threadIdx.x;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  const bool cand = P.pin_xcc < 0 ? blockIdx.x == 0 : xcc_id() == (uint32_t)P.pin_xcc;
+  if (!cand) return;
+  if (tid == 0) srv_won = atomicMax(P.ticket, P.seq) < P.seq;
+  __syncthreads();
+  if (!uni(srv_won)) return;
+  if (tid == 0) __hip_atomic_store(&box->alive, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (;;) {
+    if (wid == 0) {
+      if (tid == 0) __hip_atomic_store(&box->stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      uint32_t stop = 0, polls = 0;
+      uint4 rq;
+      unsigned long long tl = t0, lat = 0;
+      for (;;) {
+        ++polls;
+        // One 16-byte system-scope load (bypasses the caches; relaxed: an
+        // acquire would invalidate this XCD's L2 -- the hot graph -- per poll).
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 r4;
+        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                     : "=v"(r4)
+                     : "v"(box)
+                     : "memory");
+        rq.x = uni(r4.x), rq.y = uni(r4.y), rq.z = uni(r4.z), rq.w = uni(r4.w);
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        lat = tn - tl;  // one poll round trip (100 MHz ticks)
+        tl = tn;
+        const bool whole = (rq.w >> 8) == (rq.x & 0xffffffu);  // not torn
+        if (whole && rq.x != last_seq) {
+          stop = rq.w & kReqStop;
+          break;
+        }
+        if (tn - t0 > idle_ticks) {
+          stop = 1;
+          break;
+        }
+      }
+      if (tid == 0) {
+        __hip_atomic_store(&box->stage, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&box->seen, rq.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&box->pad[0], (uint32_t)lat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&box->pad[1], polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        cmd[0] = stop;
+        cmd[1] = rq.x;
+        cmd[2] = rq.y;
+        cmd[3] = rq.z;
+        cmd[4] = (rq.w >> 2) & 3u;
+        cmd[5] = (rq.w & kReqLockstep) ? 1u : 0u;
+      }
+    }
+    __syncthreads();
+    if (uni(cmd[0])) break;
+    LdsParams<OffT> Q = P;
+    Q.seq = uni(cmd[1]);
+    // the host validated src/dst against n; clamp anyway so a torn mailbox can never fault
+    Q.src = min(uni(cmd[2]), P.n - 1);
+    Q.dst = min(uni(cmd[3]), P.n - 1);
+    Q.side_policy = (int)uni(cmd[4]);
+    Q.lockstep = (int)uni(cmd[5]);
+    Q.trace = 0;
+    last_seq = Q.seq;
+    __syncthreads();  // every wave has read cmd before thread 0 may overwrite it
+    lds_search_body<OffT, false, kBm>(Q, true);
+    if (tid == 0) __hip_atomic_store(&box->stage, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (tid == 0) {
     __threadfence_system();
-    __hip_atomic_store(&Rr->seq, P.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&box->alive, ~P.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);  // exited
   }
 }
 
@@ -1071,20 +1317,38 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   // 16 blocks = 2 per XCD under round-robin dispatch; only the elected one works
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   if (g.row_off32) {
-    LdsParams<uint32_t> P{g.row_off32, g.col, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
+    LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), b, h};
-    if (trace == 2)
-      k_lds_bibfs<uint32_t, true><<<blocks, kLdsThreads, 0, s>>>(P);
-    else
-      k_lds_bibfs<uint32_t, false><<<blocks, kLdsThreads, 0, s>>>(P);
+    const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
+    if (trace == 2) {
+      if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
+      else k_lds_bibfs<uint32_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
+    } else {
+      if (bm) k_lds_bibfs<uint32_t, false, true><<<blocks, kLdsThreads, 0, s>>>(P);
+      else k_lds_bibfs<uint32_t, false, false><<<blocks, kLdsThreads, 0, s>>>(P);
+    }
   } else {
-    LdsParams<uint64_t> P{g.row_off, g.col, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
+    LdsParams<uint64_t> P{g.row_off, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), b, h};
     if (trace == 2)
-      k_lds_bibfs<uint64_t, true><<<blocks, kLdsThreads, 0, s>>>(P);
+      k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
     else
-      k_lds_bibfs<uint64_t, false><<<blocks, kLdsThreads, 0, s>>>(P);
+      k_lds_bibfs<uint64_t, false, false><<<blocks, kLdsThreads, 0, s>>>(P);
   }
+  HIP_CHECK(hipGetLastError());
+}
+
+void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, dev::ServerBox* box,
+                uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
+                unsigned long long idle_ticks, hipStream_t s) {
+  const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
+  BIBFS_REQUIRE(g.row_off32 != nullptr, "resident server: 32-bit row offsets required");
+  LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
+                         (uint32_t)(g.nnz ? g.nnz - 1 : 0), b, h};
+  if (g.n <= kBmMaxN)
+    k_lds_server<uint32_t, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
+  else
+    k_lds_server<uint32_t, false><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
   HIP_CHECK(hipGetLastError());
 }
 

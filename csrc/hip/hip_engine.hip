@@ -10,6 +10,7 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -34,6 +35,7 @@ struct HipBiBfs::Impl {
   uint64_t* d_row_off = nullptr;
   uint32_t* d_row_off32 = nullptr;
   uint32_t* d_col = nullptr;
+  uint4* d_padj = nullptr;   // packed adjacency (LDS engine), when it fits the budget
   uint32_t* d_uv = nullptr;  // last generated edge list (kept for small graphs / tests)
   uint64_t uv_m = 0;
   double build_ms = 0.0;
@@ -54,24 +56,111 @@ struct HipBiBfs::Impl {
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
+  // resident server (k_lds_server)
+  hipStream_t sstream = nullptr;
+  ServerBox* h_box = nullptr;
+  bool resident = false;         // user setting
+  bool srv_running = false;      // a server kernel was launched and has not been seen to exit
+  uint32_t srv_launch_seq = 0;
+  unsigned long long srv_idle_ticks = 20000000ull;  // 200 ms of s_memrealtime
+
   // step-wise API
   int dir[2] = {1, 1};
   bool fbits_valid[2] = {false, false};
   vid_t step_src = 0, step_dst = 0;
 
   launch::GraphView view() const {
-    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col};
+    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj};
+  }
+
+  bool server_usable() const { return d_row_off32 != nullptr && n > 0 && n <= 0x7fffffffu; }
+
+  static bool dbg() {
+    static const bool on = std::getenv("BIBFS_DEBUG") != nullptr;
+    return on;
+  }
+
+  // one aligned 16-byte store: the server reads the request with one load
+  void post(uint32_t s, uint32_t src, uint32_t dst, uint32_t flags) {
+    const __m128i v = _mm_set_epi32((int)req_tag(s, flags), (int)dst, (int)src, (int)s);
+    _mm_store_si128(reinterpret_cast<__m128i*>(h_box), v);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+  }
+
+  void launch_server(int pin) {
+    srv_launch_seq = ++seq == 0 ? ++seq : seq;
+    if (dbg()) std::fprintf(stderr, "[server] launch seq %u pin %d\n", srv_launch_seq, pin);
+    __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
+    const uint32_t last = __atomic_load_n(&h_box->seq, __ATOMIC_ACQUIRE);
+    launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap}, h_box, srv_launch_seq, last, pin,
+                       d_flag + 4, srv_idle_ticks, sstream);
+    srv_running = true;
+  }
+
+  void stop_server() {
+    if (!srv_running) return;
+    const uint32_t s = ++seq == 0 ? ++seq : seq;
+    post(s, 0, 0, kReqStop);
+    if (dbg()) std::fprintf(stderr, "[server] stop (stage %u alive %u)\n", h_box->stage, h_box->alive);
+    HIP_CHECK(hipStreamSynchronize(sstream));
+    if (dbg()) std::fprintf(stderr, "[server] stopped\n");
+    srv_running = false;
+  }
+
+  // Post one query to the server and wait for its answer.
+  void server_query(uint32_t src, uint32_t dst, const SearchOptions& opt, uint32_t qseq) {
+    if (srv_running && __atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) == ~srv_launch_seq)
+      srv_running = false;  // idled out (a relaunch queues behind its last instructions)
+    if (!srv_running) launch_server(pin_xcc);
+    post(qseq, src, dst, (opt.lockstep ? kReqLockstep : 0u) | ((uint32_t)opt.side & 3u) << 2);
+    if (dbg()) std::fprintf(stderr, "[server] post %u (stage %u alive %u)\n", qseq, h_box->stage, h_box->alive);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t it = 1;; ++it) {
+      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq) return;
+      if ((it & 8191) == 0) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+          char msg[512];
+          std::snprintf(msg, sizeof msg,
+                        "bibfs: resident server did not answer query %u in 5 s (alive %u launch %u stage %u seen %u "
+                        "result seq %u)",
+                        qseq, h_box->alive, srv_launch_seq, h_box->stage, h_box->seen, h_res->seq);
+          std::fprintf(stderr, "%s\n", msg);
+          post(++seq == 0 ? ++seq : seq, 0, 0, kReqStop);
+          throw Error(msg);
+        }
+        const hipError_t e = hipStreamQuery(sstream);
+        if (e == hipSuccess) {  // server gone: idle exit raced this query, or no block won the election
+          if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq) return;
+          if (__atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) != srv_launch_seq) pin_xcc = -1;
+          // relaunch so the pending request (box seq != last) is served
+          srv_running = false;
+          const uint32_t pending = qseq;
+          srv_launch_seq = ++seq == 0 ? ++seq : seq;
+          __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
+          launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap}, h_box, srv_launch_seq,
+                             pending - 1, pin_xcc, d_flag + 4, srv_idle_ticks, sstream);
+          srv_running = true;
+        } else if (e != hipErrorNotReady) {
+          throw Error(std::string("bibfs: resident server failed: ") + hipGetErrorString(e));
+        }
+      } else {
+        _mm_pause();
+      }
+    }
   }
 
   void free_graph() {
+    stop_server();
     if (d_row_off) HIP_CHECK(hipFree(d_row_off));
     if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
     if (d_col) HIP_CHECK(hipFree(d_col));
+    if (d_padj) HIP_CHECK(hipFree(d_padj));
     if (d_uv) HIP_CHECK(hipFree(d_uv));
     if (state_block) HIP_CHECK(hipFree(state_block));
     d_row_off = nullptr;
     d_row_off32 = nullptr;
     d_col = nullptr;
+    d_padj = nullptr;
     d_uv = nullptr;
     state_block = nullptr;
     n = 0;
@@ -132,6 +221,16 @@ struct HipBiBfs::Impl {
     if (nnz < 0xFFFFFFFFULL) {
       HIP_CHECK(hipMalloc(&d_row_off32, ((size_t)n + 1) * 4));
       launch::make_row_off32(d_row_off, n, d_row_off32, stream);
+    }
+    // Packed adjacency: 16 B per directed edge next to the 4 B CSR column.
+    // Budget BIBFS_PADJ_MAX_MB (default 4096 MiB; 0 disables) -- a 10M-vertex
+    // G(n, 2.2/n) needs 352 MB, a scale-27 Kronecker graph would need ~69 GB,
+    // where the plain CSR path is used instead.
+    const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
+    const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
+    if (nnz && nnz * 16 <= budget) {
+      HIP_CHECK(hipMalloc(&d_padj, nnz * 16));
+      launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
     }
     alloc_state();
     build_ms = ms;
@@ -271,6 +370,11 @@ struct HipBiBfs::Impl {
     if (t.discovered)
       std::fprintf(stderr, "[stamp] shader clock %.0f MHz over %.2f us\n", (double)t.edges / (double)t.discovered * 100.0,
                    (double)t.discovered / 100.0);
+    LevelTraceDev u{};
+    HIP_CHECK(hipMemcpyAsync(&u, buf.trace + buf.trace_cap - 2, sizeof u, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    std::fprintf(stderr, "[stamp] cycles: election %u init %u search-loop %llu path-walk %u publish %u\n", u.side,
+                 u.depth, (unsigned long long)t.edges, u.frontier, u.mode);
   }
 
   void fetch_trace(SearchResult& r) {
@@ -301,6 +405,10 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
   HIP_CHECK(hipGetDeviceProperties(&p_->prop, device));
   p_->cus = p_->prop.multiProcessorCount > 0 ? p_->prop.multiProcessorCount : 256;
   HIP_CHECK(hipStreamCreateWithFlags(&p_->stream, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&p_->sstream, hipStreamNonBlocking));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_box), sizeof(ServerBox),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(p_->h_box, 0, sizeof(ServerBox));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_res), sizeof(HostResult),
                           hipHostMallocMapped | hipHostMallocCoherent));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_path), (size_t)p_->h_path_cap * 4,
@@ -320,6 +428,8 @@ HipBiBfs::~HipBiBfs() {
     p_->free_graph();
   } catch (...) {
   }
+  (void)hipStreamDestroy(p_->sstream);
+  (void)hipHostFree(p_->h_box);
   (void)hipHostFree(p_->h_res);
   (void)hipHostFree(p_->h_path);
   (void)hipHostFree(p_->h_state);
@@ -413,6 +523,15 @@ void HipBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, do
   I.finish_graph(ms);
 }
 
+void HipBiBfs::set_resident(bool on, double idle_ms) {
+  auto& I = *p_;
+  HIP_CHECK(hipSetDevice(I.device));
+  if (!on) I.stop_server();
+  I.resident = on;
+  I.srv_idle_ticks = (unsigned long long)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
+}
+bool HipBiBfs::resident() const { return p_->resident; }
+
 uint32_t HipBiBfs::n() const { return p_->n; }
 uint64_t HipBiBfs::nnz() const { return p_->nnz; }
 uint64_t HipBiBfs::m_input() const { return p_->m_input; }
@@ -420,6 +539,7 @@ double HipBiBfs::last_build_ms() const { return p_->build_ms; }
 size_t HipBiBfs::device_bytes() const {
   const auto& I = *p_;
   return ((size_t)I.n + 1) * 8 + (I.d_row_off32 ? ((size_t)I.n + 1) * 4 : 0) + I.nnz * 4 +
+         (I.d_padj ? I.nnz * 16 : 0) +
          (I.d_uv ? I.uv_m * 8 : 0) + I.state_bytes;
 }
 int HipBiBfs::device() const { return p_->device; }
@@ -465,8 +585,17 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   if (!grid) {
     const int tr = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
     const int lock = (opt.lockstep && I.n <= 0x7fffffffu) ? 1 : 0;
-    launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, I.pin_xcc, I.d_flag + 4, lock, I.stream);
-    if (!I.wait_seq_or_done(seq)) {
+    if (I.resident && !opt.trace && I.server_usable()) {
+      I.server_query(src, dst, opt, seq);
+      if (I.dbg())
+        std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",
+                     I.h_res->seq, I.h_res->status, I.h_res->hops, I.h_res->levels, I.h_box->stage,
+                     I.h_box->pad[0] * 0.01, I.h_box->pad[1]);
+    } else {
+      launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, I.pin_xcc, I.d_flag + 4, lock,
+                         I.stream);
+    }
+    if (I.h_res->seq != seq && !I.wait_seq_or_done(seq)) {
       // no block reached the pinned XCD: relaunch unpinned, and stop pinning
       I.pin_xcc = -1;
       launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, -1, I.d_flag + 4, lock, I.stream);

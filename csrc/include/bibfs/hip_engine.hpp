@@ -52,6 +52,13 @@ class HipBiBfs {
   // --- search ---------------------------------------------------------------
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
 
+  // Resident query server: one workgroup stays on the GPU and takes queries
+  // from a pinned mailbox, so a query costs no kernel launch.  It exits by
+  // itself after `idle_ms` without a query (and is relaunched on demand),
+  // and is stopped before any graph change or destruction.
+  void set_resident(bool on, double idle_ms = 200.0);
+  bool resident() const;
+
   // --- step-wise API (parity with the reference's per-level C API,
   //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)
   void begin(vid_t src, vid_t dst);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# A/B builds of the search kernels: scripts/build_variants.sh NAME "-DKNOB=.." [NAME "-D.."]...
+# -> build/var/NAME/libbibfs.so (run a tool with LD_LIBRARY_PATH=build/var/NAME).
+set -euo pipefail
+ROOT="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
+cd "$ROOT"
+make -s -j8 gpu >/dev/null
+OBJS=$(ls build/obj/{io,gen,csr,cpu}/*.o | grep -v mpi_) 
+OTHER="build/obj/hip/capi.o build/obj/hip/csr_device.o build/obj/hip/hip_engine.o build/obj/dist/dist_engine.o"
+while [ $# -ge 2 ]; do
+  name=$1; flags=$2; shift 2
+  mkdir -p build/var/$name
+  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -mcode-object-version=5 -munsafe-fp-atomics \
+    -Icsrc/include -Icsrc/hip $flags -c csrc/hip/engine_kernels.hip -o build/var/$name/engine_kernels.o &
+done
+wait
+for d in build/var/*/; do
+  [ -f $d/engine_kernels.o ] || continue
+  /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $d/libbibfs.so $OBJS $OTHER $d/engine_kernels.o \
+    -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib -lrccl -pthread
+done
+ls build/var

@@ -1,5 +1,5 @@
 // bibfs_hip <bin-file> <src> <dst> [--repeat R] [--warmup W] [--json] [--verify]
-//           [--trace] [--force-grid] [--direction auto|topdown|bottomup] [--device D]
+//           [--trace] [--force-grid] [--direction auto|topdown|bottomup] [--device D] [--resident]
 //           [--host-csr] [--csr-cache FILE]
 // (also installed as bibfs_cuda_only, the reference v3 binary name)
 //
@@ -61,6 +61,7 @@ int main(int argc, char** argv) {
       return 1;
     }
     auto opt = cli::options_from(a);
+    if (a.has("resident")) eng.set_resident(true);  // resident query server: no launch per query
     const int warmup = (int)a.geti("warmup", 3);
     const int repeat = (int)std::max(1LL, a.geti("repeat", 5));
     for (int i = 0; i < warmup; ++i) eng.search(src, dst, opt);
@@ -81,9 +82,15 @@ int main(int argc, char** argv) {
       std::printf("DEBUG: gpu bfs time = %f ms\n", med_s);
       std::printf("GPU BFS: %s\n", r.found ? "PATH FOUND" : "NO PATH");
       if (opt.trace && std::getenv("BIBFS_STAMP")) {
-        for (auto& t : r.stats.trace)
-          std::printf("Stamp cycles: %s level=%d barrier=%d book=%llu\n", bibfs_mode_name(t.mode), t.side,
-                      t.depth, (unsigned long long)t.frontier);
+        for (auto& t : r.stats.trace) {
+          if (t.mode == 1 || t.mode == 2)  // wave rounds: phase split of wave 0 / the working wave
+            std::printf("Stamp cycles: %s round=%d barrier_wait=%d rec+col=%llu row_off=%llu claim=%llu append=%llu\n",
+                        bibfs_mode_name(t.mode), t.side, t.depth, t.edges & 0xffff, (t.edges >> 16) & 0xffff,
+                        (t.edges >> 32) & 0xffff, (t.edges >> 48) & 0xffff);
+          else
+            std::printf("Stamp cycles: %s level=%d barrier=%d book=%llu\n", bibfs_mode_name(t.mode), t.side,
+                        t.depth, (unsigned long long)t.frontier);
+        }
       } else if (opt.trace) {
         for (auto& t : r.stats.trace)
           std::printf("Level side=%d depth=%d frontier=%llu edges=%llu new=%llu mode=%s\n", t.side, t.depth,

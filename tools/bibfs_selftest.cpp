@@ -78,6 +78,7 @@ static void check_searches(HipBiBfs& eng, const Csr& g, int nq, uint64_t seed, c
 }
 
 int main(int argc, char** argv) {
+  std::setvbuf(stdout, nullptr, _IOLBF, 0);  // line-buffered: a killed run still shows how far it got
   std::vector<std::string> specs;
   for (int i = 1; i < argc; ++i) specs.push_back(argv[i]);
   if (specs.empty()) specs = {"gnp:1000::1", "gnp:100000::6", "rmat:65536:1048576:3"};
@@ -103,6 +104,12 @@ int main(int argc, char** argv) {
       SearchOptions al;
       al.side = SidePolicy::kAlternate;
       check_searches(eng, host, 10, 17, al, "lds-alt");
+      // resident server: queries through the pinned mailbox, interleaved with
+      // one-shot and grid queries (the server must stay consistent)
+      eng.set_resident(true);
+      check_searches(eng, host, 40, 18, o, "lds-resident");
+      check_searches(eng, host, 5, 19, nl, "lds-resident-nolock");
+      eng.set_resident(false);
       SearchOptions g;
       g.force_grid = true;
       check_searches(eng, host, 20, 12, g, "grid-auto");
