@@ -75,6 +75,8 @@ def main() -> int:
                     help="second config reported under 'extra' (empty to skip)")
     ap.add_argument("--extra-steps", type=int, default=50)
     ap.add_argument("--pairs", type=int, default=64)
+    ap.add_argument("--no-resident", action="store_true",
+                    help="launch one kernel per query instead of the resident query server")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,6 +112,7 @@ def main() -> int:
             m = eng.m
         else:
             eng = HipEngine(local).generate_gnp(n, p, seed)
+            eng.set_resident(not a.no_resident)
             m = eng.m
         build_s = time.perf_counter() - t0
         pairs = pick_pairs(eng, n, a.pairs, 12345)
@@ -125,9 +128,20 @@ def main() -> int:
             assert r.found and len(path) == r.hops + 1
             return r
 
+        resident = hasattr(eng, "set_resident") and not a.no_resident
+
+        def park():
+            # A device-wide synchronize waits for every kernel, the resident
+            # server included: stop it first (it relaunches on the next query).
+            if resident:
+                eng.set_resident(False)
+
         for i in range(warmup):
             query(i)
+        park()
         barrier()
+        if resident:
+            eng.set_resident(True)  # lazily relaunched by the first timed query (launch cost is timed)
         t0 = time.perf_counter()
         hops = insp = 0
         dev_ms = 0.0
@@ -136,6 +150,7 @@ def main() -> int:
             hops += r.hops
             insp += r.edges_inspected
             dev_ms += r.search_ms
+        park()  # server shutdown is inside the timed region
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         queries = steps * (1 if a.mode == "partitioned" else world)
@@ -183,6 +198,7 @@ def main() -> int:
                 "gteps_inspected": head["gteps_inspected"],
                 "mean_hops": head["mean_hops"],
                 "graph_build_ms": round(head["build_ms"], 3),
+                "resident_server": a.mode == "replicated" and not a.no_resident,
                 "extra": extra,
             },
         }

@@ -152,3 +152,51 @@ def test_trace_and_stats(gpu_engine):
     assert len(tr) == r.stats["levels"] == 17
     assert all(t["mode"] in (1, 2, 3) for t in tr)
     assert sum(t["edges"] for t in tr) == r.stats["edges_inspected"]
+
+
+@pytest.mark.parametrize("spec", ["gnp:100000::6", "gnp:1000000::2", "rmat:65536:1048576:3"])
+def test_resident_server_vs_oracle(gpu_engine, spec):
+    """Resident query server (pinned mailbox, no launch per query), interleaved
+    with one-shot grid / trace queries that must not disturb it."""
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 30, 21)
+    gpu_engine.set_resident(True)
+    try:
+        assert gpu_engine.resident
+        assert_engine(gpu_engine, g, pairs)
+        assert_engine(gpu_engine, g, pairs[:4], force_grid=True)
+        assert_engine(gpu_engine, g, pairs[:4], trace=True)
+        assert_engine(gpu_engine, g, pairs[:10], lockstep=False, side="alternate")
+        assert_engine(gpu_engine, g, pairs)
+    finally:
+        gpu_engine.set_resident(False)
+
+
+def test_resident_idle_exit_and_relaunch(gpu_engine):
+    import time
+
+    g = gnp(100000, seed=6)
+    gpu_engine.load(g)
+    gpu_engine.set_resident(True, idle_ms=5.0)
+    try:
+        for k in range(3):
+            r = gpu_engine.search(0, 99999)
+            assert r.found and r.hops == 17
+            time.sleep(0.05)  # the server idles out; the next query relaunches it
+    finally:
+        gpu_engine.set_resident(False)
+
+
+@pytest.mark.parametrize("resident", [False, True])
+def test_path_longer_than_lds_staging(gpu_engine, resident):
+    n = 50_000  # 50k-vertex path: longer than the LDS staging buffer, shorter than the pinned buffer
+    g = Graph.from_edges(n, np.stack([np.arange(n - 1), np.arange(1, n)], 1).astype(np.uint32))
+    gpu_engine.load(g)
+    gpu_engine.set_resident(resident)
+    try:
+        r = gpu_engine.search(0, n - 1)
+        assert r.hops == n - 1
+        assert np.array_equal(np.asarray(r.path), np.arange(n))
+    finally:
+        gpu_engine.set_resident(False)
