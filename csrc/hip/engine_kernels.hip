@@ -77,7 +77,14 @@ constexpr uint32_t kHashSize = 1u << kHashBits;  // slots per side
 constexpr uint32_t kHashMask = kHashSize - 1;
 constexpr uint32_t kHashLimit = kHashSize * 3 / 4;  // max visited per side in LDS
 constexpr int kBatch = 4;                           // edges per thread per round (big levels)
-constexpr uint32_t kSmallEdges = 256;               // a level this small runs on one wave
+#ifndef BIBFS_KNOB_SMALL_EDGES
+#define BIBFS_KNOB_SMALL_EDGES 128
+#endif
+#ifndef BIBFS_KNOB_DUAL_EDGES
+#define BIBFS_KNOB_DUAL_EDGES 256
+#endif
+constexpr uint32_t kSmallEdges = BIBFS_KNOB_SMALL_EDGES;  // a level this small runs on one wave
+constexpr uint32_t kDualEdges = BIBFS_KNOB_DUAL_EDGES;    // both sides together this small: one lockstep round
 constexpr uint32_t kDegClamp = 65535;               // per-lane edge contribution to the packed counter
 constexpr uint32_t kParity = 0x80000000u;           // depth-parity bit of a hash key
 constexpr uint32_t kIdMask = 0x7fffffffu;
@@ -211,16 +218,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
-// Result of one level expanded by one wave (lockstep / single rounds).
-struct WaveLevel {
-  uint32_t ncnt, necl;               // claims, clamped degree sum of the claims
-  uint32_t mlen, mv, md_self, md_other;  // best meet candidate (mlen = ~0 when none)
-  uint32_t pad[2];
-};
 
 // Published by wave 0 for the parked waves: the big level to run (or the end).
 struct LevelPlan {
-  uint32_t status, side, E, cur, nxt, qbase, depth_self, depth_other;
+  uint32_t status, side, E, cur, off, nxt, qbase, depth_self, depth_other;
 };
 
 // One whole search by one workgroup.  `elected`: the caller already owns the
@@ -233,10 +234,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   __shared__ Rec R[4][CAP];
   __shared__ unsigned long long ctr[2];  // big levels: (count << 32) | clamped edge sum
   __shared__ uint32_t meetv[2];          // big levels: a meet vertex of the level
-  __shared__ WaveLevel res[2][2];        // [round parity][worker wave]: a wave rewrites a slot only
-                                         // two rounds later, after the other wave has read it
   __shared__ LevelPlan plan;
-  __shared__ uint32_t rsync;             // two-wave round counter
   __shared__ uint32_t won;
   __shared__ Rec junk[kWave];            // record writes of finished lanes land here (no divergence)
 
@@ -298,19 +296,19 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     ctr[tid] = 0;
     meetv[tid] = kEmpty;
   }
-  if (tid == 0) rsync = 0;
 
   // ---- replicated search state: identical in waves 0 and 1 (the workers);
   // two structs selected field-wise (a struct-level `?:` or an array indexed
   // by the runtime side is lowered through scratch memory).
   struct SideState {
-    uint32_t cur, cnt, hcnt, qend, fbeg, ovf;
+    uint32_t cur, off, cnt, hcnt, qend, fbeg, ovf;  // records: R[cur][off .. off + fed)
     int depth;
     unsigned long long fed, ved;
   };
   auto sel = [](bool one, const SideState& a, const SideState& b) {
     SideState x;
     x.cur = one ? b.cur : a.cur;
+    x.off = one ? b.off : a.off;
     x.cnt = one ? b.cnt : a.cnt;
     x.hcnt = one ? b.hcnt : a.hcnt;
     x.qend = one ? b.qend : a.qend;
@@ -326,6 +324,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     const uint32_t r = q ? P.dst : P.src;
     const OffT b = P.row_off[r], e = P.row_off[r + 1];
     x.cur = (uint32_t)q;
+    x.off = 0;
     x.cnt = 1;
     x.hcnt = 1;
     x.qend = 1;
@@ -343,7 +342,11 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     return x;
   };
   SideState s0 = init_side(0), s1 = init_side(1);
-  uint32_t free0 = 2, free1 = 3;  // record buffers not holding a current frontier
+  // a record buffer that holds neither side's current frontier (4 buffers, <= 2 in use)
+  auto free_buf = [&]() -> uint32_t {
+    const uint32_t used = (1u << s0.cur) | (1u << s1.cur);
+    return (uint32_t)__builtin_ctz(~used & 0xfu);
+  };
   uint32_t levels = 0, status = kRunning, meet = kEmpty, md0 = 0, md1 = 0, rounds = 0, bigs = 0;
   unsigned long long einsp = 0;
   int turn = 0;
@@ -372,7 +375,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
   };
   // apply a finished level of side q to the replicated state
-  auto apply = [&](int q, uint32_t E, uint32_t nxt, uint32_t ncnt, uint32_t necl, uint32_t mode) {
+  auto apply = [&](int q, uint32_t E, uint32_t nxt, uint32_t noff, uint32_t ncnt, uint32_t necl, uint32_t mode) {
     SideState x = sel(q, s0, s1);
     record_trace(q, x, E, ncnt, mode);
     ++levels;
@@ -383,57 +386,61 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     x.qend += ncnt;
     if (ncnt) {
       x.fbeg = qbase;
-      const uint32_t old = x.cur;
       x.cur = nxt;
-      // the consumed buffer replaces the one just filled in the free pair
-      if (free0 == nxt) free0 = old;
-      else free1 = old;
+      x.off = noff;
     }
     x.cnt = ncnt;
     x.fed = necl;
     x.ved += necl;
-    x.ovf = necl > CAP ? 1u : 0u;
+    x.ovf = (unsigned long long)noff + necl > CAP ? 1u : 0u;  // records live at [noff, noff + necl)
     s0 = sel(q, x, s0);
     s1 = sel(q, s1, x);
   };
 
-  // One wave expands one level of side q (depth a -> a+1) while the other side
-  // sits at depth b (or concurrently goes b -> b+1 when `both`).
-  auto wave_level = [&](int q, uint32_t nxt) -> WaveLevel {
-    const SideState me = sel(q, s0, s1);
-    const SideState ot = sel(q, s1, s0);
-    const uint32_t E = (uint32_t)me.fed;
-    const uint32_t a1 = (uint32_t)me.depth + 1, b = (uint32_t)ot.depth;
-    const uint32_t keybit = (a1 & 1) ? kParity : 0u;
-    const Rec* Rc = R[me.cur];
-    Rec* Rn = R[nxt];
-    uint32_t* __restrict__ par = q ? P.b.parent[1] : P.b.parent[0];
-    uint32_t* __restrict__ que = q ? P.b.queue[1] : P.b.queue[0];
-    uint32_t* Hs = H[q];
-    const uint32_t* Ho = H[q ^ 1];
-    WaveLevel w;
-    w.ncnt = 0;
-    w.necl = 0;
-    w.mlen = kEmpty;
-    w.mv = kEmpty;
-    w.md_self = a1;
-    w.md_other = b;
-    w.pad[0] = w.pad[1] = 0;
-    if (E == 0) return w;  // isolated frontier: the side is exhausted
-    auto run = [&](auto bc) {
+  // ---- wave 0 expands one level of side 0 (E0 records) and/or side 1 (E1
+  // records) in the same instructions: lanes [0, E0) of the virtual edge list
+  // are side 0, [E0, E0 + E1) side 1.  With both sides active this is a
+  // lockstep round; the meet rule is the parity rule above (a claim and the
+  // opposite read are ordered per lane, and one wave's LDS ops execute in
+  // order, so two same-round claims of one vertex always see each other).
+  // Returns the round's best meet candidate through mlen/mv/m0/m1.
+  struct Dual {
+    uint32_t ncnt[2], necl[2];
+    uint32_t mlen, mv, m0, m1;
+    uint32_t pad[2];  // kStamp: phase split
+  };
+  // New records of both sides go to ONE buffer: all side-0 lanes precede the
+  // side-1 lanes in (batch, lane) order, so one running prefix puts side 0's
+  // records at [0, necl[0]) and side 1's right after -- one scan and one
+  // append per batch, and the next round reads the two runs back-to-back.
+  auto dual_level = [&](uint32_t E0, uint32_t E1, uint32_t nxt) -> Dual {
+    Dual out;
+    out.ncnt[0] = out.ncnt[1] = out.necl[0] = out.necl[1] = 0;
+    out.mlen = kEmpty;
+    out.mv = kEmpty;
+    out.m0 = out.m1 = 0;
+    out.pad[0] = out.pad[1] = 0;
+    const uint32_t ET = E0 + E1;
+    if (ET == 0) return out;
+    const bool both = E0 != 0 && E1 != 0;
+    const uint32_t b0 = (uint32_t)s0.depth, b1 = (uint32_t)s1.depth;  // current frontier depths
+    const Rec* R0 = &R[s0.cur][s0.off];
+    const Rec* R1 = &R[s1.cur][s1.off];
+    Rec* Nb = R[nxt];
+    auto run = [&](auto bc, uint32_t base) {
       constexpr int B = decltype(bc)::value;
       uint32_t vv[B], uu[B];
-      OffT ob[B], oe[B];
-      bool ok[B], isnew[B];
-      // kStamp: per-phase cycle split (explicit waits serialise the phases)
-      unsigned long long sp0 = 0, sp1 = 0, sp2 = 0, sp3 = 0;
+      OffT ob[B], oe[B], kk[B];
+      bool ok[B], sd[B], isnew[B];
+      unsigned long long sp0 = 0, sp1 = 0, sp2 = 0;
       if constexpr (kStamp) sp0 = stamp();
-      OffT kk[B];
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        const uint32_t e = k * kWave + lane;
-        ok[k] = e < E;
-        const Rec r = Rc[ok[k] ? e : 0u];  // invalid lanes re-read record 0: loads stay branch-free
+        const uint32_t e = base + k * kWave + lane;
+        ok[k] = e < ET;
+        sd[k] = e >= E0;
+        const uint32_t i = ok[k] ? (sd[k] ? e - E0 : e) : 0u;  // invalid lanes re-read record 0
+        const Rec r = sd[k] ? R1[i] : R0[i];
         uu[k] = r.x;
         kk[k] = min(rec_k(r), P.nnz_m1);  // clamp: a bad record can never fault
       }
@@ -442,86 +449,92 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         sp1 = stamp();
       }
-      if constexpr (kStamp) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        sp2 = stamp();
-      }
-      uint32_t hl = kEmpty, hv = 0, hdo = 0;  // this lane's best meet candidate
+      uint32_t hl = kEmpty, hv = 0, hd = 0;  // this lane's best meet: length, vertex, own claim depth
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        uint32_t f;  // other side's state of vv[k]: 0 = absent, else 1 + parity (3 = older claim)
+        const uint32_t a = (sd[k] ? b1 : b0) + 1;  // claim depth on this lane's side
+        const uint32_t bo = sd[k] ? b0 : b1;       // opposite side's frontier depth
+        uint32_t f;  // opposite state: 0 absent, else 1 + parity (3 = an older claim)
         if constexpr (kBm) {
-          isnew[k] = ok[k] && bm_claim(W(q), vv[k], a1 & 1);
-          f = isnew[k] ? bm_state(W(q ^ 1), vv[k]) : 0u;
+          isnew[k] = ok[k] && bm_claim(W(sd[k]), vv[k], a & 1);
+          f = isnew[k] ? bm_state(W(!sd[k]), vv[k]) : 0u;
         } else {
-          isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
-          const uint32_t key = isnew[k] ? hash_find(Ho, vv[k]) : kEmpty;
+          isnew[k] = ok[k] && hash_insert(sd[k] ? H[1] : H[0], vv[k], vv[k] | ((a & 1) ? kParity : 0u));
+          const uint32_t key = isnew[k] ? hash_find(sd[k] ? H[0] : H[1], vv[k]) : kEmpty;
           f = key == kEmpty ? 0u : 1u + (key >> 31);
         }
-        if (isnew[k]) {
-          if (f != 0) {
-            const uint32_t dob = (f == 3 || (f - 1) == (b & 1)) ? b : b + 1;
-            if (a1 + dob < hl) {
-              hl = a1 + dob;
-              hv = vv[k];
-              hdo = dob;
-            }
+        if (f != 0) {
+          // opposite side idle: the hit has its frontier depth; in lockstep
+          // its parity says frontier depth or the one being claimed now
+          const uint32_t dob = (!both || f == 3 || (f - 1) == (bo & 1)) ? bo : bo + 1;
+          if (a + dob < hl) {
+            hl = a + dob;
+            hv = vv[k];
+            hd = sd[k] ? dob | (a << 16) : a | (dob << 16);  // (side-0 depth, side-1 depth)
           }
         }
       }
       if constexpr (kStamp) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        sp3 = stamp();
+        sp2 = stamp();
       }
       unsigned long long hm = __ballot(hl != kEmpty);
       while (hm) {  // rare: only in the meeting round
         const int l = __ffsll((long long)hm) - 1;
         hm &= hm - 1;
         const uint32_t len = __builtin_amdgcn_readlane(hl, l);
-        if (len < w.mlen) {
-          w.mlen = len;
-          w.mv = __builtin_amdgcn_readlane(hv, l);
-          w.md_other = __builtin_amdgcn_readlane(hdo, l);
+        if (len < out.mlen) {
+          out.mlen = len;
+          out.mv = __builtin_amdgcn_readlane(hv, l);
+          const uint32_t dd = __builtin_amdgcn_readlane(hd, l);
+          out.m0 = dd & 0xffffu;
+          out.m1 = dd >> 16;
         }
       }
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         const unsigned long long mask = __ballot(isnew[k]);
-        if (!mask) continue;
+        if (!mask) continue;  // wave-uniform
+        const unsigned long long m1 = __ballot(isnew[k] && sd[k]);  // side-1 lanes: the upper ones
         const OffT d = isnew[k] ? oe[k] - ob[k] : (OffT)0;
         const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
         const uint32_t incl = wave_incl_scan(dc);
-        const uint32_t eb = w.necl + incl - dc;
+        const uint32_t eb = out.necl[0] + out.necl[1] + incl - dc;  // one running prefix
         if (isnew[k]) {
-          const uint32_t idx = w.ncnt + mbcnt64(mask);
-          par[vv[k]] = uu[k];
-          if (me.qend + idx < P.n) que[me.qend + idx] = vv[k];
+          // queue rank within the lane's own side
+          const uint32_t idx = sd[k] ? out.ncnt[1] + mbcnt64(m1) : out.ncnt[0] + mbcnt64(mask);
+          const uint32_t qe = sd[k] ? s1.qend : s0.qend;
+          (sd[k] ? P.b.parent[1] : P.b.parent[0])[vv[k]] = uu[k];
+          if (qe + idx < P.n) (sd[k] ? P.b.queue[1] : P.b.queue[0])[qe + idx] = vv[k];
         }
-        append_records(Rn, isnew[k] && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, vv[k], ob[k]);
-        w.ncnt += (uint32_t)__popcll(mask);
-        w.necl += __builtin_amdgcn_readlane(incl, 63);
+        append_records(Nb, isnew[k] && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, vv[k], ob[k]);
+        // per-side totals: side 0's part of the scan ends at its last lane
+        const uint32_t n1 = (uint32_t)__popcll(m1);
+        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t e1 = __ballot(sd[k]) ? tot - __builtin_amdgcn_readlane(incl, __ffsll((long long)__ballot(sd[k])) - 1) +
+                                                  __builtin_amdgcn_readlane(dc, __ffsll((long long)__ballot(sd[k])) - 1)
+                                            : 0u;
+        out.ncnt[0] += (uint32_t)__popcll(mask) - n1;
+        out.ncnt[1] += n1;
+        out.necl[0] += tot - e1;
+        out.necl[1] += e1;
       }
       if constexpr (kStamp) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const unsigned long long sp4 = stamp();
+        const unsigned long long sp3 = stamp();
         auto c16 = [](unsigned long long d) { return (uint32_t)(d > 0xffff ? 0xffff : d); };
-        w.pad[0] = c16(sp1 - sp0) | (c16(sp2 - sp1) << 16);
-        w.pad[1] = c16(sp3 - sp2) | (c16(sp4 - sp3) << 16);
+        out.pad[0] = c16(sp1 - sp0);
+        out.pad[1] = c16(sp2 - sp1) | (c16(sp3 - sp2) << 16);
       }
     };
-    if (E <= (uint32_t)kWave) run(std::integral_constant<int, 1>{});
-    else run(std::integral_constant<int, kSmallEdges / kWave>{});
-    return w;
-  };
-
-  // fold a round's candidates into the result (identical in both workers)
-  auto take_meet = [&](int q, const WaveLevel& w) {
-    if (w.mlen == kEmpty) return;
-    if (meet == kEmpty || w.mlen < md0 + md1) {
-      meet = w.mv;
-      md0 = q ? w.md_other : w.md_self;
-      md1 = q ? w.md_self : w.md_other;
+    if (ET <= (uint32_t)kWave) {
+      run(std::integral_constant<int, 1>{}, 0u);
+    } else if (ET <= 2u * kWave) {
+      run(std::integral_constant<int, 2>{}, 0u);
+    } else {
+      for (uint32_t base = 0; base < ET; base += kWave * 4) run(std::integral_constant<int, 4>{}, base);
     }
+    return out;
   };
 
   unsigned long long clk0 = 0;
@@ -529,69 +542,41 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
   uint32_t fstatus = kRunning;
   for (;;) {
-    if (wid < 2) {
-      // ---- worker waves: lockstep and single-wave rounds
+    if (wid == 0) {
+      // ---- wave 0 alone: dual-side (lockstep) and single-side rounds while
+      // the frontiers are small; no barrier, the other waves stay parked
       for (;;) {
         if (status != kRunning) break;
         const bool f0 = fits(s0), f1 = fits(s1);
-        const bool small0 = s0.fed <= kSmallEdges, small1 = s1.fed <= kSmallEdges;
         int q;
-        if (P.side_policy == 2) {
-          q = turn;
-        } else if (P.side_policy == 1) {
-          q = s0.cnt <= s1.cnt ? 0 : 1;
-        } else {
-          q = s0.fed <= s1.fed ? 0 : 1;
-        }
-        const bool lock = P.lockstep && small0 && small1 && f0 && f1;
+        if (P.side_policy == 2) q = turn;
+        else if (P.side_policy == 1) q = s0.cnt <= s1.cnt ? 0 : 1;
+        else q = s0.fed <= s1.fed ? 0 : 1;
+        const bool dual = P.lockstep && f0 && f1 && s0.fed + s1.fed <= kDualEdges;
         const bool fq = q ? f1 : f0;
-        const bool smallq = q ? small1 : small0;
-        if (!lock && (!fq || !smallq)) {
+        const unsigned long long eq = q ? s1.fed : s0.fed;
+        if (!dual && (!fq || eq > kSmallEdges)) {
           if (!fq) status = kHandoff;
           break;  // big level (all waves) or hand-off
         }
         unsigned long long ts0 = 0;
         if (kStamp && tid == 0) ts0 = stamp();
-        // expand: both sides (lockstep) or side q only
-        const int mine = wid;  // wave w owns side w
-        const bool work = lock || mine == q;
-        if (work) {
-          const uint32_t nxt = (lock && mine == 1) ? free1 : free0;
-          const WaveLevel w = wave_level(mine, nxt);
-          if (lane == 0) res[rounds & 1][mine] = w;
+        const uint32_t E0 = dual || q == 0 ? (uint32_t)s0.fed : 0u;
+        const uint32_t E1 = dual || q == 1 ? (uint32_t)s1.fed : 0u;
+        const uint32_t nb = free_buf();
+        const Dual w = dual_level(E0, E1, nb);
+        if (w.mlen != kEmpty && (meet == kEmpty || w.mlen < md0 + md1)) {
+          meet = w.mv;
+          md0 = w.m0;
+          md1 = w.m1;
         }
-        // two-wave round barrier through LDS (the hardware barrier would also
-        // release the parked waves)
-        // Only LDS data (records, hash, res) crosses between the two waves, so
-        // the round barrier orders LDS only: a workgroup-scope fence would also
-        // wait for this wave's global parent/queue stores (~1k cycles), which
-        // nobody reads before the final vmcnt(0) + s_barrier.
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        unsigned long long ts_pre = 0, ts_bar = 0;
-        if (kStamp && tid == 0) ts_pre = stamp();
-        if (lane == 0) atomicAdd(&rsync, 1u);
-        const uint32_t target = 2 * (rounds + 1);
-        while (__hip_atomic_load(&rsync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < target)
-          __builtin_amdgcn_s_sleep(0);
-        asm volatile("" ::: "memory");
-        if (kStamp && tid == 0) ts_bar = stamp();
-        const uint32_t rp = rounds & 1;
-        ++rounds;
-        const uint32_t fz0 = free0, fz1 = free1;
-        if (lock) {
-          WaveLevel w0, w1;
-          w0 = res[rp][0];
-          w1 = res[rp][1];
-          take_meet(0, w0);
-          take_meet(1, w1);
-          apply(0, (uint32_t)s0.fed, fz0, uni(w0.ncnt), uni(w0.necl), 1);
-          apply(1, (uint32_t)s1.fed, fz1, uni(w1.ncnt), uni(w1.necl), 1);
+        if (dual) {
+          apply(0, E0, nb, 0u, w.ncnt[0], w.necl[0], 1);
+          apply(1, E1, nb, w.necl[0], w.ncnt[1], w.necl[1], 1);
           if (meet != kEmpty) status = kFound;
           else if (s0.cnt == 0 || s1.cnt == 0) status = kNoPath;
         } else {
-          WaveLevel w = res[rp][q];
-          take_meet(q, w);
-          apply(q, (uint32_t)(q ? s1.fed : s0.fed), fz0, uni(w.ncnt), uni(w.necl), 2);
+          apply(q, q ? E1 : E0, nb, 0u, q ? w.ncnt[1] : w.ncnt[0], q ? w.necl[1] : w.necl[0], 2);  // no runtime index
           if (P.side_policy == 2) turn ^= 1;
           if (meet != kEmpty) status = kFound;
           else if ((q ? s1.cnt : s0.cnt) == 0) status = kNoPath;
@@ -599,15 +584,14 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         if (kStamp && tid == 0 && levels - 1 < P.b.trace_cap) {
           LevelTraceDev& t = P.b.trace[levels - 1];
           t.side = (uint32_t)(stamp() - ts0);
-          t.depth = (uint32_t)(ts_bar - ts_pre);  // wave 0's wait in the round barrier
+          t.depth = 0;
           t.frontier = 0;
-          t.mode = lock ? 1 : 2;
-          const WaveLevel& wl = res[rp][lock ? 0 : q];
-          t.edges = (unsigned long long)wl.pad[0] | ((unsigned long long)wl.pad[1] << 32);
+          t.mode = dual ? 1 : 2;
+          t.edges = (unsigned long long)w.pad[0] | ((unsigned long long)w.pad[1] << 32);
         }
       }
       // publish the plan for a big level (or the end)
-      if (wid == 0 && lane == 0) {
+      if (lane == 0) {
         int q;
         if (P.side_policy == 2) q = turn;
         else if (P.side_policy == 1) q = s0.cnt <= s1.cnt ? 0 : 1;
@@ -618,7 +602,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         p.side = (uint32_t)q;
         p.E = (uint32_t)x.fed;
         p.cur = x.cur;
-        p.nxt = free0;
+        p.off = x.off;
+        p.nxt = free_buf();
         p.qbase = x.qend;
         p.depth_self = (uint32_t)x.depth;
         p.depth_other = (uint32_t)y.depth;
@@ -637,13 +622,13 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     const uint32_t nxt = uni(plan.nxt);
     const uint32_t a1 = uni(plan.depth_self) + 1;
     const uint32_t keybit = (a1 & 1) ? kParity : 0u;
-    const Rec* Rc = R[uni(plan.cur)];
+    const Rec* Rc = &R[uni(plan.cur)][uni(plan.off)];
     Rec* Rn = R[nxt];
     uint32_t* __restrict__ par = so ? P.b.parent[1] : P.b.parent[0];
     uint32_t* __restrict__ que = so ? P.b.queue[1] : P.b.queue[0];
     uint32_t* Hs = H[so];
     const uint32_t* Ho = H[o];
-    const uint32_t slot = bigs & 1;  // double-buffered: both workers read it after B2
+    const uint32_t slot = bigs & 1;  // double-buffered: wave 0 reads it after B2
     auto batch = [&](auto bc, uint32_t base) {
       constexpr int B = decltype(bc)::value;
       uint32_t vv[B], uu[B];
@@ -703,14 +688,14 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     if (kStamp && tid == 0) ts1 = stamp();
     __syncthreads();  // B2: every claim of the big level is in LDS
     if (kStamp && tid == 0) ts2 = stamp();
-    if (wid < 2) {
+    if (wid == 0) {
       const unsigned long long pk = ctr[slot];
       const uint32_t ncnt = uni((uint32_t)(pk >> 32));
       const uint32_t necl = uni((uint32_t)pk);
       const uint32_t mv = uni(meetv[slot]);
-      // the other slot is used by the next big level; both workers read it
-      // (one big level ago) before this point
-      if (wid == 0 && lane == 0) {
+      // the other slot is used by the next big level (wave 0 read it one big
+      // level ago)
+      if (lane == 0) {
         ctr[slot ^ 1] = 0;
         meetv[slot ^ 1] = kEmpty;
       }
@@ -720,7 +705,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         md0 = so ? (uint32_t)y.depth : (uint32_t)x.depth + 1;
         md1 = so ? (uint32_t)x.depth + 1 : (uint32_t)y.depth;
       }
-      apply(so, E, nxt, ncnt, necl, 3);
+      apply(so, E, nxt, 0u, ncnt, necl, 3);
       if (P.side_policy == 2) turn ^= 1;
       if (meet != kEmpty) status = kFound;
       else if (ncnt == 0) status = kNoPath;
@@ -741,7 +726,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     t.discovered = __builtin_amdgcn_s_memrealtime() - rt0;
   }
 
-  // state is valid in waves 0/1; fstatus (from the final plan) in every wave
+  // search state is valid in wave 0; fstatus (from the final plan) in every wave
   HostResult* Rr = P.h.res;
   // Parent stores of every wave must have reached L2 before the walkers'
   // L1-bypassing loads read them.

@@ -8,7 +8,7 @@ for g in "gnp:100000::6 0 99999" "gnp:1000000::2 0 999999"; do
   for rep in 1 2; do
     for d in build/var/*/; do
       v=$(basename $d)
-      r=$(LD_LIBRARY_PATH=$d timeout -k 5 60 ./build/bin/bibfs_hip $g --json --repeat 300) || exit 1
+      r=$(LD_LIBRARY_PATH=$d timeout -k 5 60 ./build/bin/bibfs_hip $g --json --repeat 300 --resident) || exit 1
       echo "$v $g $(echo "$r" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print("hops", d["hops"], "query_ms %.4f search_ms %.4f" % (d["query_ms"], d["search_ms"]))')" >> $out
     done
   done
