@@ -72,8 +72,19 @@ class HipEngine:
             options = make_options(**kw) if kw else _DEFAULT_OPTIONS
         return self._e.search(int(src), int(dst), options)
 
+    def release(self) -> None:
+        """Free the graph and search state on the device."""
+        self._e.release()
+
     # resident query server (no kernel launch per query; see docs/DESIGN.md)
     def set_resident(self, on: bool = True, idle_ms: float = 200.0) -> "HipEngine":
+        """Serve queries from a resident workgroup (no kernel launch per query).
+
+        The server kernel stays on the GPU until ``idle_ms`` pass without a
+        query, so a device-wide synchronize (``torch.cuda.synchronize()``)
+        waits for it: call ``set_resident(False)`` before one (the next query
+        with ``set_resident(True)`` relaunches it).
+        """
         self._e.set_resident(bool(on), float(idle_ms))
         return self
 

@@ -107,7 +107,7 @@ int bibfs_finish(bibfs_ctx* ctx, bibfs_result* out, uint32_t* path, size_t cap) 
 }
 
 int bibfs_free_graph(bibfs_ctx* ctx) {
-  return guarded([&] { ctx->eng.load_edges(bibfs::EdgeList{}); });
+  return guarded([&] { ctx->eng.release(); });  // v4/comp.cu:121-133 cudaFreeGraph
 }
 
 }  // extern "C"

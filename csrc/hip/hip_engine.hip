@@ -532,6 +532,12 @@ void HipBiBfs::set_resident(bool on, double idle_ms) {
 }
 bool HipBiBfs::resident() const { return p_->resident; }
 
+void HipBiBfs::release() {
+  HIP_CHECK(hipSetDevice(p_->device));
+  HIP_CHECK(hipStreamSynchronize(p_->stream));
+  p_->free_graph();
+}
+
 uint32_t HipBiBfs::n() const { return p_->n; }
 uint64_t HipBiBfs::nnz() const { return p_->nnz; }
 uint64_t HipBiBfs::m_input() const { return p_->m_input; }

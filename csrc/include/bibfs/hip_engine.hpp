@@ -43,6 +43,7 @@ class HipBiBfs {
   void generate_gnp(uint32_t n, double p, uint64_t seed);                // on device
   void generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a = 0.57, double b = 0.19,
                      double c = 0.19);                                     // on device
+  void release();                              // free the graph and all search state (HBM)
   uint32_t n() const;
   uint64_t nnz() const;
   uint64_t m_input() const;

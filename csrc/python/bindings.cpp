@@ -222,6 +222,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("device", &HipBiBfs::device)
       .def("search", &HipBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
            py::call_guard<py::gil_scoped_release>())
+      .def("release", &HipBiBfs::release, py::call_guard<py::gil_scoped_release>())
       .def("set_resident", &HipBiBfs::set_resident, py::arg("on"), py::arg("idle_ms") = 200.0,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("resident", &HipBiBfs::resident)
