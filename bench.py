@@ -77,17 +77,25 @@ def main() -> int:
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--no-resident", action="store_true",
                     help="launch one kernel per query instead of the resident query server")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="also measure batched serving: K queries per launch, one CU each (0 = skip)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for the bench's own barriers/reductions (nccl = RCCL; "
+                         "gloo lets several ranks share one GPU for rehearsals)")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev  # one rank per GPU; with gloo, extra ranks may share a GPU
+    torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        if a.dist_backend == "nccl":
+            dist.init_process_group(backend="nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend="gloo")
 
     from bidirectional_bfs_amd.ops import HipEngine
     from bidirectional_bfs_amd.parallel import DistEngine
@@ -100,7 +108,7 @@ def main() -> int:
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -154,13 +162,34 @@ def main() -> int:
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         queries = steps * (1 if a.mode == "partitioned" else world)
+        batched = None
+        if a.batch > 0 and a.mode == "replicated" and hasattr(eng, "search_batch"):
+            # throughput serving: K distinct queries per launch (pairs cycled), steady state
+            park()
+            bp = [pairs[(i * world + rank) % len(pairs)] for i in range(a.batch)]
+            bs = [s for s, _ in bp]
+            bd = [d for _, d in bp]
+            for _ in range(3):
+                eng.search_batch_arrays(bs, bd)
+            barrier()
+            reps = max(3, steps // 40)
+            tb = time.perf_counter()
+            for _ in range(reps):
+                bh, boff, _paths = eng.search_batch_arrays(bs, bd)
+                assert (bh >= 0).all() and (boff[1:] - boff[:-1] == bh + 1).all()
+            barrier()
+            bdt = max_over_ranks(time.perf_counter() - tb)
+            bq = reps * a.batch * world
+            batched = {"batch": a.batch, "launches": reps, "ms_per_batch": bdt * 1e3 / reps,
+                       "us_per_query": bdt * 1e6 / (reps * a.batch), "queries_per_s": bq / bdt,
+                       "gteps": m * bq / bdt / 1e9}
         return {
             "n": n, "m": m, "seed": seed, "wall_s": dt, "ms_per_step": dt * 1e3 / steps,
             "gteps": m * queries / dt / 1e9,
             "gteps_inspected": insp * (1 if a.mode == "partitioned" else world) / dt / 1e9,
             "mean_hops": hops / steps, "device_ms_per_query": dev_ms / steps,
             "build_ms": build_s * 1e3, "end_to_end_first_query_ms": build_s * 1e3 + dt * 1e3 / steps,
-            "queries": queries,
+            "queries": queries, "batched": batched,
         }
 
     head = run_config(a.graph, a.steps, a.warmup)
@@ -199,6 +228,7 @@ def main() -> int:
                 "mean_hops": head["mean_hops"],
                 "graph_build_ms": round(head["build_ms"], 3),
                 "resident_server": a.mode == "replicated" and not a.no_resident,
+                "batched_serving": head["batched"],
                 "extra": extra,
             },
         }

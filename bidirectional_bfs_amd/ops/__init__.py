@@ -72,6 +72,23 @@ class HipEngine:
             options = make_options(**kw) if kw else _DEFAULT_OPTIONS
         return self._e.search(int(src), int(dst), options)
 
+    def search_batch(self, pairs, options: Optional["native.SearchOptions"] = None, **kw):
+        """Answer many queries with one launch, one CU per query (throughput serving)."""
+        if options is None:
+            options = make_options(**kw) if kw else _DEFAULT_OPTIONS
+        src = [int(s) for s, _ in pairs]
+        dst = [int(d) for _, d in pairs]
+        return self._e.search_batch(src, dst, options)
+
+    def search_batch_arrays(self, src, dst, options: Optional["native.SearchOptions"] = None, **kw):
+        """Batched queries with a compact result: (hops[K] (-1 = no path), path offsets[K+1], flat paths)."""
+        import numpy as np
+
+        if options is None:
+            options = make_options(**kw) if kw else _DEFAULT_OPTIONS
+        return self._e.search_batch_arrays(np.asarray(src, dtype=np.uint32), np.asarray(dst, dtype=np.uint32),
+                                           options)
+
     def release(self) -> None:
         """Free the graph and search state on the device."""
         self._e.release()

@@ -167,6 +167,9 @@ size_t lds_bytes(bool wide);
 void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, dev::ServerBox* box,
                 uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
                 unsigned long long idle_ticks, hipStream_t s);
+void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* h_src, uint32_t* h_dst,
+               uint32_t k, uint32_t* d_slots, dev::HostResult* h_res, uint32_t* h_path, uint32_t path_cap,
+               uint32_t seq, hipStream_t s);
 void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
                 hipStream_t s);
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);

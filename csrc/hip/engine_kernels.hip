@@ -122,6 +122,7 @@ struct LdsParams {
   uint32_t* ticket;   // monotonic election word (atomicMax with seq)
   int lockstep;       // allow concurrent two-sided rounds
   OffT nnz_m1;        // last valid CSR index (clamp for record-driven loads)
+  int batch;          // batched search: no hand-off state / device path (the host re-runs those queries)
   launch::SearchBuffers b;
   launch::HostSide h;
 };
@@ -735,14 +736,15 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   if (wid == 0) {
     const uint32_t hops = md0 + md1;
     const uint32_t path_len = status == kFound ? hops + 1 : 0u;
-    const bool path_dev = status == kFound && path_len > P.h.path_cap;
+    const bool path_dev = status == kFound && path_len > P.h.path_cap && !P.batch;
+    const bool path_skip = status == kFound && path_len > P.h.path_cap && P.batch;  // host re-runs it
     // Two lanes walk the two parent chains side by side into LDS (the record
     // buffers are free now); then the whole wave streams the path to the
     // pinned host buffer with write-through stores, 64 entries per instruction.
     uint32_t* pbuf = reinterpret_cast<uint32_t*>(&R[0][0]);
     constexpr uint32_t kPbufCap = sizeof(R) / sizeof(uint32_t);
-    const bool staged = !path_dev && path_len <= kPbufCap;
-    if (status == kFound && tid < 2)
+    const bool staged = !path_dev && !path_skip && path_len <= kPbufCap;
+    if (status == kFound && !path_skip && tid < 2)
       walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1,
                 staged ? pbuf : (path_dev ? P.b.dpath : P.h.path));
     if (staged) {
@@ -751,7 +753,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         __hip_atomic_store(&P.h.path[i], pbuf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (kStamp && tid == 0) e4 = __builtin_amdgcn_s_memtime();
-    if (status == kHandoff && tid == 0) {
+    if (status == kHandoff && tid == 0 && !P.batch) {
       DevState* st = P.b.st;
       st->status = kRunning;
       st->meet = kEmpty;
@@ -784,12 +786,12 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       put(&Rr->depth[0], status == kFound ? (int32_t)md0 : s0.depth);
       put(&Rr->depth[1], status == kFound ? (int32_t)md1 : s1.depth);
       put(&Rr->path_len, path_len);
-      put(&Rr->path_on_device, path_dev ? 1u : 0u);
+      put(&Rr->path_on_device, path_dev ? 1u : path_skip ? 2u : 0u);
       put(&Rr->rt_begin, rt0);
       put(&Rr->rt_end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
   }
-  if (fstatus == kHandoff) {
+  if (fstatus == kHandoff && !P.batch) {
     // Materialise the LDS visited sets as global bitmaps for the grid engine.
     if constexpr (kBm) {
       const uint32_t words = (P.n + 31) >> 5;  // <= kHashSize / 2 per side
@@ -833,6 +835,40 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
 template <typename OffT, bool kStamp, bool kBm>
 __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_bibfs(LdsParams<OffT> P) {
   lds_search_body<OffT, kStamp, kBm>(P, false);
+}
+
+// ---- batched search: block b answers query b with its own parent/queue slot,
+// result slot and pinned path slot (throughput serving: one CU per query,
+// 256 queries in flight on a full MI355X).
+struct BatchArgs {
+  uint32_t* src;             // K (pinned host)
+  uint32_t* dst;             // K (pinned host)
+  uint32_t* slots;           // per slot: parent[2] + queue[2], n words each
+  HostResult* res;           // K pinned results
+  uint32_t* path;            // K pinned path slots of path_cap words
+  uint32_t path_cap;
+  uint32_t seq;
+};
+
+template <typename OffT, bool kBm>
+__global__ __launch_bounds__(kLdsThreads, 1) void k_lds_batch(LdsParams<OffT> P, BatchArgs A) {
+  const uint32_t b = blockIdx.x;
+  LdsParams<OffT> Q = P;
+  // src/dst come straight from the pinned host array (no staging copy)
+  Q.src = min(__hip_atomic_load(&A.src[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), P.n - 1);
+  Q.dst = min(__hip_atomic_load(&A.dst[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM), P.n - 1);
+  Q.seq = A.seq;
+  uint32_t* base = A.slots + (size_t)b * 4 * P.n;
+  Q.b.parent[0] = base;
+  Q.b.parent[1] = base + P.n;
+  Q.b.queue[0] = base + 2 * (size_t)P.n;
+  Q.b.queue[1] = base + 3 * (size_t)P.n;
+  Q.h.res = A.res + b;
+  Q.h.path = A.path + (size_t)b * A.path_cap;
+  Q.h.path_cap = A.path_cap;
+  Q.batch = 1;
+  Q.trace = 0;
+  lds_search_body<OffT, false, kBm>(Q, true);
 }
 
 // ---- resident query server -------------------------------------------------
@@ -1303,7 +1339,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   if (g.row_off32) {
     LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
-                           lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), b, h};
+                           lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
       if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -1314,7 +1350,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
     }
   } else {
     LdsParams<uint64_t> P{g.row_off, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
-                           lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), b, h};
+                           lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     if (trace == 2)
       k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
     else
@@ -1329,11 +1365,25 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, d
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   BIBFS_REQUIRE(g.row_off32 != nullptr, "resident server: 32-bit row offsets required");
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
-                         (uint32_t)(g.nnz ? g.nnz - 1 : 0), b, h};
+                         (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   if (g.n <= kBmMaxN)
     k_lds_server<uint32_t, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
   else
     k_lds_server<uint32_t, false><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
+  HIP_CHECK(hipGetLastError());
+}
+
+void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* d_src, uint32_t* d_dst,
+               uint32_t k, uint32_t* d_slots, dev::HostResult* h_res, uint32_t* h_path, uint32_t path_cap,
+               uint32_t seq, hipStream_t s) {
+  BIBFS_REQUIRE(g.row_off32 != nullptr, "batched search: 32-bit row offsets required");
+  LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, seq, 0, 0, -1, nullptr, 1,
+                         (uint32_t)(g.nnz ? g.nnz - 1 : 0), 1, b, HostSide{h_res, h_path, path_cap}};
+  BatchArgs A{d_src, d_dst, d_slots, h_res, h_path, path_cap, seq};
+  if (g.n <= kBmMaxN)
+    k_lds_batch<uint32_t, true><<<k, kLdsThreads, 0, s>>>(P, A);
+  else
+    k_lds_batch<uint32_t, false><<<k, kLdsThreads, 0, s>>>(P, A);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -56,6 +56,41 @@ struct HipBiBfs::Impl {
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
+  // batched search (k_lds_batch)
+  uint32_t* d_bslots = nullptr;   // per slot parent[2] + queue[2]
+  uint32_t* d_bq = nullptr;       // src[K], dst[K]
+  HostResult* h_bres = nullptr;   // pinned
+  uint32_t* h_bpath = nullptr;    // pinned, K * kBatchPath
+  uint32_t* h_bq = nullptr;       // pinned staging for src/dst
+  uint32_t bcap = 0;              // slots allocated
+  static constexpr uint32_t kBatchPath = 4096;
+
+  void free_batch() {
+    if (d_bslots) HIP_CHECK(hipFree(d_bslots));
+    if (d_bq) HIP_CHECK(hipFree(d_bq));
+    if (h_bres) HIP_CHECK(hipHostFree(h_bres));
+    if (h_bpath) HIP_CHECK(hipHostFree(h_bpath));
+    if (h_bq) HIP_CHECK(hipHostFree(h_bq));
+    d_bslots = d_bq = nullptr;
+    h_bres = nullptr;
+    h_bpath = h_bq = nullptr;
+    bcap = 0;
+  }
+
+  void ensure_batch(uint32_t k) {
+    if (k <= bcap) return;
+    free_batch();
+    HIP_CHECK(hipMalloc(&d_bslots, (size_t)k * 4 * n * sizeof(uint32_t)));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_bres), (size_t)k * sizeof(HostResult),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_bpath), (size_t)k * kBatchPath * sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_bq), (size_t)k * 2 * sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent));  // read by the kernel directly
+    std::memset(h_bres, 0, (size_t)k * sizeof(HostResult));
+    bcap = k;
+  }
+
   // resident server (k_lds_server)
   hipStream_t sstream = nullptr;
   ServerBox* h_box = nullptr;
@@ -151,6 +186,7 @@ struct HipBiBfs::Impl {
 
   void free_graph() {
     stop_server();
+    free_batch();
     if (d_row_off) HIP_CHECK(hipFree(d_row_off));
     if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
     if (d_col) HIP_CHECK(hipFree(d_col));
@@ -531,6 +567,74 @@ void HipBiBfs::set_resident(bool on, double idle_ms) {
   I.srv_idle_ticks = (unsigned long long)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
 }
 bool HipBiBfs::resident() const { return p_->resident; }
+
+std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, const std::vector<vid_t>& dst,
+                                                 const SearchOptions& opt) {
+  auto& I = *p_;
+  BIBFS_REQUIRE(src.size() == dst.size(), "search_batch: src and dst sizes differ");
+  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
+  HIP_CHECK(hipSetDevice(I.device));
+  const size_t K = src.size();
+  std::vector<SearchResult> out(K);
+  if (K == 0) return out;
+  for (size_t i = 0; i < K; ++i) BIBFS_REQUIRE(src[i] < I.n && dst[i] < I.n, "src/dst out of range");
+  if (opt.force_grid || opt.trace || !I.server_usable()) {  // the batch kernel is the LDS engine only
+    for (size_t i = 0; i < K; ++i) out[i] = search(src[i], dst[i], opt);
+    return out;
+  }
+  // slots: up to 1024 per launch, and at most ~8 GiB of per-slot state
+  const uint64_t per_slot = 16ull * I.n;
+  const uint32_t kmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (8ull << 30) / per_slot));
+  for (size_t c0 = 0; c0 < K; c0 += kmax) {
+    const uint32_t k = (uint32_t)std::min<size_t>(kmax, K - c0);
+    const auto t0 = std::chrono::steady_clock::now();
+    I.ensure_batch(k);
+    std::memcpy(I.h_bq, src.data() + c0, k * 4);
+    std::memcpy(I.h_bq + k, dst.data() + c0, k * 4);
+    const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
+    launch::lds_batch(I.view(), I.buf, I.h_bq, I.h_bq + k, k, I.d_bslots, I.h_bres, I.h_bpath, Impl::kBatchPath,
+                      seq, I.stream);
+    for (uint32_t i = 0; i < k; ++i) {
+      for (uint64_t it = 1; __atomic_load_n(&I.h_bres[i].seq, __ATOMIC_ACQUIRE) != seq; ++it) {
+        if ((it & 8191) == 0) {
+          const hipError_t e = hipStreamQuery(I.stream);
+          if (e == hipSuccess && __atomic_load_n(&I.h_bres[i].seq, __ATOMIC_ACQUIRE) != seq)
+            throw Error("bibfs: batched search finished without publishing every result");
+          if (e != hipSuccess && e != hipErrorNotReady)
+            throw Error(std::string("bibfs: batched search failed: ") + hipGetErrorString(e));
+        } else {
+          _mm_pause();
+        }
+      }
+    }
+    const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    for (uint32_t i = 0; i < k; ++i) {
+      const HostResult& R = I.h_bres[i];
+      SearchResult& r = out[c0 + i];
+      const vid_t s = src[c0 + i], d = dst[c0 + i];
+      if (s == d) {
+        r = search(s, d, opt);
+        continue;
+      }
+      if (R.status == kHandoff || R.path_on_device == 2 || (R.status != kFound && R.status != kNoPath)) {
+        r = search(s, d, opt);  // frontier outgrew LDS / path longer than the slot: single-query engines
+        continue;
+      }
+      r.found = R.status == kFound;
+      r.hops = r.found ? R.hops : -1;
+      r.meet = r.found ? R.meet : kNoVertex;
+      r.stats.levels = (int)R.levels;
+      r.stats.edges_inspected = R.einsp;
+      r.stats.visited = R.visited;
+      if (r.found && opt.want_path) r.path.assign(I.h_bpath + (size_t)i * Impl::kBatchPath,
+                                                  I.h_bpath + (size_t)i * Impl::kBatchPath + R.path_len);
+      r.search_ms = (double)(R.rt_end - R.rt_begin) * 1e-5;
+      r.total_ms = wall;  // the whole batch's wall time
+    }
+  }
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  return out;
+}
 
 void HipBiBfs::release() {
   HIP_CHECK(hipSetDevice(p_->device));

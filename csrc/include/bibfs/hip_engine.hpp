@@ -53,6 +53,13 @@ class HipBiBfs {
   // --- search ---------------------------------------------------------------
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
 
+  // Throughput serving: answer K queries with one launch, one workgroup (one
+  // CU) per query, up to 256 in flight.  Same results as K search() calls
+  // (queries whose frontier outgrows LDS, or whose path is longer than the
+  // batch path slot, are re-run through search()).
+  std::vector<SearchResult> search_batch(const std::vector<vid_t>& src, const std::vector<vid_t>& dst,
+                                         const SearchOptions& opt = {});
+
   // Resident query server: one workgroup stays on the GPU and takes queries
   // from a pinned mailbox, so a query costs no kernel launch.  It exits by
   // itself after `idle_ms` without a query (and is relaunched on demand),

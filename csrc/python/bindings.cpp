@@ -223,6 +223,38 @@ PYBIND11_MODULE(_native, m) {
       .def("search", &HipBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
            py::call_guard<py::gil_scoped_release>())
       .def("release", &HipBiBfs::release, py::call_guard<py::gil_scoped_release>())
+      .def("search_batch", &HipBiBfs::search_batch, py::arg("src"), py::arg("dst"),
+           py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "search_batch_arrays",
+          [](HipBiBfs& e, py::array_t<uint32_t, py::array::c_style | py::array::forcecast> src,
+             py::array_t<uint32_t, py::array::c_style | py::array::forcecast> dst, const SearchOptions& opt) {
+            std::vector<vid_t> s(src.data(), src.data() + src.size()), d(dst.data(), dst.data() + dst.size());
+            std::vector<SearchResult> rs;
+            {
+              py::gil_scoped_release rel;
+              rs = e.search_batch(s, d, opt);
+            }
+            // compact result: hops (-1 = no path), CSR-style paths (offsets + flat vertex list)
+            py::array_t<int64_t> hops(rs.size());
+            py::array_t<int64_t> off(rs.size() + 1);
+            size_t total = 0;
+            for (auto& r : rs) total += r.path.size();
+            py::array_t<uint32_t> flat(total);
+            auto h = hops.mutable_unchecked<1>();
+            auto o = off.mutable_unchecked<1>();
+            uint32_t* f = flat.mutable_data();
+            size_t pos = 0;
+            for (size_t i = 0; i < rs.size(); ++i) {
+              h(i) = rs[i].hops;
+              o(i) = (int64_t)pos;
+              std::memcpy(f + pos, rs[i].path.data(), rs[i].path.size() * 4);
+              pos += rs[i].path.size();
+            }
+            o(rs.size()) = (int64_t)pos;
+            return py::make_tuple(hops, off, flat);
+          },
+          py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{})
       .def("set_resident", &HipBiBfs::set_resident, py::arg("on"), py::arg("idle_ms") = 200.0,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("resident", &HipBiBfs::resident)

@@ -110,6 +110,31 @@ int main(int argc, char** argv) {
       check_searches(eng, host, 40, 18, o, "lds-resident");
       check_searches(eng, host, 5, 19, nl, "lds-resident-nolock");
       eng.set_resident(false);
+      {  // batched: one workgroup per query
+        std::mt19937_64 rng(23);
+        std::vector<vid_t> bs, bd;
+        for (int q = 0; q < 300; ++q) {
+          bs.push_back(q == 0 ? 0 : (vid_t)(rng() % host.n));
+          bd.push_back(q == 0 ? host.n - 1 : (vid_t)(rng() % host.n));
+        }
+        const double tb = cli::now_s();
+        auto rs = eng.search_batch(bs, bd, o);
+        const double dt = (cli::now_s() - tb) * 1e3;
+        int bad = 0;
+        for (size_t q = 0; q < rs.size(); ++q) {
+          auto orc = bfs_oracle(host, bs[q], bd[q]);
+          std::string why;
+          bool ok = orc.hops == rs[q].hops &&
+                    (!rs[q].found || validate_path(host, bs[q], bd[q], rs[q].hops, rs[q].path, &why));
+          if (!ok && bad < 5)
+            std::printf("  [lds-batch] query %u->%u: oracle %lld got %lld %s\n", bs[q], bd[q],
+                        (long long)orc.hops, (long long)rs[q].hops, why.c_str());
+          bad += !ok;
+        }
+        std::printf("  [lds-batch] %d/%zu queries correct, %.3f ms for the batch (%.1f us/query)\n",
+                    (int)rs.size() - bad, rs.size(), dt, dt * 1e3 / rs.size());
+        CHECK(bad == 0, "lds-batch: %d wrong answers", bad);
+      }
       SearchOptions g;
       g.force_grid = true;
       check_searches(eng, host, 20, 12, g, "grid-auto");
