@@ -172,10 +172,12 @@ void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* h_src, uint
                uint32_t seq, hipStream_t s);
 void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
                 hipStream_t s);
-void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
+void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
+                  hipStream_t s);
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
 void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);
-void finish_level(const SearchBuffers& b, int side, int mode, int trace, hipStream_t s);
+void finish_level(const SearchBuffers& b, int side, int mode, int trace, dev::DevState* mirror, uint32_t seq,
+                  hipStream_t s);
 void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
                uint32_t n, hipStream_t s);

@@ -22,6 +22,9 @@
 //     Beamer direction switch driven by the host.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstddef>
+
 #include <type_traits>
 
 #include "device.hpp"
@@ -1197,8 +1200,30 @@ __global__ void k_frontier_bits(launch::SearchBuffers b, int s) {
 }
 
 // Single-thread level bookkeeping (avoids a host round trip for state updates).
-__global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int trace) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__device__ void k_finish_level_body(launch::SearchBuffers b, int s, int mode, int trace, DevState& out);
+
+// Copy a DevState into the pinned host mirror: one write-through store per
+// lane (one wide PCIe write instead of ~30 serial ones), drained, then `seq`.
+__device__ void publish_state(const DevState& v, DevState* mirror, uint32_t seq, uint32_t lane) {
+  constexpr uint32_t kWords = (uint32_t)(offsetof(DevState, pad) / sizeof(uint32_t));
+  static_assert(kWords <= 64, "one lane per word");
+  if (lane < kWords)
+    __hip_atomic_store(&reinterpret_cast<uint32_t*>(mirror)[lane], reinterpret_cast<const uint32_t*>(&v)[lane],
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_store(&mirror->pad[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int trace, DevState* mirror,
+                               uint32_t seq) {
+  __shared__ DevState sv;
+  if (blockIdx.x != 0) return;
+  if (threadIdx.x == 0) k_finish_level_body(b, s, mode, trace, sv);
+  __syncthreads();
+  if (mirror && threadIdx.x < 64) publish_state(sv, mirror, seq, threadIdx.x);
+}
+
+__device__ void k_finish_level_body(launch::SearchBuffers b, int s, int mode, int trace, DevState& out) {
   DevState* st = b.st;
   const uint32_t ncnt = st->qtail[s] - st->fend[s];
   if (trace && st->levels < b.trace_cap) {
@@ -1227,6 +1252,7 @@ __global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int tra
   st->chunk = 0;
   st->hub_count = 0;
   st->hub_edge_cursor = 0;
+  out = *st;
 }
 
 // Seed a search for the grid engine / step-wise API.
@@ -1396,16 +1422,23 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
   HIP_CHECK(hipGetLastError());
 }
 
-void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s) {
-  const unsigned blocks = (unsigned)(cus * 4);  // 4 x 256-thread blocks per CU, dynamic chunks
+void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
+                  hipStream_t s) {
+  // Dynamic chunks of 256 frontier vertices; never more blocks than chunks:
+  // every block takes at least one ticket from ONE counter, and 1024 blocks
+  // contending on it cost ~12 us even for a 3-vertex frontier.  Hubs: one
+  // block per deferred vertex at most.
+  const uint64_t chunks = (frontier + kGridThreads - 1) / kGridThreads;
+  const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, chunks));
+  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier));
   if (g.row_off32) {
     auto P = gp<uint32_t>(g, b, side);
     k_grid_topdown<uint32_t><<<blocks, kGridThreads, 0, s>>>(P);
-    k_grid_hubs<uint32_t><<<blocks, kGridThreads, 0, s>>>(P);
+    k_grid_hubs<uint32_t><<<hblocks, kGridThreads, 0, s>>>(P);
   } else {
     auto P = gp<uint64_t>(g, b, side);
     k_grid_topdown<uint64_t><<<blocks, kGridThreads, 0, s>>>(P);
-    k_grid_hubs<uint64_t><<<blocks, kGridThreads, 0, s>>>(P);
+    k_grid_hubs<uint64_t><<<hblocks, kGridThreads, 0, s>>>(P);
   }
   HIP_CHECK(hipGetLastError());
 }
@@ -1433,8 +1466,9 @@ void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, h
   HIP_CHECK(hipGetLastError());
 }
 
-void finish_level(const SearchBuffers& b, int side, int mode, int trace, hipStream_t s) {
-  k_finish_level<<<1, 64, 0, s>>>(b, side, mode, trace);
+void finish_level(const SearchBuffers& b, int side, int mode, int trace, DevState* mirror, uint32_t seq,
+                  hipStream_t s) {
+  k_finish_level<<<1, 64, 0, s>>>(b, side, mode, trace, mirror, seq);
   HIP_CHECK(hipGetLastError());
 }
 

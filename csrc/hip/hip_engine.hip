@@ -314,6 +314,23 @@ struct HipBiBfs::Impl {
     }
   }
 
+  uint32_t level_seq = 0;  // k_finish_level publishes DevState into pinned h_state with this seq
+
+  // wait for the pinned DevState mirror of the last finished level
+  void wait_level() {
+    for (uint64_t it = 1; __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != level_seq; ++it) {
+      if ((it & 8191) == 0) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess && __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != level_seq)
+          throw Error("bibfs: grid level finished without publishing its state");
+        if (e != hipSuccess && e != hipErrorNotReady)
+          throw Error(std::string("bibfs: grid level failed: ") + hipGetErrorString(e));
+      } else {
+        _mm_pause();
+      }
+    }
+  }
+
   void sync_state() {
     HIP_CHECK(hipMemcpyAsync(h_state, buf.st, sizeof(DevState), hipMemcpyDeviceToHost, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -328,10 +345,11 @@ struct HipBiBfs::Impl {
       std::swap(buf.fbits[s], buf.nbits[s]);
       fbits_valid[s] = true;
     } else {
-      launch::grid_topdown(g, buf, s, cus, stream);
+      launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), stream);
       fbits_valid[s] = false;
     }
-    launch::finish_level(buf, s, mode, trace, stream);
+    const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
+    launch::finish_level(buf, s, mode, trace, h_state, ls, stream);
   }
 
   int choose_mode(int s, const SearchOptions& opt) {
@@ -365,7 +383,8 @@ struct HipBiBfs::Impl {
     int turn = 0;
     const int trace = opt.trace ? 1 : 0;
     for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
-      sync_state();
+      if (guard == 0) sync_state();  // state left by the seed / the LDS hand-off
+      else wait_level();             // pinned mirror of the level just finished
       if (h_state->status != kRunning || h_state->meet != kEmpty) break;
       const int s = choose_side(opt, turn);
       const int mode = choose_mode(s, opt);
@@ -450,7 +469,7 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_path), (size_t)p_->h_path_cap * 4,
                           hipHostMallocMapped | hipHostMallocCoherent));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_state), sizeof(DevState),
-                          hipHostMallocDefault));
+                          hipHostMallocMapped | hipHostMallocCoherent));  // k_finish_level writes it
   std::memset(p_->h_res, 0, sizeof(HostResult));
   HIP_CHECK(hipEventCreate(&p_->ev0));
   HIP_CHECK(hipEventCreate(&p_->ev1));
