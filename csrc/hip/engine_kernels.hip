@@ -88,6 +88,7 @@ constexpr int kBatch = 4;                           // edges per thread per roun
 #endif
 constexpr uint32_t kSmallEdges = BIBFS_KNOB_SMALL_EDGES;  // a level this small runs on one wave
 constexpr uint32_t kDualEdges = BIBFS_KNOB_DUAL_EDGES;    // both sides together this small: one lockstep round
+constexpr uint32_t kDualBigEdges = 4096;                  // balanced sides up to this many edges: lockstep big level
 constexpr uint32_t kDegClamp = 65535;               // per-lane edge contribution to the packed counter
 constexpr uint32_t kParity = 0x80000000u;           // depth-parity bit of a hash key
 constexpr uint32_t kIdMask = 0x7fffffffu;
@@ -224,8 +225,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 
 
 // Published by wave 0 for the parked waves: the big level to run (or the end).
+// Published by wave 0 for the parked waves: the big level to run (or the end).
+// E[q] = records of side q to expand (0 = side q idle this level).
 struct LevelPlan {
-  uint32_t status, side, E, cur, off, nxt, qbase, depth_self, depth_other;
+  uint32_t status;
+  uint32_t E[2], cur[2], off[2], nxt[2], qbase[2], depth[2];
 };
 
 // One whole search by one workgroup.  `elected`: the caller already owns the
@@ -236,8 +240,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   constexpr uint32_t CAP = LdsRec<OffT>::cap;
   __shared__ uint32_t H[2][kHashSize];
   __shared__ Rec R[4][CAP];
-  __shared__ unsigned long long ctr[2];  // big levels: (count << 32) | clamped edge sum
-  __shared__ uint32_t meetv[2];          // big levels: a meet vertex of the level
+  __shared__ unsigned long long ctr[2][2];  // big levels [slot][side]: (count << 32) | clamped edge sum
+  __shared__ unsigned long long meetk[2];   // big levels [slot]: min (len << 32 | side << 31 | vertex)
   __shared__ LevelPlan plan;
   __shared__ uint32_t won;
   __shared__ Rec junk[kWave];            // record writes of finished lanes land here (no divergence)
@@ -296,10 +300,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) Hflat[i] = kBm ? 0u : kEmpty;
   // side q's bitmap view of the same LDS (kBm)
   auto W = [&](int q) { return reinterpret_cast<unsigned long long*>(q ? H[1] : H[0]); };
-  if (tid < 2) {
-    ctr[tid] = 0;
-    meetv[tid] = kEmpty;
-  }
+  if (tid < 4) ctr[tid >> 1][tid & 1] = 0;
+  if (tid < 2) meetk[tid] = ~0ull;
 
   // ---- replicated search state: identical in waves 0 and 1 (the workers);
   // two structs selected field-wise (a struct-level `?:` or an array indexed
@@ -541,6 +543,139 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     return out;
   };
 
+  // ---- lean lockstep rounds (bitmap mode, both sides together <= 64 edges):
+  // the common early phase of a query, written for a short instruction
+  // stream -- one edge per lane, both sides' records read from and written to
+  // one buffer each round, the state held in a few scalars and written back
+  // to s0/s1 when the phase ends (round too big, meet, dead side, overflow).
+  auto lean_rounds = [&]() {
+    uint32_t E0 = (uint32_t)s0.fed, E1 = (uint32_t)s1.fed;
+    const Rec* rp0 = &R[s0.cur][s0.off];
+    const Rec* rp1 = &R[s1.cur][s1.off];
+    uint32_t d0 = (uint32_t)s0.depth, d1 = (uint32_t)s1.depth;
+    uint32_t qe0 = s0.qend, qe1 = s1.qend, c0 = s0.cnt, c1 = s1.cnt, h0 = s0.hcnt, h1 = s1.hcnt;
+    unsigned long long v0 = s0.ved, v1 = s1.ved;
+    uint32_t nb = free_buf(), cb = kEmpty;
+    uint32_t rounds_done = 0;
+    bool ovf = false;
+    uint32_t* const par0 = P.b.parent[0];
+    uint32_t* const par1 = P.b.parent[1];
+    uint32_t* const que0 = P.b.queue[0];
+    uint32_t* const que1 = P.b.queue[1];
+    unsigned long long* const W0 = W(0);
+    unsigned long long* const W1 = W(1);
+    for (;;) {
+      const uint32_t ET = E0 + E1;
+      if (ET > (uint32_t)kWave || E0 == 0 || E1 == 0 || status != kRunning || ovf) break;
+      unsigned long long lt0 = 0;
+      if constexpr (kStamp) lt0 = stamp();
+      Rec* Nb = R[nb];
+      const uint32_t e = lane;
+      const bool ok = e < ET;
+      const bool sd = e >= E0;
+      const Rec r = sd ? rp1[ok ? e - E0 : 0u] : rp0[e];
+      const uint32_t u = r.x;
+      const OffT k = min(rec_k(r), P.nnz_m1);
+      uint32_t v;
+      OffT ob, oe;
+      if (P.padj) {
+        const uint4 pq = P.padj[k];
+        v = pq.x;
+        ob = (OffT)((uint64_t)pq.z | ((uint64_t)pq.w << 32));
+        oe = ob + (OffT)pq.y;
+      } else {
+        v = P.col[k];
+        ob = P.row_off[v];
+        oe = P.row_off[v + 1];
+      }
+      const uint32_t a = (sd ? d1 : d0) + 1;
+      const uint32_t bit = v & 31u;
+      const unsigned long long old = atomicOr(&(sd ? W1 : W0)[v >> 5], 1ull << (bit + ((a & 1u) << 5)));
+      const bool isnew = ok && ((old >> bit) & 0x100000001ull) == 0;
+      uint32_t hl = kEmpty, hv = 0, hd = 0;
+      if (isnew) {
+        const unsigned long long w = (sd ? W0 : W1)[v >> 5];
+        const uint32_t f = (uint32_t)((w >> bit) & 1ull) | ((uint32_t)((w >> (32 + bit)) & 1ull) << 1);
+        if (f != 0) {
+          const uint32_t bo = sd ? d0 : d1;
+          const uint32_t dob = (f == 3 || (f - 1) == (bo & 1u)) ? bo : bo + 1;
+          hl = a + dob;
+          hv = v;
+          hd = sd ? dob | (a << 16) : a | (dob << 16);
+        }
+      }
+      unsigned long long hm = __ballot(hl != kEmpty);
+      while (hm) {  // the meeting round only
+        const int l = __ffsll((long long)hm) - 1;
+        hm &= hm - 1;
+        const uint32_t len = __builtin_amdgcn_readlane(hl, l);
+        if (meet == kEmpty || len < md0 + md1) {
+          meet = __builtin_amdgcn_readlane(hv, l);
+          const uint32_t dd = __builtin_amdgcn_readlane(hd, l);
+          md0 = dd & 0xffffu;
+          md1 = dd >> 16;
+        }
+      }
+      const unsigned long long mask = __ballot(isnew);
+      const unsigned long long m1 = __ballot(isnew && sd);
+      uint32_t l0 = 0, l1 = 0;
+      if (mask) {
+        const OffT d = isnew ? oe - ob : (OffT)0;
+        const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
+        const uint32_t incl = wave_incl_scan(dc);
+        const uint32_t eb = incl - dc;
+        if (isnew) {
+          if (sd) {
+            par1[v] = u;
+            const uint32_t i = qe1 + mbcnt64(m1);
+            if (i < P.n) que1[i] = v;
+          } else {
+            par0[v] = u;
+            const uint32_t i = qe0 + mbcnt64(mask);
+            if (i < P.n) que0[i] = v;
+          }
+        }
+        append_records(Nb, isnew && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, v, ob);
+        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+        l0 = __builtin_amdgcn_readlane(incl, E0 - 1);  // side-0 lanes are [0, E0)
+        l1 = tot - l0;
+      }
+      const uint32_t n1 = (uint32_t)__popcll(m1), n0 = (uint32_t)__popcll(mask) - n1;
+      if constexpr (kStamp) {
+        if (lane == 0 && levels + 1 < P.b.trace_cap) {
+          LevelTraceDev& t = P.b.trace[levels + 1];
+          t.side = (uint32_t)(stamp() - lt0);
+          t.depth = t.frontier = 0;
+          t.mode = 6;
+          t.edges = ET;
+        }
+      }
+      levels += 2;
+      einsp += ET;
+      ++rounds_done;
+      ++d0, ++d1;
+      qe0 += n0, qe1 += n1;
+      h0 += n0, h1 += n1;
+      c0 = n0, c1 = n1;
+      v0 += l0, v1 += l1;
+      ovf = (unsigned long long)l0 + l1 > CAP;
+      E0 = l0, E1 = l1;
+      rp0 = Nb;
+      rp1 = Nb + l0;
+      cb = nb;
+      if (meet != kEmpty) status = kFound;
+      else if (n0 == 0 || n1 == 0) status = kNoPath;
+      // next output: the buffer no side reads any more (the old current ones are free)
+      nb = (uint32_t)__builtin_ctz(~(1u << cb) & 0xfu);
+    }
+    if (rounds_done == 0) return false;
+    s0.cur = cb, s0.off = 0, s0.fed = E0, s0.depth = (int)d0, s0.fbeg = qe0 - c0, s0.qend = qe0;
+    s0.cnt = c0, s0.hcnt = h0, s0.ved = v0, s0.ovf = E0 > CAP ? 1u : 0u;
+    s1.cur = cb, s1.off = E0, s1.fed = E1, s1.depth = (int)d1, s1.fbeg = qe1 - c1, s1.qend = qe1;
+    s1.cnt = c1, s1.hcnt = h1, s1.ved = v1, s1.ovf = (unsigned long long)E0 + E1 > CAP ? 1u : 0u;
+    return true;
+  };
+
   unsigned long long clk0 = 0;
   const unsigned long long rt0 = tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
@@ -562,6 +697,11 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         if (!dual && (!fq || eq > kSmallEdges)) {
           if (!fq) status = kHandoff;
           break;  // big level (all waves) or hand-off
+        }
+        if constexpr (kBm) {
+          if (dual && (!P.trace || kStamp) && s0.fed + s1.fed <= (unsigned long long)kWave && s0.fed && s1.fed &&
+              lean_rounds())
+            continue;  // state written back; re-decide
         }
         unsigned long long ts0 = 0;
         if (kStamp && tid == 0) ts0 = stamp();
@@ -594,23 +734,29 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           t.edges = (unsigned long long)w.pad[0] | ((unsigned long long)w.pad[1] << 32);
         }
       }
-      // publish the plan for a big level (or the end)
+      // publish the plan for a big level (or the end): both sides in lockstep
+      // while both fit and are balanced (one pass of 1024 lanes, or within 2x),
+      // else the policy's side
       if (lane == 0) {
         int q;
         if (P.side_policy == 2) q = turn;
         else if (P.side_policy == 1) q = s0.cnt <= s1.cnt ? 0 : 1;
         else q = s0.fed <= s1.fed ? 0 : 1;
-        const SideState x = sel(q, s0, s1), y = sel(q, s1, s0);
+        const unsigned long long lo = min(s0.fed, s1.fed), hi = max(s0.fed, s1.fed);
+        const bool both = P.lockstep && fits(s0) && fits(s1) &&
+                          (lo + hi <= (unsigned long long)kLdsThreads || (hi <= 2 * lo && lo + hi <= kDualBigEdges));
         LevelPlan p;
         p.status = status;
-        p.side = (uint32_t)q;
-        p.E = (uint32_t)x.fed;
-        p.cur = x.cur;
-        p.off = x.off;
-        p.nxt = free_buf();
-        p.qbase = x.qend;
-        p.depth_self = (uint32_t)x.depth;
-        p.depth_other = (uint32_t)y.depth;
+        const uint32_t fa = free_buf();
+        const uint32_t fb = (uint32_t)__builtin_ctz(~((1u << s0.cur) | (1u << s1.cur) | (1u << fa)) & 0xfu);
+        p.E[0] = both || q == 0 ? (uint32_t)s0.fed : 0u;
+        p.E[1] = both || q == 1 ? (uint32_t)s1.fed : 0u;
+        p.cur[0] = s0.cur, p.cur[1] = s1.cur;
+        p.off[0] = s0.off, p.off[1] = s1.off;
+        p.nxt[0] = fa;
+        p.nxt[1] = both ? fb : fa;
+        p.qbase[0] = s0.qend, p.qbase[1] = s1.qend;
+        p.depth[0] = (uint32_t)s0.depth, p.depth[1] = (uint32_t)s1.depth;
         plan = p;
       }
     }
@@ -619,100 +765,125 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     if (kStamp && tid == 0) ts0 = stamp();
     fstatus = uni(plan.status);
     if (fstatus != kRunning) break;
-    // ---- big level: every wave, one edge per lane, LDS counters for the appends
-    const int so = (int)uni(plan.side), o = so ^ 1;
-    const uint32_t E = uni(plan.E);
-    const uint32_t qbase = uni(plan.qbase);
-    const uint32_t nxt = uni(plan.nxt);
-    const uint32_t a1 = uni(plan.depth_self) + 1;
-    const uint32_t keybit = (a1 & 1) ? kParity : 0u;
-    const Rec* Rc = &R[uni(plan.cur)][uni(plan.off)];
-    Rec* Rn = R[nxt];
-    uint32_t* __restrict__ par = so ? P.b.parent[1] : P.b.parent[0];
-    uint32_t* __restrict__ que = so ? P.b.queue[1] : P.b.queue[0];
-    uint32_t* Hs = H[so];
-    const uint32_t* Ho = H[o];
+    // ---- big level: every wave, one edge per lane; side 0's records then side
+    // 1's (virtual list as in dual_level); per-side LDS counters place the
+    // appends, one packed atomicMin keeps the shortest meet candidate
+    const uint32_t E0 = uni(plan.E[0]), E1 = uni(plan.E[1]);
+    const uint32_t ET = E0 + E1;
+    const bool bboth = E0 != 0 && E1 != 0;
+    const uint32_t bd0 = uni(plan.depth[0]), bd1 = uni(plan.depth[1]);
+    const uint32_t qb0 = uni(plan.qbase[0]), qb1 = uni(plan.qbase[1]);
+    const Rec* Rc0 = &R[uni(plan.cur[0])][uni(plan.off[0])];
+    const Rec* Rc1 = &R[uni(plan.cur[1])][uni(plan.off[1])];
+    Rec* Rn0 = R[uni(plan.nxt[0])];
+    Rec* Rn1 = R[uni(plan.nxt[1])];
     const uint32_t slot = bigs & 1;  // double-buffered: wave 0 reads it after B2
     auto batch = [&](auto bc, uint32_t base) {
       constexpr int B = decltype(bc)::value;
       uint32_t vv[B], uu[B];
       OffT ob[B], oe[B];
-      bool ok[B];
+      bool ok[B], sd[B];
       OffT kk[B];
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         const uint32_t e = base + k * kLdsThreads + tid;
-        ok[k] = e < E;
-        const Rec r = Rc[ok[k] ? e : 0u];
+        ok[k] = e < ET;
+        sd[k] = e >= E0;
+        const uint32_t i = ok[k] ? (sd[k] ? e - E0 : e) : 0u;
+        const Rec r = sd[k] ? Rc1[i] : Rc0[i];
         uu[k] = r.x;
         kk[k] = min(rec_k(r), P.nnz_m1);
       }
       fetch_edges(bc, kk, vv, ob, oe);
       bool isnew[B];
+      unsigned long long best = ~0ull;
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        // the other side is idle during a big level: any hit has its current depth
+        const uint32_t a = (sd[k] ? bd1 : bd0) + 1;
+        const uint32_t bo = sd[k] ? bd0 : bd1;
+        uint32_t f;
         if constexpr (kBm) {
-          isnew[k] = ok[k] && bm_claim(W(so), vv[k], a1 & 1);
-          if (isnew[k] && bm_state(W(o), vv[k]) != 0) meetv[slot] = vv[k];
+          isnew[k] = ok[k] && bm_claim(W(sd[k]), vv[k], a & 1);
+          f = isnew[k] ? bm_state(W(!sd[k]), vv[k]) : 0u;
         } else {
-          isnew[k] = ok[k] && hash_insert(Hs, vv[k], vv[k] | keybit);
-          if (isnew[k] && hash_find(Ho, vv[k]) != kEmpty) meetv[slot] = vv[k];
+          isnew[k] = ok[k] && hash_insert(sd[k] ? H[1] : H[0], vv[k], vv[k] | ((a & 1) ? kParity : 0u));
+          const uint32_t key = isnew[k] ? hash_find(sd[k] ? H[0] : H[1], vv[k]) : kEmpty;
+          f = key == kEmpty ? 0u : 1u + (key >> 31);
         }
+        if (f != 0) {
+          const uint32_t dob = (!bboth || f == 3 || (f - 1) == (bo & 1)) ? bo : bo + 1;
+          const unsigned long long key = ((unsigned long long)(a + dob) << 32) | ((sd[k] ? 1ull : 0ull) << 31) | vv[k];
+          best = key < best ? key : best;
+        }
+      }
+      if (__ballot(best != ~0ull)) {  // rare: the meeting level
+        unsigned long long m = best;
+        for (int off = 32; off >= 1; off >>= 1) {
+          const unsigned long long y = __shfl_xor(m, off);
+          m = y < m ? y : m;
+        }
+        if (lane == 0) atomicMin(&meetk[slot], m);
       }
 #pragma unroll
       for (int k = 0; k < B; ++k) {
-        const unsigned long long mask = __ballot(isnew[k]);
-        if (!mask) continue;  // wave-uniform
-        const OffT d = isnew[k] ? oe[k] - ob[k] : (OffT)0;
-        const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
-        const uint32_t incl = wave_incl_scan(dc);
-        const uint32_t wtot = __builtin_amdgcn_readlane(incl, 63);
-        const int leader = __ffsll((long long)mask) - 1;
-        unsigned long long old = 0;
-        if (lane == (uint32_t)leader)
-          old = atomicAdd(&ctr[slot], ((unsigned long long)__popcll(mask) << 32) | wtot);
-        const uint32_t olo = __builtin_amdgcn_readlane((uint32_t)old, leader);
-        const uint32_t ohi = __builtin_amdgcn_readlane((uint32_t)(old >> 32), leader);
-        const uint32_t eb = olo + incl - dc;
-        if (isnew[k]) {
-          const uint32_t idx = ohi + mbcnt64(mask);
-          par[vv[k]] = uu[k];
-          if (qbase + idx < P.n) que[qbase + idx] = vv[k];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const bool mine = isnew[k] && sd[k] == (q == 1);
+          const unsigned long long mask = __ballot(mine);
+          if (!mask) continue;  // wave-uniform
+          const OffT d = mine ? oe[k] - ob[k] : (OffT)0;
+          const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
+          const uint32_t incl = wave_incl_scan(dc);
+          const uint32_t wtot = __builtin_amdgcn_readlane(incl, 63);
+          const int leader = __ffsll((long long)mask) - 1;
+          unsigned long long old = 0;
+          if (lane == (uint32_t)leader)
+            old = atomicAdd(&ctr[slot][q], ((unsigned long long)__popcll(mask) << 32) | wtot);
+          const uint32_t olo = __builtin_amdgcn_readlane((uint32_t)old, leader);
+          const uint32_t ohi = __builtin_amdgcn_readlane((uint32_t)(old >> 32), leader);
+          const uint32_t eb = olo + incl - dc;
+          if (mine) {
+            const uint32_t idx = ohi + mbcnt64(mask);
+            const uint32_t qb = q ? qb1 : qb0;
+            (q ? P.b.parent[1] : P.b.parent[0])[vv[k]] = uu[k];
+            if (qb + idx < P.n) (q ? P.b.queue[1] : P.b.queue[0])[qb + idx] = vv[k];
+          }
+          append_records(q ? Rn1 : Rn0, mine && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, vv[k], ob[k]);
         }
-        append_records(Rn, isnew[k] && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, vv[k], ob[k]);
       }
     };
-    if (E <= (uint32_t)kLdsThreads) {
-      if ((uint32_t)wid * kWave < E) batch(std::integral_constant<int, 1>{}, 0u);
+    if (ET <= (uint32_t)kLdsThreads) {
+      if ((uint32_t)wid * kWave < ET) batch(std::integral_constant<int, 1>{}, 0u);
     } else {
-      for (uint32_t base = 0; base < E; base += kLdsThreads * kBatch)
-        if (base + (uint32_t)wid * kWave < E) batch(std::integral_constant<int, kBatch>{}, base);
+      for (uint32_t base = 0; base < ET; base += kLdsThreads * kBatch)
+        if (base + (uint32_t)wid * kWave < ET) batch(std::integral_constant<int, kBatch>{}, base);
     }
     if (kStamp && tid == 0) ts1 = stamp();
     __syncthreads();  // B2: every claim of the big level is in LDS
     if (kStamp && tid == 0) ts2 = stamp();
     if (wid == 0) {
-      const unsigned long long pk = ctr[slot];
-      const uint32_t ncnt = uni((uint32_t)(pk >> 32));
-      const uint32_t necl = uni((uint32_t)pk);
-      const uint32_t mv = uni(meetv[slot]);
+      const unsigned long long p0 = ctr[slot][0], p1 = ctr[slot][1];
+      const unsigned long long mk = meetk[slot];
       // the other slot is used by the next big level (wave 0 read it one big
       // level ago)
-      if (lane == 0) {
-        ctr[slot ^ 1] = 0;
-        meetv[slot ^ 1] = kEmpty;
+      if (lane < 2) ctr[slot ^ 1][lane] = 0;
+      if (lane == 0) meetk[slot ^ 1] = ~0ull;
+      const uint32_t mk_hi = uni((uint32_t)(mk >> 32)), mk_lo = uni((uint32_t)mk);
+      if (mk != ~0ull && (meet == kEmpty || mk_hi < md0 + md1)) {
+        const uint32_t side = mk_lo >> 31;
+        const uint32_t a = (side ? bd1 : bd0) + 1;
+        meet = mk_lo & kIdMask;
+        md0 = side ? mk_hi - a : a;
+        md1 = side ? a : mk_hi - a;
       }
-      const SideState x = sel(so, s0, s1), y = sel(so, s1, s0);
-      if (mv != kEmpty) {
-        meet = mv;
-        md0 = so ? (uint32_t)y.depth : (uint32_t)x.depth + 1;
-        md1 = so ? (uint32_t)x.depth + 1 : (uint32_t)y.depth;
-      }
-      apply(so, E, nxt, 0u, ncnt, necl, 3);
-      if (P.side_policy == 2) turn ^= 1;
+      const uint32_t n0 = uni((uint32_t)(p0 >> 32)), l0 = uni((uint32_t)p0);
+      const uint32_t n1 = uni((uint32_t)(p1 >> 32)), l1 = uni((uint32_t)p1);
+      const uint32_t nb0 = uni(plan.nxt[0]), nb1 = uni(plan.nxt[1]);
+      if (E0) apply(0, E0, nb0, 0u, n0, l0, 3);
+      if (E1) apply(1, E1, nb1, 0u, n1, l1, 3);
+      if (!bboth && P.side_policy == 2) turn ^= 1;
       if (meet != kEmpty) status = kFound;
-      else if (ncnt == 0) status = kNoPath;
+      else if ((E0 && n0 == 0) || (E1 && n1 == 0)) status = kNoPath;
       if (kStamp && tid == 0 && levels - 1 < P.b.trace_cap) {
         LevelTraceDev& t = P.b.trace[levels - 1];
         t.side = (uint32_t)(ts1 - ts0);
@@ -936,6 +1107,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
         __hip_atomic_store(&box->seen, rq.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&box->pad[0], (uint32_t)lat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&box->pad[1], polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&P.h.res->rt_pickup, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         cmd[0] = stop;
         cmd[1] = rq.x;
         cmd[2] = rq.y;

@@ -151,7 +151,16 @@ struct HipBiBfs::Impl {
     if (dbg()) std::fprintf(stderr, "[server] post %u (stage %u alive %u)\n", qseq, h_box->stage, h_box->alive);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t it = 1;; ++it) {
-      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq) return;
+      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq) {
+        if (dbg()) {
+          const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+          const double dev_us = (double)(h_res->rt_end - h_res->rt_pickup) * 0.01;
+          const double srch_us = (double)(h_res->rt_end - h_res->rt_begin) * 0.01;
+          std::fprintf(stderr, "[server] host round trip %.2f us, device pickup->result %.2f us (search %.2f)\n",
+                       host_us, dev_us, srch_us);
+        }
+        return;
+      }
       if ((it & 8191) == 0) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
           char msg[512];

@@ -16,6 +16,7 @@ static const char* bibfs_mode_name(int m) {
     case 3: return "lds-all-waves";
     case 4: return "grid-topdown";
     case 5: return "grid-bottomup";
+    case 6: return "lds-lean";
     default: return "cpu";
   }
 }
