@@ -174,7 +174,8 @@ void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* h_src, uint
 void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
                 hipStream_t s);
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
-                  hipStream_t s);
+                  dev::DevState* mirror, uint32_t seq, int trace, hipStream_t s);
+void grid_hubs(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t hubs, hipStream_t s);
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
 void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);
 void finish_level(const SearchBuffers& b, int side, int mode, int trace, dev::DevState* mirror, uint32_t seq,

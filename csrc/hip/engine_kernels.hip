@@ -1150,7 +1150,13 @@ struct GridParams {
   uint32_t n;
   int side;
   launch::SearchBuffers b;
+  DevState* mirror;  // fused level end: pinned state mirror (nullptr = separate finish kernel)
+  uint32_t seq;
+  int trace;
 };
+
+__device__ void fused_finish(const launch::SearchBuffers& b, int s, int mode, int trace, DevState* mirror,
+                             uint32_t seq);
 
 // Claim v for side s from parent u; wave-uniform call (every lane calls it,
 // `valid` masks lanes with no edge).  Appends claimed vertices to the queue
@@ -1253,6 +1259,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     }
     __syncthreads();
   }
+  if (P.mirror) fused_finish(P.b, P.side, 1, P.trace, P.mirror, P.seq);
 }
 
 // Hub vertices (degree > kHubDegree) deferred by k_grid_topdown: every
@@ -1372,7 +1379,7 @@ __global__ void k_frontier_bits(launch::SearchBuffers b, int s) {
 }
 
 // Single-thread level bookkeeping (avoids a host round trip for state updates).
-__device__ void k_finish_level_body(launch::SearchBuffers b, int s, int mode, int trace, DevState& out);
+__device__ void finish_state(DevState& st, const launch::SearchBuffers& b, int s, int mode, int trace);
 
 // Copy a DevState into the pinned host mirror: one write-through store per
 // lane (one wide PCIe write instead of ~30 serial ones), drained, then `seq`.
@@ -1390,13 +1397,18 @@ __global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int tra
                                uint32_t seq) {
   __shared__ DevState sv;
   if (blockIdx.x != 0) return;
-  if (threadIdx.x == 0) k_finish_level_body(b, s, mode, trace, sv);
+  if (threadIdx.x == 0) {
+    finish_state(*b.st, b, s, mode, trace);
+    sv = *b.st;
+  }
   __syncthreads();
   if (mirror && threadIdx.x < 64) publish_state(sv, mirror, seq, threadIdx.x);
 }
 
-__device__ void k_finish_level_body(launch::SearchBuffers b, int s, int mode, int trace, DevState& out) {
-  DevState* st = b.st;
+// End-of-level bookkeeping of the grid engine on a DevState (device memory
+// or a workgroup's LDS copy).
+__device__ void finish_state(DevState& sref, const launch::SearchBuffers& b, int s, int mode, int trace) {
+  DevState* st = &sref;
   const uint32_t ncnt = st->qtail[s] - st->fend[s];
   if (trace && st->levels < b.trace_cap) {
     LevelTraceDev& t = b.trace[st->levels];
@@ -1424,7 +1436,53 @@ __device__ void k_finish_level_body(launch::SearchBuffers b, int s, int mode, in
   st->chunk = 0;
   st->hub_count = 0;
   st->hub_edge_cursor = 0;
-  out = *st;
+}
+
+// Fused end of a grid level: the LAST workgroup of the level's kernel (told by
+// a done counter) finishes the level itself -- no extra kernel launch.  Every
+// DevState word is read with a device-scope atomic (the counters were updated
+// by atomics from every XCD; a plain load could see a stale L2 line), the
+// bookkeeping runs on an LDS copy, the words go back with plain stores (the
+// next level is a new launch) and the pinned mirror is published.  With hubs
+// deferred, the mirror says so (pad[1] = 1) and the host runs the hub kernel
+// and the separate finish kernel instead.
+__device__ void fused_finish(const launch::SearchBuffers& b, int s, int mode, int trace, DevState* mirror,
+                             uint32_t seq) {
+  __shared__ DevState sv;
+  __shared__ uint32_t slast;
+  constexpr uint32_t kWords = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
+  static_assert(kWords <= 64, "one lane per word");
+  const uint32_t tid = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's atomics have completed
+  __syncthreads();
+  if (tid == 0) slast = atomicAdd(&b.st->pad[1], 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!__builtin_amdgcn_readfirstlane(slast)) return;
+  uint32_t* w = reinterpret_cast<uint32_t*>(b.st);
+  if (tid < kWords) reinterpret_cast<uint32_t*>(&sv)[tid] = atomicAdd(&w[tid], 0u);
+  __syncthreads();
+  const bool hubs = sv.hub_count != 0;
+  if (tid == 0) {
+    sv.pad[1] = 0;  // done counter, for the next level
+    if (!hubs) finish_state(sv, b, s, mode, trace);
+  }
+  __syncthreads();
+  if (hubs) {
+    if (tid == 0) {
+      atomicExch(&b.st->pad[1], 0u);
+      if (mirror) {
+        __hip_atomic_store(&mirror->pad[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(&mirror->pad[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    return;
+  }
+  if (tid < kWords) w[tid] = reinterpret_cast<const uint32_t*>(&sv)[tid];
+  if (mirror && tid < 64) {
+    if (tid == 0) __hip_atomic_store(&mirror->pad[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    publish_state(sv, mirror, seq, tid);
+  }
 }
 
 // Seed a search for the grid engine / step-wise API.
@@ -1517,6 +1575,9 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.n = g.n;
   P.side = side;
   P.b = b;
+  P.mirror = nullptr;
+  P.seq = 0;
+  P.trace = 0;
   return P;
 }
 
@@ -1595,7 +1656,7 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
 }
 
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
-                  hipStream_t s) {
+                  dev::DevState* mirror, uint32_t seq, int trace, hipStream_t s) {
   // Dynamic chunks of 256 frontier vertices; never more blocks than chunks:
   // every block takes at least one ticket from ONE counter, and 1024 blocks
   // contending on it cost ~12 us even for a 3-vertex frontier.  Hubs: one
@@ -1605,11 +1666,26 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier));
   if (g.row_off32) {
     auto P = gp<uint32_t>(g, b, side);
+    P.mirror = mirror, P.seq = seq, P.trace = trace;
     k_grid_topdown<uint32_t><<<blocks, kGridThreads, 0, s>>>(P);
+    if (!mirror) k_grid_hubs<uint32_t><<<hblocks, kGridThreads, 0, s>>>(P);
+  } else {
+    auto P = gp<uint64_t>(g, b, side);
+    P.mirror = mirror, P.seq = seq, P.trace = trace;
+    k_grid_topdown<uint64_t><<<blocks, kGridThreads, 0, s>>>(P);
+    if (!mirror) k_grid_hubs<uint64_t><<<hblocks, kGridThreads, 0, s>>>(P);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+// Hubs deferred by a fused top-down level (the host saw pad[1] in the mirror).
+void grid_hubs(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t hubs, hipStream_t s) {
+  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, hubs));
+  if (g.row_off32) {
+    auto P = gp<uint32_t>(g, b, side);
     k_grid_hubs<uint32_t><<<hblocks, kGridThreads, 0, s>>>(P);
   } else {
     auto P = gp<uint64_t>(g, b, side);
-    k_grid_topdown<uint64_t><<<blocks, kGridThreads, 0, s>>>(P);
     k_grid_hubs<uint64_t><<<hblocks, kGridThreads, 0, s>>>(P);
   }
   HIP_CHECK(hipGetLastError());

@@ -354,8 +354,19 @@ struct HipBiBfs::Impl {
       std::swap(buf.fbits[s], buf.nbits[s]);
       fbits_valid[s] = true;
     } else {
-      launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), stream);
+      // fused: the kernel's last workgroup finishes the level and publishes
+      // the mirror; hub vertices (if any) need the hub kernel + finish
+      const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
+      launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), h_state, ls, trace,
+                           stream);
       fbits_valid[s] = false;
+      wait_level();
+      if (h_state->pad[1]) {
+        launch::grid_hubs(g, buf, s, cus, (uint64_t)h_state->hub_count, stream);
+        const uint32_t l2 = ++level_seq == 0 ? ++level_seq : level_seq;
+        launch::finish_level(buf, s, mode, trace, h_state, l2, stream);
+      }
+      return;
     }
     const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
     launch::finish_level(buf, s, mode, trace, h_state, ls, stream);
