@@ -200,3 +200,20 @@ def test_path_longer_than_lds_staging(gpu_engine, resident):
         assert np.array_equal(np.asarray(r.path), np.arange(n))
     finally:
         gpu_engine.set_resident(False)
+
+
+@pytest.mark.parametrize("spec", ["gnp:100000::6", "gnp:1000000::2", "rmat:65536:1048576:3"])
+def test_search_batch_vs_oracle(gpu_engine, spec):
+    """Batched serving (one workgroup per query) gives the single-query answers;
+    queries that outgrow LDS are re-run through the single-query engines."""
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 300, 31)
+    rs = gpu_engine.search_batch(pairs)
+    assert len(rs) == len(pairs)
+    for (s, d), r in zip(pairs, rs):
+        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+    hops, off, flat = gpu_engine.search_batch_arrays([s for s, _ in pairs[:64]], [d for _, d in pairs[:64]])
+    for i, (s, d) in enumerate(pairs[:64]):
+        path = list(flat[off[i]:off[i + 1]])
+        check_result(g.csr, s, d, int(hops[i]), path, native.bfs_oracle(g.csr, s, d).hops)
