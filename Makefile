@@ -39,14 +39,14 @@ PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_
 
 CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp
 HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/hip_engine.hip \
-             csrc/hip/capi.hip csrc/dist/dist_engine.hip
+             csrc/hip/capi.hip csrc/dist/comm.hip csrc/dist/dist_engine.hip
 MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp
 
 CORE_OBJ  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CORE_SRC))
 HIP_OBJ   := $(patsubst csrc/%.hip,$(OBJ)/%.o,$(HIP_SRC))
 MPI_OBJ   := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(MPI_SRC))
 
-HEADERS   := $(wildcard csrc/include/bibfs/*.hpp csrc/include/bibfs/*.h csrc/hip/*.hpp)
+HEADERS   := $(wildcard csrc/include/bibfs/*.hpp csrc/include/bibfs/*.h csrc/hip/*.hpp csrc/dist/*.hpp)
 
 CPU_TOOLS := $(BIN)/bibfs_serial $(BIN)/show_matrix $(BIN)/bibfs_gen
 MPI_TOOLS := $(BIN)/second_try $(BIN)/mpi_queue_bibfs

@@ -1,10 +1,14 @@
 """Multi-GPU and multi-process execution (v2 / v4 capabilities).
 
 * ``DistEngine``: one process per GPU, graph 1-D partitioned, every per-level
-  exchange an RCCL collective over xGMI (native ``DistBiBfs``).  The RCCL
-  communicator is bootstrapped from a unique id broadcast over
-  ``torch.distributed`` (``from_torch_distributed``) or over MPI by the
+  exchange an RCCL collective over xGMI (native ``DistBiBfs``); in lockstep
+  rounds one side's exchange runs on a comm stream while the other side
+  expands.  The RCCL communicator is bootstrapped from a unique id broadcast
+  over ``torch.distributed`` (``from_torch_distributed``) or over MPI by the
   ``mpi_bibfs`` CLI.
+* ``dist_local_run``: the same native engine with P ranks as P threads on ONE
+  GPU, exchanging through an in-process group instead of RCCL -- how the
+  partition / exchange logic is tested with P > 1 on a one-GPU box.
 * ``ReplicatedServer``: query-parallel serving -- every GPU holds the whole
   graph (a 10M-vertex graph is ~0.2 GB of a 288 GB HBM3E part) and answers its
   own share of queries; throughput scales with the number of GPUs.
@@ -93,6 +97,27 @@ class DistEngine:
     def owned(self):
         return self._e.lo, self._e.hi
 
+    @property
+    def last_stats(self) -> dict:
+        """Rounds, lockstep rounds, sparse / dense / overflow levels, exchanged bytes of the last search."""
+        return self._e.last_stats
+
+    @property
+    def backend(self) -> str:
+        return self._e.backend
+
+
+def dist_local_run(ranks: int, graph: Graph, queries: Sequence, device: int = 0, options=None, **kw) -> List:
+    """Partitioned native engine, ``ranks`` ranks as threads sharing one GPU (test harness).
+
+    Every rank answers every query; the result list is rank 0's, after a check
+    that all ranks agree.
+    """
+    if options is None:
+        options = make_options(**kw) if kw else _DEFAULT_OPTIONS
+    q = [(int(s), int(d)) for s, d in queries]
+    return native.dist_local_run(int(ranks), int(device), graph.edges, q, options)
+
 
 class ReplicatedServer:
     """Query-parallel serving: rank r answers queries r, r+W, r+2W, ... on its own GPU."""
@@ -121,4 +146,4 @@ def run_mpi(tool: str, args: Sequence[str], np: int = 2, timeout: float = 300.0,
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
 
 
-__all__ = ["DistEngine", "ReplicatedServer", "run_mpi", "MPIEXEC"]
+__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "run_mpi", "MPIEXEC"]

@@ -13,8 +13,9 @@ frontier exchange, v2/main-v2.cpp:59-83):
 * 1-D block partition, blocks rounded to 64 vertices: rank r owns
   ``[r * chunk, min(n, (r + 1) * chunk))`` -- its CSR rows and the owned
   slices of both visited sets, parents and frontier queues.
-* Per level the replicated policy picks a side (smaller frontier-edge sum by
-  default) and a direction (Beamer alpha/beta, as the single-GPU engine).
+* Per round the replicated policy expands both sides in lockstep while their
+  frontiers are comparable, else one side (smaller frontier-edge sum by
+  default), each with a direction (Beamer alpha/beta, as the single-GPU engine).
 * Top-down: owned frontier vertices claim owned neighbours locally and emit
   ``(v, u)`` candidates for remote owners; ``all_reduce(MAX)`` of the
   candidate count sizes one padded ``all_gather``; owners claim from it
@@ -22,10 +23,10 @@ frontier exchange, v2/main-v2.cpp:59-83):
   above the capacity switches the level to bottom-up.
 * Bottom-up: ``all_gather`` of the owned frontier bitmap slices; every
   unvisited owned vertex scans its row for a frontier neighbour.
-* One ``all_reduce(SUM)`` of (new vertices, their degree sum) and one
-  ``all_reduce(MIN)`` of the local meet candidate end the level; the first
-  level with a meet stops the search (hops = depth_S + depth_T, the
-  first-meet argument of SURVEY.md §2.2).
+* One ``all_reduce(SUM)`` of (new vertices, their degree sum) per side and
+  one ``all_reduce(MIN)`` of the meet key (length << 32 | vertex, lengths
+  exact from per-vertex depths) end the round; the first round with a meet
+  stops the search and its minimum key is the distance.
 * The path is walked with one ``all_reduce(MIN)`` per step: the owner of the
   current vertex contributes its parent, every other rank contributes ~0.
 """
@@ -37,6 +38,8 @@ from typing import List, Optional
 import numpy as np
 
 NONE = np.uint32(0xFFFFFFFF)
+NO_KEY = 1 << 62          # meet key (length << 32 | vertex) when no meet
+LOCKSTEP_EDGES = 1 << 16  # both frontiers this small (edges): lockstep round (native: kLockstepEdges)
 
 
 @dataclass
@@ -101,8 +104,77 @@ class TorchDistBiBfs:
         return np.asarray(v, dtype=np.int64) // self.chunk
 
     # ---------------------------------------------------------------- search
+    def _mode(self, s, direction, dirn, cnt, fed, ved, nnz_total):
+        if direction == "topdown":
+            return 1
+        if direction == "bottomup":
+            return 2
+        m_u = nnz_total - ved[s]
+        if dirn[s] == 1 and fed[s] > m_u / self.alpha:
+            dirn[s] = 2
+        elif dirn[s] == 2 and cnt[s] < self.n / self.beta:
+            dirn[s] = 1
+        return dirn[s]
+
+    def _level(self, s, mode, dnew, front, vis, parent, dep, res) -> np.ndarray:
+        """One level of side s (same phases as the native engine); returns the
+        owned vertices it claimed (sorted global ids)."""
+        ROp = self.dist.ReduceOp
+        new_local: List[int] = []
+
+        def claim(lv, u):
+            vis[s][lv] = True
+            parent[s][lv] = int(u)
+            dep[s][lv] = dnew
+            new_local.append(int(lv + self.lo))
+
+        if mode == 1:
+            # local claims + remote candidates
+            cand_v, cand_u = [], []
+            for u in front[s]:
+                lu = u - self.lo
+                for v in self.col[self.row_off[lu]:self.row_off[lu + 1]]:
+                    if self.lo <= v < self.hi:
+                        if not vis[s][v - self.lo]:
+                            claim(v - self.lo, u)
+                    else:
+                        cand_v.append(int(v))
+                        cand_u.append(int(u))
+            maxc = int(self._allreduce([len(cand_v)], ROp.MAX)[0])
+            if maxc > self.cap:
+                mode = 2  # finish the level bottom-up; local claims stay valid
+                res.dense_levels += 1
+            else:
+                res.sparse_levels += 1
+                if maxc > 0:
+                    blk = np.full(1 + 2 * maxc, -1, dtype=np.int64)
+                    blk[0] = len(cand_v)
+                    blk[1:1 + len(cand_v)] = cand_v
+                    blk[1 + maxc:1 + maxc + len(cand_u)] = cand_u
+                    allb = self._allgather(blk)
+                    got_v = np.concatenate([b[1:1 + b[0]] for b in allb])
+                    got_u = np.concatenate([b[1 + maxc:1 + maxc + b[0]] for b in allb])
+                    mine = (got_v >= self.lo) & (got_v < self.hi)
+                    got_v, got_u = got_v[mine], got_u[mine]
+                    order = np.lexsort((got_u, got_v))  # per vertex: lowest parent first
+                    for v, u in zip(got_v[order], got_u[order]):
+                        if not vis[s][int(v) - self.lo]:
+                            claim(int(v) - self.lo, u)
+        else:
+            res.dense_levels += 1
+        if mode == 2:
+            fbits = np.zeros(self.chunk, dtype=np.int64)
+            fbits[front[s] - self.lo] = 1
+            gb = self._allgather(fbits).reshape(-1)  # global frontier membership, index = vertex id
+            for lv in np.nonzero(~vis[s])[0]:
+                nb = self.col[self.row_off[lv]:self.row_off[lv + 1]]
+                hit = nb[gb[nb] == 1] if nb.size else nb
+                if hit.size:
+                    claim(lv, hit.min())
+        return np.array(sorted(new_local), dtype=np.int64)
+
     def search(self, src: int, dst: int, side: str = "edges", direction: str = "auto",
-               want_path: bool = True) -> DistSearchResult:
+               want_path: bool = True, lockstep: bool = True) -> DistSearchResult:
         ROp = self.dist.ReduceOp
         src, dst = int(src), int(dst)
         if src == dst:
@@ -110,6 +182,7 @@ class TorchDistBiBfs:
         L = self.hi - self.lo
         vis = [np.zeros(L, dtype=bool), np.zeros(L, dtype=bool)]
         parent = [np.full(L, -1, dtype=np.int64), np.full(L, -1, dtype=np.int64)]
+        dep = [np.full(L, -1, dtype=np.int64), np.full(L, -1, dtype=np.int64)]
         front: List[np.ndarray] = [np.zeros(0, np.int64), np.zeros(0, np.int64)]  # owned global ids
         root = (src, dst)
         root_deg = [0, 0]
@@ -117,6 +190,7 @@ class TorchDistBiBfs:
             if self.lo <= root[s] < self.hi:
                 li = root[s] - self.lo
                 vis[s][li] = True
+                dep[s][li] = 0
                 front[s] = np.array([root[s]], np.int64)
                 root_deg[s] = int(self.deg[li])
         rd = self._allreduce(root_deg, ROp.SUM)
@@ -125,117 +199,80 @@ class TorchDistBiBfs:
         depth, dirn, turn = [0, 0], [1, 1], 0
         res = DistSearchResult(False, -1, [], int(NONE))
         nnz_total = 2 * int(self._allreduce([self.m_input if self.rank == 0 else 0], ROp.SUM)[0])
-        meet = -1
+        key = NO_KEY
         while True:
-            if side == "alternate":
-                s, turn = turn, turn ^ 1
+            # rounds: both sides in lockstep while their frontiers are comparable
+            flo, fhi = min(fed), max(fed)
+            if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or fhi <= 2 * flo):
+                sides = [0, 1]
+            elif side == "alternate":
+                sides, turn = [turn], turn ^ 1
             elif side == "frontier":
-                s = 0 if cnt[0] <= cnt[1] else 1
+                sides = [0 if cnt[0] <= cnt[1] else 1]
             else:
-                s = 0 if fed[0] <= fed[1] else 1
-            o = s ^ 1
-            if direction == "topdown":
-                mode = 1
-            elif direction == "bottomup":
-                mode = 2
-            else:
-                m_u = nnz_total - ved[s]
-                if dirn[s] == 1 and fed[s] > m_u / self.alpha:
-                    dirn[s] = 2
-                elif dirn[s] == 2 and cnt[s] < self.n / self.beta:
-                    dirn[s] = 1
-                mode = dirn[s]
-            res.edges_inspected += fed[s]
-            new_local: List[int] = []
-            if mode == 1:
-                # local claims + remote candidates
-                cand_v, cand_u = [], []
-                for u in front[s]:
-                    lu = u - self.lo
-                    nb = self.col[self.row_off[lu]:self.row_off[lu + 1]]
-                    for v in nb:
-                        if self.lo <= v < self.hi:
-                            lv = v - self.lo
-                            if not vis[s][lv]:
-                                vis[s][lv] = True
-                                parent[s][lv] = u
-                                new_local.append(int(v))
-                        else:
-                            cand_v.append(int(v))
-                            cand_u.append(int(u))
-                maxc = int(self._allreduce([len(cand_v)], ROp.MAX)[0])
-                if maxc > self.cap:
-                    mode = 2  # finish the level bottom-up; local claims stay valid
-                    res.dense_levels += 1
-                else:
-                    res.sparse_levels += 1
-                    if maxc > 0:
-                        blk = np.full(1 + 2 * maxc, -1, dtype=np.int64)
-                        blk[0] = len(cand_v)
-                        blk[1:1 + len(cand_v)] = cand_v
-                        blk[1 + maxc:1 + maxc + len(cand_u)] = cand_u
-                        allb = self._allgather(blk)
-                        got_v = np.concatenate([b[1:1 + b[0]] for b in allb])
-                        got_u = np.concatenate([b[1 + maxc:1 + maxc + b[0]] for b in allb])
-                        mine = (got_v >= self.lo) & (got_v < self.hi)
-                        got_v, got_u = got_v[mine], got_u[mine]
-                        order = np.lexsort((got_u, got_v))  # per vertex: lowest parent first
-                        for v, u in zip(got_v[order], got_u[order]):
-                            lv = int(v) - self.lo
-                            if not vis[s][lv]:
-                                vis[s][lv] = True
-                                parent[s][lv] = int(u)
-                                new_local.append(int(v))
-            if mode == 2:
-                words = self.chunk
-                fbits = np.zeros(words, dtype=np.int64)
-                fbits[front[s] - self.lo] = 1
-                gb = self._allgather(fbits).reshape(-1)  # global frontier membership, index = vertex id
-                for lv in np.nonzero(~vis[s])[0]:
-                    nb = self.col[self.row_off[lv]:self.row_off[lv + 1]]
-                    hit = nb[gb[nb] == 1] if nb.size else nb
-                    if hit.size:
-                        vis[s][lv] = True
-                        parent[s][lv] = int(hit.min())
-                        new_local.append(int(lv + self.lo))
-            new_local_arr = np.array(sorted(new_local), dtype=np.int64)
-            lm = NONE
-            if new_local_arr.size:
-                hits = new_local_arr[vis[o][new_local_arr - self.lo]]
-                if hits.size:
-                    lm = np.uint32(hits.min())
-            sums = self._allreduce([new_local_arr.size, int(self.deg[new_local_arr - self.lo].sum()) if new_local_arr.size else 0],
-                                   ROp.SUM)
-            gmeet = int(self._allreduce([int(lm)], ROp.MIN)[0])
-            res.levels += 1
-            res.trace.append((s, depth[s], cnt[s], fed[s], int(sums[0]), mode))
-            depth[s] += 1
-            front[s] = new_local_arr
-            if gmeet != int(NONE):
-                meet = gmeet
+                sides = [0 if fed[0] <= fed[1] else 1]
+            new = {}
+            for s in sides:
+                mode = self._mode(s, direction, dirn, cnt, fed, ved, nnz_total)
+                res.edges_inspected += fed[s]
+                new[s] = self._level(s, mode, depth[s] + 1, front, vis, parent, dep, res)
+                res.levels += 1
+            # meet: a vertex claimed this round that the other side holds closes
+            # a path of exactly depth_s + depth_o; the round's minimum is the distance
+            best = NO_KEY
+            for s in sides:
+                arr = new[s]
+                if arr.size:
+                    li = arr - self.lo
+                    hit = vis[s ^ 1][li]
+                    if hit.any():
+                        keys = (depth[s] + 1 + dep[s ^ 1][li[hit]]) * (1 << 32) + arr[hit]
+                        best = min(best, int(keys.min()))
+            contrib = []
+            for s in (0, 1):
+                arr = new.get(s)
+                contrib += [0, 0] if arr is None else [arr.size, int(self.deg[arr - self.lo].sum()) if arr.size else 0]
+            sums = self._allreduce(contrib, ROp.SUM)
+            gkey = int(self._allreduce([best], ROp.MIN)[0])
+            for s in sides:
+                res.trace.append((s, depth[s], cnt[s], fed[s], int(sums[2 * s]), len(sides)))
+                depth[s] += 1
+                front[s] = new[s]
+            if gkey != NO_KEY:
+                key = gkey
                 break
-            if int(sums[0]) == 0:
+            dead = False
+            for s in sides:
+                cnt[s], fed[s] = int(sums[2 * s]), int(sums[2 * s + 1])
+                ved[s] += fed[s]
+                dead = dead or cnt[s] == 0  # that side's component is exhausted
+            if dead:
                 break
-            cnt[s], fed[s] = int(sums[0]), int(sums[1])
-            ved[s] += fed[s]
-        if meet < 0:
+        if key == NO_KEY:
             return res
-        res.found, res.meet, res.hops = True, meet, depth[0] + depth[1]
+        meet, hops = key & 0xFFFFFFFF, key >> 32
+        res.found, res.meet, res.hops = True, meet, hops
         if want_path:
+            own = self.lo <= meet < self.hi
+            big = int(NONE)
+            md = self._allreduce([int(dep[0][meet - self.lo]) if own else big,
+                                  int(dep[1][meet - self.lo]) if own else big], ROp.MIN)
+            dd = [int(md[0]), int(md[1])]
+            assert dd[0] + dd[1] == hops, (dd, hops)
             chains = [[meet], [meet]]
             cur = [meet, meet]
-            for i in range(max(depth)):
+            for i in range(max(dd)):
                 contrib = []
                 for q in (0, 1):
-                    c = int(NONE)
-                    if i < depth[q] and cur[q] != root[q] and self.lo <= cur[q] < self.hi:
+                    c = big
+                    if i < dd[q] and self.lo <= cur[q] < self.hi:
                         c = int(parent[q][cur[q] - self.lo])
-                    elif i >= depth[q] or cur[q] == root[q]:
-                        c = cur[q] if self.rank == 0 else int(NONE)
+                    elif i >= dd[q]:
+                        c = cur[q] if self.rank == 0 else big
                     contrib.append(c)
                 red = self._allreduce(contrib, ROp.MIN)
                 for q in (0, 1):
-                    if i < depth[q]:
+                    if i < dd[q]:
                         cur[q] = int(red[q])
                         chains[q].append(cur[q])
             res.path = chains[0][::-1] + chains[1][1:]

@@ -1,216 +1,386 @@
-// Multi-GPU bidirectional BFS over RCCL (see include/bibfs/dist_engine.hpp).
+// Multi-GPU bidirectional BFS (see include/bibfs/dist_engine.hpp).
 //
 // Reference parity: v4/mpi_bas.cpp:79-132 (per-level loop), v4/comp.cu:20-38
 // (expand kernel with a vertex-ownership filter that the reference disabled
-// by launching with rank=0,size=1, v4/comp.cu:99), and the collective sites
-// of SURVEY.md §2.5 (MPI_Allreduce BOR over N ints per level, LOR flags).
-// Here the ownership is real, the exchange is sparse when the frontier is
-// small (allgather of candidates) and a bitmap when it is large (allgather of
-// owned slices, N/8 bytes in total), and all state stays on the GPU.
-#include <rccl/rccl.h>
-
+// by launching with rank=0,size=1, v4/comp.cu:99), v2/main-v2.cpp:59-83 (the
+// frontier-list exchange and the min-candidate meet rule) and the collective
+// sites of SURVEY.md §2.5 (MPI_Allreduce BOR over N ints, LOR flags per level).
+//
+// A search runs in ROUNDS.  A round expands one side or -- when the two
+// frontiers are comparable -- both sides in lockstep.  One side's level is
+//   pre      (compute stream) top-down: expand the owned frontier, claim owned
+//                             neighbours, emit (v, parent) candidates for
+//                             remote owners (each remote vertex at most once
+//                             per search and side); bottom-up: the owned slice
+//                             of the frontier bitmap
+//   exchange (comm stream)    ONE allgather: candidate blocks or bitmap slices
+//   post     (comm stream)    owners claim the candidates addressed to them, or
+//                             scan their unvisited vertices against the bitmap
+// In a lockstep round the exchange + post of the source side run on the comm
+// stream while the target side's pre runs on the compute stream: the
+// opposite-direction expand overlaps the RCCL transfer.  The
+// round ends with a meet check over the vertices claimed in it (exact lengths
+// from per-vertex depths, so the minimum over a lockstep round is the
+// distance) and ONE grouped allreduce -- {claimed counts, degree sums} (sum)
+// and the meet key (min) -- read back with one host sync: the only host
+// round trip of a round, except when a top-down candidate block cannot be
+// sized from host-known bounds (then one allreduce(MAX) of the per-rank
+// counts sizes it).
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <thread>
 
 #include "bibfs/dist_engine.hpp"
 #include "bibfs/io.hpp"
+#include "comm.hpp"
 #include "device.hpp"
 
 namespace bibfs {
 
 using namespace dev;
-
-#define RCCL_CHECK(expr)                                                                  \
-  do {                                                                                    \
-    ncclResult_t _r = (expr);                                                             \
-    if (_r != ncclSuccess)                                                                \
-      throw ::bibfs::Error(std::string("RCCL error ") + ncclGetErrorString(_r) + " at " + \
-                           __FILE__ + ":" + std::to_string(__LINE__));                    \
-  } while (0)
+using dist::DType;
+using dist::ROp;
 
 namespace {
 
 constexpr int kThreads = 256;
+constexpr unsigned long long kNoKey = ~0ull;
+constexpr uint64_t kCapMax = 1u << 20;          // candidate pairs per rank per level
+constexpr uint64_t kNoSyncBytes = 1u << 20;     // candidate allgather sized from host bounds up to this many bytes
+constexpr uint64_t kLockstepEdges = 1u << 16;   // both frontiers at most this many edges: always lockstep
 
 struct DState {
-  uint32_t fbeg[2], fend[2], qtail[2];
-  uint32_t send_count;
-  uint32_t pad0;
-  unsigned long long new_edges;  // degree sum of vertices claimed this level (owned)
-  unsigned long long root_edges[2];
-  uint32_t meet;                 // local meet candidate
-  uint32_t pad1;
+  uint32_t fbeg[2], fend[2], qtail[2];  // queue[s][fbeg, fend) = frontier; qtail = append cursor
+  uint32_t send_count[2];               // candidates this rank emitted for side s this level
+  uint32_t pad[2];
+  unsigned long long new_edges[2];      // degree sum of the vertices side s claimed this level
 };
 
-// reduced every level: [0] = new count (sum), [1] = new degree sum (sum)
+// Reduced across ranks (device words, read back into pinned memory).
 struct Reduced {
-  unsigned long long sums[2];
-  uint32_t meet;  // min
-  uint32_t maxsend;  // max
+  unsigned long long sums[4];  // [2s] vertices side s claimed this round, [2s+1] their degree sum (sum)
+  unsigned long long meetkey;  // (path length << 32) | meet vertex (min)
+  uint32_t maxsend[2];         // candidates of side s on this rank (max)
+  uint32_t md[2];              // depth of the meet vertex from each root (owner contributes; min)
 };
 
 struct DView {
-  uint32_t n, lo, hi, chunk;  // owned = [lo, hi), owner(v) = v / chunk
-  const uint64_t* row_off;    // local rows
-  const uint32_t* col;
-  uint32_t* vis[2];           // owned slices (chunk/32 words)
-  uint32_t* parent[2];        // chunk entries
-  uint32_t* queue[2];         // chunk entries
-  uint32_t* obits;            // owned frontier slice (chunk/32 words)
-  const uint32_t* gbits;      // allgathered frontier bitmap (P * chunk/32 words)
-  uint32_t* send;             // [count, pad, (v, u) pairs ...]
-  const uint32_t* recv;       // P blocks of `block` u32
-  uint32_t cap;               // candidate capacity per rank
-  uint32_t block;             // u32 per rank block in recv
+  uint32_t n, lo, hi, chunk;  // owned = [lo, hi); owner(v) = v / chunk
+  const uint64_t* row_off;    // owned rows
+  const uint32_t* col;        // global column ids
+  uint32_t* vis[2];           // owned slices, chunk/32 words
+  uint32_t* parent[2];        // chunk entries, valid where visited
+  uint32_t* depth[2];         // chunk entries, valid where visited
+  uint32_t* queue[2];         // owned vertices (global ids) in claim order
+  uint32_t* sent[2];          // bitmaps over ALL vertices: remote vertices already offered this search
+  uint32_t* obits[2];         // owned frontier slice (chunk/32 words)
+  uint32_t* gbits[2];         // allgathered frontier bitmap (P * chunk/32 words: global index)
+  uint32_t* send[2];          // {count, pad, (v, u) pairs}
+  uint32_t* recv[2];          // P blocks
+  uint32_t cap;               // candidate pairs per rank per level
   int P;
   DState* st;
   Reduced* red;
 };
 
-__device__ __forceinline__ uint32_t* pick(uint32_t* const* a, int s) { return s ? a[1] : a[0]; }
-
-// Claim owned vertex v (global id) for side s from parent u.  Returns true if new.
-__device__ __forceinline__ bool claim_local(const DView& V, int s, uint32_t v, uint32_t u) {
-  const uint32_t li = v - V.lo;
-  uint32_t* vis = s ? V.vis[1] : V.vis[0];
-  const uint32_t bit = 1u << (li & 31);
-  if (vis[li >> 5] & bit) return false;
-  if (atomicOr(&vis[li >> 5], bit) & bit) return false;
-  (s ? V.parent[1] : V.parent[0])[li] = u;
-  const uint32_t pos = atomicAdd(&V.st->qtail[s], 1u);
-  (s ? V.queue[1] : V.queue[0])[pos] = v;
-  atomicAdd(&V.st->new_edges, (unsigned long long)(V.row_off[li + 1] - V.row_off[li]));
-  const uint32_t* ovis = s ? V.vis[0] : V.vis[1];
-  if (ovis[li >> 5] & bit) atomicMin(&V.st->meet, v);
-  return true;
+template <typename T>
+__device__ __forceinline__ T* pick(T* const (&a)[2], int s) {
+  return s ? a[1] : a[0];
 }
 
-// Sparse expansion: one wave per owned frontier vertex, lanes over neighbours.
-__global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s) {
-  const uint32_t fb = V.st->fbeg[s], fe = V.st->fend[s];
-  const uint32_t* q = s ? V.queue[1] : V.queue[0];
-  const int lane = __lane_id();
-  const uint64_t w0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 64;
-  const uint64_t ws = (uint64_t)gridDim.x * blockDim.x / 64;
-  for (uint64_t i = fb + w0; i < fe; i += ws) {
-    const uint32_t u = q[i];
-    const uint32_t li = u - V.lo;
-    const uint64_t b = V.row_off[li], e = V.row_off[li + 1];
-    for (uint64_t k = b + lane; k < e; k += 64) {
-      const uint32_t v = V.col[k];
-      if (v >= V.lo && v < V.hi) {
-        claim_local(V, s, v, u);
-      } else {
-        const uint32_t pos = atomicAdd(&V.st->send_count, 1u);
-        if (pos < V.cap) {
-          V.send[2 + 2 * pos] = v;
-          V.send[3 + 2 * pos] = u;
+// Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
+// every lane of the wave calls it, `want` masks lanes.  One queue append and
+// one degree-sum atomic per wave.
+__device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uint32_t v, uint32_t u,
+                                           uint32_t dnew) {
+  const uint32_t li = v - V.lo;
+  uint32_t* vis = pick(V.vis, s);
+  bool mine = false;
+  if (want) {
+    const uint32_t bit = 1u << (li & 31);
+    if (!(vis[li >> 5] & bit)) mine = !(atomicOr(&vis[li >> 5], bit) & bit);
+  }
+  const unsigned long long mask = __ballot(mine);
+  if (!mask) return;  // wave-uniform
+  const uint32_t lane = __lane_id();
+  const int leader = __ffsll((long long)mask) - 1;
+  unsigned long long deg = 0;
+  if (mine) {
+    pick(V.parent, s)[li] = u;
+    pick(V.depth, s)[li] = dnew;
+    deg = V.row_off[li + 1] - V.row_off[li];
+  }
+  uint32_t pos = 0;
+  if (lane == (uint32_t)leader) pos = atomicAdd(&V.st->qtail[s], (uint32_t)__popcll(mask));
+  pos = __shfl(pos, leader);
+  if (mine) pick(V.queue, s)[pos + mbcnt64(mask)] = v;
+  deg = wave_sum(deg);
+  if (lane == (uint32_t)leader) atomicAdd(&V.st->new_edges[s], deg);
+}
+
+// Offer remote vertex v (parent u) to its owner -- at most once per search and
+// side: after the level that offered it, v is visited by its owner (claimed
+// from the exchange, or by the bottom-up fallback of an overflowing level).
+__device__ __forceinline__ void wave_emit(const DView& V, int s, bool want, uint32_t v, uint32_t u) {
+  uint32_t* sb = pick(V.sent, s);
+  bool emit = false;
+  if (want) {
+    const uint32_t bit = 1u << (v & 31);
+    if (!(sb[v >> 5] & bit)) emit = !(atomicOr(&sb[v >> 5], bit) & bit);
+  }
+  const unsigned long long mask = __ballot(emit);
+  if (!mask) return;  // wave-uniform
+  const uint32_t lane = __lane_id();
+  const int leader = __ffsll((long long)mask) - 1;
+  uint32_t pos = 0;
+  if (lane == (uint32_t)leader) pos = atomicAdd(&V.st->send_count[s], (uint32_t)__popcll(mask));
+  pos = __shfl(pos, leader) + mbcnt64(mask);
+  if (emit && pos < V.cap) reinterpret_cast<uint2*>(pick(V.send, s))[1 + pos] = make_uint2(v, u);
+}
+
+// Top-down pre phase: edge-balanced expansion of the owned frontier.  A
+// workgroup takes 256 frontier vertices, scans their degrees in LDS and walks
+// the chunk's edges one per lane (binary search for the owning vertex), so a
+// hub costs the same per edge as a leaf and no lane idles on a short row.
+__global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t dnew, int first) {
+  __shared__ uint32_t su[kThreads];
+  __shared__ unsigned long long sb[kThreads], se[kThreads];
+  __shared__ unsigned long long wsum[kThreads / kWave];
+  if (first && blockIdx.x == 0 && threadIdx.x == 0) V.red->meetkey = kNoKey;  // new round
+  const uint32_t fb = V.st->fbeg[s], F = V.st->fend[s] - fb;
+  const uint32_t* q = pick(V.queue, s);
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * kThreads; c0 < F; c0 += (uint64_t)gridDim.x * kThreads) {
+    const uint64_t i = c0 + tid;
+    unsigned long long deg = 0, b = 0;
+    uint32_t u = 0;
+    if (i < F) {
+      u = q[fb + i];
+      const uint32_t li = u - V.lo;
+      b = V.row_off[li];
+      deg = V.row_off[li + 1] - b;
+    }
+    su[tid] = u;
+    sb[tid] = b;
+    unsigned long long x = deg;  // inclusive wave scan
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const unsigned long long y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == kWave - 1) wsum[wid] = x;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kThreads / kWave; ++k) {
+      pre += k < wid ? wsum[k] : 0ull;
+      tot += wsum[k];
+    }
+    se[tid] = pre + x - deg;
+    __syncthreads();
+    for (unsigned long long base = 0; base < tot; base += kThreads) {
+      const unsigned long long e = base + tid;
+      const bool valid = e < tot;
+      uint32_t uu = 0, v = 0;
+      if (valid) {
+        uint32_t a = 0, z = kThreads;  // last slot whose edge range starts at or before e
+        while (z - a > 1) {
+          const uint32_t mid = (a + z) >> 1;
+          if (se[mid] <= e) a = mid;
+          else z = mid;
         }
+        uu = su[a];
+        v = V.col[sb[a] + (e - se[a])];
+      }
+      const bool own = valid && v >= V.lo && v < V.hi;
+      wave_claim(V, s, own, v, uu, dnew);
+      wave_emit(V, s, valid && !own, v, uu);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_send_header(DView V, int s) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t c = V.st->send_count[s];
+  pick(V.send, s)[0] = c;
+  V.red->maxsend[s] = c;
+}
+
+// Top-down post phase: owners claim the candidates addressed to them (block r
+// of the gathered buffer is rank r's {count, pad, pairs}).
+__global__ __launch_bounds__(kThreads) void k_td_claim(DView V, int s, uint32_t per_rank, uint32_t dnew) {
+  const uint64_t blk = 2 + 2 * (uint64_t)per_rank;
+  const uint64_t total = (uint64_t)V.P * per_rank;
+  const uint32_t* R = pick(V.recv, s);
+  for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < total; base += (uint64_t)gridDim.x * kThreads) {
+    const uint64_t t = base + threadIdx.x;
+    bool want = false;
+    uint32_t v = 0, u = 0;
+    if (t < total) {
+      const uint64_t r = t / per_rank, i = t % per_rank;
+      const uint32_t* b = R + r * blk;
+      if (i < min(b[0], per_rank)) {
+        const uint2 p = reinterpret_cast<const uint2*>(b)[1 + i];
+        v = p.x;
+        u = p.y;
+        want = v >= V.lo && v < V.hi;
       }
     }
+    wave_claim(V, s, want, v, u, dnew);
   }
 }
 
-// Owners claim the candidates addressed to them.
-__global__ __launch_bounds__(kThreads) void k_td_claim(DView V, int s, uint32_t per_rank, uint32_t blk) {
-  const uint64_t total = (uint64_t)V.P * per_rank;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < total;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = (uint32_t)(t / per_rank), i = (uint32_t)(t % per_rank);
-    const uint32_t* b = V.recv + (uint64_t)r * blk;
-    if (i >= min(b[0], V.cap)) continue;
-    const uint32_t v = b[2 + 2 * i];
-    if (v >= V.lo && v < V.hi) claim_local(V, s, v, b[3 + 2 * i]);
-  }
-}
-
-__global__ void k_obits(DView V, int s) {
+// Bottom-up pre phase: this rank's slice of the frontier bitmap.
+__global__ void k_obits(DView V, int s, int first) {
+  if (first && blockIdx.x == 0 && threadIdx.x == 0) V.red->meetkey = kNoKey;  // new round
   const uint32_t fb = V.st->fbeg[s], fe = V.st->fend[s];
-  const uint32_t* q = s ? V.queue[1] : V.queue[0];
+  const uint32_t* q = pick(V.queue, s);
+  uint32_t* ob = pick(V.obits, s);
   for (uint64_t i = fb + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < fe;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t li = q[i] - V.lo;
-    atomicOr(&V.obits[li >> 5], 1u << (li & 31));
+    atomicOr(&ob[li >> 5], 1u << (li & 31));
   }
 }
 
-// Dense expansion: owners scan their unvisited vertices for a frontier parent.
-__global__ __launch_bounds__(kThreads) void k_bu(DView V, int s) {
+// Bottom-up post phase: one wave owns 64 consecutive owned vertices (two
+// whole visited words: the slice is 64-aligned); each unvisited one scans its
+// row for a neighbour in the gathered frontier bitmap and stops at the first
+// hit; the visited words are rebuilt from one ballot with plain stores.
+__global__ __launch_bounds__(kThreads) void k_bu(DView V, int s, uint32_t dnew) {
   const uint32_t nloc = V.hi - V.lo;
-  const uint32_t* vis = s ? V.vis[1] : V.vis[0];
-  for (uint64_t li = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; li < nloc;
-       li += (uint64_t)gridDim.x * blockDim.x) {
-    if (vis[li >> 5] & (1u << (li & 31))) continue;
-    const uint64_t b = V.row_off[li], e = V.row_off[li + 1];
-    for (uint64_t k = b; k < e; ++k) {
-      const uint32_t u = V.col[k];
-      if (V.gbits[u >> 5] & (1u << (u & 31))) {
-        claim_local(V, s, V.lo + (uint32_t)li, u);
-        break;
+  const uint32_t* __restrict__ gb = pick(V.gbits, s);
+  uint32_t* __restrict__ vis = pick(V.vis, s);
+  const uint32_t lane = __lane_id();
+  const uint64_t nw = ((uint64_t)nloc + 63) / 64;
+  const uint64_t w0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / kWave;
+  const uint64_t ws = (uint64_t)gridDim.x * blockDim.x / kWave;
+  for (uint64_t gw = w0; gw < nw; gw += ws) {
+    const uint32_t li = (uint32_t)(gw * 64 + lane);
+    const uint32_t word = vis[gw * 2 + (lane >> 5)];
+    const uint32_t bit = 1u << (lane & 31);
+    bool found = false;
+    uint32_t pu = 0;
+    unsigned long long deg = 0;
+    if (li < nloc && !(word & bit)) {
+      const uint64_t b = V.row_off[li], e = V.row_off[li + 1];
+      deg = e - b;
+      uint64_t k = b;
+      for (; k + 4 <= e && !found; k += 4) {
+        const uint32_t c0 = V.col[k], c1 = V.col[k + 1], c2 = V.col[k + 2], c3 = V.col[k + 3];
+        const bool h0 = (gb[c0 >> 5] >> (c0 & 31)) & 1u, h1 = (gb[c1 >> 5] >> (c1 & 31)) & 1u;
+        const bool h2 = (gb[c2 >> 5] >> (c2 & 31)) & 1u, h3 = (gb[c3 >> 5] >> (c3 & 31)) & 1u;
+        if (h0 | h1 | h2 | h3) {
+          found = true;
+          pu = h0 ? c0 : (h1 ? c1 : (h2 ? c2 : c3));
+        }
+      }
+      for (; k < e && !found; ++k) {
+        const uint32_t c0 = V.col[k];
+        if ((gb[c0 >> 5] >> (c0 & 31)) & 1u) {
+          found = true;
+          pu = c0;
+        }
       }
     }
+    const unsigned long long mask = __ballot(found);
+    if (!mask) continue;  // wave-uniform
+    if (lane == 0) vis[gw * 2] = word | (uint32_t)mask;
+    if (lane == 32) vis[gw * 2 + 1] = word | (uint32_t)(mask >> 32);
+    const int leader = __ffsll((long long)mask) - 1;
+    if (found) {
+      pick(V.parent, s)[li] = pu;
+      pick(V.depth, s)[li] = dnew;
+    }
+    uint32_t pos = 0;
+    if (lane == (uint32_t)leader) pos = atomicAdd(&V.st->qtail[s], (uint32_t)__popcll(mask));
+    pos = __shfl(pos, leader);
+    if (found) pick(V.queue, s)[pos + mbcnt64(mask)] = V.lo + li;
+    const unsigned long long ds = wave_sum(found ? deg : 0ull);
+    if (lane == (uint32_t)leader) atomicAdd(&V.st->new_edges[s], ds);
+  }
+}
+
+// Meet check for side s over the vertices it claimed this round: one the other
+// side also holds closes a path of length dnew + depth_other(v).
+__global__ __launch_bounds__(kThreads) void k_meet(DView V, int s, uint32_t dnew) {
+  const uint32_t* q = pick(V.queue, s);
+  const uint32_t* ov = pick(V.vis, s ^ 1);
+  const uint32_t* od = pick(V.depth, s ^ 1);
+  const uint32_t b = V.st->fend[s], e = V.st->qtail[s];
+  unsigned long long best = kNoKey;
+  for (uint64_t i = b + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < e;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = q[i], li = v - V.lo;
+    if ((ov[li >> 5] >> (li & 31)) & 1u) {
+      const unsigned long long key = ((unsigned long long)(dnew + od[li]) << 32) | v;
+      best = key < best ? key : best;
+    }
+  }
+#pragma unroll
+  for (int o = kWave / 2; o >= 1; o >>= 1) {
+    const unsigned long long y = __shfl_xor(best, o);
+    best = y < best ? y : best;
+  }
+  if (__lane_id() == 0 && best != kNoKey) atomicMin(&V.red->meetkey, best);
+}
+
+// Round bookkeeping, identical on every rank: publish the per-side counts for
+// the reduction and advance the frontiers of the sides that expanded.
+__global__ void k_round_end(DView V, int sides) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  DState* st = V.st;
+  for (int s = 0; s < 2; ++s) {
+    const bool on = (sides >> s) & 1;
+    V.red->sums[2 * s] = on ? (unsigned long long)(st->qtail[s] - st->fend[s]) : 0ull;
+    V.red->sums[2 * s + 1] = on ? st->new_edges[s] : 0ull;
+    if (on) {
+      st->fbeg[s] = st->fend[s];
+      st->fend[s] = st->qtail[s];
+    }
+    st->send_count[s] = 0;
+    st->new_edges[s] = 0;
   }
 }
 
 __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   DState* st = V.st;
-  const uint32_t r[2] = {src, dst};
   for (int s = 0; s < 2; ++s) {
-    st->fbeg[s] = 0;
-    st->fend[s] = 0;
-    st->qtail[s] = 0;
-    st->root_edges[s] = 0;
-    const uint32_t v = r[s];
+    st->fbeg[s] = st->fend[s] = st->qtail[s] = 0;
+    st->send_count[s] = 0;
+    st->new_edges[s] = 0;
+    V.red->sums[2 * s] = V.red->sums[2 * s + 1] = 0;
+    const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
       const uint32_t li = v - V.lo;
-      (s ? V.vis[1] : V.vis[0])[li >> 5] |= 1u << (li & 31);
-      (s ? V.parent[1] : V.parent[0])[li] = kEmpty;
-      (s ? V.queue[1] : V.queue[0])[0] = v;
-      st->fend[s] = 1;
-      st->qtail[s] = 1;
-      st->root_edges[s] = V.row_off[li + 1] - V.row_off[li];
+      pick(V.vis, s)[li >> 5] |= 1u << (li & 31);
+      pick(V.parent, s)[li] = kEmpty;
+      pick(V.depth, s)[li] = 0;
+      pick(V.queue, s)[0] = v;
+      st->fend[s] = st->qtail[s] = 1;
+      V.red->sums[2 * s] = 1;
+      V.red->sums[2 * s + 1] = V.row_off[li + 1] - V.row_off[li];
     }
   }
-  st->send_count = 0;
-  st->new_edges = 0;
-  st->meet = kEmpty;
-  V.red->sums[0] = st->root_edges[0];
-  V.red->sums[1] = st->root_edges[1];
-  V.red->meet = kEmpty;
-  V.red->maxsend = 0;
+  V.red->meetkey = kNoKey;
+  V.red->maxsend[0] = V.red->maxsend[1] = 0;
+  V.red->md[0] = V.red->md[1] = kEmpty;
 }
 
-// Before the stats reduction: publish this rank's contribution.
-__global__ void k_stats(DView V, int s) {
+// The owner of the meet vertex contributes its two depths (others ~0, min-reduced).
+__global__ void k_meet_depth(DView V, uint32_t meet) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  DState* st = V.st;
-  V.red->sums[0] = st->qtail[s] - st->fend[s];
-  V.red->sums[1] = st->new_edges;
-  V.red->meet = st->meet;
+  const bool own = meet >= V.lo && meet < V.hi;
+  V.red->md[0] = own ? V.depth[0][meet - V.lo] : kEmpty;
+  V.red->md[1] = own ? V.depth[1][meet - V.lo] : kEmpty;
 }
 
-__global__ void k_send_header(DView V) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  V.send[0] = V.st->send_count;
-  V.red->maxsend = V.st->send_count;
-}
-
-// Level bookkeeping, identical on every rank.
-__global__ void k_advance(DView V, int s) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  DState* st = V.st;
-  st->fbeg[s] = st->fend[s];
-  st->fend[s] = st->qtail[s];
-  st->send_count = 0;
-  st->new_edges = 0;
-}
-
-// Path reconstruction step: cur[q] -> parent (only the owner knows it; the
-// others contribute UINT_MAX to the ncclMin that follows).
-__global__ void k_path_step(DView V, uint32_t* cur, uint32_t* pathS, uint32_t* pathT, int i, int dS,
-                            int dT) {
+// Path reconstruction step: cur[q] -> its parent (only the owner knows it; the
+// others contribute ~0 to the ncclMin that follows).
+__global__ void k_path_step(DView V, uint32_t* cur, uint32_t* pathS, uint32_t* pathT, int i, int dS, int dT) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   for (int q = 0; q < 2; ++q) {
     const int d = q ? dT : dS;
@@ -225,14 +395,16 @@ __global__ void k_path_step(DView V, uint32_t* cur, uint32_t* pathS, uint32_t* p
   }
 }
 
+// Reset the visited words of every vertex this search claimed (all of them are
+// in the queues): no O(N) clear per search.
 __global__ void k_cleanup(DView V) {
   for (int s = 0; s < 2; ++s) {
-    const uint32_t q = V.st->qtail[s];
-    const uint32_t* qq = s ? V.queue[1] : V.queue[0];
-    uint32_t* vis = s ? V.vis[1] : V.vis[0];
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < q;
+    const uint32_t qn = V.st->qtail[s];
+    const uint32_t* q = pick(V.queue, s);
+    uint32_t* vis = pick(V.vis, s);
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < qn;
          i += (uint64_t)gridDim.x * blockDim.x)
-      vis[(qq[i] - V.lo) >> 5] = 0u;
+      vis[(q[i] - V.lo) >> 5] = 0u;
   }
 }
 
@@ -244,21 +416,21 @@ unsigned blocks_for(uint64_t work, int cus) {
 
 }  // namespace
 
-std::vector<uint8_t> dist_unique_id() {
-  ncclUniqueId id;
-  RCCL_CHECK(ncclGetUniqueId(&id));
-  return std::vector<uint8_t>(reinterpret_cast<uint8_t*>(&id), reinterpret_cast<uint8_t*>(&id) + sizeof(id));
-}
+std::vector<uint8_t> dist_unique_id() { return dist::rccl_unique_id(); }
 
 struct DistBiBfs::Impl {
   int rank = 0, size = 1, device = 0, cus = 256;
-  hipStream_t stream = nullptr;
-  ncclComm_t comm = nullptr;
-  uint32_t n = 0, lo = 0, hi = 0, chunk = 0;
+  hipStream_t stream = nullptr;   // compute: pre phases, graph build
+  hipStream_t cstream = nullptr;  // comm: exchanges, post phases, round end
+  hipEvent_t ev_pre[2] = {nullptr, nullptr};
+  hipEvent_t ev_round = nullptr;
+  std::unique_ptr<dist::Comm> comm;
+  uint32_t n = 0, lo = 0, hi = 0, chunk = 0, gwords = 0, cap = 0;
   uint64_t m_input = 0, nnz = 0;
   uint64_t* d_row_off = nullptr;
   uint32_t* d_col = nullptr;
   void* state = nullptr;
+  uint32_t* sent_base = nullptr;  // both sides' sent bitmaps, contiguous (one memset)
   DView V{};
   uint32_t* d_cur = nullptr;
   uint32_t* d_pathS = nullptr;
@@ -266,7 +438,24 @@ struct DistBiBfs::Impl {
   Reduced* h_red = nullptr;  // pinned
   double* d_scalar = nullptr;
   DistLevelStats stats;
-  uint32_t cap = 1u << 20;  // candidate pairs per rank per level
+
+  void setup(int dev) {
+    device = dev;
+    rank = comm->rank();
+    size = comm->size();
+    HIP_CHECK(hipSetDevice(device));
+    hipDeviceProp_t prop;
+    HIP_CHECK(hipGetDeviceProperties(&prop, device));
+    cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    int lo_pri = 0, hi_pri = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
+    HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    // the exchange path is the critical one: its stream gets the higher priority
+    HIP_CHECK(hipStreamCreateWithPriority(&cstream, hipStreamNonBlocking, hi_pri));
+    for (auto& e : ev_pre) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_round, hipEventDisableTiming));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
+  }
 
   void set_partition(uint32_t nn) {
     n = nn;
@@ -287,6 +476,8 @@ struct DistBiBfs::Impl {
 
   void alloc_state() {
     const uint64_t words = chunk / 32;
+    gwords = (uint32_t)(((uint64_t)n + 31) / 32 + 1);
+    cap = (uint32_t)std::min<uint64_t>(kCapMax, std::max<uint64_t>(n, 1));
     const uint64_t block = 2 + 2ULL * cap;
     size_t off = 0;
     auto take = [&](size_t bytes) {
@@ -294,16 +485,20 @@ struct DistBiBfs::Impl {
       off += (bytes + 255) & ~(size_t)255;
       return o;
     };
-    size_t o_vis[2], o_par[2], o_q[2];
+    size_t o_vis[2], o_par[2], o_dep[2], o_q[2], o_ob[2], o_gb[2], o_send[2], o_recv[2];
     for (int s = 0; s < 2; ++s) {
       o_vis[s] = take(words * 4);
       o_par[s] = take((size_t)chunk * 4);
+      o_dep[s] = take((size_t)chunk * 4);
       o_q[s] = take((size_t)chunk * 4);
+      o_ob[s] = take(words * 4);
+      o_gb[s] = take(words * 4 * size);
+      o_send[s] = take(block * 4);
+      o_recv[s] = take(block * 4 * size);
     }
-    size_t o_ob = take(words * 4), o_gb = take(words * 4 * size), o_send = take(block * 4),
-           o_recv = take(block * 4 * size), o_st = take(sizeof(DState)), o_red = take(sizeof(Reduced)),
-           o_cur = take(64), o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4),
-           o_sc = take(64);
+    const size_t o_sent = take((size_t)gwords * 4 * 2);
+    const size_t o_st = take(sizeof(DState)), o_red = take(sizeof(Reduced)), o_cur = take(64),
+                 o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4), o_sc = take(64);
     HIP_CHECK(hipMalloc(&state, off));
     char* b = static_cast<char*>(state);
     V.n = n;
@@ -312,18 +507,21 @@ struct DistBiBfs::Impl {
     V.chunk = chunk;
     V.row_off = d_row_off;
     V.col = d_col;
+    sent_base = reinterpret_cast<uint32_t*>(b + o_sent);
     for (int s = 0; s < 2; ++s) {
       V.vis[s] = reinterpret_cast<uint32_t*>(b + o_vis[s]);
       V.parent[s] = reinterpret_cast<uint32_t*>(b + o_par[s]);
+      V.depth[s] = reinterpret_cast<uint32_t*>(b + o_dep[s]);
       V.queue[s] = reinterpret_cast<uint32_t*>(b + o_q[s]);
+      V.obits[s] = reinterpret_cast<uint32_t*>(b + o_ob[s]);
+      V.gbits[s] = reinterpret_cast<uint32_t*>(b + o_gb[s]);
+      V.send[s] = reinterpret_cast<uint32_t*>(b + o_send[s]);
+      V.recv[s] = reinterpret_cast<uint32_t*>(b + o_recv[s]);
+      V.sent[s] = sent_base + (size_t)s * gwords;
       HIP_CHECK(hipMemsetAsync(V.vis[s], 0, words * 4, stream));
     }
-    V.obits = reinterpret_cast<uint32_t*>(b + o_ob);
-    V.gbits = reinterpret_cast<uint32_t*>(b + o_gb);
-    V.send = reinterpret_cast<uint32_t*>(b + o_send);
-    V.recv = reinterpret_cast<uint32_t*>(b + o_recv);
+    HIP_CHECK(hipMemsetAsync(sent_base, 0, (size_t)gwords * 4 * 2, stream));
     V.cap = cap;
-    V.block = (uint32_t)block;
     V.P = size;
     V.st = reinterpret_cast<DState*>(b + o_st);
     V.red = reinterpret_cast<Reduced*>(b + o_red);
@@ -332,6 +530,7 @@ struct DistBiBfs::Impl {
     d_pathT = reinterpret_cast<uint32_t*>(b + o_pt);
     d_scalar = reinterpret_cast<double*>(b + o_sc);
     HIP_CHECK(hipMemsetAsync(V.st, 0, sizeof(DState), stream));
+    HIP_CHECK(hipMemsetAsync(d_scalar, 0, 64, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
   }
 
@@ -357,32 +556,22 @@ struct DistBiBfs::Impl {
     nnz = rows.nnz();
   }
 
-  // grouped allreduce of the level stats + host read-back
-  void reduce_stats() {
-    RCCL_CHECK(ncclGroupStart());
-    RCCL_CHECK(ncclAllReduce(V.red->sums, V.red->sums, 2, ncclUint64, ncclSum, comm, stream));
-    RCCL_CHECK(ncclAllReduce(&V.red->meet, &V.red->meet, 1, ncclUint32, ncclMin, comm, stream));
-    RCCL_CHECK(ncclGroupEnd());
-    HIP_CHECK(hipMemcpyAsync(h_red, V.red, sizeof(Reduced), hipMemcpyDeviceToHost, stream));
-    HIP_CHECK(hipStreamSynchronize(stream));
+  void read_back(hipStream_t s) {
+    HIP_CHECK(hipMemcpyAsync(h_red, V.red, sizeof(Reduced), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
   }
 };
 
 DistBiBfs::DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& uid) : p_(new Impl) {
-  auto& I = *p_;
-  I.rank = rank;
-  I.size = size;
-  I.device = device;
-  BIBFS_REQUIRE(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
   HIP_CHECK(hipSetDevice(device));
-  hipDeviceProp_t prop;
-  HIP_CHECK(hipGetDeviceProperties(&prop, device));
-  I.cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-  HIP_CHECK(hipStreamCreateWithFlags(&I.stream, hipStreamNonBlocking));
-  ncclUniqueId id;
-  std::memcpy(&id, uid.data(), sizeof(id));
-  RCCL_CHECK(ncclCommInitRank(&I.comm, size, id, rank));
-  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&I.h_red), sizeof(Reduced), hipHostMallocDefault));
+  p_->comm = dist::make_rccl_comm(rank, size, uid);
+  p_->setup(device);
+}
+
+DistBiBfs::DistBiBfs(std::unique_ptr<dist::Comm> comm, int device) : p_(new Impl) {
+  HIP_CHECK(hipSetDevice(device));
+  p_->comm = std::move(comm);
+  p_->setup(device);
 }
 
 DistBiBfs::~DistBiBfs() {
@@ -390,11 +579,15 @@ DistBiBfs::~DistBiBfs() {
   try {
     (void)hipSetDevice(p_->device);
     (void)hipStreamSynchronize(p_->stream);
+    (void)hipStreamSynchronize(p_->cstream);
     p_->free_all();
   } catch (...) {
   }
-  if (p_->comm) (void)ncclCommDestroy(p_->comm);
+  p_->comm.reset();
   (void)hipHostFree(p_->h_red);
+  for (auto e : p_->ev_pre) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(p_->ev_round);
+  (void)hipStreamDestroy(p_->cstream);
   (void)hipStreamDestroy(p_->stream);
 }
 
@@ -476,114 +669,174 @@ SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return r;
   }
-  const int cus = I.cus;
-  k_seed<<<1, 64, 0, I.stream>>>(V, src, dst);
-  RCCL_CHECK(ncclAllReduce(V.red->sums, V.red->sums, 2, ncclUint64, ncclSum, I.comm, I.stream));
-  HIP_CHECK(hipMemcpyAsync(I.h_red, V.red, sizeof(Reduced), hipMemcpyDeviceToHost, I.stream));
-  HIP_CHECK(hipStreamSynchronize(I.stream));
+  const int cus = I.cus, P = I.size;
+  hipStream_t ps = I.stream, cs = I.cstream;
+  dist::Comm& comm = *I.comm;
+  const uint32_t words = I.chunk / 32, nloc = I.hi - I.lo;
+
+  k_seed<<<1, 64, 0, cs>>>(V, src, dst);
+  comm.allreduce(V.red->sums, 4, DType::kU64, ROp::kSum, cs);
+  HIP_CHECK(hipEventRecord(I.ev_round, cs));
+  I.read_back(cs);
   // replicated host bookkeeping (identical on every rank)
-  uint64_t cnt[2] = {1, 1}, fed[2] = {I.h_red->sums[0], I.h_red->sums[1]}, ved[2] = {fed[0], fed[1]};
+  uint64_t cnt[2] = {1, 1}, fed[2] = {I.h_red->sums[1], I.h_red->sums[3]};
+  uint64_t ved[2] = {fed[0], fed[1]};
   int depth[2] = {0, 0}, dir[2] = {1, 1}, turn = 0;
   const uint64_t nnz_total = 2 * I.m_input;
-  uint32_t meet = kEmpty;
-  bool found = false;
-  const uint32_t words = I.chunk / 32;
-  for (uint64_t guard = 0; guard <= 2ULL * I.n + 2; ++guard) {
-    int s;
-    if (opt.side == SidePolicy::kAlternate) {
-      s = turn;
+  unsigned long long key = kNoKey;
+  bool dead = false;
+  for (uint64_t guard = 0; guard <= 2ULL * I.n + 2 && key == kNoKey && !dead; ++guard) {
+    const auto tr0 = std::chrono::steady_clock::now();
+    // ---- which sides expand this round
+    int sides[2] = {0, 1}, ns = 1;
+    const uint64_t flo = std::min(fed[0], fed[1]), fhi = std::max(fed[0], fed[1]);
+    if (opt.lockstep && opt.side != SidePolicy::kAlternate && (fhi <= kLockstepEdges || fhi <= 2 * flo)) {
+      ns = 2;
+    } else if (opt.side == SidePolicy::kAlternate) {
+      sides[0] = turn;
       turn ^= 1;
     } else if (opt.side == SidePolicy::kSmallerFrontier) {
-      s = cnt[0] <= cnt[1] ? 0 : 1;
+      sides[0] = cnt[0] <= cnt[1] ? 0 : 1;
     } else {
-      s = fed[0] <= fed[1] ? 0 : 1;
+      sides[0] = fed[0] <= fed[1] ? 0 : 1;
     }
-    int mode;
-    if (opt.direction == Direction::kTopDown) mode = 1;
-    else if (opt.direction == Direction::kBottomUp) mode = 2;
-    else {
-      const double m_u = (double)nnz_total - (double)ved[s];
-      if (dir[s] == 1 && (double)fed[s] > m_u / opt.alpha) dir[s] = 2;
-      else if (dir[s] == 2 && (double)cnt[s] < (double)I.n / opt.beta) dir[s] = 1;
-      mode = dir[s];
-    }
-    r.stats.edges_inspected += fed[s];
-    const auto tc0 = std::chrono::steady_clock::now();
-    if (mode == 1) {
-      k_td_expand<<<blocks_for(cnt[s] * 64 / std::max(1, I.size) + 64, cus), kThreads, 0, I.stream>>>(V, s);
-      k_send_header<<<1, 64, 0, I.stream>>>(V);
-      RCCL_CHECK(ncclAllReduce(&V.red->maxsend, &V.red->maxsend, 1, ncclUint32, ncclMax, I.comm, I.stream));
-      HIP_CHECK(hipMemcpyAsync(I.h_red, V.red, sizeof(Reduced), hipMemcpyDeviceToHost, I.stream));
-      HIP_CHECK(hipStreamSynchronize(I.stream));
-      const uint32_t maxc = I.h_red->maxsend;
-      if (maxc > I.cap) {
-        mode = 2;  // candidates overflowed: finish this level bottom-up (local claims already made stay valid)
-        I.stats.overflow_levels++;
+    int mode[2] = {1, 1};  // 1 top-down, 2 bottom-up
+    for (int i = 0; i < ns; ++i) {
+      const int s = sides[i];
+      if (opt.direction == Direction::kTopDown) {
+        mode[s] = 1;
+      } else if (opt.direction == Direction::kBottomUp) {
+        mode[s] = 2;
       } else {
-        I.stats.sparse_levels++;
-        if (maxc > 0) {
-          // sized to the largest contribution, not to the capacity
-          const uint32_t blk = 2 + 2 * maxc;
-          RCCL_CHECK(ncclAllGather(V.send, const_cast<uint32_t*>(V.recv), blk, ncclUint32, I.comm, I.stream));
-          k_td_claim<<<blocks_for((uint64_t)maxc * I.size, cus), kThreads, 0, I.stream>>>(V, s, maxc, blk);
-          I.stats.candidates_sent += 0;
+        const double m_u = (double)nnz_total - (double)ved[s];
+        if (dir[s] == 1 && (double)fed[s] > m_u / opt.alpha) dir[s] = 2;
+        else if (dir[s] == 2 && (double)cnt[s] < (double)I.n / opt.beta) dir[s] = 1;
+        mode[s] = dir[s];
+      }
+    }
+    // ---- pre phases on the compute stream (behind the previous round)
+    HIP_CHECK(hipStreamWaitEvent(ps, I.ev_round, 0));
+    for (int i = 0; i < ns; ++i) {
+      const int s = sides[i];
+      const uint32_t dnew = (uint32_t)depth[s] + 1;
+      const unsigned fblocks = blocks_for(cnt[s] / (uint64_t)P + kThreads, cus);
+      if (mode[s] == 1) {
+        k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, i == 0);
+        k_send_header<<<1, 64, 0, ps>>>(V, s);
+      } else {
+        HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
+        k_obits<<<fblocks, kThreads, 0, ps>>>(V, s, i == 0);
+      }
+      HIP_CHECK(hipGetLastError());
+      HIP_CHECK(hipEventRecord(I.ev_pre[i], ps));
+    }
+    // ---- exchange + post phases on the comm stream: side 0's run while side
+    // 1's pre phase is still computing on the other stream
+    for (int i = 0; i < ns; ++i) {
+      const int s = sides[i];
+      const uint32_t dnew = (uint32_t)depth[s] + 1;
+      HIP_CHECK(hipStreamWaitEvent(cs, I.ev_pre[i], 0));
+      bool bottomup = mode[s] == 2;
+      if (!bottomup) {
+        uint64_t per;
+        const uint64_t bound = std::min<uint64_t>(fed[s], I.cap);
+        if (fed[s] <= I.cap && (2 + 2 * bound) * 4 * (uint64_t)P <= kNoSyncBytes) {
+          per = bound;  // no rank emits more than the side's frontier edges: no count exchange
+        } else {
+          comm.allreduce(V.red->maxsend + s, 1, DType::kU32, ROp::kMax, cs);
+          I.read_back(cs);
+          per = I.h_red->maxsend[s];
+          I.stats.count_syncs++;
+          if (per > I.cap) {
+            bottomup = true;  // finish the level bottom-up; the local claims made stay valid
+            I.stats.overflow_levels++;
+          }
+        }
+        if (!bottomup) {
+          I.stats.sparse_levels++;
+          if (per > 0) {
+            const uint64_t blk = 2 + 2 * per;
+            comm.allgather(V.send[s], V.recv[s], blk * 4, cs);
+            k_td_claim<<<blocks_for((uint64_t)P * per, cus), kThreads, 0, cs>>>(V, s, (uint32_t)per, dnew);
+            I.stats.exchanged_bytes += blk * 4 * (uint64_t)P;
+          }
+        } else {
+          HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, cs));
+          k_obits<<<blocks_for(cnt[s] / (uint64_t)P + kThreads, cus), kThreads, 0, cs>>>(V, s, 0);
         }
       }
+      if (bottomup) {
+        I.stats.dense_levels++;
+        comm.allgather(V.obits[s], V.gbits[s], (size_t)words * 4, cs);
+        k_bu<<<blocks_for(nloc, cus), kThreads, 0, cs>>>(V, s, dnew);
+        I.stats.exchanged_bytes += (uint64_t)words * 4 * P;
+        ++r.stats.bottomup_levels;
+      }
+      HIP_CHECK(hipGetLastError());
+      r.stats.edges_inspected += fed[s];
+      ++r.stats.levels;
     }
-    if (mode == 2) {
-      I.stats.dense_levels++;
-      HIP_CHECK(hipMemsetAsync(V.obits, 0, (size_t)words * 4, I.stream));
-      k_obits<<<blocks_for(cnt[s], cus), kThreads, 0, I.stream>>>(V, s);
-      RCCL_CHECK(ncclAllGather(V.obits, const_cast<uint32_t*>(V.gbits), words, ncclUint32, I.comm, I.stream));
-      k_bu<<<blocks_for(I.hi - I.lo, cus), kThreads, 0, I.stream>>>(V, s);
+    int mask = 0;
+    for (int i = 0; i < ns; ++i) {
+      const int s = sides[i];
+      k_meet<<<blocks_for(std::min<uint64_t>(fed[s], nloc), cus), kThreads, 0, cs>>>(V, s, (uint32_t)depth[s] + 1);
+      mask |= 1 << s;
     }
-    k_stats<<<1, 64, 0, I.stream>>>(V, s);
-    I.reduce_stats();
-    I.stats.comm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc0).count();
-    I.stats.levels++;
-    r.stats.levels++;
-    ++depth[s];
-    const uint64_t ncnt = I.h_red->sums[0], nedg = I.h_red->sums[1];
-    if (I.h_red->meet != kEmpty) {
-      found = true;
-      meet = I.h_red->meet;
-      k_advance<<<1, 64, 0, I.stream>>>(V, s);
-      break;
+    k_round_end<<<1, 64, 0, cs>>>(V, mask);
+    HIP_CHECK(hipGetLastError());
+    comm.group_begin();
+    comm.allreduce(V.red->sums, 4, DType::kU64, ROp::kSum, cs);
+    comm.allreduce(&V.red->meetkey, 1, DType::kU64, ROp::kMin, cs);
+    comm.group_end();
+    HIP_CHECK(hipEventRecord(I.ev_round, cs));
+    I.read_back(cs);
+    I.stats.rounds++;
+    if (ns == 2) I.stats.lockstep_rounds++;
+    I.stats.levels += ns;
+    I.stats.comm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
+    for (int i = 0; i < ns; ++i) ++depth[sides[i]];
+    key = I.h_red->meetkey;
+    if (key != kNoKey) break;
+    for (int i = 0; i < ns; ++i) {
+      const int s = sides[i];
+      cnt[s] = I.h_red->sums[2 * s];
+      fed[s] = I.h_red->sums[2 * s + 1];
+      ved[s] += fed[s];
+      if (cnt[s] == 0) dead = true;  // that side's component is exhausted without a meet
     }
-    if (ncnt == 0) {
-      k_advance<<<1, 64, 0, I.stream>>>(V, s);
-      break;
-    }
-    k_advance<<<1, 64, 0, I.stream>>>(V, s);
-    cnt[s] = ncnt;
-    fed[s] = nedg;
-    ved[s] += nedg;
   }
-  if (found) {
+  if (key != kNoKey) {
+    const uint32_t meet = (uint32_t)(key & 0xffffffffull);
     r.found = true;
     r.meet = meet;
-    r.hops = depth[0] + depth[1];
+    r.hops = (int64_t)(key >> 32);
     if (opt.want_path) {
-      const int dS = depth[0], dT = depth[1], K = std::max(dS, dT);
-      uint32_t init[2] = {meet, meet};
-      HIP_CHECK(hipMemcpyAsync(I.d_cur, init, 8, hipMemcpyHostToDevice, I.stream));
+      k_meet_depth<<<1, 64, 0, cs>>>(V, meet);
+      comm.allreduce(V.red->md, 2, DType::kU32, ROp::kMin, cs);
+      I.read_back(cs);
+      const int dS = (int)I.h_red->md[0], dT = (int)I.h_red->md[1];
+      BIBFS_REQUIRE((int64_t)dS + dT == r.hops, "dist: meet depths disagree with the path length");
+      const int K = std::max(dS, dT);
+      const uint32_t init[2] = {meet, meet};
+      HIP_CHECK(hipMemcpyAsync(I.d_cur, init, 8, hipMemcpyHostToDevice, cs));
       for (int i = 0; i <= K; ++i) {
-        k_path_step<<<1, 64, 0, I.stream>>>(V, I.d_cur, I.d_pathS, I.d_pathT, i, dS, dT);
-        if (i < K) RCCL_CHECK(ncclAllReduce(I.d_cur, I.d_cur, 2, ncclUint32, ncclMin, I.comm, I.stream));
+        k_path_step<<<1, 64, 0, cs>>>(V, I.d_cur, I.d_pathS, I.d_pathT, i, dS, dT);
+        if (i < K) comm.allreduce(I.d_cur, 2, DType::kU32, ROp::kMin, cs);
       }
-      std::vector<uint32_t> ps(dS + 1), pt(dT + 1);
-      HIP_CHECK(hipMemcpyAsync(ps.data(), I.d_pathS, ps.size() * 4, hipMemcpyDeviceToHost, I.stream));
-      HIP_CHECK(hipMemcpyAsync(pt.data(), I.d_pathT, pt.size() * 4, hipMemcpyDeviceToHost, I.stream));
-      HIP_CHECK(hipStreamSynchronize(I.stream));
-      r.path.assign(ps.rbegin(), ps.rend());
-      r.path.insert(r.path.end(), pt.begin() + 1, pt.end());
+      std::vector<uint32_t> pS((size_t)dS + 1), pT((size_t)dT + 1);
+      HIP_CHECK(hipMemcpyAsync(pS.data(), I.d_pathS, pS.size() * 4, hipMemcpyDeviceToHost, cs));
+      HIP_CHECK(hipMemcpyAsync(pT.data(), I.d_pathT, pT.size() * 4, hipMemcpyDeviceToHost, cs));
+      HIP_CHECK(hipStreamSynchronize(cs));
+      r.path.assign(pS.rbegin(), pS.rend());
+      r.path.insert(r.path.end(), pT.begin() + 1, pT.end());
     }
   }
-  k_cleanup<<<blocks_for(I.chunk, cus), kThreads, 0, I.stream>>>(V);
+  k_cleanup<<<blocks_for(I.chunk, cus), kThreads, 0, cs>>>(V);
+  HIP_CHECK(hipMemsetAsync(I.sent_base, 0, (size_t)I.gwords * 4 * 2, cs));
   HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipStreamSynchronize(I.stream));
-  r.stats.grid_levels = I.stats.levels;
-  r.stats.bottomup_levels = I.stats.dense_levels;
+  HIP_CHECK(hipEventRecord(I.ev_round, cs));
+  HIP_CHECK(hipStreamSynchronize(cs));
+  r.stats.grid_levels = r.stats.levels;
   r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   r.search_ms = r.total_ms;
   return r;
@@ -592,18 +845,18 @@ SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
 void DistBiBfs::barrier() {
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
-  RCCL_CHECK(ncclAllReduce(I.d_scalar, I.d_scalar, 1, ncclFloat64, ncclMax, I.comm, I.stream));
-  HIP_CHECK(hipStreamSynchronize(I.stream));
+  I.comm->allreduce(I.d_scalar, 1, DType::kF64, ROp::kMax, I.cstream);
+  HIP_CHECK(hipStreamSynchronize(I.cstream));
 }
 
 double DistBiBfs::allreduce_max(double x) {
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
   double y = x;
-  HIP_CHECK(hipMemcpyAsync(I.d_scalar, &y, 8, hipMemcpyHostToDevice, I.stream));
-  RCCL_CHECK(ncclAllReduce(I.d_scalar, I.d_scalar, 1, ncclFloat64, ncclMax, I.comm, I.stream));
-  HIP_CHECK(hipMemcpyAsync(&y, I.d_scalar, 8, hipMemcpyDeviceToHost, I.stream));
-  HIP_CHECK(hipStreamSynchronize(I.stream));
+  HIP_CHECK(hipMemcpyAsync(I.d_scalar, &y, 8, hipMemcpyHostToDevice, I.cstream));
+  I.comm->allreduce(I.d_scalar, 1, DType::kF64, ROp::kMax, I.cstream);
+  HIP_CHECK(hipMemcpyAsync(&y, I.d_scalar, 8, hipMemcpyDeviceToHost, I.cstream));
+  HIP_CHECK(hipStreamSynchronize(I.cstream));
   return y;
 }
 
@@ -615,5 +868,37 @@ uint64_t DistBiBfs::local_nnz() const { return p_->nnz; }
 uint32_t DistBiBfs::lo() const { return p_->lo; }
 uint32_t DistBiBfs::hi() const { return p_->hi; }
 const DistLevelStats& DistBiBfs::last_stats() const { return p_->stats; }
+const char* DistBiBfs::backend() const { return p_->comm->name(); }
+
+std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& el,
+                                         const std::vector<std::pair<vid_t, vid_t>>& queries,
+                                         const SearchOptions& opt) {
+  BIBFS_REQUIRE(ranks >= 1 && ranks <= 16, "dist_local_run: 1..16 ranks");
+  auto group = dist::make_local_group(ranks);
+  std::vector<std::vector<SearchResult>> out((size_t)ranks);
+  std::vector<std::string> err((size_t)ranks);
+  std::vector<std::thread> th;
+  for (int r = 0; r < ranks; ++r)
+    th.emplace_back([&, r] {
+      try {
+        DistBiBfs e(dist::make_local_comm(group, r), device);
+        e.load_edges(el);
+        for (const auto& q : queries) out[(size_t)r].push_back(e.search(q.first, q.second, opt));
+      } catch (const std::exception& ex) {
+        err[(size_t)r] = ex.what();
+        dist::abort_local_group(*group);
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int pass = 0; pass < 2; ++pass)  // the failing rank's own message before the others' "aborted"
+    for (int r = 0; r < ranks; ++r)
+      if (!err[(size_t)r].empty() && (pass == 1 || err[(size_t)r].find("aborted") == std::string::npos))
+        throw Error("dist_local_run rank " + std::to_string(r) + ": " + err[(size_t)r]);
+  for (int r = 1; r < ranks; ++r)
+    for (size_t i = 0; i < queries.size(); ++i)
+      BIBFS_REQUIRE(out[(size_t)r][i].hops == out[0][i].hops && out[(size_t)r][i].path == out[0][i].path,
+                    "dist_local_run: ranks returned different results");
+  return out[0];
+}
 
 }  // namespace bibfs

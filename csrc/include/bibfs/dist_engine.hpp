@@ -10,16 +10,19 @@
 // replicated the whole graph and all state on every rank
 // (v2/second_try.cpp:44-50, v4/mpi_bas.cpp:42-64, v4/comp.cu:99).
 //
-// Per level (side s, chosen identically on every rank from allreduced stats):
+// Per round (one side, or both in lockstep; decided identically on every rank
+// from allreduced stats), each expanding side runs one level:
 //   sparse (top-down): owners expand their frontier vertices; neighbours they
-//     own are claimed on the spot, the rest become (v, parent) candidates that
-//     are exchanged with ONE ncclAllGather sized to the largest contribution;
-//     owners then claim the candidates addressed to them.
+//     own are claimed on the spot, the rest become (v, parent) candidates
+//     (each remote vertex offered once per search) exchanged with ONE
+//     ncclAllGather; owners then claim the candidates addressed to them.
 //   dense (bottom-up): the owned frontier bitmap slices are allgathered into a
 //     full bitmap and every owner scans its unvisited vertices for a parent.
-//   The owner of a vertex holds both sides' visited bits, so the meet test is
-//   local; {claimed count, claimed degree sum} (ncclSum) and the meet vertex
-//   (ncclMin) are reduced in one grouped call.
+//   In a lockstep round side S's exchange runs on a comm stream while side T
+//   expands on the compute stream.  The owner of a vertex holds both sides'
+//   visited bits and depths, so the meet test is local and exact; claimed
+//   counts / degree sums (ncclSum) and the meet key (ncclMin over
+//   length << 32 | vertex) are reduced in one grouped call per round.
 // MPI is not needed at runtime: the communicator is bootstrapped from a
 // unique id distributed by MPI (mpi_bibfs), torch.distributed (bench.py) or
 // any other channel.
@@ -27,6 +30,7 @@
 
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "bibfs/graph.hpp"
@@ -36,15 +40,23 @@ namespace bibfs {
 
 std::vector<uint8_t> dist_unique_id();  // ncclGetUniqueId as bytes
 
+namespace dist {
+class Comm;  // collective backend (RCCL, or the in-process test group): csrc/dist/comm.hpp
+}
+
 struct DistLevelStats {
-  int levels = 0, sparse_levels = 0, dense_levels = 0, overflow_levels = 0;
-  uint64_t candidates_sent = 0;   // this rank
-  double comm_ms = 0.0;           // host-visible time in collectives (this rank)
+  int levels = 0;                  // side-levels expanded
+  int rounds = 0, lockstep_rounds = 0;
+  int sparse_levels = 0, dense_levels = 0, overflow_levels = 0;
+  int count_syncs = 0;             // extra host round trips to size a candidate exchange
+  uint64_t exchanged_bytes = 0;    // bytes this rank received from allgathers
+  double comm_ms = 0.0;            // host wall time of the rounds (this rank)
 };
 
 class DistBiBfs {
  public:
-  DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& unique_id);
+  DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& unique_id);  // RCCL
+  DistBiBfs(std::unique_ptr<dist::Comm> comm, int device);                          // any backend
   ~DistBiBfs();
   DistBiBfs(const DistBiBfs&) = delete;
   DistBiBfs& operator=(const DistBiBfs&) = delete;
@@ -70,10 +82,19 @@ class DistBiBfs {
   uint32_t lo() const;
   uint32_t hi() const;
   const DistLevelStats& last_stats() const;
+  const char* backend() const;  // "rccl" or "local"
 
  private:
   struct Impl;
   std::unique_ptr<Impl> p_;
 };
+
+// Test harness: `ranks` ranks as threads of this process
+// sharing `device`, exchanging through the in-process local group instead of
+// RCCL.  Every rank loads `el` and answers `queries`; returns rank 0's results
+// after checking that every rank returned the same hop counts and paths.
+std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& el,
+                                         const std::vector<std::pair<vid_t, vid_t>>& queries,
+                                         const SearchOptions& opt = {});
 
 }  // namespace bibfs

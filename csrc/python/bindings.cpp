@@ -308,5 +308,22 @@ PYBIND11_MODULE(_native, m) {
       .def("search", &DistBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
            py::call_guard<py::gil_scoped_release>())
       .def("barrier", &DistBiBfs::barrier, py::call_guard<py::gil_scoped_release>())
-      .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>());
+      .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("backend", &DistBiBfs::backend)
+      .def_property_readonly("last_stats", [](const DistBiBfs& e) {
+        const DistLevelStats& s = e.last_stats();
+        py::dict d;
+        d["levels"] = s.levels;
+        d["rounds"] = s.rounds;
+        d["lockstep_rounds"] = s.lockstep_rounds;
+        d["sparse_levels"] = s.sparse_levels;
+        d["dense_levels"] = s.dense_levels;
+        d["overflow_levels"] = s.overflow_levels;
+        d["count_syncs"] = s.count_syncs;
+        d["exchanged_bytes"] = s.exchanged_bytes;
+        d["comm_ms"] = s.comm_ms;
+        return d;
+      });
+  m.def("dist_local_run", &dist_local_run, py::arg("ranks"), py::arg("device"), py::arg("edges"),
+        py::arg("queries"), py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>());
 }

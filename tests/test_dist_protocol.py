@@ -68,6 +68,8 @@ def test_partitioned_protocol_matches_oracle(world):
         ("rmat:4096:40000:2", 1 << 16, _pairs(4096, 6, 3), {}),   # hubs: Beamer switches to bottom-up
         ("gnp:3000::3", 1 << 16, _pairs(3000, 3, 4), {"direction": "bottomup"}),
         ("gnp:3000::3", 1 << 16, _pairs(3000, 3, 5), {"side": "alternate"}),
+        ("gnp:3000::3", 1 << 16, _pairs(3000, 4, 6), {"lockstep": False}),
+        ("rmat:4096:40000:2", 4, _pairs(4096, 3, 7), {"lockstep": False}),
     ]
     out = _run(world, specs)
     graphs = {}
