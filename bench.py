@@ -3,7 +3,8 @@
 shape, reported as GTEPS(M/t) (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--graph gnp:100000::6]
-                    [--mode replicated|partitioned] [--extra-graph gnp:10000000::1]
+                    [--mode replicated|partitioned] [--extra-graph gnp:10000000::1,kron:22:16:1]
+                    [--dist-graphs gnp:1000000::2,kron:22:16:1]
 
 One step = one bidirectional-BFS query per GPU: host call -> search on the
 MI355X -> hop count AND the full path back in host memory ("end-to-end ms to
@@ -22,6 +23,13 @@ Modes (N > 1 is launched by torch.distributed.run, one rank per GPU):
 value = whole-job GTEPS = M * (queries answered by all GPUs) / max-rank wall
 time; vs_baseline divides by the best published 100k number in BASELINE.md
 (v1 serial: 0.116 ms -> 0.952 GTEPS(M/t)).
+
+Secondary configs (BASELINE.json), reported under detail and never folded
+into `value`: `extra` = the same serving loop on 10M-vertex G(n,p) and on a
+scale-22 Kronecker (R-MAT, Graph500 parameters; the direction-optimizing grid
+engine); with N > 1 GPUs, `partitioned` = the 1-D partitioned RCCL engine
+(one collective search over all GPUs, strong scaling) on 1M G(n,p) (the v4
+config) and on Kronecker scale 22.
 """
 from __future__ import annotations
 
@@ -42,12 +50,26 @@ BASELINE_100K_MS = 0.115546
 
 
 def parse_spec(spec: str):
+    """gnp:N[:p[:seed]], rmat:N:M[:seed] or kron:SCALE[:EF[:seed]] -> (kind, n, arg, seed)."""
     f = spec.split(":")
-    assert f[0] == "gnp", "bench graphs are G(n,p) specs gnp:N[:p[:seed]]"
-    n = int(f[1])
-    p = float(f[2]) if len(f) > 2 and f[2] else 2.2000000001 / n
-    seed = int(f[3]) if len(f) > 3 else 1
-    return n, p, seed
+    if f[0] == "gnp":
+        n = int(f[1])
+        return "gnp", n, (float(f[2]) if len(f) > 2 and f[2] else 2.2000000001 / n), (int(f[3]) if len(f) > 3 else 1)
+    if f[0] == "rmat":
+        return "rmat", int(f[1]), int(f[2]), (int(f[3]) if len(f) > 3 else 1)
+    if f[0] == "kron":
+        scale, ef = int(f[1]), (int(f[2]) if len(f) > 2 else 16)
+        return "rmat", 1 << scale, ef << scale, (int(f[3]) if len(f) > 3 else 1)
+    raise ValueError(f"bench graph spec must be gnp:/rmat:/kron:, got {spec!r}")
+
+
+def generate(eng, spec: str):
+    kind, n, arg, seed = parse_spec(spec)
+    if kind == "gnp":
+        eng.generate_gnp(n, arg, seed)
+    else:
+        eng.generate_rmat(n, arg, seed)
+    return eng
 
 
 def pick_pairs(eng, n: int, count: int, seed: int):
@@ -71,8 +93,11 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--graph", default="gnp:100000::6")
     ap.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated")
-    ap.add_argument("--extra-graph", default="gnp:10000000::1",
-                    help="second config reported under 'extra' (empty to skip)")
+    ap.add_argument("--extra-graph", default="gnp:10000000::1,kron:22:16:1",
+                    help="comma-separated secondary configs reported under 'extra' (empty to skip)")
+    ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1",
+                    help="N > 1 only: configs run through the partitioned RCCL engine (empty to skip)")
+    ap.add_argument("--dist-steps", type=int, default=20)
     ap.add_argument("--extra-steps", type=int, default=50)
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--no-resident", action="store_true",
@@ -112,22 +137,22 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def run_config(spec: str, steps: int, warmup: int):
-        n, p, seed = parse_spec(spec)
+    def run_config(spec: str, steps: int, warmup: int, mode: str = a.mode):
+        _, n, _, seed = parse_spec(spec)
         t0 = time.perf_counter()
-        if a.mode == "partitioned" and world > 1:
-            eng = DistEngine.from_torch_distributed(local).generate_gnp(n, p, seed)
+        if mode == "partitioned" and world > 1:
+            eng = generate(DistEngine.from_torch_distributed(local), spec)
             m = eng.m
         else:
-            eng = HipEngine(local).generate_gnp(n, p, seed)
+            eng = generate(HipEngine(local), spec)
             eng.set_resident(not a.no_resident)
             m = eng.m
         build_s = time.perf_counter() - t0
-        pairs = pick_pairs(eng, n, a.pairs, 12345)
+        pairs = pick_pairs(eng, n, a.pairs if mode != "partitioned" else min(a.pairs, steps + warmup), 12345)
         assert pairs, f"no connected pairs found in {spec}"
 
         def query(i):
-            if a.mode == "partitioned" and world > 1:
+            if mode == "partitioned" and world > 1:
                 s, d = pairs[i % len(pairs)]
             else:
                 s, d = pairs[(i * world + rank) % len(pairs)]
@@ -161,9 +186,9 @@ def main() -> int:
         park()  # server shutdown is inside the timed region
         barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
-        queries = steps * (1 if a.mode == "partitioned" else world)
+        queries = steps * (1 if mode == "partitioned" else world)
         batched = None
-        if a.batch > 0 and a.mode == "replicated" and hasattr(eng, "search_batch"):
+        if a.batch > 0 and mode == "replicated" and hasattr(eng, "search_batch"):
             # throughput serving: K distinct queries per launch (pairs cycled), steady state
             park()
             bp = [pairs[(i * world + rank) % len(pairs)] for i in range(a.batch)]
@@ -183,22 +208,35 @@ def main() -> int:
             batched = {"batch": a.batch, "launches": reps, "ms_per_batch": bdt * 1e3 / reps,
                        "us_per_query": bdt * 1e6 / (reps * a.batch), "queries_per_s": bq / bdt,
                        "gteps": m * bq / bdt / 1e9}
-        return {
+        out = {
             "n": n, "m": m, "seed": seed, "wall_s": dt, "ms_per_step": dt * 1e3 / steps,
             "gteps": m * queries / dt / 1e9,
-            "gteps_inspected": insp * (1 if a.mode == "partitioned" else world) / dt / 1e9,
+            "gteps_inspected": insp * (1 if mode == "partitioned" else world) / dt / 1e9,
             "mean_hops": hops / steps, "device_ms_per_query": dev_ms / steps,
             "build_ms": build_s * 1e3, "end_to_end_first_query_ms": build_s * 1e3 + dt * 1e3 / steps,
             "queries": queries, "batched": batched,
         }
+        if mode == "partitioned" and world > 1:
+            out["engine"] = f"DistBiBfs/{eng.backend} x{world}"
+            out["last_query_stats"] = eng.last_stats
+        if hasattr(eng, "release"):
+            eng.release()  # free HBM before the next config
+        return out
 
     head = run_config(a.graph, a.steps, a.warmup)
     extra = {}
-    if a.extra_graph:
+    for spec in filter(None, a.extra_graph.split(",")):
         try:
-            extra[a.extra_graph] = run_config(a.extra_graph, a.extra_steps, min(a.warmup, 10))
+            extra[spec] = run_config(spec, a.extra_steps, min(a.warmup, 10), "replicated")
         except Exception as exc:  # report, never hide, a failing secondary config
-            extra[a.extra_graph] = {"error": repr(exc)}
+            extra[spec] = {"error": repr(exc)}
+    partitioned = {}
+    if world > 1 and a.mode == "replicated" and a.dist_backend == "nccl":
+        for spec in filter(None, a.dist_graphs.split(",")):
+            try:
+                partitioned[spec] = run_config(spec, a.dist_steps, 3, "partitioned")
+            except Exception as exc:
+                partitioned[spec] = {"error": repr(exc)}
 
     if rank == 0:
         out = {
@@ -230,6 +268,7 @@ def main() -> int:
                 "resident_server": a.mode == "replicated" and not a.no_resident,
                 "batched_serving": head["batched"],
                 "extra": extra,
+                "partitioned": partitioned,
             },
         }
         print(json.dumps(out))
