@@ -38,6 +38,7 @@ import json
 import os
 import random
 import sys
+import threading
 import time
 
 import torch  # first: the HIP runtime torch ships is the one our extension then binds to
@@ -86,6 +87,42 @@ def pick_pairs(eng, n: int, count: int, seed: int):
     return pairs
 
 
+def report(a, world: int, head: dict, extra: dict, partitioned: dict) -> dict:
+    """The one JSON line rank 0 prints (driver contract)."""
+    return {
+        "metric": "GTEPS(M/t), end-to-end bi-BFS shortest-path query (G(n,2.2/n), path returned to host)",
+        "value": round(head["gteps"], 4),
+        "unit": "GTEPS",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(head["ms_per_step"], 6),
+        "higher_is_better": True,
+        "scaling": "strong" if a.mode == "partitioned" else "weak",
+        "vs_baseline": round(head["gteps"] / BASELINE_100K_GTEPS, 3) if head["n"] == 100000 else None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {
+            "model": f"G(n={head['n']}, p=2.2/n) seed={head['seed']}, M={head['m']}",
+            "global_batch": world if a.mode == "replicated" else 1,
+            "seq_len": head["n"],
+            "parallelism": (f"dp{world}" if a.mode == "replicated" else f"vertex-partition{world}"),
+        },
+        "detail": {
+            "query_ms": round(head["ms_per_step"], 6),
+            "device_ms_per_query": round(head["device_ms_per_query"], 6),
+            "baseline_best_100k_ms": BASELINE_100K_MS,
+            "gteps_inspected": head["gteps_inspected"],
+            "mean_hops": head["mean_hops"],
+            "graph_build_ms": round(head["build_ms"], 3),
+            "resident_server": a.mode == "replicated" and not a.no_resident,
+            "batched_serving": head["batched"],
+            "extra": extra,
+            "partitioned": partitioned,
+        },
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -98,6 +135,9 @@ def main() -> int:
     ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1",
                     help="N > 1 only: configs run through the partitioned RCCL engine (empty to skip)")
     ap.add_argument("--dist-steps", type=int, default=20)
+    ap.add_argument("--secondary-timeout", type=float, default=240.0,
+                    help="seconds allowed for the extra + partitioned configs together; past it the "
+                         "headline line is printed with the unfinished configs marked and every rank exits")
     ap.add_argument("--extra-steps", type=int, default=50)
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--no-resident", action="store_true",
@@ -225,56 +265,46 @@ def main() -> int:
 
     head = run_config(a.graph, a.steps, a.warmup)
     extra = {}
+    partitioned = {}
+    printed = threading.Lock()
+
+    def emit():
+        if rank == 0 and printed.acquire(blocking=False):
+            print(json.dumps(report(a, world, head, extra, partitioned)), flush=True)
+
+    def watchdog():
+        # A secondary config that hangs (e.g. a collective that never completes
+        # on some rank) must not take the headline measurement with it.
+        for d in (extra, partitioned):
+            for k, v in list(d.items()):
+                if v is None:
+                    d[k] = {"error": f"watchdog: unfinished after {a.secondary_timeout:.0f} s"}
+        emit()
+        sys.stdout.flush()
+        os._exit(0)
+
+    dog = threading.Timer(a.secondary_timeout, watchdog)
+    dog.daemon = True
+    dog.start()
     for spec in filter(None, a.extra_graph.split(",")):
+        extra[spec] = None
         try:
             extra[spec] = run_config(spec, a.extra_steps, min(a.warmup, 10), "replicated")
         except Exception as exc:  # report, never hide, a failing secondary config
             extra[spec] = {"error": repr(exc)}
-    partitioned = {}
     if world > 1 and a.mode == "replicated" and a.dist_backend == "nccl":
         for spec in filter(None, a.dist_graphs.split(",")):
+            partitioned[spec] = None
             try:
                 partitioned[spec] = run_config(spec, a.dist_steps, 3, "partitioned")
             except Exception as exc:
                 partitioned[spec] = {"error": repr(exc)}
 
-    if rank == 0:
-        out = {
-            "metric": "GTEPS(M/t), end-to-end bi-BFS shortest-path query (G(n,2.2/n), path returned to host)",
-            "value": round(head["gteps"], 4),
-            "unit": "GTEPS",
-            "n_gpus": world,
-            "steps": a.steps,
-            "warmup": a.warmup,
-            "ms_per_step": round(head["ms_per_step"], 6),
-            "higher_is_better": True,
-            "scaling": "strong" if a.mode == "partitioned" else "weak",
-            "vs_baseline": round(head["gteps"] / BASELINE_100K_GTEPS, 3) if head["n"] == 100000 else None,
-            "dtype": "int32",
-            "data": "synthetic",
-            "config": {
-                "model": f"G(n={head['n']}, p=2.2/n) seed={head['seed']}, M={head['m']}",
-                "global_batch": world if a.mode == "replicated" else 1,
-                "seq_len": head["n"],
-                "parallelism": (f"dp{world}" if a.mode == "replicated" else f"vertex-partition{world}"),
-            },
-            "detail": {
-                "query_ms": round(head["ms_per_step"], 6),
-                "device_ms_per_query": round(head["device_ms_per_query"], 6),
-                "baseline_best_100k_ms": BASELINE_100K_MS,
-                "gteps_inspected": head["gteps_inspected"],
-                "mean_hops": head["mean_hops"],
-                "graph_build_ms": round(head["build_ms"], 3),
-                "resident_server": a.mode == "replicated" and not a.no_resident,
-                "batched_serving": head["batched"],
-                "extra": extra,
-                "partitioned": partitioned,
-            },
-        }
-        print(json.dumps(out))
+    emit()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    dog.cancel()  # after the teardown: a hung final barrier is covered too
     return 0
 
 
