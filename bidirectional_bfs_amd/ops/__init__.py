@@ -106,6 +106,16 @@ class HipEngine:
         return self
 
     @property
+    def batch_edge_cap(self) -> int:
+        """Largest level (frontier edges) the batched HBM-bitmap pass expands
+        before handing the query to the single-query engine."""
+        return self._e.batch_edge_cap
+
+    @batch_edge_cap.setter
+    def batch_edge_cap(self, edges: int) -> None:
+        self._e.batch_edge_cap = int(edges)
+
+    @property
     def resident(self) -> bool:
         return self._e.resident
 

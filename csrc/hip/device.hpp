@@ -82,6 +82,17 @@ struct alignas(16) ServerBox {
 constexpr uint32_t kReqStop = 1u, kReqLockstep = 2u;  // tag flags; side policy in bits 2..3
 __host__ __device__ inline uint32_t req_tag(uint32_t seq, uint32_t flags) { return (flags & 0xffu) | (seq << 8); }
 
+// Result of one query of the batched global-visited kernel (batch_global.hip).
+struct BatchOut {
+  uint32_t status;
+  int32_t hops;
+  uint32_t meet;
+  uint32_t levels;
+  uint32_t visited;
+  uint32_t path_len;
+  unsigned long long einsp;
+};
+
 struct LevelTraceDev {
   uint32_t side, depth, frontier, mode;
   unsigned long long edges, discovered;
@@ -173,6 +184,10 @@ void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* h_src, uint
                uint32_t seq, hipStream_t s);
 void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32_t dst,
                 hipStream_t s);
+// batch_global.hip: one workgroup per query, bitmaps in HBM (queries that outgrow LDS)
+void batch_global(const GraphView& g, uint32_t words, const uint32_t* qidx, uint32_t k, const uint32_t* src,
+                  const uint32_t* dst, uint32_t* slots, uint32_t* bits, dev::BatchOut* out, uint32_t* path,
+                  uint32_t path_cap, unsigned long long edge_cap, hipStream_t s);
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
                   dev::DevState* mirror, uint32_t seq, int trace, hipStream_t s);
 void grid_hubs(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t hubs, hipStream_t s);

@@ -63,6 +63,10 @@ struct HipBiBfs::Impl {
   uint32_t* h_bpath = nullptr;    // pinned, K * kBatchPath
   uint32_t* h_bq = nullptr;       // pinned staging for src/dst
   uint32_t bcap = 0;              // slots allocated
+  uint64_t bedge_cap = 1ull << 18;  // batch_global: larger levels go to search()
+  uint32_t* d_bbits = nullptr;    // per slot 2 visited bitmaps (batch_global), all-zero between launches
+  uint32_t* h_bqidx = nullptr;    // pinned: queries handed to batch_global
+  BatchOut* h_bout = nullptr;     // pinned: batch_global results
   static constexpr uint32_t kBatchPath = 4096;
 
   void free_batch() {
@@ -71,6 +75,11 @@ struct HipBiBfs::Impl {
     if (h_bres) HIP_CHECK(hipHostFree(h_bres));
     if (h_bpath) HIP_CHECK(hipHostFree(h_bpath));
     if (h_bq) HIP_CHECK(hipHostFree(h_bq));
+    if (d_bbits) HIP_CHECK(hipFree(d_bbits));
+    if (h_bqidx) HIP_CHECK(hipHostFree(h_bqidx));
+    if (h_bout) HIP_CHECK(hipHostFree(h_bout));
+    d_bbits = h_bqidx = nullptr;
+    h_bout = nullptr;
     d_bslots = d_bq = nullptr;
     h_bres = nullptr;
     h_bpath = h_bq = nullptr;
@@ -88,6 +97,12 @@ struct HipBiBfs::Impl {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_bq), (size_t)k * 2 * sizeof(uint32_t),
                             hipHostMallocMapped | hipHostMallocCoherent));  // read by the kernel directly
     std::memset(h_bres, 0, (size_t)k * sizeof(HostResult));
+    HIP_CHECK(hipMalloc(&d_bbits, (size_t)k * 2 * buf.words * sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(d_bbits, 0, (size_t)k * 2 * buf.words * sizeof(uint32_t), stream));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_bqidx), (size_t)k * sizeof(uint32_t),
+                            hipHostMallocMapped | hipHostMallocCoherent));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_bout), (size_t)k * sizeof(BatchOut),
+                            hipHostMallocMapped | hipHostMallocCoherent));
     bcap = k;
   }
 
@@ -606,6 +621,8 @@ void HipBiBfs::set_resident(bool on, double idle_ms) {
   I.srv_idle_ticks = (unsigned long long)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
 }
 bool HipBiBfs::resident() const { return p_->resident; }
+void HipBiBfs::set_batch_edge_cap(uint64_t edges) { p_->bedge_cap = edges; }
+uint64_t HipBiBfs::batch_edge_cap() const { return p_->bedge_cap; }
 
 std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, const std::vector<vid_t>& dst,
                                                  const SearchOptions& opt) {
@@ -621,9 +638,14 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
     for (size_t i = 0; i < K; ++i) out[i] = search(src[i], dst[i], opt);
     return out;
   }
-  // slots: up to 1024 per launch, and at most ~8 GiB of per-slot state
-  const uint64_t per_slot = 16ull * I.n;
-  const uint32_t kmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, (8ull << 30) / per_slot));
+  // slots: up to 1024 per launch.  Per-slot state (parent + queue, 16n B) is
+  // touched sparsely, so the budget is generous: up to 40 GiB or half the free
+  // HBM -- enough for 256 concurrent 10M-vertex queries on one MI355X.
+  size_t hbm_free = 0, hbm_total = 0;
+  HIP_CHECK(hipMemGetInfo(&hbm_free, &hbm_total));
+  const uint64_t budget = std::min<uint64_t>(40ull << 30, (uint64_t)hbm_free / 2 + (uint64_t)I.bcap * (16ull * I.n));
+  const uint64_t per_slot = 16ull * I.n + 8ull * I.buf.words;
+  const uint32_t kmax = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, budget / per_slot));
   for (size_t c0 = 0; c0 < K; c0 += kmax) {
     const uint32_t k = (uint32_t)std::min<size_t>(kmax, K - c0);
     const auto t0 = std::chrono::steady_clock::now();
@@ -646,6 +668,20 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
         }
       }
     }
+    // queries whose visited sets outgrew LDS: one more batched pass with the
+    // visited bitmaps in HBM (batch_global.hip) instead of one-by-one re-runs
+    uint32_t nglobal = 0;
+    for (uint32_t i = 0; i < k; ++i) {
+      const HostResult& R = I.h_bres[i];
+      if (src[c0 + i] != dst[c0 + i] && R.status == kHandoff) I.h_bqidx[nglobal++] = i;
+    }
+    if (nglobal) {
+      launch::batch_global(I.view(), I.buf.words, I.h_bqidx, nglobal, I.h_bq, I.h_bq + k, I.d_bslots, I.d_bbits,
+                           I.h_bout, I.h_bpath, Impl::kBatchPath, I.bedge_cap, I.stream);
+      HIP_CHECK(hipStreamSynchronize(I.stream));
+    }
+    std::vector<char> via_global(k, 0);
+    for (uint32_t j = 0; j < nglobal; ++j) via_global[I.h_bqidx[j]] = 1;
     const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     for (uint32_t i = 0; i < k; ++i) {
       const HostResult& R = I.h_bres[i];
@@ -655,8 +691,27 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
         r = search(s, d, opt);
         continue;
       }
+      if (via_global[i]) {
+        const BatchOut& G = I.h_bout[i];
+        if (G.status != kFound && G.status != kNoPath) {
+          r = search(s, d, opt);  // a level above the edge cap / path longer than the slot
+          continue;
+        }
+        r.found = G.status == kFound;
+        r.hops = r.found ? G.hops : -1;
+        r.meet = r.found ? G.meet : kNoVertex;
+        r.stats.levels = (int)G.levels;
+        r.stats.edges_inspected = G.einsp;
+        r.stats.visited = G.visited;
+        r.stats.handoff = true;
+        if (r.found && opt.want_path) r.path.assign(I.h_bpath + (size_t)i * Impl::kBatchPath,
+                                                    I.h_bpath + (size_t)i * Impl::kBatchPath + G.path_len);
+        r.search_ms = wall;
+        r.total_ms = wall;
+        continue;
+      }
       if (R.status == kHandoff || R.path_on_device == 2 || (R.status != kFound && R.status != kNoPath)) {
-        r = search(s, d, opt);  // frontier outgrew LDS / path longer than the slot: single-query engines
+        r = search(s, d, opt);  // path longer than the slot: single-query engines
         continue;
       }
       r.found = R.status == kFound;

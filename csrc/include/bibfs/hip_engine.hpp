@@ -54,11 +54,15 @@ class HipBiBfs {
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
 
   // Throughput serving: answer K queries with one launch, one workgroup (one
-  // CU) per query, up to 256 in flight.  Same results as K search() calls
-  // (queries whose frontier outgrows LDS, or whose path is longer than the
-  // batch path slot, are re-run through search()).
+  // CU) per query, up to 256 in flight.  Same results as K search() calls.
+  // Queries whose visited sets outgrow LDS get a second batched pass with
+  // HBM bitmaps (one 256-thread workgroup each); a query with a level above
+  // `batch_edge_cap` edges, or a path longer than the batch path slot, is
+  // re-run through search().
   std::vector<SearchResult> search_batch(const std::vector<vid_t>& src, const std::vector<vid_t>& dst,
                                          const SearchOptions& opt = {});
+  void set_batch_edge_cap(uint64_t edges);
+  uint64_t batch_edge_cap() const;
 
   // Resident query server: one workgroup stays on the GPU and takes queries
   // from a pinned mailbox, so a query costs no kernel launch.  It exits by

@@ -258,6 +258,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_resident", &HipBiBfs::set_resident, py::arg("on"), py::arg("idle_ms") = 200.0,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("resident", &HipBiBfs::resident)
+      .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
       .def("begin", &HipBiBfs::begin, py::call_guard<py::gil_scoped_release>())
       .def(
           "expand",

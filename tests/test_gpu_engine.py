@@ -217,3 +217,31 @@ def test_search_batch_vs_oracle(gpu_engine, spec):
     for i, (s, d) in enumerate(pairs[:64]):
         path = list(flat[off[i]:off[i + 1]])
         check_result(g.csr, s, d, int(hops[i]), path, native.bfs_oracle(g.csr, s, d).hops)
+
+
+@pytest.mark.parametrize("spec", ["gnp:1000000::2", "gnp:3000000::5", "rmat:262144:4194304:4"])
+def test_search_batch_global_pass(gpu_engine, spec):
+    """Queries that outgrow LDS take the batched HBM-bitmap pass (batch_global.hip):
+    exact hops + valid paths, bitmaps left clean for the next batch (three
+    back-to-back batches agree), and the edge-cap fallback gives the same answers."""
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 200, 57) + [(5, 5), (g.n - 1, g.n - 1)]
+    truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
+    cap0 = gpu_engine.batch_edge_cap
+    try:
+        runs = []
+        for _ in range(3):
+            rs = gpu_engine.search_batch(pairs)
+            for (s, d), r, h in zip(pairs, rs, truth):
+                check_result(g.csr, s, d, r.hops, r.path, h)
+            runs.append([r.hops for r in rs])
+        assert runs[0] == runs[1] == runs[2]
+        if g.n > 131072:
+            assert any(r.handoff for r in rs), "expected queries to take the HBM-bitmap pass"
+        gpu_engine.batch_edge_cap = 16  # almost every query falls back to search()
+        rs = gpu_engine.search_batch(pairs[:40])
+        for (s, d), r, h in zip(pairs[:40], rs, truth[:40]):
+            check_result(g.csr, s, d, r.hops, r.path, h)
+    finally:
+        gpu_engine.batch_edge_cap = cap0
