@@ -115,6 +115,12 @@ class HipEngine:
     def batch_edge_cap(self, edges: int) -> None:
         self._e.batch_edge_cap = int(edges)
 
+    def set_batch_tuning(self, lds_first: int = -1, threads: int = 0) -> "HipEngine":
+        """Batched serving knobs: LDS pass first (1), HBM-bitmap pass only (0) or
+        auto by graph size (-1); HBM-pass workgroup size 256/1024 (0 = auto)."""
+        self._e.set_batch_tuning(int(lds_first), int(threads))
+        return self
+
     @property
     def resident(self) -> bool:
         return self._e.resident

@@ -187,7 +187,7 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
 // batch_global.hip: one workgroup per query, bitmaps in HBM (queries that outgrow LDS)
 void batch_global(const GraphView& g, uint32_t words, const uint32_t* qidx, uint32_t k, const uint32_t* src,
                   const uint32_t* dst, uint32_t* slots, uint32_t* bits, dev::BatchOut* out, uint32_t* path,
-                  uint32_t path_cap, unsigned long long edge_cap, hipStream_t s);
+                  uint32_t path_cap, unsigned long long edge_cap, int threads, hipStream_t s);
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
                   dev::DevState* mirror, uint32_t seq, int trace, hipStream_t s);
 void grid_hubs(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t hubs, hipStream_t s);

@@ -63,7 +63,9 @@ struct HipBiBfs::Impl {
   uint32_t* h_bpath = nullptr;    // pinned, K * kBatchPath
   uint32_t* h_bq = nullptr;       // pinned staging for src/dst
   uint32_t bcap = 0;              // slots allocated
-  uint64_t bedge_cap = 1ull << 18;  // batch_global: larger levels go to search()
+  uint64_t bedge_cap = 1ull << 20;  // batch_global: larger levels go to search()
+  int blds = -1;                    // batch: LDS pass first (1), never (0), auto (-1)
+  int bthreads = 0;                 // batch_global workgroup size (256 / 1024), 0 = auto
   uint32_t* d_bbits = nullptr;    // per slot 2 visited bitmaps (batch_global), all-zero between launches
   uint32_t* h_bqidx = nullptr;    // pinned: queries handed to batch_global
   BatchOut* h_bout = nullptr;     // pinned: batch_global results
@@ -622,6 +624,11 @@ void HipBiBfs::set_resident(bool on, double idle_ms) {
 }
 bool HipBiBfs::resident() const { return p_->resident; }
 void HipBiBfs::set_batch_edge_cap(uint64_t edges) { p_->bedge_cap = edges; }
+void HipBiBfs::set_batch_tuning(int lds_first, int threads) {
+  BIBFS_REQUIRE(threads == 0 || threads == 256 || threads == 1024, "batch threads must be 0, 256 or 1024");
+  p_->blds = lds_first;
+  p_->bthreads = threads;
+}
 uint64_t HipBiBfs::batch_edge_cap() const { return p_->bedge_cap; }
 
 std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, const std::vector<vid_t>& dst,
@@ -653,8 +660,22 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
     std::memcpy(I.h_bq, src.data() + c0, k * 4);
     std::memcpy(I.h_bq + k, dst.data() + c0, k * 4);
     const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
-    launch::lds_batch(I.view(), I.buf, I.h_bq, I.h_bq + k, k, I.d_bslots, I.h_bres, I.h_bpath, Impl::kBatchPath,
-                      seq, I.stream);
+    // auto: the HBM-bitmap pass alone.  Measured at 256 queries
+    // (benchmarks/batch_serving.py, profiles/r1_batch_serving.jsonl) it beats
+    // LDS-pass-first at every size: 100k G(n,p) 1.12 -> 0.56 us/query, 1M
+    // 2.00 -> 1.01, 10M 3.43 -> 2.37, Kronecker-22 13.1 -> 12.4.  The LDS
+    // engine stays the single-query (latency) path.
+    const bool lds_first = I.blds >= 0 ? I.blds != 0 : false;
+    if (lds_first) {
+      launch::lds_batch(I.view(), I.buf, I.h_bq, I.h_bq + k, k, I.d_bslots, I.h_bres, I.h_bpath, Impl::kBatchPath,
+                        seq, I.stream);
+    } else {
+      for (uint32_t i = 0; i < k; ++i) {
+        I.h_bres[i].status = kHandoff;
+        I.h_bres[i].path_on_device = 0;
+        __atomic_store_n(&I.h_bres[i].seq, seq, __ATOMIC_RELEASE);
+      }
+    }
     for (uint32_t i = 0; i < k; ++i) {
       for (uint64_t it = 1; __atomic_load_n(&I.h_bres[i].seq, __ATOMIC_ACQUIRE) != seq; ++it) {
         if ((it & 8191) == 0) {
@@ -677,7 +698,9 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
     }
     if (nglobal) {
       launch::batch_global(I.view(), I.buf.words, I.h_bqidx, nglobal, I.h_bq, I.h_bq + k, I.d_bslots, I.d_bbits,
-                           I.h_bout, I.h_bpath, Impl::kBatchPath, I.bedge_cap, I.stream);
+                           I.h_bout, I.h_bpath, Impl::kBatchPath, I.bedge_cap,
+                           I.bthreads ? I.bthreads : 1024,
+                           I.stream);
       HIP_CHECK(hipStreamSynchronize(I.stream));
     }
     std::vector<char> via_global(k, 0);

@@ -63,6 +63,9 @@ class HipBiBfs {
                                          const SearchOptions& opt = {});
   void set_batch_edge_cap(uint64_t edges);
   uint64_t batch_edge_cap() const;
+  // lds_first: 1 = LDS pass first, 0 = HBM-bitmap pass only, -1 = auto (by n);
+  // threads: HBM-pass workgroup size 256 / 1024, 0 = auto (by query count)
+  void set_batch_tuning(int lds_first, int threads);
 
   // Resident query server: one workgroup stays on the GPU and takes queries
   // from a pinned mailbox, so a query costs no kernel launch.  It exits by

@@ -239,9 +239,16 @@ def test_search_batch_global_pass(gpu_engine, spec):
         assert runs[0] == runs[1] == runs[2]
         if g.n > 131072:
             assert any(r.handoff for r in rs), "expected queries to take the HBM-bitmap pass"
+        for lds_first, threads in ((0, 1024), (0, 256), (1, 1024)):
+            gpu_engine.set_batch_tuning(lds_first, threads)
+            rs = gpu_engine.search_batch(pairs)
+            for (s, d), r, h in zip(pairs, rs, truth):
+                check_result(g.csr, s, d, r.hops, r.path, h)
+        gpu_engine.set_batch_tuning(-1, 0)
         gpu_engine.batch_edge_cap = 16  # almost every query falls back to search()
         rs = gpu_engine.search_batch(pairs[:40])
         for (s, d), r, h in zip(pairs[:40], rs, truth[:40]):
             check_result(g.csr, s, d, r.hops, r.path, h)
     finally:
         gpu_engine.batch_edge_cap = cap0
+        gpu_engine.set_batch_tuning(-1, 0)
