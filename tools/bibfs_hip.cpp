@@ -86,8 +86,9 @@ int main(int argc, char** argv) {
         for (auto& t : r.stats.trace) {
           if (t.mode == 1 || t.mode == 2)  // wave rounds: phase split of wave 0 / the working wave
             std::printf("Stamp cycles: %s round=%d barrier_wait=%d rec+col=%llu row_off=%llu claim=%llu append=%llu\n",
-                        bibfs_mode_name(t.mode), t.side, t.depth, t.edges & 0xffff, (t.edges >> 16) & 0xffff,
-                        (t.edges >> 32) & 0xffff, (t.edges >> 48) & 0xffff);
+                        bibfs_mode_name(t.mode), t.side, t.depth, (unsigned long long)(t.edges & 0xffff),
+                        (unsigned long long)((t.edges >> 16) & 0xffff), (unsigned long long)((t.edges >> 32) & 0xffff),
+                        (unsigned long long)((t.edges >> 48) & 0xffff));
           else
             std::printf("Stamp cycles: %s level=%d barrier=%d book=%llu\n", bibfs_mode_name(t.mode), t.side,
                         t.depth, (unsigned long long)t.frontier);
