@@ -73,6 +73,23 @@ def kronecker(scale: int, edgefactor: int = 16, seed: int = 1) -> Graph:
     return Graph(native.gen_kronecker(int(scale), int(edgefactor), int(seed)), name=f"kron:{scale}:{edgefactor}:{seed}")
 
 
+def parse_spec(spec: str):
+    """Generator spec -> ``(kind, n, arg, seed)``: kind ``"gnp"`` (arg = p) or
+    ``"rmat"`` (arg = undirected edge count; ``kron:S:EF`` is R-MAT with
+    n = 2^S, m = EF * 2^S).  For engines that generate on the device."""
+    f = spec.split(":")
+    if f[0] == "gnp":
+        n = int(f[1])
+        p = float(f[2]) if len(f) > 2 and f[2] else reference_p(n)
+        return "gnp", n, p, int(f[3]) if len(f) > 3 else 1
+    if f[0] == "rmat":
+        return "rmat", int(f[1]), int(f[2]), int(f[3]) if len(f) > 3 else 1
+    if f[0] == "kron":
+        scale, ef = int(f[1]), int(f[2]) if len(f) > 2 else 16
+        return "rmat", 1 << scale, ef << scale, int(f[3]) if len(f) > 3 else 1
+    raise ValueError(f"generator spec must be gnp:/rmat:/kron:, got {spec!r}")
+
+
 def from_spec(spec: str) -> Graph:
     """``gnp:N[:p[:seed]]``, ``rmat:N:M[:seed]``, ``kron:S[:EF[:seed]]`` or a ``.bin`` path."""
     f = spec.split(":")
@@ -87,4 +104,4 @@ def from_spec(spec: str) -> Graph:
     return Graph.from_bin(spec)
 
 
-__all__ = ["Graph", "gnp", "rmat", "kronecker", "from_spec", "reference_p", "REFERENCE_SIZES", "REFERENCE_AVG_DEG"]
+__all__ = ["Graph", "gnp", "rmat", "kronecker", "from_spec", "parse_spec", "reference_p", "REFERENCE_SIZES", "REFERENCE_AVG_DEG"]

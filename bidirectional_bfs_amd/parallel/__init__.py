@@ -22,7 +22,7 @@ import subprocess
 from typing import List, Optional, Sequence
 
 from .._lib import native, tool_path
-from ..models import Graph
+from ..models import Graph, parse_spec
 from ..ops import _DEFAULT_OPTIONS, HipEngine, make_options
 
 MPIEXEC = os.environ.get("BIBFS_MPIEXEC", "/opt/conda/bin/mpiexec")
@@ -119,6 +119,19 @@ def dist_local_run(ranks: int, graph: Graph, queries: Sequence, device: int = 0,
     return native.dist_local_run(int(ranks), int(device), graph.edges, q, options)
 
 
+def dist_local_generate_run(ranks: int, spec: str, queries: Sequence, device: int = 0, options=None, **kw):
+    """Like :func:`dist_local_run`, but every rank generates ``spec``
+    (``gnp:``/``rmat:``/``kron:``) on the device and keeps only its own CSR
+    shard, as the multi-GPU bench does.  Returns ``(results, timing)`` with
+    ``timing = {"build_ms", "query_ms": [rank 0 wall per query], "local_nnz": [per rank]}``.
+    """
+    if options is None:
+        options = make_options(**kw) if kw else _DEFAULT_OPTIONS
+    kind, n, arg, seed = parse_spec(spec)
+    q = [(int(s), int(d)) for s, d in queries]
+    return native.dist_local_generate_run(int(ranks), int(device), kind, n, float(arg), seed, q, options)
+
+
 class ReplicatedServer:
     """Query-parallel serving: rank r answers queries r, r+W, r+2W, ... on its own GPU."""
 
@@ -146,4 +159,4 @@ def run_mpi(tool: str, args: Sequence[str], np: int = 2, timeout: float = 300.0,
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
 
 
-__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "run_mpi", "MPIEXEC"]
+__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "dist_local_generate_run", "run_mpi", "MPIEXEC"]

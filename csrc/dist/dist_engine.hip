@@ -901,4 +901,55 @@ std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& 
   return out[0];
 }
 
+std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
+                                                  double arg, uint64_t seed,
+                                                  const std::vector<std::pair<vid_t, vid_t>>& queries,
+                                                  const SearchOptions& opt, DistLocalTiming* timing) {
+  BIBFS_REQUIRE(ranks >= 1 && ranks <= 16, "dist_local_generate_run: 1..16 ranks");
+  BIBFS_REQUIRE(kind == "gnp" || kind == "rmat", "dist_local_generate_run: kind must be gnp or rmat");
+  auto group = dist::make_local_group(ranks);
+  std::vector<std::vector<SearchResult>> out((size_t)ranks);
+  std::vector<std::string> err((size_t)ranks);
+  std::vector<double> build_ms((size_t)ranks, 0.0), qms;
+  std::vector<uint64_t> nnz((size_t)ranks, 0);
+  std::vector<std::thread> th;
+  for (int r = 0; r < ranks; ++r)
+    th.emplace_back([&, r] {
+      try {
+        DistBiBfs e(dist::make_local_comm(group, r), device);
+        const auto t0 = std::chrono::steady_clock::now();
+        if (kind == "gnp")
+          e.generate_gnp(n, arg, seed);
+        else
+          e.generate_rmat(n, (uint64_t)arg, seed);  // ends with hipFree of the edge list: synchronous
+        build_ms[(size_t)r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        nnz[(size_t)r] = e.local_nnz();
+        for (const auto& q : queries) {
+          const auto q0 = std::chrono::steady_clock::now();
+          out[(size_t)r].push_back(e.search(q.first, q.second, opt));
+          if (r == 0)
+            qms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count());
+        }
+      } catch (const std::exception& ex) {
+        err[(size_t)r] = ex.what();
+        dist::abort_local_group(*group);
+      }
+    });
+  for (auto& t : th) t.join();
+  for (int pass = 0; pass < 2; ++pass)
+    for (int r = 0; r < ranks; ++r)
+      if (!err[(size_t)r].empty() && (pass == 1 || err[(size_t)r].find("aborted") == std::string::npos))
+        throw Error("dist_local_generate_run rank " + std::to_string(r) + ": " + err[(size_t)r]);
+  for (int r = 1; r < ranks; ++r)
+    for (size_t i = 0; i < queries.size(); ++i)
+      BIBFS_REQUIRE(out[(size_t)r][i].hops == out[0][i].hops && out[(size_t)r][i].path == out[0][i].path,
+                    "dist_local_generate_run: ranks returned different results");
+  if (timing) {
+    timing->build_ms = *std::max_element(build_ms.begin(), build_ms.end());
+    timing->query_ms = std::move(qms);
+    timing->local_nnz = std::move(nnz);
+  }
+  return out[0];
+}
+
 }  // namespace bibfs

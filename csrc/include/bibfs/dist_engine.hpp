@@ -97,4 +97,19 @@ std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& 
                                          const std::vector<std::pair<vid_t, vid_t>>& queries,
                                          const SearchOptions& opt = {});
 
+// Same harness, but every rank generates the graph on the device itself
+// (kind "gnp": arg = p; kind "rmat": arg = edge count) and keeps only its
+// vertex block's CSR rows -- the path the multi-GPU bench takes, so a
+// CSR-sharded Kronecker graph can be rehearsed on one GPU.  Fills rank 0's
+// wall time per query and the slowest rank's build time.
+struct DistLocalTiming {
+  double build_ms = 0.0;
+  std::vector<double> query_ms;
+  std::vector<uint64_t> local_nnz;  // per rank
+};
+std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
+                                                  double arg, uint64_t seed,
+                                                  const std::vector<std::pair<vid_t, vid_t>>& queries,
+                                                  const SearchOptions& opt, DistLocalTiming* timing);
+
 }  // namespace bibfs

@@ -328,4 +328,22 @@ PYBIND11_MODULE(_native, m) {
       });
   m.def("dist_local_run", &dist_local_run, py::arg("ranks"), py::arg("device"), py::arg("edges"),
         py::arg("queries"), py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "dist_local_generate_run",
+      [](int ranks, int device, const std::string& kind, uint32_t n, double arg, uint64_t seed,
+         const std::vector<std::pair<vid_t, vid_t>>& queries, const SearchOptions& opt) {
+        DistLocalTiming t;
+        std::vector<SearchResult> rs;
+        {
+          py::gil_scoped_release nogil;
+          rs = dist_local_generate_run(ranks, device, kind, n, arg, seed, queries, opt, &t);
+        }
+        py::dict d;
+        d["build_ms"] = t.build_ms;
+        d["query_ms"] = t.query_ms;
+        d["local_nnz"] = t.local_nnz;
+        return py::make_tuple(rs, d);
+      },
+      py::arg("ranks"), py::arg("device"), py::arg("kind"), py::arg("n"), py::arg("arg"), py::arg("seed"),
+      py::arg("queries"), py::arg("options") = SearchOptions{});
 }
