@@ -30,7 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--specs", default="kron:22,kron:27")
     ap.add_argument("--ranks", default="2,4")
-    ap.add_argument("--queries", type=int, default=16)
+    ap.add_argument("--queries", type=int, default=48)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--out")
     a = ap.parse_args()
@@ -43,13 +43,18 @@ def main():
             t0 = time.perf_counter()
             rs, t = dist_local_generate_run(ranks, spec, qs)
             wall = time.perf_counter() - t0
-            found = [(r, ms) for r, ms in zip(rs, t["query_ms"]) if r.found and r.hops > 0]
-            qms = [ms for _, ms in found]
+            found = [(r, ms, st) for r, ms, st in zip(rs, t["query_ms"], t["stats"]) if r.found and r.hops > 0]
+            qms = [ms for _, ms, _ in found]
             rec = {
                 "spec": spec, "n": n, "ranks": ranks, "queries": len(qs), "found": len(found),
                 "build_ms": round(t["build_ms"], 3), "wall_s": round(wall, 3),
                 "median_query_ms": round(statistics.median(qms), 4) if qms else None,
-                "mean_hops": round(statistics.mean(r.hops for r, _ in found), 3) if found else None,
+                "mean_hops": round(statistics.mean(r.hops for r, _, _ in found), 3) if found else None,
+                "mean_rounds": round(statistics.mean(st["rounds"] for _, _, st in found), 3) if found else None,
+                "median_round_ms": round(statistics.median(ms / max(1, st["rounds"]) for _, ms, st in found), 4)
+                if found else None,
+                "mean_exchanged_bytes": round(statistics.mean(st["exchanged_bytes"] for _, _, st in found)) if found else None,
+                "dense_levels": sum(st["dense_levels"] for _, _, st in found),
                 "local_nnz": t["local_nnz"], "max_shard_fraction": round(max(t["local_nnz"]) / max(1, sum(t["local_nnz"])), 4),
             }
             line = json.dumps(rec)

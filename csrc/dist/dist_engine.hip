@@ -911,6 +911,7 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
   std::vector<std::vector<SearchResult>> out((size_t)ranks);
   std::vector<std::string> err((size_t)ranks);
   std::vector<double> build_ms((size_t)ranks, 0.0), qms;
+  std::vector<DistLevelStats> qstats;
   std::vector<uint64_t> nnz((size_t)ranks, 0);
   std::vector<std::thread> th;
   for (int r = 0; r < ranks; ++r)
@@ -927,8 +928,10 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
         for (const auto& q : queries) {
           const auto q0 = std::chrono::steady_clock::now();
           out[(size_t)r].push_back(e.search(q.first, q.second, opt));
-          if (r == 0)
+          if (r == 0) {
             qms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count());
+            qstats.push_back(e.last_stats());
+          }
         }
       } catch (const std::exception& ex) {
         err[(size_t)r] = ex.what();
@@ -948,6 +951,7 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
     timing->build_ms = *std::max_element(build_ms.begin(), build_ms.end());
     timing->query_ms = std::move(qms);
     timing->local_nnz = std::move(nnz);
+    timing->stats = std::move(qstats);
   }
   return out[0];
 }

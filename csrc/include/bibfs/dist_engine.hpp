@@ -106,6 +106,7 @@ struct DistLocalTiming {
   double build_ms = 0.0;
   std::vector<double> query_ms;
   std::vector<uint64_t> local_nnz;  // per rank
+  std::vector<DistLevelStats> stats;  // rank 0, per query
 };
 std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
                                                   double arg, uint64_t seed,

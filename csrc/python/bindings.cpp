@@ -59,6 +59,20 @@ py::dict stats_dict(const SearchStats& s) {
 
 }  // namespace
 
+static py::dict dist_stats_dict(const DistLevelStats& s) {
+  py::dict d;
+  d["levels"] = s.levels;
+  d["rounds"] = s.rounds;
+  d["lockstep_rounds"] = s.lockstep_rounds;
+  d["sparse_levels"] = s.sparse_levels;
+  d["dense_levels"] = s.dense_levels;
+  d["overflow_levels"] = s.overflow_levels;
+  d["count_syncs"] = s.count_syncs;
+  d["exchanged_bytes"] = s.exchanged_bytes;
+  d["comm_ms"] = s.comm_ms;
+  return d;
+}
+
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native bidirectional BFS core (HIP/CDNA4 + RCCL)";
 
@@ -312,20 +326,7 @@ PYBIND11_MODULE(_native, m) {
       .def("barrier", &DistBiBfs::barrier, py::call_guard<py::gil_scoped_release>())
       .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("backend", &DistBiBfs::backend)
-      .def_property_readonly("last_stats", [](const DistBiBfs& e) {
-        const DistLevelStats& s = e.last_stats();
-        py::dict d;
-        d["levels"] = s.levels;
-        d["rounds"] = s.rounds;
-        d["lockstep_rounds"] = s.lockstep_rounds;
-        d["sparse_levels"] = s.sparse_levels;
-        d["dense_levels"] = s.dense_levels;
-        d["overflow_levels"] = s.overflow_levels;
-        d["count_syncs"] = s.count_syncs;
-        d["exchanged_bytes"] = s.exchanged_bytes;
-        d["comm_ms"] = s.comm_ms;
-        return d;
-      });
+      .def_property_readonly("last_stats", [](const DistBiBfs& e) { return dist_stats_dict(e.last_stats()); });
   m.def("dist_local_run", &dist_local_run, py::arg("ranks"), py::arg("device"), py::arg("edges"),
         py::arg("queries"), py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>());
   m.def(
@@ -342,6 +343,9 @@ PYBIND11_MODULE(_native, m) {
         d["build_ms"] = t.build_ms;
         d["query_ms"] = t.query_ms;
         d["local_nnz"] = t.local_nnz;
+        py::list st;
+        for (const auto& x : t.stats) st.append(dist_stats_dict(x));
+        d["stats"] = st;
         return py::make_tuple(rs, d);
       },
       py::arg("ranks"), py::arg("device"), py::arg("kind"), py::arg("n"), py::arg("arg"), py::arg("seed"),
