@@ -74,3 +74,18 @@ def test_partition_rows_union(P):
             cols.append(sorted(part.col[part.row_off[i]:part.row_off[i + 1]]))
     assert len(cols) == 1001
     assert cols == [sorted(full.col[full.row_off[v]:full.row_off[v + 1]]) for v in range(1001)]
+
+
+def test_parse_spec_device_generator_args():
+    from bidirectional_bfs_amd.models import parse_spec, reference_p
+
+    assert parse_spec("kron:27") == ("rmat", 1 << 27, 16 << 27, 1)
+    assert parse_spec("kron:20:8:3") == ("rmat", 1 << 20, 8 << 20, 3)
+    assert parse_spec("rmat:65536:1048576:4") == ("rmat", 65536, 1048576, 4)
+    kind, n, p, seed = parse_spec("gnp:100000::6")
+    assert (kind, n, seed) == ("gnp", 100000, 6) and p == reference_p(100000)
+    assert parse_spec("gnp:1000:0.01")[2] == 0.01
+    import pytest
+
+    with pytest.raises(ValueError):
+        parse_spec("graph.bin")
