@@ -1,0 +1,35 @@
+"""bench.py's output line (driver contract) built from synthetic per-config
+numbers, no GPU: required keys, whole-job value, weak vs strong scaling,
+vs_baseline only for the 100k headline graph."""
+import argparse
+import json
+
+import bench
+
+
+def _head(n=100000, gteps=4.5, ms=0.024):
+    return {"n": n, "m": 110201, "seed": 6, "gteps": gteps, "ms_per_step": ms, "device_ms_per_query": 0.017,
+            "gteps_inspected": 0.08, "mean_hops": 14.3, "build_ms": 80.0, "batched": None}
+
+
+def _args(mode="replicated", steps=400, warmup=50):
+    return argparse.Namespace(mode=mode, steps=steps, warmup=warmup, no_resident=False)
+
+
+def test_report_contract_keys_and_baseline():
+    out = bench.report(_args(), 8, _head(gteps=36.0), {}, {})
+    json.dumps(out)  # one JSON line
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["n_gpus"] == 8 and out["steps"] == 400 and out["warmup"] == 50
+    assert out["higher_is_better"] is True and out["scaling"] == "weak" and out["data"] == "synthetic"
+    assert out["value"] == 36.0
+    assert abs(out["vs_baseline"] - 36.0 / bench.BASELINE_100K_GTEPS) < 1e-3
+    assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 8
+
+
+def test_report_partitioned_is_strong_scaling_and_other_graph_has_no_baseline():
+    out = bench.report(_args(mode="partitioned"), 2, _head(n=1000000), {}, {})
+    assert out["scaling"] == "strong" and out["vs_baseline"] is None
+    assert out["config"]["parallelism"] == "vertex-partition2" and out["config"]["global_batch"] == 1
