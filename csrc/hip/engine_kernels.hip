@@ -73,6 +73,14 @@ using namespace dev;
 #endif
 constexpr bool kWidUniform = BIBFS_KNOB_WID_UNIFORM;
 constexpr bool kAppendBallot = BIBFS_KNOB_APPEND_BALLOT;
+// Resident server: the mailbox diagnostics (stage / seen / poll latency) are
+// system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
+// issued them, its first global load of the search would wait for their PCIe
+// acks.  1 = the last wave issues them (it is parked during small rounds).
+#ifndef BIBFS_KNOB_DIAG_WAVE
+#define BIBFS_KNOB_DIAG_WAVE 1
+#endif
+constexpr bool kDiagOffWave0 = BIBFS_KNOB_DIAG_WAVE;
 
 constexpr int kLdsThreads = 1024;
 constexpr int kHashBits = 13;
@@ -1071,9 +1079,12 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
   __syncthreads();
   if (!uni(srv_won)) return;
   if (tid == 0) __hip_atomic_store(&box->alive, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __shared__ uint32_t diag[3];  // seen, poll latency, polls
+  __shared__ unsigned long long diag_t;
+  constexpr int kDiagTid = kDiagOffWave0 ? kLdsThreads - kWave : 0;  // lane 0 of the last wave
   for (;;) {
+    if (tid == kDiagTid) __hip_atomic_store(&box->stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (wid == 0) {
-      if (tid == 0) __hip_atomic_store(&box->stage, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t stop = 0, polls = 0;
       uint4 rq;
@@ -1103,11 +1114,10 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
         }
       }
       if (tid == 0) {
-        __hip_atomic_store(&box->stage, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&box->seen, rq.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&box->pad[0], (uint32_t)lat, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&box->pad[1], polls, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&P.h.res->rt_pickup, tl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        diag[0] = rq.x;
+        diag[1] = (uint32_t)lat;
+        diag[2] = polls;
+        diag_t = tl;
         cmd[0] = stop;
         cmd[1] = rq.x;
         cmd[2] = rq.y;
@@ -1117,6 +1127,13 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
       }
     }
     __syncthreads();
+    if (tid == kDiagTid) {
+      __hip_atomic_store(&box->stage, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->seen, diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->pad[0], diag[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&box->pad[1], diag[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&P.h.res->rt_pickup, diag_t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     if (uni(cmd[0])) break;
     LdsParams<OffT> Q = P;
     Q.seq = uni(cmd[1]);
@@ -1129,7 +1146,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
     last_seq = Q.seq;
     __syncthreads();  // every wave has read cmd before thread 0 may overwrite it
     lds_search_body<OffT, false, kBm>(Q, true);
-    if (tid == 0) __hip_atomic_store(&box->stage, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (tid == kDiagTid) __hip_atomic_store(&box->stage, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (tid == 0) {
     __threadfence_system();
