@@ -870,10 +870,15 @@ uint32_t DistBiBfs::hi() const { return p_->hi; }
 const DistLevelStats& DistBiBfs::last_stats() const { return p_->stats; }
 const char* DistBiBfs::backend() const { return p_->comm->name(); }
 
-std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& el,
-                                         const std::vector<std::pair<vid_t, vid_t>>& queries,
-                                         const SearchOptions& opt) {
-  BIBFS_REQUIRE(ranks >= 1 && ranks <= 16, "dist_local_run: 1..16 ranks");
+namespace {
+
+// Runs `body(engine, rank, results)` on `ranks` threads, each with a DistBiBfs
+// on `device` over one in-process local group.  A failing rank aborts the
+// group (so peers blocked in a collective return); its own message is thrown.
+// Returns rank 0's results after checking that every rank agrees.
+template <typename Body>
+std::vector<SearchResult> run_local_ranks(const char* who, int ranks, int device, size_t nq, Body&& body) {
+  BIBFS_REQUIRE(ranks >= 1 && ranks <= 16, std::string(who) + ": 1..16 ranks");
   auto group = dist::make_local_group(ranks);
   std::vector<std::vector<SearchResult>> out((size_t)ranks);
   std::vector<std::string> err((size_t)ranks);
@@ -882,8 +887,7 @@ std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& 
     th.emplace_back([&, r] {
       try {
         DistBiBfs e(dist::make_local_comm(group, r), device);
-        e.load_edges(el);
-        for (const auto& q : queries) out[(size_t)r].push_back(e.search(q.first, q.second, opt));
+        body(e, r, out[(size_t)r]);
       } catch (const std::exception& ex) {
         err[(size_t)r] = ex.what();
         dist::abort_local_group(*group);
@@ -893,31 +897,37 @@ std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& 
   for (int pass = 0; pass < 2; ++pass)  // the failing rank's own message before the others' "aborted"
     for (int r = 0; r < ranks; ++r)
       if (!err[(size_t)r].empty() && (pass == 1 || err[(size_t)r].find("aborted") == std::string::npos))
-        throw Error("dist_local_run rank " + std::to_string(r) + ": " + err[(size_t)r]);
+        throw Error(std::string(who) + " rank " + std::to_string(r) + ": " + err[(size_t)r]);
   for (int r = 1; r < ranks; ++r)
-    for (size_t i = 0; i < queries.size(); ++i)
+    for (size_t i = 0; i < nq; ++i)
       BIBFS_REQUIRE(out[(size_t)r][i].hops == out[0][i].hops && out[(size_t)r][i].path == out[0][i].path,
-                    "dist_local_run: ranks returned different results");
-  return out[0];
+                    std::string(who) + ": ranks returned different results");
+  return std::move(out[0]);
+}
+
+}  // namespace
+
+std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& el,
+                                         const std::vector<std::pair<vid_t, vid_t>>& queries,
+                                         const SearchOptions& opt) {
+  return run_local_ranks("dist_local_run", ranks, device, queries.size(),
+                         [&](DistBiBfs& e, int, std::vector<SearchResult>& out) {
+                           e.load_edges(el);
+                           for (const auto& q : queries) out.push_back(e.search(q.first, q.second, opt));
+                         });
 }
 
 std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
                                                   double arg, uint64_t seed,
                                                   const std::vector<std::pair<vid_t, vid_t>>& queries,
                                                   const SearchOptions& opt, DistLocalTiming* timing) {
-  BIBFS_REQUIRE(ranks >= 1 && ranks <= 16, "dist_local_generate_run: 1..16 ranks");
   BIBFS_REQUIRE(kind == "gnp" || kind == "rmat", "dist_local_generate_run: kind must be gnp or rmat");
-  auto group = dist::make_local_group(ranks);
-  std::vector<std::vector<SearchResult>> out((size_t)ranks);
-  std::vector<std::string> err((size_t)ranks);
-  std::vector<double> build_ms((size_t)ranks, 0.0), qms;
+  std::vector<double> build_ms((size_t)std::max(ranks, 1), 0.0), qms;
+  std::vector<uint64_t> nnz((size_t)std::max(ranks, 1), 0);
   std::vector<DistLevelStats> qstats;
-  std::vector<uint64_t> nnz((size_t)ranks, 0);
-  std::vector<std::thread> th;
-  for (int r = 0; r < ranks; ++r)
-    th.emplace_back([&, r] {
-      try {
-        DistBiBfs e(dist::make_local_comm(group, r), device);
+  auto rs = run_local_ranks(
+      "dist_local_generate_run", ranks, device, queries.size(),
+      [&](DistBiBfs& e, int r, std::vector<SearchResult>& out) {
         const auto t0 = std::chrono::steady_clock::now();
         if (kind == "gnp")
           e.generate_gnp(n, arg, seed);
@@ -927,33 +937,20 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
         nnz[(size_t)r] = e.local_nnz();
         for (const auto& q : queries) {
           const auto q0 = std::chrono::steady_clock::now();
-          out[(size_t)r].push_back(e.search(q.first, q.second, opt));
+          out.push_back(e.search(q.first, q.second, opt));
           if (r == 0) {
             qms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count());
             qstats.push_back(e.last_stats());
           }
         }
-      } catch (const std::exception& ex) {
-        err[(size_t)r] = ex.what();
-        dist::abort_local_group(*group);
-      }
-    });
-  for (auto& t : th) t.join();
-  for (int pass = 0; pass < 2; ++pass)
-    for (int r = 0; r < ranks; ++r)
-      if (!err[(size_t)r].empty() && (pass == 1 || err[(size_t)r].find("aborted") == std::string::npos))
-        throw Error("dist_local_generate_run rank " + std::to_string(r) + ": " + err[(size_t)r]);
-  for (int r = 1; r < ranks; ++r)
-    for (size_t i = 0; i < queries.size(); ++i)
-      BIBFS_REQUIRE(out[(size_t)r][i].hops == out[0][i].hops && out[(size_t)r][i].path == out[0][i].path,
-                    "dist_local_generate_run: ranks returned different results");
+      });
   if (timing) {
     timing->build_ms = *std::max_element(build_ms.begin(), build_ms.end());
     timing->query_ms = std::move(qms);
     timing->local_nnz = std::move(nnz);
     timing->stats = std::move(qstats);
   }
-  return out[0];
+  return rs;
 }
 
 }  // namespace bibfs
