@@ -4,7 +4,7 @@ shape, reported as GTEPS(M/t) (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--graph gnp:100000::6]
                     [--mode replicated|partitioned] [--extra-graph gnp:10000000::1,kron:22:16:1]
-                    [--dist-graphs gnp:1000000::2,kron:22:16:1]
+                    [--dist-graphs gnp:1000000::2,kron:22:16:1,kron:27:16:1]
 
 One step = one bidirectional-BFS query per GPU: host call -> search on the
 MI355X -> hop count AND the full path back in host memory ("end-to-end ms to
@@ -14,22 +14,27 @@ there is no dataset); queries are seeded random vertex pairs that are
 connected (the first is (0, N-1) like benchmark_test.sh:43), fixed before
 timing and rotated over every step, so no result is reused.
 
-Modes (N > 1 is launched by torch.distributed.run, one rank per GPU):
-  replicated  (default, weak scaling) every GPU holds the whole graph and
-              answers its own queries -- production query serving;
-  partitioned (strong scaling) the graph is 1-D partitioned over the GPUs and
-              every query is one collective search over RCCL (v4 capability).
+Launch: N > 1 runs one rank per GPU.  Under torch.distributed.run (the
+driver's launcher) the ranks come from the environment; `python bench.py
+--gpus N` without a launcher starts torch.distributed.run itself as a child
+process BEFORE anything touches the GPU, forwards rank 0's line and exits with
+the child's status.
 
-value = whole-job GTEPS = M * (queries answered by all GPUs) / max-rank wall
-time; vs_baseline divides by the best published 100k number in BASELINE.md
-(v1 serial: 0.116 ms -> 0.952 GTEPS(M/t)).
+Two scaling curves, both measured at every N:
+  headline    (`value`, weak scaling, mode "replicated") every GPU holds the
+              whole graph and answers its own queries -- production query
+              serving; value = aggregate GTEPS over all GPUs;
+  partitioned (`detail.partitioned`, strong scaling, the v4 capability) the
+              graph is 1-D partitioned over the N GPUs (device-generated CSR
+              shards) and every query is ONE collective search over RCCL;
+              configs: 1M G(n,p) (BASELINE config 3), Kronecker 22 (config 4)
+              and Kronecker 27, 2.15B edges (config 5).  Each is checked
+              against the single-GPU engine's hop counts (`verified`).
+`--mode partitioned` makes the partitioned engine the headline instead.
 
-Secondary configs (BASELINE.json), reported under detail and never folded
-into `value`: `extra` = the same serving loop on 10M-vertex G(n,p) and on a
-scale-22 Kronecker (R-MAT, Graph500 parameters; the direction-optimizing grid
-engine); with N > 1 GPUs, `partitioned` = the 1-D partitioned RCCL engine
-(one collective search over all GPUs, strong scaling) on 1M G(n,p) (the v4
-config) and on Kronecker scale 22.
+vs_baseline divides by the best published 100k number in BASELINE.md (v1
+serial: 0.116 ms -> 0.952 GTEPS(M/t)); `cpu_serial_ms` is this repo's own -O3
+serial engine on the same graph and pairs, for an explicit CPU comparison.
 """
 from __future__ import annotations
 
@@ -37,19 +42,86 @@ import argparse
 import json
 import os
 import random
+import socket
+import subprocess
 import sys
 import threading
 import time
 
-import torch  # first: the HIP runtime torch ships is the one our extension then binds to
-import torch.distributed as dist
-
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
 
 BASELINE_100K_GTEPS = 110000 / (0.115546e-3) / 1e9  # v1 @ 100k, M ~ 1.1 (N - 1)
 BASELINE_100K_MS = 0.115546
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--graph", default="gnp:100000::6")
+    ap.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated")
+    ap.add_argument("--extra-graph", default="gnp:10000000::1,kron:22:16:1",
+                    help="comma-separated secondary configs reported under 'extra' (empty to skip)")
+    ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1,kron:27:16:1",
+                    help="configs run through the partitioned RCCL engine at every N (empty to skip)")
+    ap.add_argument("--dist-steps", type=int, default=20)
+    ap.add_argument("--secondary-timeout", type=float, default=420.0,
+                    help="seconds allowed for the extra + partitioned configs together; past it the "
+                         "headline line is printed with the unfinished configs marked and every rank exits "
+                         "non-zero")
+    ap.add_argument("--extra-steps", type=int, default=50)
+    ap.add_argument("--pairs", type=int, default=64)
+    ap.add_argument("--no-resident", action="store_true",
+                    help="launch one kernel per query instead of the resident query server")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="also measure batched serving: K queries per launch, one CU each (0 = skip)")
+    ap.add_argument("--no-cpu-ref", action="store_true", help="skip the CPU serial comparison")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for the bench's own barriers/reductions (nccl = RCCL; "
+                         "gloo lets several ranks share one GPU for rehearsals; the partitioned engine "
+                         "needs one GPU per rank and runs only with nccl)")
+    return ap.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# self-launch (no GPU is touched in this process)
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(nproc: int, argv) -> list:
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(nproc: int, argv, cmd=None) -> int:
+    """Run the N-rank job as a child process group, forward rank 0's JSON line.
+
+    Returns the child's exit status, or 1 when it exited 0 without a line."""
+    cmd = cmd or launcher_cmd(nproc, argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.run(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    line = None
+    for ln in proc.stdout.splitlines():
+        s = ln.strip()
+        if s.startswith("{") and '"metric"' in s:
+            line = s
+        elif s:
+            print(s, file=sys.stderr)
+    if line is not None:
+        print(line, flush=True)
+    if proc.returncode != 0:
+        return proc.returncode
+    return 0 if line is not None else 1
+
+
+# ---------------------------------------------------------------------------
 def parse_spec(spec: str):
     """gnp:N[:p[:seed]], rmat:N:M[:seed] or kron:SCALE[:EF[:seed]] -> (kind, n, arg, seed)."""
     f = spec.split(":")
@@ -74,7 +146,8 @@ def generate(eng, spec: str):
 
 
 def pick_pairs(eng, n: int, count: int, seed: int):
-    """Seeded connected (src, dst) pairs; (0, N-1) first (benchmark_test.sh:43)."""
+    """Seeded connected (src, dst) pairs; (0, N-1) first (benchmark_test.sh:43).
+    Returns [(src, dst, hops)]."""
     rng = random.Random(seed)
     pairs, tries = [], 0
     cand = [(0, n - 1)]
@@ -83,12 +156,13 @@ def pick_pairs(eng, n: int, count: int, seed: int):
         tries += 1
         r = eng.search(s, d)
         if r.found and r.hops > 0:
-            pairs.append((s, d))
+            pairs.append((s, d, int(r.hops)))
     return pairs
 
 
-def report(a, world: int, head: dict, extra: dict, partitioned: dict) -> dict:
+def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks=None) -> dict:
     """The one JSON line rank 0 prints (driver contract)."""
+    part = a.mode == "partitioned"
     return {
         "metric": "GTEPS(M/t), end-to-end bi-BFS shortest-path query (G(n,2.2/n), path returned to host)",
         "value": round(head["gteps"], 4),
@@ -98,62 +172,71 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict) -> dict:
         "warmup": a.warmup,
         "ms_per_step": round(head["ms_per_step"], 6),
         "higher_is_better": True,
-        "scaling": "strong" if a.mode == "partitioned" else "weak",
+        "scaling": "strong" if part else "weak",
         "vs_baseline": round(head["gteps"] / BASELINE_100K_GTEPS, 3) if head["n"] == 100000 else None,
         "dtype": "int32",
         "data": "synthetic",
         "config": {
             "model": f"G(n={head['n']}, p=2.2/n) seed={head['seed']}, M={head['m']}",
-            "global_batch": world if a.mode == "replicated" else 1,
+            "global_batch": 1 if part else world,
             "seq_len": head["n"],
-            "parallelism": (f"dp{world}" if a.mode == "replicated" else f"vertex-partition{world}"),
+            "parallelism": (f"vertex-partition{world}" if part else f"dp{world}"),
         },
         "detail": {
             "query_ms": round(head["ms_per_step"], 6),
             "device_ms_per_query": round(head["device_ms_per_query"], 6),
+            "cpu_serial_ms": head.get("cpu_serial_ms"),
             "baseline_best_100k_ms": BASELINE_100K_MS,
             "gteps_inspected": head["gteps_inspected"],
             "mean_hops": head["mean_hops"],
             "graph_build_ms": round(head["build_ms"], 3),
-            "resident_server": a.mode == "replicated" and not a.no_resident,
+            "resident_server": (not part) and not a.no_resident,
             "batched_serving": head["batched"],
+            "rccl_ranks": rccl_ranks,
+            "weak_scaling": "headline: replicated graph, every GPU answers its own queries (no inter-GPU traffic)",
+            "strong_scaling": "partitioned: one query = one collective search over all GPUs (RCCL over xGMI)",
             "extra": extra,
             "partitioned": partitioned,
         },
     }
 
 
-def main() -> int:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=400)
-    ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--graph", default="gnp:100000::6")
-    ap.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated")
-    ap.add_argument("--extra-graph", default="gnp:10000000::1,kron:22:16:1",
-                    help="comma-separated secondary configs reported under 'extra' (empty to skip)")
-    ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1",
-                    help="N > 1 only: configs run through the partitioned RCCL engine (empty to skip)")
-    ap.add_argument("--dist-steps", type=int, default=20)
-    ap.add_argument("--secondary-timeout", type=float, default=240.0,
-                    help="seconds allowed for the extra + partitioned configs together; past it the "
-                         "headline line is printed with the unfinished configs marked and every rank exits")
-    ap.add_argument("--extra-steps", type=int, default=50)
-    ap.add_argument("--pairs", type=int, default=64)
-    ap.add_argument("--no-resident", action="store_true",
-                    help="launch one kernel per query instead of the resident query server")
-    ap.add_argument("--batch", type=int, default=256,
-                    help="also measure batched serving: K queries per launch, one CU each (0 = skip)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process-group backend for the bench's own barriers/reductions (nccl = RCCL; "
-                         "gloo lets several ranks share one GPU for rehearsals)")
-    a = ap.parse_args()
+def cpu_serial_ms(spec: str, pairs, reps: int = 20):
+    """Median search time of this repo's -O3 serial engine (v1 parity) on the same graph and pairs."""
+    from bidirectional_bfs_amd import native
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    kind, n, arg, seed = parse_spec(spec)
+    el = native.gen_gnp(n, arg, seed) if kind == "gnp" else native.gen_rmat(n, int(arg), seed, 0.57, 0.19, 0.19)
+    eng = native.SerialBiBfs(native.build_csr(el))
+    ts = []
+    for i in range(reps * len(pairs)):
+        s, d, h = pairs[i % len(pairs)]
+        r = eng.search(s, d)
+        assert r.hops == h, (s, d, r.hops, h)
+        ts.append(r.search_ms)
+    ts.sort()
+    return ts[len(ts) // 2], sum(ts) / len(ts)
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else list(argv)
+    a = parse_args(argv)
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        return spawn_ranks(a.gpus, argv)  # before any GPU call in this process
+    world = int(env_world or "1")
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+
+    import torch  # first: the HIP runtime torch ships is the one our extension then binds to
+    import torch.distributed as dist
+
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = max(1, torch.cuda.device_count())
-    local = local % ndev  # one rank per GPU; with gloo, extra ranks may share a GPU
+    shared_gpu = local >= ndev  # gloo rehearsal: several ranks on one GPU
+    local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -177,31 +260,31 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def run_config(spec: str, steps: int, warmup: int, mode: str = a.mode):
+    def all_ranks_ok(ok: bool) -> bool:
+        if world == 1:
+            return ok
+        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64, device=dev if a.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) == 0.0
+
+    def run_replicated(spec: str, steps: int, warmup: int, cpu_ref: bool = False):
         _, n, _, seed = parse_spec(spec)
         t0 = time.perf_counter()
-        if mode == "partitioned" and world > 1:
-            eng = generate(DistEngine.from_torch_distributed(local), spec)
-            m = eng.m
-        else:
-            eng = generate(HipEngine(local), spec)
-            eng.set_resident(not a.no_resident)
-            m = eng.m
+        eng = generate(HipEngine(local), spec)
+        eng.set_resident(not a.no_resident)
+        m = eng.m
         build_s = time.perf_counter() - t0
-        pairs = pick_pairs(eng, n, a.pairs if mode != "partitioned" else min(a.pairs, steps + warmup), 12345)
+        pairs = pick_pairs(eng, n, a.pairs, 12345)
         assert pairs, f"no connected pairs found in {spec}"
 
         def query(i):
-            if mode == "partitioned" and world > 1:
-                s, d = pairs[i % len(pairs)]
-            else:
-                s, d = pairs[(i * world + rank) % len(pairs)]
+            s, d, h = pairs[(i * world + rank) % len(pairs)]
             r = eng.search(s, d)
             path = r.path  # the path is part of every answer (materialised on the host)
-            assert r.found and len(path) == r.hops + 1
+            assert r.found and r.hops == h and len(path) == h + 1
             return r
 
-        resident = hasattr(eng, "set_resident") and not a.no_resident
+        resident = not a.no_resident
 
         def park():
             # A device-wide synchronize waits for every kernel, the resident
@@ -225,14 +308,15 @@ def main() -> int:
         hops = sum(r.hops for r in done)
         insp = sum(r.edges_inspected for r in done)
         dev_ms = sum(r.search_ms for r in done)
-        queries = steps * (1 if mode == "partitioned" else world)
+        queries = steps * world
         batched = None
-        if a.batch > 0 and mode == "replicated" and hasattr(eng, "search_batch"):
+        if a.batch > 0:
             # throughput serving: K distinct queries per launch (pairs cycled), steady state
             park()
             bp = [pairs[(i * world + rank) % len(pairs)] for i in range(a.batch)]
-            bs = [s for s, _ in bp]
-            bd = [d for _, d in bp]
+            bs = [s for s, _, _ in bp]
+            bd = [d for _, d, _ in bp]
+            bh_ref = [h for _, _, h in bp]
             for _ in range(3):
                 eng.search_batch_arrays(bs, bd)
             barrier()
@@ -243,6 +327,7 @@ def main() -> int:
                 assert (bh >= 0).all() and (boff[1:] - boff[:-1] == bh + 1).all()
             barrier()
             bdt = max_over_ranks(time.perf_counter() - tb)
+            assert list(bh) == bh_ref
             bq = reps * a.batch * world
             batched = {"batch": a.batch, "launches": reps, "ms_per_batch": bdt * 1e3 / reps,
                        "us_per_query": bdt * 1e6 / (reps * a.batch), "queries_per_s": bq / bdt,
@@ -250,61 +335,139 @@ def main() -> int:
         out = {
             "n": n, "m": m, "seed": seed, "wall_s": dt, "ms_per_step": dt * 1e3 / steps,
             "gteps": m * queries / dt / 1e9,
-            "gteps_inspected": insp * (1 if mode == "partitioned" else world) / dt / 1e9,
+            "gteps_inspected": insp * world / dt / 1e9,
             "mean_hops": hops / steps, "device_ms_per_query": dev_ms / steps,
             "build_ms": build_s * 1e3, "end_to_end_first_query_ms": build_s * 1e3 + dt * 1e3 / steps,
             "queries": queries, "batched": batched,
         }
-        if mode == "partitioned" and world > 1:
-            out["engine"] = f"DistBiBfs/{eng.backend} x{world}"
-            out["last_query_stats"] = eng.last_stats
-        if hasattr(eng, "release"):
-            eng.release()  # free HBM before the next config
+        eng.release()  # free HBM before the next config
+        if cpu_ref and not a.no_cpu_ref:
+            med, mean = cpu_serial_ms(spec, pairs)
+            out["cpu_serial_ms"] = round(med, 6)
+            out["cpu_serial_mean_ms"] = round(mean, 6)
         return out
 
-    head = run_config(a.graph, a.steps, a.warmup)
+    def dist_engine():
+        if world == 1:
+            return DistEngine(0, 1, local, DistEngine.unique_id())
+        return DistEngine.from_torch_distributed(local)
+
+    def run_partitioned(spec: str, steps: int, warmup: int):
+        """Strong scaling: the graph sharded over all ranks, one collective search per query.
+        Pairs and their hop counts come from the single-GPU engine on the same graph."""
+        _, n, _, seed = parse_spec(spec)
+        ref = generate(HipEngine(local), spec)
+        pairs = pick_pairs(ref, n, min(a.pairs, steps + warmup), 12345)
+        ref.release()
+        del ref
+        assert pairs, f"no connected pairs found in {spec}"
+        barrier()
+        t0 = time.perf_counter()
+        eng = generate(dist_engine(), spec)
+        build_ms = max_over_ranks((time.perf_counter() - t0) * 1e3)
+        m = eng.m
+        wrong = []
+
+        def query(i):
+            s, d, h = pairs[i % len(pairs)]
+            r = eng.search(s, d)
+            if not (r.found and r.hops == h and len(r.path) == h + 1 and r.path[0] == s and r.path[-1] == d):
+                wrong.append((s, d, h, r.hops))
+            return r
+
+        for i in range(warmup):
+            query(i)
+        eng.barrier()
+        barrier()
+        done = []
+        t0 = time.perf_counter()
+        for i in range(steps):
+            done.append((query(warmup + i), eng.last_stats))
+        eng.barrier()
+        dt = max_over_ranks(time.perf_counter() - t0)
+        ok = all_ranks_ok(not wrong)
+        st = [s for _, s in done]
+        rounds = sum(s["rounds"] for s in st) / steps
+        out = {
+            "engine": f"DistBiBfs/{eng.backend}", "ranks": world, "rccl_ranks": eng.world,
+            "n": n, "m": m, "seed": seed, "build_ms": round(build_ms, 3),
+            "local_nnz_max": int(max_over_ranks(float(eng.local_nnz))),
+            "queries": steps, "ms_per_query": round(dt * 1e3 / steps, 5),
+            "gteps": m * steps / dt / 1e9,
+            "device_ms_per_query": round(sum(r.search_ms for r, _ in done) / steps, 5),
+            "mean_hops": sum(r.hops for r, _ in done) / steps,
+            "mean_rounds": rounds,
+            "ms_per_round": round(dt * 1e3 / steps / max(rounds, 1e-9), 5),
+            "host_syncs_per_query": sum(s["host_syncs"] for s in st) / steps,
+            "exchanged_bytes_per_query": sum(s["exchanged_bytes"] for s in st) / steps,
+            "speculative_rounds_per_query": sum(s["spec_rounds"] for s in st) / steps,
+            "dense_levels_per_query": sum(s["dense_levels"] for s in st) / steps,
+            "verified": ok, "checked_queries": steps + warmup,
+        }
+        if wrong:
+            out["mismatch"] = wrong[:4]
+        eng.release()
+        return out, eng.world
+
+    if a.mode == "partitioned":
+        ph, rccl_ranks = run_partitioned(a.graph, a.steps, a.warmup)
+        head = {"n": ph["n"], "m": ph["m"], "seed": ph["seed"], "gteps": ph["gteps"],
+                "ms_per_step": ph["ms_per_query"], "device_ms_per_query": ph["device_ms_per_query"],
+                "gteps_inspected": None, "mean_hops": ph["mean_hops"], "build_ms": ph["build_ms"],
+                "batched": None, "partitioned": ph}
+    else:
+        head = run_replicated(a.graph, a.steps, a.warmup, cpu_ref=True)
+        rccl_ranks = None
     extra = {}
     partitioned = {}
     printed = threading.Lock()
+    state = {"rccl_ranks": rccl_ranks}
 
     def emit():
         if rank == 0 and printed.acquire(blocking=False):
-            print(json.dumps(report(a, world, head, extra, partitioned)), flush=True)
+            print(json.dumps(report(a, world, head, extra, partitioned, state["rccl_ranks"])), flush=True)
 
     def watchdog():
         # A secondary config that hangs (e.g. a collective that never completes
-        # on some rank) must not take the headline measurement with it.
+        # on some rank) must not take the headline measurement with it; the
+        # run still fails (non-zero exit) so the hang is not mistaken for success.
         for d in (extra, partitioned):
             for k, v in list(d.items()):
                 if v is None:
                     d[k] = {"error": f"watchdog: unfinished after {a.secondary_timeout:.0f} s"}
         emit()
         sys.stdout.flush()
-        os._exit(0)
+        sys.stderr.write("bench.py: secondary configs unfinished at the watchdog deadline\n")
+        os._exit(3)
 
     dog = threading.Timer(a.secondary_timeout, watchdog)
     dog.daemon = True
     dog.start()
+    failed = False
     for spec in filter(None, a.extra_graph.split(",")):
         extra[spec] = None
         try:
-            extra[spec] = run_config(spec, a.extra_steps, min(a.warmup, 10), "replicated")
+            extra[spec] = run_replicated(spec, a.extra_steps, min(a.warmup, 10))
         except Exception as exc:  # report, never hide, a failing secondary config
             extra[spec] = {"error": repr(exc)}
-    if world > 1 and a.mode == "replicated" and a.dist_backend == "nccl":
+            failed = True
+    if a.mode == "replicated" and (world == 1 or (a.dist_backend == "nccl" and not shared_gpu)):
         for spec in filter(None, a.dist_graphs.split(",")):
             partitioned[spec] = None
             try:
-                partitioned[spec] = run_config(spec, a.dist_steps, 3, "partitioned")
+                partitioned[spec], state["rccl_ranks"] = run_partitioned(spec, a.dist_steps, 3)
+                if not partitioned[spec]["verified"]:
+                    failed = True
             except Exception as exc:
                 partitioned[spec] = {"error": repr(exc)}
+                failed = True
 
     emit()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     dog.cancel()  # after the teardown: a hung final barrier is covered too
-    return 0
+    return 4 if failed else 0
 
 
 if __name__ == "__main__":

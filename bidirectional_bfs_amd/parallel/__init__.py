@@ -1,11 +1,14 @@
 """Multi-GPU and multi-process execution (v2 / v4 capabilities).
 
 * ``DistEngine``: one process per GPU, graph 1-D partitioned, every per-level
-  exchange an RCCL collective over xGMI (native ``DistBiBfs``); in lockstep
-  rounds one side's exchange runs on a comm stream while the other side
-  expands.  The RCCL communicator is bootstrapped from a unique id broadcast
-  over ``torch.distributed`` (``from_torch_distributed``) or over MPI by the
-  ``mpi_bibfs`` CLI.
+  exchange an RCCL collective over xGMI (native ``DistBiBfs``).  The round
+  policy runs on the device and the host enqueues several rounds per wait
+  (``DistTuning.spec_rounds``); dense or oversized levels are planned by the
+  host, where one side's exchange overlaps the other side's expand.  The RCCL
+  communicator is bootstrapped from a unique id broadcast over
+  ``torch.distributed`` (``from_torch_distributed``) or over MPI by the
+  ``mpi_bibfs`` CLI.  An error or a watchdog timeout on any rank aborts the
+  communicator (``ncclCommAbort``) so no peer is left hanging.
 * ``dist_local_run``: the same native engine with P ranks as P threads on ONE
   GPU, exchanging through an in-process group instead of RCCL -- how the
   partition / exchange logic is tested with P > 1 on a one-GPU box.
@@ -26,6 +29,18 @@ from ..models import Graph, parse_spec
 from ..ops import _DEFAULT_OPTIONS, HipEngine, make_options
 
 MPIEXEC = os.environ.get("BIBFS_MPIEXEC", "/opt/conda/bin/mpiexec")
+
+
+def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] = None, cap: Optional[int] = None,
+                nosync_bytes: Optional[int] = None, timeout_s: Optional[float] = None,
+                walk_max: Optional[int] = None) -> "native.DistTuning":
+    """Knobs of the partitioned engine; unset ones keep the production default."""
+    t = native.DistTuning()
+    for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
+                 ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max)):
+        if v is not None:
+            setattr(t, k, v)
+    return t
 
 
 class DistEngine:
@@ -74,6 +89,22 @@ class DistEngine:
     def barrier(self) -> None:
         self._e.barrier()
 
+    def release(self) -> None:
+        """Free this rank's graph shard and search state (the communicator stays)."""
+        self._e.release()
+
+    def set_tuning(self, tuning=None, **kw) -> "DistEngine":
+        self._e.set_tuning(tuning if tuning is not None else make_tuning(**kw))
+        return self
+
+    def inject_fault(self, at: int, mode: int = 1) -> None:
+        """Test hook: from round ``at`` on this rank throws (1) or stalls past the timeout (2)."""
+        self._e.inject_fault(int(at), int(mode))
+
+    @property
+    def local_nnz(self) -> int:
+        return self._e.local_nnz
+
     def allreduce_max(self, x: float) -> float:
         return self._e.allreduce_max(float(x))
 
@@ -107,19 +138,29 @@ class DistEngine:
         return self._e.backend
 
 
-def dist_local_run(ranks: int, graph: Graph, queries: Sequence, device: int = 0, options=None, **kw) -> List:
+def dist_local_run(ranks: int, graph: Graph, queries: Sequence, device: int = 0, options=None, tuning=None,
+                   fault=None, return_stats: bool = False, **kw):
     """Partitioned native engine, ``ranks`` ranks as threads sharing one GPU (test harness).
 
     Every rank answers every query; the result list is rank 0's, after a check
-    that all ranks agree.
+    that all ranks agree.  ``tuning``: a ``native.DistTuning`` (see
+    :func:`make_tuning`); ``fault``: ``(rank, at, mode)`` arms
+    ``inject_fault`` on one rank.  With ``return_stats`` also returns rank 0's
+    per-query ``last_stats`` dicts.
     """
     if options is None:
         options = make_options(**kw) if kw else _DEFAULT_OPTIONS
     q = [(int(s), int(d)) for s, d in queries]
-    return native.dist_local_run(int(ranks), int(device), graph.edges, q, options)
+    f = native.DistLocalFault()
+    if fault is not None:
+        f.rank, f.at, f.mode = (int(x) for x in fault)
+    rs, st = native.dist_local_run(int(ranks), int(device), graph.edges, q, options,
+                                   tuning if tuning is not None else native.DistTuning(), f)
+    return (rs, st) if return_stats else rs
 
 
-def dist_local_generate_run(ranks: int, spec: str, queries: Sequence, device: int = 0, options=None, **kw):
+def dist_local_generate_run(ranks: int, spec: str, queries: Sequence, device: int = 0, options=None, tuning=None,
+                            **kw):
     """Like :func:`dist_local_run`, but every rank generates ``spec``
     (``gnp:``/``rmat:``/``kron:``) on the device and keeps only its own CSR
     shard, as the multi-GPU bench does.  Returns ``(results, timing)`` with
@@ -129,7 +170,8 @@ def dist_local_generate_run(ranks: int, spec: str, queries: Sequence, device: in
         options = make_options(**kw) if kw else _DEFAULT_OPTIONS
     kind, n, arg, seed = parse_spec(spec)
     q = [(int(s), int(d)) for s, d in queries]
-    return native.dist_local_generate_run(int(ranks), int(device), kind, n, float(arg), seed, q, options)
+    return native.dist_local_generate_run(int(ranks), int(device), kind, n, float(arg), seed, q, options,
+                                          tuning if tuning is not None else native.DistTuning())
 
 
 class ReplicatedServer:
@@ -159,4 +201,5 @@ def run_mpi(tool: str, args: Sequence[str], np: int = 2, timeout: float = 300.0,
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
 
 
-__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "dist_local_generate_run", "run_mpi", "MPIEXEC"]
+__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "dist_local_generate_run", "make_tuning", "run_mpi",
+           "MPIEXEC"]

@@ -11,6 +11,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <mutex>
@@ -56,43 +58,78 @@ class RcclComm final : public Comm {
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
     RCCL_CHECK(ncclCommInitRank(&comm_, size, id, rank));
+    int count = 0;
+    RCCL_CHECK(ncclCommCount(comm_, &count));  // the rank count the communicator itself reports
+    BIBFS_REQUIRE(count == size, "RCCL communicator has " + std::to_string(count) + " ranks, expected " +
+                                     std::to_string(size));
   }
   ~RcclComm() override {
-    if (comm_) (void)ncclCommDestroy(comm_);
+    if (comm_ && !aborted_) (void)ncclCommDestroy(comm_);
   }
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   const char* name() const override { return "rccl"; }
-  void group_begin() override { RCCL_CHECK(ncclGroupStart()); }
+  void group_begin() override {
+    live();
+    RCCL_CHECK(ncclGroupStart());
+  }
   void group_end() override { RCCL_CHECK(ncclGroupEnd()); }
   void allreduce(void* buf, size_t count, DType t, ROp op, hipStream_t s) override {
+    live();
     RCCL_CHECK(ncclAllReduce(buf, buf, count, nccl_type(t), nccl_op(op), comm_, s));
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    live();
     if (bytes % 4 == 0)
       RCCL_CHECK(ncclAllGather(send, recv, bytes / 4, ncclUint32, comm_, s));
     else
       RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
+  void check() override {
+    live();
+    ncclResult_t e = ncclSuccess;
+    RCCL_CHECK(ncclCommGetAsyncError(comm_, &e));
+    if (e != ncclSuccess && e != ncclInProgress)
+      throw Error(std::string("RCCL asynchronous error on rank ") + std::to_string(rank_) + ": " +
+                  ncclGetErrorString(e));
+  }
+  void abort() override {
+    if (aborted_.exchange(true)) return;
+    (void)ncclCommAbort(comm_);  // outstanding collectives of every rank on this comm return
+  }
+  bool aborted() const override { return aborted_; }
 
  private:
+  void live() const {
+    if (aborted_) throw Error("RCCL communicator was aborted after an earlier failure");
+  }
   int rank_, size_;
   ncclComm_t comm_ = nullptr;
+  std::atomic<bool> aborted_{false};
 };
 
 }  // namespace
 
-// P ranks = P host threads of one process.  Every collective: drain the
-// caller's stream, stage its bytes in the rank's slot, barrier, combine, barrier.
+// P ranks = P host threads of one process sharing one GPU.  A collective is a
+// host rendezvous that swaps {buffer pointer, "ready" event} between the
+// ranks; the data then moves with device-to-device copies on each rank's own
+// stream, ordered by stream-waits on the other ranks' events -- no stream is
+// drained and no byte goes through the host.
 struct LocalGroup {
-  explicit LocalGroup(int p) : P(p), slot((size_t)p) {}
+  LocalGroup(int p, double t) : P(p), timeout_s(t), slot((size_t)p) {}
+  struct Slot {
+    const void* src = nullptr;
+    hipEvent_t ready = nullptr;  // recorded after the source bytes are final
+    hipEvent_t done = nullptr;   // recorded after this rank copied everyone's bytes
+  };
   const int P;
+  const double timeout_s;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
   bool aborted = false;
-  std::vector<std::vector<uint8_t>> slot;
+  std::vector<Slot> slot;
 
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
@@ -104,7 +141,12 @@ struct LocalGroup {
       cv.notify_all();
       return;
     }
-    cv.wait(lk, [&] { return gen != g || aborted; });
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
+    if (!cv.wait_until(lk, deadline, [&] { return gen != g || aborted; })) {
+      aborted = true;  // a peer never arrived: fail the whole group, not just this rank
+      cv.notify_all();
+      throw Error("local group collective timed out after " + std::to_string(timeout_s) + " s");
+    }
     if (gen == g) throw Error("local group aborted by another rank");
   }
 };
@@ -112,59 +154,114 @@ struct LocalGroup {
 namespace {
 
 template <typename T>
-void combine(T* acc, const T* x, size_t n, ROp op) {
-  for (size_t i = 0; i < n; ++i)
-    acc[i] = op == ROp::kSum ? acc[i] + x[i] : (op == ROp::kMin ? std::min(acc[i], x[i]) : std::max(acc[i], x[i]));
+__global__ void k_local_reduce(const T* __restrict__ parts, T* __restrict__ out, size_t count, int P, int op) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+    T acc = parts[i];
+    for (int r = 1; r < P; ++r) {
+      const T x = parts[(size_t)r * count + i];
+      acc = op == 0 ? acc + x : (op == 1 ? (x < acc ? x : acc) : (x > acc ? x : acc));
+    }
+    out[i] = acc;
+  }
 }
 
 class LocalComm final : public Comm {
  public:
-  LocalComm(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {}
+  LocalComm(std::shared_ptr<LocalGroup> g, int rank) : g_(std::move(g)), rank_(rank) {
+    HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+  }
+  ~LocalComm() override {
+    if (scratch_) (void)hipFree(scratch_);
+    (void)hipEventDestroy(ready_);
+    (void)hipEventDestroy(done_);
+  }
   int rank() const override { return rank_; }
   int size() const override { return g_->P; }
   const char* name() const override { return "local"; }
 
   void allreduce(void* buf, size_t count, DType t, ROp op, hipStream_t s) override {
+    if (g_->P == 1 || count == 0) return;
     const size_t bytes = count * type_size(t);
-    HIP_CHECK(hipStreamSynchronize(s));
-    auto& mine = g_->slot[(size_t)rank_];
-    mine.resize(bytes);
-    if (bytes) HIP_CHECK(hipMemcpy(mine.data(), buf, bytes, hipMemcpyDeviceToHost));
-    g_->barrier();
-    std::vector<uint8_t> acc(g_->slot[0]);
-    for (int r = 1; r < g_->P; ++r) {
-      const uint8_t* x = g_->slot[(size_t)r].data();
-      switch (t) {
-        case DType::kU32:
-          combine(reinterpret_cast<uint32_t*>(acc.data()), reinterpret_cast<const uint32_t*>(x), count, op);
-          break;
-        case DType::kU64:
-          combine(reinterpret_cast<uint64_t*>(acc.data()), reinterpret_cast<const uint64_t*>(x), count, op);
-          break;
-        case DType::kF64:
-          combine(reinterpret_cast<double*>(acc.data()), reinterpret_cast<const double*>(x), count, op);
-          break;
-      }
+    if (scratch_bytes_ < bytes * g_->P) {
+      HIP_CHECK(hipStreamSynchronize(s));
+      if (scratch_) HIP_CHECK(hipFree(scratch_));
+      scratch_bytes_ = std::max<size_t>(bytes * g_->P, 4096);
+      HIP_CHECK(hipMalloc(&scratch_, scratch_bytes_));
     }
-    g_->barrier();  // every rank has read every slot before any is rewritten
-    if (bytes) HIP_CHECK(hipMemcpy(buf, acc.data(), bytes, hipMemcpyHostToDevice));
+    exchange(buf, scratch_, bytes, s);
+    const int o = op == ROp::kSum ? 0 : (op == ROp::kMin ? 1 : 2);
+    const unsigned blocks = (unsigned)std::min<size_t>((count + 255) / 256, 64);
+    switch (t) {
+      case DType::kU32:
+        k_local_reduce<uint32_t><<<blocks, 256, 0, s>>>(static_cast<const uint32_t*>(scratch_),
+                                                        static_cast<uint32_t*>(buf), count, g_->P, o);
+        break;
+      case DType::kU64:
+        k_local_reduce<unsigned long long><<<blocks, 256, 0, s>>>(
+            static_cast<const unsigned long long*>(scratch_), static_cast<unsigned long long*>(buf), count, g_->P, o);
+        break;
+      case DType::kF64:
+        k_local_reduce<double><<<blocks, 256, 0, s>>>(static_cast<const double*>(scratch_),
+                                                      static_cast<double*>(buf), count, g_->P, o);
+        break;
+    }
+    HIP_CHECK(hipGetLastError());
   }
 
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
-    HIP_CHECK(hipStreamSynchronize(s));
-    auto& mine = g_->slot[(size_t)rank_];
-    mine.resize(bytes);
-    if (bytes) HIP_CHECK(hipMemcpy(mine.data(), send, bytes, hipMemcpyDeviceToHost));
-    g_->barrier();
-    for (int r = 0; r < g_->P && bytes; ++r)
-      HIP_CHECK(hipMemcpy(static_cast<char*>(recv) + (size_t)r * bytes, g_->slot[(size_t)r].data(), bytes,
-                          hipMemcpyHostToDevice));
-    g_->barrier();
+    if (g_->P == 1) {
+      if (bytes && send != recv) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+      return;
+    }
+    exchange(send, recv, bytes, s);
   }
 
+  void abort() override {
+    aborted_ = true;
+    abort_local_group(*g_);
+  }
+  bool aborted() const override { return aborted_; }
+
  private:
+  // recv[r] = rank r's src, for every r; ordered on `s` after every rank's
+  // producer work, and every rank's later writes to its src ordered after
+  // every copy out of it.
+  void exchange(const void* src, void* recv, size_t bytes, hipStream_t s) {
+    if (aborted_) throw Error("local group communicator was aborted after an earlier failure");
+    LocalGroup& G = *g_;
+    HIP_CHECK(hipEventRecord(ready_, s));
+    {
+      std::lock_guard<std::mutex> lk(G.mu);
+      G.slot[(size_t)rank_] = {src, ready_, done_};
+    }
+    G.barrier();  // every rank's {src, ready} published
+    std::vector<LocalGroup::Slot> peers;
+    {
+      std::lock_guard<std::mutex> lk(G.mu);
+      peers = G.slot;
+    }
+    for (int r = 0; r < G.P; ++r) {
+      const LocalGroup::Slot& x = peers[(size_t)r];
+      if (r != rank_) HIP_CHECK(hipStreamWaitEvent(s, x.ready, 0));
+      if (bytes)
+        HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)r * bytes, x.src, bytes,
+                                 hipMemcpyDeviceToDevice, s));
+    }
+    HIP_CHECK(hipEventRecord(done_, s));
+    G.barrier();  // every rank's copies enqueued and its `done` recorded
+    for (int r = 0; r < G.P; ++r)
+      if (r != rank_) HIP_CHECK(hipStreamWaitEvent(s, peers[(size_t)r].done, 0));
+    // No third rendezvous: a rank re-records `ready` only before the next
+    // collective's first barrier, which every peer reaches after its waits above.
+  }
+
   std::shared_ptr<LocalGroup> g_;
   int rank_;
+  hipEvent_t ready_ = nullptr, done_ = nullptr;
+  void* scratch_ = nullptr;
+  size_t scratch_bytes_ = 0;
+  bool aborted_ = false;
 };
 
 }  // namespace
@@ -180,9 +277,10 @@ std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8
   return std::unique_ptr<Comm>(new RcclComm(rank, size, uid));
 }
 
-std::shared_ptr<LocalGroup> make_local_group(int size) {
+std::shared_ptr<LocalGroup> make_local_group(int size, double timeout_s) {
   BIBFS_REQUIRE(size >= 1, "local group needs at least one rank");
-  return std::make_shared<LocalGroup>(size);
+  BIBFS_REQUIRE(timeout_s > 0, "local group timeout must be positive");
+  return std::make_shared<LocalGroup>(size, timeout_s);
 }
 
 std::unique_ptr<Comm> make_local_comm(std::shared_ptr<LocalGroup> g, int rank) {

@@ -3,10 +3,19 @@
 // Production: RCCL over xGMI, one process per GPU (make_rccl_comm).  The
 // engine only ever issues the handful of collectives below, always on a HIP
 // stream, so the same engine code also runs over an in-process "local group"
-// (make_local_comm): P host threads that share one GPU and exchange through
-// host staging.  The local group is test infrastructure (SURVEY.md §4 item 5:
-// validate the partition / ownership / exchange logic with P > 1 on a box
-// with one GPU); it is never used for a measured number.
+// (make_local_comm): P host threads that share one GPU.  The local group
+// moves data with device-to-device copies ordered by HIP events between the
+// ranks' streams (the host only rendezvouses to swap buffer pointers and
+// events), so stream ordering, overlap and the engine's no-host-sync rounds
+// behave as they do over RCCL.  It is test infrastructure (SURVEY.md §4 item
+// 5: validate the partition / ownership / exchange logic with P > 1 on a box
+// with one GPU); it is never used for a measured multi-GPU number.
+//
+// Failure handling (the reference aborts the job on any error:
+// v2/second_try.cpp:35, v4/mpi_bas.cpp:33, v3/bibfs_cuda_only.cu:6-10):
+// `abort()` tears the communicator down so peers blocked in a collective
+// return (ncclCommAbort / waking the local group), `check()` surfaces an
+// asynchronous RCCL error, and the local group's rendezvous has a timeout.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -36,13 +45,20 @@ class Comm {
   virtual void allreduce(void* buf, size_t count, DType t, ROp op, hipStream_t s) = 0;
   // recv = P consecutive blocks of `bytes` (block r from rank r); device memory.
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // Throw if the communicator reported an asynchronous error (peer failure).
+  virtual void check() {}
+  // Abort every outstanding and future collective of this communicator
+  // (peers blocked in one return with an error).  Idempotent.
+  virtual void abort() = 0;
+  virtual bool aborted() const = 0;
 };
 
 std::vector<uint8_t> rccl_unique_id();
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& uid);
 
 struct LocalGroup;
-std::shared_ptr<LocalGroup> make_local_group(int size);
+// `timeout_s`: a rank waiting longer than this in a rendezvous aborts the group.
+std::shared_ptr<LocalGroup> make_local_group(int size, double timeout_s = 120.0);
 std::unique_ptr<Comm> make_local_comm(std::shared_ptr<LocalGroup> g, int rank);
 // Wake every rank blocked in a local collective with an error (a rank failed).
 void abort_local_group(LocalGroup& g);

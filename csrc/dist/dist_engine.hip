@@ -8,24 +8,35 @@
 //
 // A search runs in ROUNDS.  A round expands one side or -- when the two
 // frontiers are comparable -- both sides in lockstep.  One side's level is
-//   pre      (compute stream) top-down: expand the owned frontier, claim owned
-//                             neighbours, emit (v, parent) candidates for
-//                             remote owners (each remote vertex at most once
-//                             per search and side); bottom-up: the owned slice
-//                             of the frontier bitmap
-//   exchange (comm stream)    ONE allgather: candidate blocks or bitmap slices
-//   post     (comm stream)    owners claim the candidates addressed to them, or
-//                             scan their unvisited vertices against the bitmap
-// In a lockstep round the exchange + post of the source side run on the comm
-// stream while the target side's pre runs on the compute stream: the
-// opposite-direction expand overlaps the RCCL transfer.  The
-// round ends with a meet check over the vertices claimed in it (exact lengths
-// from per-vertex depths, so the minimum over a lockstep round is the
-// distance) and ONE grouped allreduce -- {claimed counts, degree sums} (sum)
-// and the meet key (min) -- read back with one host sync: the only host
-// round trip of a round, except when a top-down candidate block cannot be
-// sized from host-known bounds (then one allreduce(MAX) of the per-rank
-// counts sizes it).
+//   pre      top-down: expand the owned frontier, claim owned neighbours, emit
+//            (v, parent) candidates for remote owners (each remote vertex at
+//            most once per search and side); bottom-up: the owned slice of
+//            the frontier bitmap
+//   exchange ONE allgather: candidate blocks or bitmap slices
+//   post     owners claim the candidates addressed to them, or scan their
+//            unvisited vertices against the gathered bitmap
+// and every round ends with a meet check over the vertices claimed in it
+// (exact lengths from per-vertex depths, so the minimum over a lockstep round
+// is the distance) and ONE grouped allreduce {claimed counts, degree sums
+// (sum); meet key (min)}.
+//
+// Where the reference (and this engine's first version) went back to the host
+// after every level (v4/mpi_bas.cpp:85,107,124: three blocking collectives and
+// host scans per level), the round POLICY now lives on the device: `Ctl` is
+// recomputed at the start of each round from the previous round's reduced
+// values -- the same bytes on every rank, so every rank plans the same round
+// -- and the host enqueues `spec_rounds` sparse rounds back to back, each
+// with a fixed-capacity candidate exchange:
+//   k_spec_expand (plan + both sides' pre) -> allgather -> k_spec_claim (both
+//   sides' post) -> k_meet_end (meet + round end) -> grouped allreduce
+// A round whose plan says "done", "no path" or "stalled" runs as no-ops; the
+// host reads `Ctl` once per batch.  A round the speculative shape cannot
+// carry (bottom-up, or a frontier with more edges than the enqueued block
+// capacity, so a rank could overflow it) stalls the batch, and the host plans
+// that one round itself with exact sizing (and, in lockstep, the comm-stream
+// overlap of one side's exchange with the other side's expand).
+// In a host-planned lockstep round side S's exchange + post run on the comm
+// stream while side T's pre runs on the compute stream.
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -46,23 +57,69 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr unsigned long long kNoKey = ~0ull;
-constexpr uint64_t kCapMax = 1u << 20;          // candidate pairs per rank per level
-constexpr uint64_t kNoSyncBytes = 1u << 20;     // candidate allgather sized from host bounds up to this many bytes
+constexpr uint64_t kCapMax = 1u << 20;          // host-planned round: candidate pairs per rank per level
 constexpr uint64_t kLockstepEdges = 1u << 16;   // both frontiers at most this many edges: always lockstep
+constexpr uint32_t kSpecCapMin = 1024;          // smallest speculative candidate block (pairs)
+// A frontier vertex with more edges than this is not expanded by the block
+// that holds it: it is deferred to a hub list whose edges the whole grid then
+// walks edge-parallel (a degree-10^6 hub would otherwise serialise on one CU).
+constexpr uint64_t kHubDeg = 512;
+constexpr uint64_t kNoHubs = ~0ull;
+constexpr int kHubTile = 1024;                  // hubs staged in LDS per pass
+constexpr uint32_t kSpecHubCap = 4096;          // speculative blocks up to this size skip the hub pass
+
+// Search control state: identical on every rank (computed from reduced
+// values only).  Double-buffered by round parity: round `it` reads
+// ctl[(it-1)&1] and writes ctl[it&1].
+enum : uint32_t { kRun = 0, kDone = 1, kDead = 2, kStall = 3 };
+enum : uint32_t { kStallNone = 0, kStallDense = 1, kStallCap = 2, kStallHost = 3 };
+constexpr uint32_t kSeedBit = 4;                       // Ctl::sides of the seeding pseudo-round
+// plan_round flags: account only / run the stalled plan speculatively / run it
+// as a host-planned round / plan, then stall for the host (host-only mode)
+enum : int { kPlanAccountOnly = 1, kPlanResume = 2, kPlanForce = 4, kPlanStall = 8 };
+
+struct Ctl {
+  unsigned long long cnt[2];   // current frontier sizes (vertices)
+  unsigned long long fed[2];   // current frontier degree sums
+  unsigned long long ved[2];   // degree sum of everything side s claimed
+  unsigned long long vis[2];   // vertices side s claimed (incl. the root)
+  unsigned long long key;      // (length << 32) | meet vertex, once found
+  unsigned long long einsp;    // edges inspected by the expanded levels
+  uint32_t depth[2];           // depth of the current frontier
+  uint32_t dir[2];             // 1 top-down, 2 bottom-up (Beamer state)
+  uint32_t turn;               // alternate policy
+  uint32_t state;              // kRun / kDone / kDead / kStall
+  uint32_t sides;              // sides THIS round expands (0 = no-op round)
+  uint32_t modes;              // bit s: side s bottom-up this round
+  uint32_t want, want_modes;   // the planned round (kept when it stalls)
+  uint32_t stall;              // kStall* reason
+  uint32_t rounds, lockstep_rounds, levels, sparse_levels;
+  uint32_t pad;
+};
+
+struct Policy {
+  double alpha, beta;
+  unsigned long long nnz_total;
+  uint32_t n;
+  int lockstep, side, direction;
+};
+
+// Reduced across ranks (device words), double-buffered like Ctl.
+struct Reduced {
+  unsigned long long sums[4];  // [2s] vertices side s claimed this round, [2s+1] their degree sum (sum)
+  unsigned long long meetkey;  // (path length << 32) | meet vertex (min)
+  uint32_t maxsend[2];         // candidates of side s on this rank (max; host-planned rounds)
+  uint32_t md[2];              // depth of the meet vertex from each root (owner contributes; min)
+  uint32_t pad[2];
+};
 
 struct DState {
   uint32_t fbeg[2], fend[2], qtail[2];  // queue[s][fbeg, fend) = frontier; qtail = append cursor
   uint32_t send_count[2];               // candidates this rank emitted for side s this level
-  uint32_t pad[2];
+  uint32_t done_blocks[3];              // last-block detection (expand, meet, hubs)
+  uint32_t hub_count[2];                // deferred hubs of side s this level
+  uint32_t pad;
   unsigned long long new_edges[2];      // degree sum of the vertices side s claimed this level
-};
-
-// Reduced across ranks (device words, read back into pinned memory).
-struct Reduced {
-  unsigned long long sums[4];  // [2s] vertices side s claimed this round, [2s+1] their degree sum (sum)
-  unsigned long long meetkey;  // (path length << 32) | meet vertex (min)
-  uint32_t maxsend[2];         // candidates of side s on this rank (max)
-  uint32_t md[2];              // depth of the meet vertex from each root (owner contributes; min)
 };
 
 struct DView {
@@ -73,20 +130,123 @@ struct DView {
   uint32_t* parent[2];        // chunk entries, valid where visited
   uint32_t* depth[2];         // chunk entries, valid where visited
   uint32_t* queue[2];         // owned vertices (global ids) in claim order
+  uint32_t* hubs[2];          // deferred high-degree frontier vertices (this level)
   uint32_t* sent[2];          // bitmaps over ALL vertices: remote vertices already offered this search
   uint32_t* obits[2];         // owned frontier slice (chunk/32 words)
   uint32_t* gbits[2];         // allgathered frontier bitmap (P * chunk/32 words: global index)
-  uint32_t* send[2];          // {count, pad, (v, u) pairs}
-  uint32_t* recv[2];          // P blocks
-  uint32_t cap;               // candidate pairs per rank per level
+  uint32_t* sendbuf;          // candidate blocks {count, pad, (v, u) pairs}: 2 sides
+  uint32_t* recvbuf;          // P ranks x 2 sides of blocks
+  uint32_t cap;               // host-planned round: candidate pairs per rank per level
   int P;
   DState* st;
-  Reduced* red;
+  Ctl* ctl;                   // [2]
+  Reduced* red;               // [2]
 };
 
 template <typename T>
 __device__ __forceinline__ T* pick(T* const (&a)[2], int s) {
   return s ? a[1] : a[0];
+}
+
+__host__ __device__ inline uint64_t block_words(uint32_t cap) { return 2 + 2 * (uint64_t)cap; }
+
+// ---------------------------------------------------------------------------
+// Round policy (device).  Accounts the previous round, then plans this one.
+// Every input is a reduced value, so every rank computes the same plan.
+// ---------------------------------------------------------------------------
+__device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, uint64_t spec_cap, int flags,
+                           Ctl& c) {
+  c = p;
+  c.sides = 0;
+  c.modes = 0;
+  uint32_t want = 0, wm = 0;
+  if (p.state == kStall) {
+    if (!(flags & (kPlanResume | kPlanForce))) return;  // stays stalled until the host acts
+    want = p.want;
+    wm = p.want_modes;
+  } else {
+    if (p.sides & kSeedBit) {  // the roots: frontier sizes of the seeding pseudo-round
+      for (int s = 0; s < 2; ++s) {
+        c.cnt[s] = rd.sums[2 * s];
+        c.fed[s] = rd.sums[2 * s + 1];
+        c.ved[s] = c.fed[s];
+        c.vis[s] = c.cnt[s];
+      }
+    } else if (p.sides) {
+      int ns = 0;
+      for (int s = 0; s < 2; ++s) {
+        if (!((p.sides >> s) & 1)) continue;
+        ++ns;
+        c.depth[s] += 1;
+        c.levels += 1;
+        c.cnt[s] = rd.sums[2 * s];
+        c.fed[s] = rd.sums[2 * s + 1];
+        c.ved[s] += c.fed[s];
+        c.vis[s] += c.cnt[s];
+      }
+      c.rounds += 1;
+      if (ns == 2) c.lockstep_rounds += 1;
+      if (rd.meetkey != kNoKey) {
+        c.state = kDone;
+        c.key = rd.meetkey;
+        return;
+      }
+      for (int s = 0; s < 2; ++s)
+        if (((p.sides >> s) & 1) && c.cnt[s] == 0) c.state = kDead;  // that side's component is exhausted
+    }
+    if (c.state != kRun || (flags & kPlanAccountOnly)) return;
+    if ((uint64_t)c.rounds > 2ull * pol.n + 2) {  // safety net (v3 parity: iteration cap N)
+      c.state = kDead;
+      return;
+    }
+    const unsigned long long flo = min(c.fed[0], c.fed[1]), fhi = max(c.fed[0], c.fed[1]);
+    if (pol.lockstep && pol.side != (int)SidePolicy::kAlternate && (fhi <= kLockstepEdges || fhi <= 2 * flo)) {
+      want = 3;
+    } else if (pol.side == (int)SidePolicy::kAlternate) {
+      want = 1u << c.turn;
+      c.turn ^= 1u;
+    } else if (pol.side == (int)SidePolicy::kSmallerFrontier) {
+      want = c.cnt[0] <= c.cnt[1] ? 1u : 2u;
+    } else {
+      want = c.fed[0] <= c.fed[1] ? 1u : 2u;
+    }
+    for (int s = 0; s < 2; ++s) {
+      if (!((want >> s) & 1)) continue;
+      uint32_t mode;
+      if (pol.direction == (int)Direction::kTopDown) {
+        mode = 1;
+      } else if (pol.direction == (int)Direction::kBottomUp) {
+        mode = 2;
+      } else {
+        const double m_u = (double)pol.nnz_total - (double)c.ved[s];
+        if (c.dir[s] == 1 && (double)c.fed[s] > m_u / pol.alpha) c.dir[s] = 2;
+        else if (c.dir[s] == 2 && (double)c.cnt[s] < (double)pol.n / pol.beta) c.dir[s] = 1;
+        mode = c.dir[s];
+      }
+      if (mode == 2) wm |= 1u << s;
+    }
+    c.want = want;
+    c.want_modes = wm;
+  }
+  if (!(flags & kPlanForce)) {
+    bool fits = wm == 0;
+    for (int s = 0; s < 2; ++s)
+      if (((want >> s) & 1) && c.fed[s] > spec_cap) fits = false;
+    if (!fits || (flags & kPlanStall)) {
+      c.state = kStall;
+      c.stall = (flags & kPlanStall) ? kStallHost : (wm ? kStallDense : kStallCap);
+      return;
+    }
+  }
+  c.state = kRun;
+  c.stall = kStallNone;
+  c.sides = want;
+  c.modes = wm;
+  for (int s = 0; s < 2; ++s)
+    if ((want >> s) & 1) {
+      c.einsp += c.fed[s];
+      if (!((wm >> s) & 1)) c.sparse_levels += 1;
+    }
 }
 
 // Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
@@ -122,7 +282,8 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
 // Offer remote vertex v (parent u) to its owner -- at most once per search and
 // side: after the level that offered it, v is visited by its owner (claimed
 // from the exchange, or by the bottom-up fallback of an overflowing level).
-__device__ __forceinline__ void wave_emit(const DView& V, int s, bool want, uint32_t v, uint32_t u) {
+__device__ __forceinline__ void wave_emit(const DView& V, int s, bool want, uint32_t v, uint32_t u, uint2* pairs,
+                                          uint32_t cap) {
   uint32_t* sb = pick(V.sent, s);
   bool emit = false;
   if (want) {
@@ -136,22 +297,23 @@ __device__ __forceinline__ void wave_emit(const DView& V, int s, bool want, uint
   uint32_t pos = 0;
   if (lane == (uint32_t)leader) pos = atomicAdd(&V.st->send_count[s], (uint32_t)__popcll(mask));
   pos = __shfl(pos, leader) + mbcnt64(mask);
-  if (emit && pos < V.cap) reinterpret_cast<uint2*>(pick(V.send, s))[1 + pos] = make_uint2(v, u);
+  if (emit && pos < cap) pairs[pos] = make_uint2(v, u);
 }
 
-// Top-down pre phase: edge-balanced expansion of the owned frontier.  A
-// workgroup takes 256 frontier vertices, scans their degrees in LDS and walks
-// the chunk's edges one per lane (binary search for the owning vertex), so a
-// hub costs the same per edge as a leaf and no lane idles on a short row.
-__global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t dnew, int first) {
+// Top-down pre phase of side s: edge-balanced expansion of the owned
+// frontier.  A workgroup takes 256 frontier vertices, scans their degrees in
+// LDS and walks the chunk's edges one per lane (binary search for the owning
+// vertex), so a hub costs the same per edge as a leaf and no lane idles on a
+// short row.  Block-uniform control flow (it contains barriers).
+__device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pairs, uint32_t cap, uint32_t b0,
+                               uint32_t nb, uint64_t hub_deg) {
   __shared__ uint32_t su[kThreads];
   __shared__ unsigned long long sb[kThreads], se[kThreads];
   __shared__ unsigned long long wsum[kThreads / kWave];
-  if (first && blockIdx.x == 0 && threadIdx.x == 0) V.red->meetkey = kNoKey;  // new round
   const uint32_t fb = V.st->fbeg[s], F = V.st->fend[s] - fb;
   const uint32_t* q = pick(V.queue, s);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  for (uint64_t c0 = (uint64_t)blockIdx.x * kThreads; c0 < F; c0 += (uint64_t)gridDim.x * kThreads) {
+  for (uint64_t c0 = (uint64_t)b0 * kThreads; c0 < F; c0 += (uint64_t)nb * kThreads) {
     const uint64_t i = c0 + tid;
     unsigned long long deg = 0, b = 0;
     uint32_t u = 0;
@@ -160,6 +322,16 @@ __global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t
       const uint32_t li = u - V.lo;
       b = V.row_off[li];
       deg = V.row_off[li + 1] - b;
+    }
+    const bool hub = deg > hub_deg;  // expanded by k_td_hubs instead
+    const unsigned long long hm = __ballot(hub);
+    if (hm) {
+      uint32_t pos = 0;
+      const int leader = __ffsll((long long)hm) - 1;
+      if (lane == leader) pos = atomicAdd(&V.st->hub_count[s], (uint32_t)__popcll(hm));
+      pos = __shfl(pos, leader);
+      if (hub) pick(V.hubs, s)[pos + mbcnt64(hm)] = u;
+      if (hub) deg = 0;
     }
     su[tid] = u;
     sb[tid] = b;
@@ -195,36 +367,271 @@ __global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t
       }
       const bool own = valid && v >= V.lo && v < V.hi;
       wave_claim(V, s, own, v, uu, dnew);
-      wave_emit(V, s, valid && !own, v, uu);
+      wave_emit(V, s, valid && !own, v, uu, pairs, cap);
     }
     __syncthreads();
   }
 }
 
-__global__ void k_send_header(DView V, int s) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  const uint32_t c = V.st->send_count[s];
-  pick(V.send, s)[0] = c;
-  V.red->maxsend[s] = c;
+// Last-block detection: true in exactly one block, after every block of the
+// grid has passed this point (its earlier global writes and atomics released).
+__device__ __forceinline__ bool last_block(uint32_t* counter, uint32_t nblocks) {
+  __shared__ int last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(counter, 1u) == nblocks - 1;
+    if (last) __threadfence();
+  }
+  __syncthreads();
+  return last != 0;
 }
 
-// Top-down post phase: owners claim the candidates addressed to them (block r
-// of the gathered buffer is rank r's {count, pad, pairs}).
-__global__ __launch_bounds__(kThreads) void k_td_claim(DView V, int s, uint32_t per_rank, uint32_t dnew) {
-  const uint64_t blk = 2 + 2 * (uint64_t)per_rank;
-  const uint64_t total = (uint64_t)V.P * per_rank;
-  const uint32_t* R = pick(V.recv, s);
+// ---- speculative round kernels ---------------------------------------------
+
+// Plan (every block computes the same plan; block 0 publishes it) + top-down
+// pre phase of both sides (blockIdx.y = side) into blocks of `cap` pairs.
+__global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
+                                                          int flags, uint64_t hub_deg, int header) {
+  const int p = it & 1;
+  __shared__ Ctl c;
+  if (threadIdx.x == 0) plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, cap, flags, c);
+  __syncthreads();
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    V.ctl[p] = c;
+    V.red[p].meetkey = kNoKey;
+  }
+  const int s = blockIdx.y;
+  if ((c.sides >> s) & 1)
+    td_expand_side(V, s, c.depth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
+                   blockIdx.x, gridDim.x, hub_deg);
+  if (!header) return;  // k_td_hubs runs next and writes the headers
+  if (last_block(&V.st->done_blocks[0], gridDim.x * gridDim.y) && threadIdx.x < 2) {
+    const int ss = threadIdx.x;
+    const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
+    V.sendbuf[ss * block_words(cap)] = ((c.sides >> ss) & 1) ? min(cnt, cap) : 0u;
+    if (ss == 0) atomicExch(&V.st->done_blocks[0], 0u);
+  }
+}
+
+// Edge-parallel expansion of the deferred hubs.  side >= 0: that side (a
+// host-planned round, depth dnew, blocks of V.cap pairs); side < 0: both
+// sides of speculative round `it` (blockIdx.y = side, blocks of `cap` pairs)
+// and the last block writes the candidate headers.  Every block stages a tile
+// of hubs with their degree prefix in LDS and walks the tile's flattened edge
+// range with a grid stride, so each hub's edges spread over all CUs.
+__global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int side, uint32_t dnew_fixed,
+                                                      uint32_t cap) {
+  __shared__ uint32_t hu[kHubTile];
+  __shared__ unsigned long long hb[kHubTile], hp[kHubTile + 1];
+  __shared__ unsigned long long wsum[kThreads / kWave];
+  const int s = side >= 0 ? side : (int)blockIdx.y;
+  uint32_t sides = 1u << s, dnew = dnew_fixed;
+  if (side < 0) {
+    const Ctl& c = V.ctl[it & 1];
+    sides = c.sides;
+    dnew = c.depth[s] + 1;
+  }
+  const uint32_t H = V.st->hub_count[s];
+  uint2* pairs = reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  if ((sides >> s) & 1) {
+    for (uint32_t t0 = 0; t0 < H; t0 += kHubTile) {
+      const uint32_t nt = min((uint32_t)kHubTile, H - t0);
+      constexpr int kPer = kHubTile / kThreads;  // hubs per thread for the scan
+      unsigned long long d[kPer], run = 0;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t j = tid * kPer + k;
+        d[k] = 0;
+        if (j < nt) {
+          const uint32_t u = pick(V.hubs, s)[t0 + j], li = u - V.lo;
+          const unsigned long long b = V.row_off[li];
+          d[k] = V.row_off[li + 1] - b;
+          hu[j] = u;
+          hb[j] = b;
+        }
+        run += d[k];
+      }
+      unsigned long long x = run;  // inclusive wave scan of per-thread sums
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const unsigned long long y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      if (lane == kWave - 1) wsum[wid] = x;
+      __syncthreads();
+      unsigned long long pre = 0, tot = 0;
+#pragma unroll
+      for (int k = 0; k < kThreads / kWave; ++k) {
+        pre += k < wid ? wsum[k] : 0ull;
+        tot += wsum[k];
+      }
+      unsigned long long e0 = pre + x - run;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        hp[tid * kPer + k] = e0;
+        e0 += d[k];
+      }
+      if (tid == 0) hp[kHubTile] = tot;
+      __syncthreads();
+      for (unsigned long long base = (unsigned long long)blockIdx.x * kThreads; base < tot;
+           base += (unsigned long long)gridDim.x * kThreads) {
+        const unsigned long long e = base + tid;
+        const bool valid = e < tot;
+        uint32_t uu = 0, v = 0;
+        if (valid) {
+          uint32_t a = 0, z = nt;  // last hub whose edge range starts at or before e
+          while (z - a > 1) {
+            const uint32_t mid = (a + z) >> 1;
+            if (hp[mid] <= e) a = mid;
+            else z = mid;
+          }
+          uu = hu[a];
+          v = V.col[hb[a] + (e - hp[a])];
+        }
+        const bool own = valid && v >= V.lo && v < V.hi;
+        wave_claim(V, s, own, v, uu, dnew);
+        wave_emit(V, s, valid && !own, v, uu, pairs, cap);
+      }
+      __syncthreads();
+    }
+  }
+  if (side >= 0) return;
+  if (last_block(&V.st->done_blocks[2], gridDim.x * gridDim.y) && threadIdx.x < 2) {
+    const int ss = threadIdx.x;
+    const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
+    V.sendbuf[ss * block_words(cap)] = ((sides >> ss) & 1) ? min(cnt, cap) : 0u;
+    if (ss == 0) atomicExch(&V.st->done_blocks[2], 0u);
+  }
+}
+
+// Post phase of both sides: owners claim the candidates addressed to them
+// (rank r's side-s block is recvbuf[(2r + s) * block_words(cap)]).
+__global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap) {
+  const Ctl& c = V.ctl[it & 1];
+  const int s = blockIdx.y;
+  if (!((c.sides >> s) & 1)) return;  // block-uniform
+  const uint32_t dnew = c.depth[s] + 1;
+  for (int r = 0; r < V.P; ++r) {
+    const uint32_t* b = V.recvbuf + (2 * (uint64_t)r + s) * block_words(cap);
+    const uint32_t cnt = min(b[0], cap);
+    const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
+    for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < cnt; base += (uint64_t)gridDim.x * kThreads) {
+      const uint64_t i = base + threadIdx.x;
+      bool want = false;
+      uint32_t v = 0, u = 0;
+      if (i < cnt) {
+        const uint2 x = pr[i];
+        v = x.x;
+        u = x.y;
+        want = v >= V.lo && v < V.hi;
+      }
+      wave_claim(V, s, want, v, u, dnew);
+    }
+  }
+}
+
+// Meet check over the vertices each expanded side claimed this round (one the
+// other side also holds closes a path of length dnew + depth_other(v)), then
+// -- last block -- the round's bookkeeping: publish the per-side counts for
+// the reduction and advance the frontiers.
+__global__ __launch_bounds__(kThreads) void k_meet_end(DView V, uint32_t it) {
+  const int p = it & 1;
+  const uint32_t sides = V.ctl[p].sides;
+  DState* st = V.st;
+  const uint32_t f0 = st->fend[0], f1 = st->fend[1];
+  const uint32_t n0 = (sides & 1) ? st->qtail[0] - f0 : 0u;
+  const uint32_t n1 = (sides & 2) ? st->qtail[1] - f1 : 0u;
+  unsigned long long best = kNoKey;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (uint64_t)n0 + n1;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const int s = i < n0 ? 0 : 1;
+    const uint32_t v = pick(V.queue, s)[s ? f1 + (uint32_t)(i - n0) : f0 + (uint32_t)i];
+    const uint32_t li = v - V.lo;
+    if ((pick(V.vis, s ^ 1)[li >> 5] >> (li & 31)) & 1u) {
+      const unsigned long long key =
+          ((unsigned long long)(V.ctl[p].depth[s] + 1 + pick(V.depth, s ^ 1)[li]) << 32) | v;
+      best = key < best ? key : best;
+    }
+  }
+#pragma unroll
+  for (int o = kWave / 2; o >= 1; o >>= 1) {
+    const unsigned long long y = __shfl_xor(best, o);
+    best = y < best ? y : best;
+  }
+  if (__lane_id() == 0 && best != kNoKey) atomicMin(&V.red[p].meetkey, best);
+  if (last_block(&st->done_blocks[1], gridDim.x) && threadIdx.x == 0) {
+    for (int s = 0; s < 2; ++s) {
+      const bool on = (sides >> s) & 1;
+      const uint32_t qt = atomicAdd(&st->qtail[s], 0u);
+      const unsigned long long ne = atomicExch(&st->new_edges[s], 0ull);
+      V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - st->fend[s]) : 0ull;
+      V.red[p].sums[2 * s + 1] = on ? ne : 0ull;
+      if (on) {
+        st->fbeg[s] = st->fend[s];
+        st->fend[s] = qt;
+      }
+      st->hub_count[s] = 0;
+    }
+    atomicExch(&st->done_blocks[1], 0u);
+  }
+}
+
+// Account the last enqueued round and publish Ctl to the host (pinned).
+// flags = kPlanAccountOnly, or kPlanStall to also plan the next round for the host.
+__global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int p = it & 1;
+  Ctl c;
+  plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, flags, c);
+  V.ctl[p] = c;
+  *host = c;
+  __threadfence_system();
+}
+
+// ---- host-planned round kernels ---------------------------------------------
+
+// Execute the stalled plan (sizes were chosen by the host from exact bounds).
+__global__ void k_plan_force(DView V, uint32_t it, Policy pol) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const int p = it & 1;
+  Ctl c;
+  plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, kPlanForce, c);
+  V.ctl[p] = c;
+  V.red[p].meetkey = kNoKey;
+}
+
+__global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t dnew, uint64_t hub_deg) {
+  td_expand_side(V, s, dnew, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(V.cap)) + 1, V.cap, blockIdx.x,
+                 gridDim.x, hub_deg);
+}
+
+__global__ void k_send_header(DView V, int s, uint32_t it) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  const uint32_t c = V.st->send_count[s];
+  V.st->send_count[s] = 0;
+  V.sendbuf[s * block_words(V.cap)] = c;
+  V.red[it & 1].maxsend[s] = c;
+}
+
+// Host-planned post phase: owners claim the candidates addressed to them
+// (rank r's block of `per` pairs at recvbuf + s * P * block_words(cap) + r * block_words(per)).
+__global__ __launch_bounds__(kThreads) void k_td_claim(DView V, int s, uint32_t per, uint32_t dnew) {
+  const uint64_t blk = block_words(per);
+  const uint64_t total = (uint64_t)V.P * per;
+  const uint32_t* R = V.recvbuf + (uint64_t)s * V.P * block_words(V.cap);
   for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < total; base += (uint64_t)gridDim.x * kThreads) {
     const uint64_t t = base + threadIdx.x;
     bool want = false;
     uint32_t v = 0, u = 0;
     if (t < total) {
-      const uint64_t r = t / per_rank, i = t % per_rank;
+      const uint64_t r = t / per, i = t % per;
       const uint32_t* b = R + r * blk;
-      if (i < min(b[0], per_rank)) {
-        const uint2 p = reinterpret_cast<const uint2*>(b)[1 + i];
-        v = p.x;
-        u = p.y;
+      if (i < min(b[0], per)) {
+        const uint2 x = reinterpret_cast<const uint2*>(b)[1 + i];
+        v = x.x;
+        u = x.y;
         want = v >= V.lo && v < V.hi;
       }
     }
@@ -233,8 +640,7 @@ __global__ __launch_bounds__(kThreads) void k_td_claim(DView V, int s, uint32_t 
 }
 
 // Bottom-up pre phase: this rank's slice of the frontier bitmap.
-__global__ void k_obits(DView V, int s, int first) {
-  if (first && blockIdx.x == 0 && threadIdx.x == 0) V.red->meetkey = kNoKey;  // new round
+__global__ void k_obits(DView V, int s) {
   const uint32_t fb = V.st->fbeg[s], fe = V.st->fend[s];
   const uint32_t* q = pick(V.queue, s);
   uint32_t* ob = pick(V.obits, s);
@@ -303,56 +709,20 @@ __global__ __launch_bounds__(kThreads) void k_bu(DView V, int s, uint32_t dnew) 
   }
 }
 
-// Meet check for side s over the vertices it claimed this round: one the other
-// side also holds closes a path of length dnew + depth_other(v).
-__global__ __launch_bounds__(kThreads) void k_meet(DView V, int s, uint32_t dnew) {
-  const uint32_t* q = pick(V.queue, s);
-  const uint32_t* ov = pick(V.vis, s ^ 1);
-  const uint32_t* od = pick(V.depth, s ^ 1);
-  const uint32_t b = V.st->fend[s], e = V.st->qtail[s];
-  unsigned long long best = kNoKey;
-  for (uint64_t i = b + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < e;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t v = q[i], li = v - V.lo;
-    if ((ov[li >> 5] >> (li & 31)) & 1u) {
-      const unsigned long long key = ((unsigned long long)(dnew + od[li]) << 32) | v;
-      best = key < best ? key : best;
-    }
-  }
-#pragma unroll
-  for (int o = kWave / 2; o >= 1; o >>= 1) {
-    const unsigned long long y = __shfl_xor(best, o);
-    best = y < best ? y : best;
-  }
-  if (__lane_id() == 0 && best != kNoKey) atomicMin(&V.red->meetkey, best);
-}
-
-// Round bookkeeping, identical on every rank: publish the per-side counts for
-// the reduction and advance the frontiers of the sides that expanded.
-__global__ void k_round_end(DView V, int sides) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  DState* st = V.st;
-  for (int s = 0; s < 2; ++s) {
-    const bool on = (sides >> s) & 1;
-    V.red->sums[2 * s] = on ? (unsigned long long)(st->qtail[s] - st->fend[s]) : 0ull;
-    V.red->sums[2 * s + 1] = on ? st->new_edges[s] : 0ull;
-    if (on) {
-      st->fbeg[s] = st->fend[s];
-      st->fend[s] = st->qtail[s];
-    }
-    st->send_count[s] = 0;
-    st->new_edges[s] = 0;
-  }
-}
-
+// Seeding pseudo-round: roots claimed by their owners; ctl[1] / red[1] hold
+// the state round 0 reads.
 __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   DState* st = V.st;
+  Reduced& r = V.red[1];
   for (int s = 0; s < 2; ++s) {
     st->fbeg[s] = st->fend[s] = st->qtail[s] = 0;
     st->send_count[s] = 0;
+    st->done_blocks[s] = 0;
+    st->done_blocks[2] = 0;
+    st->hub_count[s] = 0;
     st->new_edges[s] = 0;
-    V.red->sums[2 * s] = V.red->sums[2 * s + 1] = 0;
+    r.sums[2 * s] = r.sums[2 * s + 1] = 0;
     const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
       const uint32_t li = v - V.lo;
@@ -361,24 +731,122 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
       pick(V.depth, s)[li] = 0;
       pick(V.queue, s)[0] = v;
       st->fend[s] = st->qtail[s] = 1;
-      V.red->sums[2 * s] = 1;
-      V.red->sums[2 * s + 1] = V.row_off[li + 1] - V.row_off[li];
+      r.sums[2 * s] = 1;
+      r.sums[2 * s + 1] = V.row_off[li + 1] - V.row_off[li];
     }
   }
-  V.red->meetkey = kNoKey;
-  V.red->maxsend[0] = V.red->maxsend[1] = 0;
-  V.red->md[0] = V.red->md[1] = kEmpty;
+  r.meetkey = kNoKey;
+  Ctl c = {};
+  c.dir[0] = c.dir[1] = 1;
+  c.state = kRun;
+  c.sides = kSeedBit;
+  c.key = kNoKey;
+  V.ctl[1] = c;
 }
 
-// The owner of the meet vertex contributes its two depths (others ~0, min-reduced).
-__global__ void k_meet_depth(DView V, uint32_t meet) {
+// ---- path reconstruction ----------------------------------------------------
+
+// Pack this rank's claimed (vertex, parent) pairs of both sides: one block of
+// {count_S, count_T, S pairs[capS], T pairs[capT]} (the queues hold exactly
+// the claimed owned vertices).
+__global__ void k_pack_parents(DView V, uint32_t capS, uint32_t capT) {
+  uint32_t* out = V.sendbuf;
+  const uint32_t qn0 = V.st->qtail[0], qn1 = V.st->qtail[1];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out[0] = min(qn0, capS);
+    out[1] = min(qn1, capT);
+  }
+  uint2* pr = reinterpret_cast<uint2*>(out + 2);
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (uint64_t)qn0 + qn1;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const int s = i < qn0 ? 0 : 1;
+    const uint32_t k = s ? (uint32_t)(i - qn0) : (uint32_t)i;
+    if (k >= (s ? capT : capS)) continue;
+    const uint32_t v = pick(V.queue, s)[k];
+    pr[(s ? capS : 0) + k] = make_uint2(v, pick(V.parent, s)[v - V.lo]);
+  }
+}
+
+// One workgroup: every rank's gathered pairs into two LDS hash tables
+// (vertex -> parent, one per side), then the two parent chains from the meet
+// vertex.  out = {status, dS, dT, pad, path[hops + 1]}; status 0 = ok.
+__global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv, int P, uint32_t capS,
+                                               uint32_t capT, uint32_t slotsS, uint32_t slotsT, uint32_t meet,
+                                               uint32_t hops, uint32_t* out) {
+  extern __shared__ uint32_t lds[];
+  uint32_t* keys[2] = {lds, lds + 2 * slotsS};
+  const uint32_t mask[2] = {slotsS - 1, slotsT - 1};
+  for (uint32_t i = threadIdx.x; i < slotsS + slotsT; i += blockDim.x) {
+    const uint32_t s = i < slotsS ? 0 : 1, k = s ? i - slotsS : i;
+    keys[s][2 * k] = kEmpty;
+  }
+  __syncthreads();
+  const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
+  for (int r = 0; r < P; ++r) {
+    const uint32_t* b = recv + (uint64_t)r * blk;
+    const uint32_t c0 = b[0], c1 = b[1];
+    const uint2* pr = reinterpret_cast<const uint2*>(b + 2);
+    for (uint32_t i = threadIdx.x; i < c0 + c1; i += blockDim.x) {
+      const int s = i < c0 ? 0 : 1;
+      const uint2 x = pr[s ? capS + (i - c0) : i];
+      uint32_t h = (x.x * 2654435761u) & mask[s];
+      while (true) {
+        const uint32_t prev = atomicCAS(&keys[s][2 * h], kEmpty, x.x);
+        if (prev == kEmpty || prev == x.x) break;
+        h = (h + 1) & mask[s];
+      }
+      keys[s][2 * h + 1] = x.y;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  auto parent_of = [&](int s, uint32_t v, bool& ok) -> uint32_t {
+    uint32_t h = (v * 2654435761u) & mask[s];
+    for (uint32_t probe = 0; probe <= mask[s]; ++probe) {
+      const uint32_t k = keys[s][2 * h];
+      if (k == v) return keys[s][2 * h + 1];
+      if (k == kEmpty) break;
+      h = (h + 1) & mask[s];
+    }
+    ok = false;
+    return kEmpty;
+  };
+  bool ok = true;
+  uint32_t d[2] = {0, 0};
+  for (int s = 0; s < 2 && ok; ++s)  // chain lengths
+    for (uint32_t v = meet, u; ok && (u = parent_of(s, v, ok)) != kEmpty && d[s] <= hops; v = u) ++d[s];
+  if (!ok || d[0] + d[1] != hops) {
+    out[0] = 1;
+    out[1] = d[0];
+    out[2] = d[1];
+    return;
+  }
+  uint32_t* path = out + 4;  // src .. meet .. dst
+  uint32_t v = meet;
+  for (int i = (int)d[0]; i >= 0; --i) {
+    path[i] = v;
+    v = parent_of(0, v, ok);
+  }
+  v = meet;
+  for (uint32_t i = d[0]; i <= hops; ++i) {
+    path[i] = v;
+    v = parent_of(1, v, ok);
+  }
+  out[0] = 0;
+  out[1] = d[0];
+  out[2] = d[1];
+}
+
+// Fallback for very large visited sets: the owner of the meet vertex
+// contributes its two depths (others ~0, min-reduced) ...
+__global__ void k_meet_depth(DView V, uint32_t meet, uint32_t it) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const bool own = meet >= V.lo && meet < V.hi;
-  V.red->md[0] = own ? V.depth[0][meet - V.lo] : kEmpty;
-  V.red->md[1] = own ? V.depth[1][meet - V.lo] : kEmpty;
+  V.red[it & 1].md[0] = own ? V.depth[0][meet - V.lo] : kEmpty;
+  V.red[it & 1].md[1] = own ? V.depth[1][meet - V.lo] : kEmpty;
 }
 
-// Path reconstruction step: cur[q] -> its parent (only the owner knows it; the
+// ... and one step per hop: cur[q] -> its parent (only the owner knows it; the
 // others contribute ~0 to the ncclMin that follows).
 __global__ void k_path_step(DView V, uint32_t* cur, uint32_t* pathS, uint32_t* pathT, int i, int dS, int dT) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -414,18 +882,26 @@ unsigned blocks_for(uint64_t work, int cus) {
   return (unsigned)std::max<uint64_t>(b, 1);
 }
 
+uint32_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return (uint32_t)std::min<uint64_t>(p, 1ull << 31);
+}
+
 }  // namespace
 
 std::vector<uint8_t> dist_unique_id() { return dist::rccl_unique_id(); }
 
 struct DistBiBfs::Impl {
   int rank = 0, size = 1, device = 0, cus = 256;
-  hipStream_t stream = nullptr;   // compute: pre phases, graph build
-  hipStream_t cstream = nullptr;  // comm: exchanges, post phases, round end
+  hipStream_t stream = nullptr;   // compute: pre phases of host-planned rounds, graph build
+  hipStream_t cstream = nullptr;  // comm: everything of speculative rounds, exchanges, post phases
   hipEvent_t ev_pre[2] = {nullptr, nullptr};
   hipEvent_t ev_round = nullptr;
+  hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timing events around a search
   std::unique_ptr<dist::Comm> comm;
-  uint32_t n = 0, lo = 0, hi = 0, chunk = 0, gwords = 0, cap = 0;
+  uint32_t n = 0, lo = 0, hi = 0, chunk = 0, gwords = 0, cap_alloc = 0;
+  uint32_t block_cap = 0;  // pairs per candidate block the send buffer holds (per side)
   uint64_t m_input = 0, nnz = 0;
   uint64_t* d_row_off = nullptr;
   uint32_t* d_col = nullptr;
@@ -435,9 +911,15 @@ struct DistBiBfs::Impl {
   uint32_t* d_cur = nullptr;
   uint32_t* d_pathS = nullptr;
   uint32_t* d_pathT = nullptr;
-  Reduced* h_red = nullptr;  // pinned
+  uint32_t* d_walk = nullptr;  // k_walk output
+  Reduced* h_red = nullptr;    // pinned
+  Ctl* h_ctl = nullptr;        // pinned, written by k_final
+  uint32_t* h_walk = nullptr;  // pinned
+  size_t h_walk_cap = 0;
   double* d_scalar = nullptr;
   DistLevelStats stats;
+  DistTuning tune;
+  int fault_at = 0, fault_mode = 0;
 
   void setup(int dev) {
     device = dev;
@@ -454,7 +936,13 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipStreamCreateWithPriority(&cstream, hipStreamNonBlocking, hi_pri));
     for (auto& e : ev_pre) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_round, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreate(&ev_t0));
+    HIP_CHECK(hipEventCreate(&ev_t1));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl), sizeof(Ctl), hipHostMallocDefault));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
   }
 
   void set_partition(uint32_t nn) {
@@ -472,33 +960,42 @@ struct DistBiBfs::Impl {
     d_row_off = nullptr;
     d_col = nullptr;
     state = nullptr;
+    n = 0;
+  }
+
+  // effective host-planned block capacity (tuning may shrink it for tests)
+  uint32_t cap() const {
+    return tune.cap ? std::min<uint32_t>(tune.cap, cap_alloc) : cap_alloc;
   }
 
   void alloc_state() {
     const uint64_t words = chunk / 32;
     gwords = (uint32_t)(((uint64_t)n + 31) / 32 + 1);
-    cap = (uint32_t)std::min<uint64_t>(kCapMax, std::max<uint64_t>(n, 1));
-    const uint64_t block = 2 + 2ULL * cap;
+    cap_alloc = (uint32_t)std::min<uint64_t>(kCapMax, std::max<uint64_t>(n, 1));
+    // blocks must also hold a speculative round's two blocks and the path gather
+    block_cap = std::max<uint32_t>(cap_alloc, std::max<uint32_t>(tune.walk_max, kSpecCapMin));
+    const uint64_t block = block_words(block_cap);
     size_t off = 0;
     auto take = [&](size_t bytes) {
       size_t o = off;
       off += (bytes + 255) & ~(size_t)255;
       return o;
     };
-    size_t o_vis[2], o_par[2], o_dep[2], o_q[2], o_ob[2], o_gb[2], o_send[2], o_recv[2];
+    size_t o_vis[2], o_par[2], o_dep[2], o_q[2], o_ob[2], o_gb[2], o_hub[2];
     for (int s = 0; s < 2; ++s) {
+      o_hub[s] = take((size_t)chunk * 4);
       o_vis[s] = take(words * 4);
       o_par[s] = take((size_t)chunk * 4);
       o_dep[s] = take((size_t)chunk * 4);
       o_q[s] = take((size_t)chunk * 4);
       o_ob[s] = take(words * 4);
       o_gb[s] = take(words * 4 * size);
-      o_send[s] = take(block * 4);
-      o_recv[s] = take(block * 4 * size);
     }
+    const size_t o_send = take(2 * block * 4), o_recv = take(2 * block * 4 * size);
     const size_t o_sent = take((size_t)gwords * 4 * 2);
-    const size_t o_st = take(sizeof(DState)), o_red = take(sizeof(Reduced)), o_cur = take(64),
-                 o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4), o_sc = take(64);
+    const size_t o_st = take(sizeof(DState)), o_ctl = take(2 * sizeof(Ctl)), o_red = take(2 * sizeof(Reduced)),
+                 o_cur = take(64), o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4),
+                 o_walk = take(((size_t)n + 8) * 4), o_sc = take(64);
     HIP_CHECK(hipMalloc(&state, off));
     char* b = static_cast<char*>(state);
     V.n = n;
@@ -513,21 +1010,24 @@ struct DistBiBfs::Impl {
       V.parent[s] = reinterpret_cast<uint32_t*>(b + o_par[s]);
       V.depth[s] = reinterpret_cast<uint32_t*>(b + o_dep[s]);
       V.queue[s] = reinterpret_cast<uint32_t*>(b + o_q[s]);
+      V.hubs[s] = reinterpret_cast<uint32_t*>(b + o_hub[s]);
       V.obits[s] = reinterpret_cast<uint32_t*>(b + o_ob[s]);
       V.gbits[s] = reinterpret_cast<uint32_t*>(b + o_gb[s]);
-      V.send[s] = reinterpret_cast<uint32_t*>(b + o_send[s]);
-      V.recv[s] = reinterpret_cast<uint32_t*>(b + o_recv[s]);
       V.sent[s] = sent_base + (size_t)s * gwords;
       HIP_CHECK(hipMemsetAsync(V.vis[s], 0, words * 4, stream));
     }
+    V.sendbuf = reinterpret_cast<uint32_t*>(b + o_send);
+    V.recvbuf = reinterpret_cast<uint32_t*>(b + o_recv);
     HIP_CHECK(hipMemsetAsync(sent_base, 0, (size_t)gwords * 4 * 2, stream));
-    V.cap = cap;
+    V.cap = cap();
     V.P = size;
     V.st = reinterpret_cast<DState*>(b + o_st);
+    V.ctl = reinterpret_cast<Ctl*>(b + o_ctl);
     V.red = reinterpret_cast<Reduced*>(b + o_red);
     d_cur = reinterpret_cast<uint32_t*>(b + o_cur);
     d_pathS = reinterpret_cast<uint32_t*>(b + o_ps);
     d_pathT = reinterpret_cast<uint32_t*>(b + o_pt);
+    d_walk = reinterpret_cast<uint32_t*>(b + o_walk);
     d_scalar = reinterpret_cast<double*>(b + o_sc);
     HIP_CHECK(hipMemsetAsync(V.st, 0, sizeof(DState), stream));
     HIP_CHECK(hipMemsetAsync(d_scalar, 0, 64, stream));
@@ -556,11 +1056,350 @@ struct DistBiBfs::Impl {
     nnz = rows.nnz();
   }
 
-  void read_back(hipStream_t s) {
-    HIP_CHECK(hipMemcpyAsync(h_red, V.red, sizeof(Reduced), hipMemcpyDeviceToHost, s));
-    HIP_CHECK(hipStreamSynchronize(s));
+  // Host wait with a watchdog: poll the stream; an RCCL error reported by the
+  // communicator, or no progress within timeout_s (a dead or hung peer leaves
+  // our collective waiting forever), aborts the communicator and throws.
+  void wait(hipStream_t s) {
+    stats.host_syncs++;
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto deadline = t0 + std::chrono::duration<double>(tune.timeout_s);
+    for (uint64_t spin = 0;; ++spin) {
+      const hipError_t e = hipStreamQuery(s);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) HIP_CHECK(e);
+      if ((spin & 255) == 255) {
+        comm->check();
+        const auto now = std::chrono::steady_clock::now();
+        if (now > deadline) {
+          comm->abort();
+          throw Error("dist: rank " + std::to_string(rank) + " waited " + std::to_string(tune.timeout_s) +
+                      " s for a round (peer failure or hang); communicator aborted");
+        }
+        if (now - t0 > std::chrono::milliseconds(2)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
   }
+
+  Policy policy(const SearchOptions& opt) const {
+    Policy p;
+    p.alpha = opt.alpha;
+    p.beta = opt.beta;
+    p.nnz_total = 2 * m_input;
+    p.n = n;
+    p.lockstep = opt.lockstep ? 1 : 0;
+    p.side = (int)opt.side;
+    p.direction = (int)opt.direction;
+    return p;
+  }
+
+  void maybe_fault(int it) {
+    if (!fault_mode || it < fault_at) return;
+    const int mode = fault_mode;
+    fault_mode = 0;
+    if (mode == 2) std::this_thread::sleep_for(std::chrono::duration<double>(2 * tune.timeout_s));
+    throw Error("dist: injected fault on rank " + std::to_string(rank) + " at round " + std::to_string(it));
+  }
+
+  SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt);
+  void host_round(uint32_t it, const Policy& pol, SearchResult& r);
+  bool walk_path(uint64_t key, SearchResult& r);
+  void walk_path_per_hop(uint64_t key, uint32_t it, SearchResult& r);
 };
+
+// One round planned by the host (a stalled speculative plan: a bottom-up
+// level, or a sparse level too big for the speculative block).  Sizes come
+// from the read-back Ctl; one host wait at the end (k_final).
+void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r) {
+  const Ctl h = *h_ctl;
+  hipStream_t ps = stream, cs = cstream;
+  const int P = size;
+  const uint32_t words = chunk / 32, nloc = hi - lo;
+  const uint32_t capr = cap();
+  V.cap = capr;
+  stats.host_rounds++;
+  k_plan_force<<<1, 64, 0, cs>>>(V, it, pol);
+  HIP_CHECK(hipGetLastError());
+  int sides[2], ns = 0;
+  for (int s = 0; s < 2; ++s)
+    if ((h.want >> s) & 1) sides[ns++] = s;
+  // ---- pre phases on the compute stream
+  HIP_CHECK(hipEventRecord(ev_round, cs));
+  HIP_CHECK(hipStreamWaitEvent(ps, ev_round, 0));
+  for (int i = 0; i < ns; ++i) {
+    const int s = sides[i];
+    const uint32_t dnew = h.depth[s] + 1;
+    const unsigned fblocks = blocks_for(h.cnt[s] / (uint64_t)P + kThreads, cus);
+    if (!((h.want_modes >> s) & 1)) {
+      const bool hubs = h.fed[s] > kHubDeg;
+      k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, hubs ? kHubDeg : kNoHubs);
+      if (hubs)
+        k_td_hubs<<<blocks_for(std::min<uint64_t>(h.fed[s], (uint64_t)cus * 8 * kThreads), cus), kThreads, 0, ps>>>(
+            V, it, s, dnew, capr);
+      k_send_header<<<1, 64, 0, ps>>>(V, s, it);
+    } else {
+      HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
+      k_obits<<<fblocks, kThreads, 0, ps>>>(V, s);
+    }
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(ev_pre[i], ps));
+  }
+  // ---- exchange + post phases on the comm stream: side 0's run while side
+  // 1's pre phase is still computing on the other stream
+  for (int i = 0; i < ns; ++i) {
+    const int s = sides[i];
+    const uint32_t dnew = h.depth[s] + 1;
+    HIP_CHECK(hipStreamWaitEvent(cs, ev_pre[i], 0));
+    bool bottomup = (h.want_modes >> s) & 1;
+    if (!bottomup) {
+      uint64_t per;
+      const uint64_t bound = std::min<uint64_t>(h.fed[s], capr);
+      if (h.fed[s] <= capr && block_words(bound) * 4 * (uint64_t)P <= tune.nosync_bytes) {
+        per = bound;  // no rank emits more than the side's frontier edges: no count exchange
+      } else {
+        comm->allreduce(V.red[it & 1].maxsend + s, 1, DType::kU32, ROp::kMax, cs);
+        stats.collectives++;
+        HIP_CHECK(hipMemcpyAsync(h_red, V.red + (it & 1), sizeof(Reduced), hipMemcpyDeviceToHost, cs));
+        wait(cs);
+        per = h_red->maxsend[s];
+        stats.count_syncs++;
+        if (per > capr) {
+          bottomup = true;  // finish the level bottom-up; the local claims made stay valid
+          stats.overflow_levels++;
+        }
+      }
+      if (!bottomup) {
+        if (per > 0) {
+          // this side's exchange lands at recvbuf + s * P * block_words(per); a
+          // rank's send block is at sendbuf + s * block_words(capr)
+          uint32_t* recv = V.recvbuf + (uint64_t)s * P * block_words(capr);
+          comm->allgather(V.sendbuf + s * block_words(capr), recv, block_words(per) * 4, cs);
+          stats.collectives++;
+          k_td_claim<<<blocks_for((uint64_t)P * per, cus), kThreads, 0, cs>>>(V, s, (uint32_t)per, dnew);
+          stats.exchanged_bytes += block_words(per) * 4 * (uint64_t)P;
+        }
+      } else {
+        HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, cs));
+        k_obits<<<blocks_for(h.cnt[s] / (uint64_t)P + kThreads, cus), kThreads, 0, cs>>>(V, s);
+      }
+    }
+    if (bottomup) {
+      stats.dense_levels++;
+      comm->allgather(V.obits[s], V.gbits[s], (size_t)words * 4, cs);
+      stats.collectives++;
+      k_bu<<<blocks_for(nloc, cus), kThreads, 0, cs>>>(V, s, dnew);
+      stats.exchanged_bytes += (uint64_t)words * 4 * P;
+      ++r.stats.bottomup_levels;
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+  const uint64_t claimed_bound = std::min<uint64_t>((uint64_t)nloc, h.fed[0] + h.fed[1] + 1);
+  k_meet_end<<<blocks_for(claimed_bound, cus), kThreads, 0, cs>>>(V, it);
+  HIP_CHECK(hipGetLastError());
+  comm->group_begin();
+  comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
+  comm->allreduce(&V.red[it & 1].meetkey, 1, DType::kU64, ROp::kMin, cs);
+  comm->group_end();
+  stats.collectives += 2;
+}
+
+SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& opt) {
+  const auto t0 = std::chrono::steady_clock::now();
+  BIBFS_REQUIRE(n > 0, "no graph loaded");
+  BIBFS_REQUIRE(src < n && dst < n, "src/dst out of range");
+  if (comm->aborted()) throw Error("dist: the communicator was aborted by an earlier failure");
+  HIP_CHECK(hipSetDevice(device));
+  stats = DistLevelStats{};
+  SearchResult r;
+  if (src == dst) {
+    r.found = true;
+    r.hops = 0;
+    r.meet = src;
+    r.path = {src};
+    r.stats.visited = 1;
+    r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return r;
+  }
+  const int P = size;
+  hipStream_t cs = cstream;
+  const Policy pol = policy(opt);
+  V.cap = cap();
+
+  HIP_CHECK(hipEventRecord(ev_t0, cs));
+  k_seed<<<1, 64, 0, cs>>>(V, src, dst);
+  comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
+  stats.collectives++;
+  uint32_t it = 0;
+  uint32_t spec_cap = kSpecCapMin;
+  int flags = 0;
+  bool have_ctl = false;  // h_ctl describes the current device state
+  const int K = std::max(0, tune.spec_rounds);
+  const bool host_only = K == 0;  // A/B mode: every round planned on the host
+  const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
+  if (host_only) {
+    k_final<<<1, 64, 0, cs>>>(V, it++, pol, h_ctl, kPlanStall);
+    HIP_CHECK(hipGetLastError());
+    wait(cs);
+    have_ctl = true;
+  }
+  for (uint64_t guard = 0;; ++guard) {
+    BIBFS_REQUIRE(guard <= 4ull * n + 16, "dist: search did not terminate");
+    if (have_ctl && h_ctl->state != kRun && h_ctl->state != kStall) break;
+    if (have_ctl && h_ctl->state == kStall) {
+      const Ctl& h = *h_ctl;
+      uint64_t need = 0;
+      for (int s = 0; s < 2; ++s)
+        if ((h.want >> s) & 1) need = std::max<uint64_t>(need, h.fed[s]);
+      if (!host_only && h.stall == kStallCap && need <= spec_max) {
+        spec_cap = std::max<uint32_t>(spec_cap, next_pow2(need));
+        flags = kPlanResume;  // re-run the stalled plan speculatively with a bigger block
+      } else {
+        maybe_fault((int)it);
+        host_round(it, pol, r);
+        k_final<<<1, 64, 0, cs>>>(V, it + 1, pol, h_ctl, host_only ? kPlanStall : kPlanAccountOnly);
+        HIP_CHECK(hipGetLastError());
+        it += 2;
+        wait(cs);
+        const uint64_t fm = std::max(h_ctl->fed[0], h_ctl->fed[1]);
+        spec_cap = std::min(spec_max, std::max<uint32_t>(kSpecCapMin, next_pow2(4 * fm)));
+        continue;
+      }
+    }
+    // ---- K speculative sparse rounds, then one host wait
+    const unsigned bx = std::min<unsigned>(
+        (unsigned)cus * 2, std::max<unsigned>(1, (unsigned)((uint64_t)spec_cap / P / kThreads) + 1));
+    const unsigned cx = std::min<unsigned>((unsigned)cus * 2, std::max<unsigned>(1, spec_cap / kThreads / 4 + 1));
+    const uint64_t gather_bytes = 2 * block_words(spec_cap) * 4;
+    // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
+    // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
+    const bool hubs = spec_cap > kSpecHubCap;
+    const unsigned hx = std::min<unsigned>((unsigned)cus, spec_cap / kThreads + 1);
+    for (int k = 0; k < K; ++k) {
+      maybe_fault((int)it);
+      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, spec_cap, k == 0 ? flags : 0,
+                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, spec_cap);
+      HIP_CHECK(hipGetLastError());
+      comm->allgather(V.sendbuf, V.recvbuf, gather_bytes, cs);
+      k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, spec_cap);
+      k_meet_end<<<std::min<unsigned>(bx, 64), kThreads, 0, cs>>>(V, it);
+      HIP_CHECK(hipGetLastError());
+      comm->group_begin();
+      comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
+      comm->allreduce(&V.red[it & 1].meetkey, 1, DType::kU64, ROp::kMin, cs);
+      comm->group_end();
+      stats.collectives += 3;
+      stats.exchanged_bytes += gather_bytes * P;
+      stats.spec_rounds++;
+      ++it;
+    }
+    flags = 0;
+    k_final<<<1, 64, 0, cs>>>(V, it++, pol, h_ctl, kPlanAccountOnly);
+    HIP_CHECK(hipGetLastError());
+    wait(cs);
+    have_ctl = true;
+    if (h_ctl->state == kRun) {  // size the next batch for the frontier we have now
+      const uint64_t fm = std::max(h_ctl->fed[0], h_ctl->fed[1]);
+      spec_cap = std::min(spec_max, std::max<uint32_t>(spec_cap, next_pow2(4 * fm)));
+    }
+  }
+  const Ctl h = *h_ctl;
+  stats.rounds = (int)h.rounds;
+  stats.lockstep_rounds = (int)h.lockstep_rounds;
+  stats.levels = (int)h.levels;
+  stats.sparse_levels = (int)h.sparse_levels;
+  r.stats.levels = (int)h.levels;
+  r.stats.edges_inspected = h.einsp;
+  r.stats.visited = h.vis[0] + h.vis[1];
+  stats.comm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (h.state == kDone) {
+    const uint64_t key = h.key;
+    r.found = true;
+    r.meet = (uint32_t)(key & 0xffffffffull);
+    r.hops = (int64_t)(key >> 32);
+    if (opt.want_path) {
+      if (!walk_path(key, r)) walk_path_per_hop(key, it, r);
+    }
+  }
+  k_cleanup<<<blocks_for(std::max<uint64_t>(h.vis[0] + h.vis[1], 1), cus), kThreads, 0, cs>>>(V);
+  HIP_CHECK(hipMemsetAsync(sent_base, 0, (size_t)gwords * 4 * 2, cs));
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipEventRecord(ev_t1, cs));
+  wait(cs);
+  float dms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&dms, ev_t0, ev_t1));
+  stats.device_ms = dms;
+  r.stats.grid_levels = r.stats.levels;
+  r.search_ms = dms;
+  r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return r;
+}
+
+// Path in O(1) collectives: every rank packs the (vertex, parent) pairs it
+// claimed, ONE allgather, and a one-workgroup kernel walks both parent chains
+// from LDS tables.  False when the visited sets are too large for that.
+bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
+  const Ctl& h = *h_ctl;
+  const uint64_t vS = h.vis[0], vT = h.vis[1];
+  if (vS + vT > tune.walk_max) return false;
+  const uint32_t capS = (uint32_t)std::max<uint64_t>(vS, 1), capT = (uint32_t)std::max<uint64_t>(vT, 1);
+  const uint32_t slotsS = next_pow2(2 * (uint64_t)capS), slotsT = next_pow2(2 * (uint64_t)capT);
+  const size_t lds = (size_t)(slotsS + slotsT) * 8;
+  if (lds > 160 * 1024) return false;
+  const uint32_t meet = (uint32_t)(key & 0xffffffffull), hops = (uint32_t)(key >> 32);
+  hipStream_t cs = cstream;
+  k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(V, capS, capT);
+  const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
+  comm->allgather(V.sendbuf, V.recvbuf, blk * 4, cs);
+  stats.collectives++;
+  stats.path_collectives++;
+  stats.exchanged_bytes += blk * 4 * size;
+  k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, d_walk);
+  HIP_CHECK(hipGetLastError());
+  const size_t words = 4 + (size_t)hops + 1;
+  if (h_walk_cap < words) {
+    if (h_walk) HIP_CHECK(hipHostFree(h_walk));
+    h_walk_cap = std::max<size_t>(words, 1024);
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_walk), h_walk_cap * 4, hipHostMallocDefault));
+  }
+  HIP_CHECK(hipMemcpyAsync(h_walk, d_walk, words * 4, hipMemcpyDeviceToHost, cs));
+  wait(cs);
+  BIBFS_REQUIRE(h_walk[0] == 0, "dist: parent chains from the meet vertex do not add up to the path length (" +
+                                    std::to_string(h_walk[1]) + " + " + std::to_string(h_walk[2]) +
+                                    " != " + std::to_string(hops) + ")");
+  r.path.assign(h_walk + 4, h_walk + 4 + hops + 1);
+  return true;
+}
+
+// Fallback: one allreduce per hop (visited sets too large to gather).
+void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult& r) {
+  hipStream_t cs = cstream;
+  const uint32_t meet = (uint32_t)(key & 0xffffffffull);
+  k_meet_depth<<<1, 64, 0, cs>>>(V, meet, it);
+  comm->allreduce(V.red[it & 1].md, 2, DType::kU32, ROp::kMin, cs);
+  stats.collectives++;
+  stats.path_collectives++;
+  HIP_CHECK(hipMemcpyAsync(h_red, V.red + (it & 1), sizeof(Reduced), hipMemcpyDeviceToHost, cs));
+  wait(cs);
+  const int dS = (int)h_red->md[0], dT = (int)h_red->md[1];
+  BIBFS_REQUIRE((int64_t)dS + dT == r.hops, "dist: meet depths disagree with the path length");
+  const int K = std::max(dS, dT);
+  const uint32_t init[2] = {meet, meet};
+  HIP_CHECK(hipMemcpyAsync(d_cur, init, 8, hipMemcpyHostToDevice, cs));
+  for (int i = 0; i <= K; ++i) {
+    k_path_step<<<1, 64, 0, cs>>>(V, d_cur, d_pathS, d_pathT, i, dS, dT);
+    if (i < K) {
+      comm->allreduce(d_cur, 2, DType::kU32, ROp::kMin, cs);
+      stats.collectives++;
+      stats.path_collectives++;
+    }
+  }
+  std::vector<uint32_t> pS((size_t)dS + 1), pT((size_t)dT + 1);
+  HIP_CHECK(hipMemcpyAsync(pS.data(), d_pathS, pS.size() * 4, hipMemcpyDeviceToHost, cs));
+  HIP_CHECK(hipMemcpyAsync(pT.data(), d_pathT, pT.size() * 4, hipMemcpyDeviceToHost, cs));
+  wait(cs);
+  r.path.assign(pS.rbegin(), pS.rend());
+  r.path.insert(r.path.end(), pT.begin() + 1, pT.end());
+}
 
 DistBiBfs::DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& uid) : p_(new Impl) {
   HIP_CHECK(hipSetDevice(device));
@@ -578,15 +1417,21 @@ DistBiBfs::~DistBiBfs() {
   if (!p_) return;
   try {
     (void)hipSetDevice(p_->device);
-    (void)hipStreamSynchronize(p_->stream);
-    (void)hipStreamSynchronize(p_->cstream);
+    if (!p_->comm->aborted()) {
+      (void)hipStreamSynchronize(p_->stream);
+      (void)hipStreamSynchronize(p_->cstream);
+    }
     p_->free_all();
   } catch (...) {
   }
   p_->comm.reset();
   (void)hipHostFree(p_->h_red);
+  (void)hipHostFree(p_->h_ctl);
+  if (p_->h_walk) (void)hipHostFree(p_->h_walk);
   for (auto e : p_->ev_pre) (void)hipEventDestroy(e);
   (void)hipEventDestroy(p_->ev_round);
+  (void)hipEventDestroy(p_->ev_t0);
+  (void)hipEventDestroy(p_->ev_t1);
   (void)hipStreamDestroy(p_->cstream);
   (void)hipStreamDestroy(p_->stream);
 }
@@ -653,200 +1498,21 @@ void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, d
 
 SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   auto& I = *p_;
-  auto& V = I.V;
-  const auto t0 = std::chrono::steady_clock::now();
-  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
-  BIBFS_REQUIRE(src < I.n && dst < I.n, "src/dst out of range");
-  HIP_CHECK(hipSetDevice(I.device));
-  I.stats = DistLevelStats{};
-  SearchResult r;
-  if (src == dst) {
-    r.found = true;
-    r.hops = 0;
-    r.meet = src;
-    r.path = {src};
-    r.stats.visited = 1;
-    r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    return r;
+  try {
+    return I.search(src, dst, opt);
+  } catch (...) {
+    // A rank that fails mid-search would leave its peers blocked in a
+    // collective forever: tear the communicator down so they return too.
+    I.comm->abort();
+    throw;
   }
-  const int cus = I.cus, P = I.size;
-  hipStream_t ps = I.stream, cs = I.cstream;
-  dist::Comm& comm = *I.comm;
-  const uint32_t words = I.chunk / 32, nloc = I.hi - I.lo;
-
-  k_seed<<<1, 64, 0, cs>>>(V, src, dst);
-  comm.allreduce(V.red->sums, 4, DType::kU64, ROp::kSum, cs);
-  HIP_CHECK(hipEventRecord(I.ev_round, cs));
-  I.read_back(cs);
-  // replicated host bookkeeping (identical on every rank)
-  uint64_t cnt[2] = {1, 1}, fed[2] = {I.h_red->sums[1], I.h_red->sums[3]};
-  uint64_t ved[2] = {fed[0], fed[1]};
-  int depth[2] = {0, 0}, dir[2] = {1, 1}, turn = 0;
-  const uint64_t nnz_total = 2 * I.m_input;
-  unsigned long long key = kNoKey;
-  bool dead = false;
-  for (uint64_t guard = 0; guard <= 2ULL * I.n + 2 && key == kNoKey && !dead; ++guard) {
-    const auto tr0 = std::chrono::steady_clock::now();
-    // ---- which sides expand this round
-    int sides[2] = {0, 1}, ns = 1;
-    const uint64_t flo = std::min(fed[0], fed[1]), fhi = std::max(fed[0], fed[1]);
-    if (opt.lockstep && opt.side != SidePolicy::kAlternate && (fhi <= kLockstepEdges || fhi <= 2 * flo)) {
-      ns = 2;
-    } else if (opt.side == SidePolicy::kAlternate) {
-      sides[0] = turn;
-      turn ^= 1;
-    } else if (opt.side == SidePolicy::kSmallerFrontier) {
-      sides[0] = cnt[0] <= cnt[1] ? 0 : 1;
-    } else {
-      sides[0] = fed[0] <= fed[1] ? 0 : 1;
-    }
-    int mode[2] = {1, 1};  // 1 top-down, 2 bottom-up
-    for (int i = 0; i < ns; ++i) {
-      const int s = sides[i];
-      if (opt.direction == Direction::kTopDown) {
-        mode[s] = 1;
-      } else if (opt.direction == Direction::kBottomUp) {
-        mode[s] = 2;
-      } else {
-        const double m_u = (double)nnz_total - (double)ved[s];
-        if (dir[s] == 1 && (double)fed[s] > m_u / opt.alpha) dir[s] = 2;
-        else if (dir[s] == 2 && (double)cnt[s] < (double)I.n / opt.beta) dir[s] = 1;
-        mode[s] = dir[s];
-      }
-    }
-    // ---- pre phases on the compute stream (behind the previous round)
-    HIP_CHECK(hipStreamWaitEvent(ps, I.ev_round, 0));
-    for (int i = 0; i < ns; ++i) {
-      const int s = sides[i];
-      const uint32_t dnew = (uint32_t)depth[s] + 1;
-      const unsigned fblocks = blocks_for(cnt[s] / (uint64_t)P + kThreads, cus);
-      if (mode[s] == 1) {
-        k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, i == 0);
-        k_send_header<<<1, 64, 0, ps>>>(V, s);
-      } else {
-        HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
-        k_obits<<<fblocks, kThreads, 0, ps>>>(V, s, i == 0);
-      }
-      HIP_CHECK(hipGetLastError());
-      HIP_CHECK(hipEventRecord(I.ev_pre[i], ps));
-    }
-    // ---- exchange + post phases on the comm stream: side 0's run while side
-    // 1's pre phase is still computing on the other stream
-    for (int i = 0; i < ns; ++i) {
-      const int s = sides[i];
-      const uint32_t dnew = (uint32_t)depth[s] + 1;
-      HIP_CHECK(hipStreamWaitEvent(cs, I.ev_pre[i], 0));
-      bool bottomup = mode[s] == 2;
-      if (!bottomup) {
-        uint64_t per;
-        const uint64_t bound = std::min<uint64_t>(fed[s], I.cap);
-        if (fed[s] <= I.cap && (2 + 2 * bound) * 4 * (uint64_t)P <= kNoSyncBytes) {
-          per = bound;  // no rank emits more than the side's frontier edges: no count exchange
-        } else {
-          comm.allreduce(V.red->maxsend + s, 1, DType::kU32, ROp::kMax, cs);
-          I.read_back(cs);
-          per = I.h_red->maxsend[s];
-          I.stats.count_syncs++;
-          if (per > I.cap) {
-            bottomup = true;  // finish the level bottom-up; the local claims made stay valid
-            I.stats.overflow_levels++;
-          }
-        }
-        if (!bottomup) {
-          I.stats.sparse_levels++;
-          if (per > 0) {
-            const uint64_t blk = 2 + 2 * per;
-            comm.allgather(V.send[s], V.recv[s], blk * 4, cs);
-            k_td_claim<<<blocks_for((uint64_t)P * per, cus), kThreads, 0, cs>>>(V, s, (uint32_t)per, dnew);
-            I.stats.exchanged_bytes += blk * 4 * (uint64_t)P;
-          }
-        } else {
-          HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, cs));
-          k_obits<<<blocks_for(cnt[s] / (uint64_t)P + kThreads, cus), kThreads, 0, cs>>>(V, s, 0);
-        }
-      }
-      if (bottomup) {
-        I.stats.dense_levels++;
-        comm.allgather(V.obits[s], V.gbits[s], (size_t)words * 4, cs);
-        k_bu<<<blocks_for(nloc, cus), kThreads, 0, cs>>>(V, s, dnew);
-        I.stats.exchanged_bytes += (uint64_t)words * 4 * P;
-        ++r.stats.bottomup_levels;
-      }
-      HIP_CHECK(hipGetLastError());
-      r.stats.edges_inspected += fed[s];
-      ++r.stats.levels;
-    }
-    int mask = 0;
-    for (int i = 0; i < ns; ++i) {
-      const int s = sides[i];
-      k_meet<<<blocks_for(std::min<uint64_t>(fed[s], nloc), cus), kThreads, 0, cs>>>(V, s, (uint32_t)depth[s] + 1);
-      mask |= 1 << s;
-    }
-    k_round_end<<<1, 64, 0, cs>>>(V, mask);
-    HIP_CHECK(hipGetLastError());
-    comm.group_begin();
-    comm.allreduce(V.red->sums, 4, DType::kU64, ROp::kSum, cs);
-    comm.allreduce(&V.red->meetkey, 1, DType::kU64, ROp::kMin, cs);
-    comm.group_end();
-    HIP_CHECK(hipEventRecord(I.ev_round, cs));
-    I.read_back(cs);
-    I.stats.rounds++;
-    if (ns == 2) I.stats.lockstep_rounds++;
-    I.stats.levels += ns;
-    I.stats.comm_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tr0).count();
-    for (int i = 0; i < ns; ++i) ++depth[sides[i]];
-    key = I.h_red->meetkey;
-    if (key != kNoKey) break;
-    for (int i = 0; i < ns; ++i) {
-      const int s = sides[i];
-      cnt[s] = I.h_red->sums[2 * s];
-      fed[s] = I.h_red->sums[2 * s + 1];
-      ved[s] += fed[s];
-      if (cnt[s] == 0) dead = true;  // that side's component is exhausted without a meet
-    }
-  }
-  if (key != kNoKey) {
-    const uint32_t meet = (uint32_t)(key & 0xffffffffull);
-    r.found = true;
-    r.meet = meet;
-    r.hops = (int64_t)(key >> 32);
-    if (opt.want_path) {
-      k_meet_depth<<<1, 64, 0, cs>>>(V, meet);
-      comm.allreduce(V.red->md, 2, DType::kU32, ROp::kMin, cs);
-      I.read_back(cs);
-      const int dS = (int)I.h_red->md[0], dT = (int)I.h_red->md[1];
-      BIBFS_REQUIRE((int64_t)dS + dT == r.hops, "dist: meet depths disagree with the path length");
-      const int K = std::max(dS, dT);
-      const uint32_t init[2] = {meet, meet};
-      HIP_CHECK(hipMemcpyAsync(I.d_cur, init, 8, hipMemcpyHostToDevice, cs));
-      for (int i = 0; i <= K; ++i) {
-        k_path_step<<<1, 64, 0, cs>>>(V, I.d_cur, I.d_pathS, I.d_pathT, i, dS, dT);
-        if (i < K) comm.allreduce(I.d_cur, 2, DType::kU32, ROp::kMin, cs);
-      }
-      std::vector<uint32_t> pS((size_t)dS + 1), pT((size_t)dT + 1);
-      HIP_CHECK(hipMemcpyAsync(pS.data(), I.d_pathS, pS.size() * 4, hipMemcpyDeviceToHost, cs));
-      HIP_CHECK(hipMemcpyAsync(pT.data(), I.d_pathT, pT.size() * 4, hipMemcpyDeviceToHost, cs));
-      HIP_CHECK(hipStreamSynchronize(cs));
-      r.path.assign(pS.rbegin(), pS.rend());
-      r.path.insert(r.path.end(), pT.begin() + 1, pT.end());
-    }
-  }
-  k_cleanup<<<blocks_for(I.chunk, cus), kThreads, 0, cs>>>(V);
-  HIP_CHECK(hipMemsetAsync(I.sent_base, 0, (size_t)I.gwords * 4 * 2, cs));
-  HIP_CHECK(hipGetLastError());
-  HIP_CHECK(hipEventRecord(I.ev_round, cs));
-  HIP_CHECK(hipStreamSynchronize(cs));
-  r.stats.grid_levels = r.stats.levels;
-  r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  r.search_ms = r.total_ms;
-  return r;
 }
 
 void DistBiBfs::barrier() {
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
   I.comm->allreduce(I.d_scalar, 1, DType::kF64, ROp::kMax, I.cstream);
-  HIP_CHECK(hipStreamSynchronize(I.cstream));
+  I.wait(I.cstream);
 }
 
 double DistBiBfs::allreduce_max(double x) {
@@ -856,8 +1522,33 @@ double DistBiBfs::allreduce_max(double x) {
   HIP_CHECK(hipMemcpyAsync(I.d_scalar, &y, 8, hipMemcpyHostToDevice, I.cstream));
   I.comm->allreduce(I.d_scalar, 1, DType::kF64, ROp::kMax, I.cstream);
   HIP_CHECK(hipMemcpyAsync(&y, I.d_scalar, 8, hipMemcpyDeviceToHost, I.cstream));
-  HIP_CHECK(hipStreamSynchronize(I.cstream));
+  I.wait(I.cstream);
   return y;
+}
+
+void DistBiBfs::release() {
+  auto& I = *p_;
+  HIP_CHECK(hipSetDevice(I.device));
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  HIP_CHECK(hipStreamSynchronize(I.cstream));
+  I.free_all();
+}
+
+void DistBiBfs::set_tuning(const DistTuning& t) {
+  BIBFS_REQUIRE(t.spec_rounds >= 0 && t.timeout_s > 0 && t.walk_max >= 1, "bad DistTuning");
+  const bool realloc = p_->state && t.walk_max > p_->tune.walk_max;
+  p_->tune = t;
+  if (realloc) {  // path-gather blocks are sized from walk_max
+    HIP_CHECK(hipSetDevice(p_->device));
+    HIP_CHECK(hipFree(p_->state));
+    p_->state = nullptr;
+    p_->alloc_state();
+  }
+}
+const DistTuning& DistBiBfs::tuning() const { return p_->tune; }
+void DistBiBfs::inject_fault(int at, int mode) {
+  p_->fault_at = at;
+  p_->fault_mode = mode;
 }
 
 int DistBiBfs::rank() const { return p_->rank; }
@@ -877,9 +1568,10 @@ namespace {
 // group (so peers blocked in a collective return); its own message is thrown.
 // Returns rank 0's results after checking that every rank agrees.
 template <typename Body>
-std::vector<SearchResult> run_local_ranks(const char* who, int ranks, int device, size_t nq, Body&& body) {
+std::vector<SearchResult> run_local_ranks(const char* who, int ranks, int device, size_t nq, const DistTuning& tune,
+                                          const DistLocalFault& fault, Body&& body) {
   BIBFS_REQUIRE(ranks >= 1 && ranks <= 16, std::string(who) + ": 1..16 ranks");
-  auto group = dist::make_local_group(ranks);
+  auto group = dist::make_local_group(ranks, tune.timeout_s);
   std::vector<std::vector<SearchResult>> out((size_t)ranks);
   std::vector<std::string> err((size_t)ranks);
   std::vector<std::thread> th;
@@ -887,6 +1579,8 @@ std::vector<SearchResult> run_local_ranks(const char* who, int ranks, int device
     th.emplace_back([&, r] {
       try {
         DistBiBfs e(dist::make_local_comm(group, r), device);
+        e.set_tuning(tune);
+        if (fault.rank == r) e.inject_fault(fault.at, fault.mode);
         body(e, r, out[(size_t)r]);
       } catch (const std::exception& ex) {
         err[(size_t)r] = ex.what();
@@ -909,24 +1603,29 @@ std::vector<SearchResult> run_local_ranks(const char* who, int ranks, int device
 
 std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& el,
                                          const std::vector<std::pair<vid_t, vid_t>>& queries,
-                                         const SearchOptions& opt) {
-  return run_local_ranks("dist_local_run", ranks, device, queries.size(),
-                         [&](DistBiBfs& e, int, std::vector<SearchResult>& out) {
+                                         const SearchOptions& opt, const DistTuning& tuning,
+                                         const DistLocalFault& fault, std::vector<DistLevelStats>* stats) {
+  return run_local_ranks("dist_local_run", ranks, device, queries.size(), tuning, fault,
+                         [&](DistBiBfs& e, int r, std::vector<SearchResult>& out) {
                            e.load_edges(el);
-                           for (const auto& q : queries) out.push_back(e.search(q.first, q.second, opt));
+                           for (const auto& q : queries) {
+                             out.push_back(e.search(q.first, q.second, opt));
+                             if (r == 0 && stats) stats->push_back(e.last_stats());
+                           }
                          });
 }
 
 std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
                                                   double arg, uint64_t seed,
                                                   const std::vector<std::pair<vid_t, vid_t>>& queries,
-                                                  const SearchOptions& opt, DistLocalTiming* timing) {
+                                                  const SearchOptions& opt, DistLocalTiming* timing,
+                                                  const DistTuning& tuning) {
   BIBFS_REQUIRE(kind == "gnp" || kind == "rmat", "dist_local_generate_run: kind must be gnp or rmat");
   std::vector<double> build_ms((size_t)std::max(ranks, 1), 0.0), qms;
   std::vector<uint64_t> nnz((size_t)std::max(ranks, 1), 0);
   std::vector<DistLevelStats> qstats;
   auto rs = run_local_ranks(
-      "dist_local_generate_run", ranks, device, queries.size(),
+      "dist_local_generate_run", ranks, device, queries.size(), tuning, DistLocalFault{},
       [&](DistBiBfs& e, int r, std::vector<SearchResult>& out) {
         const auto t0 = std::chrono::steady_clock::now();
         if (kind == "gnp")

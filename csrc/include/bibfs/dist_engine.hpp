@@ -10,19 +10,26 @@
 // replicated the whole graph and all state on every rank
 // (v2/second_try.cpp:44-50, v4/mpi_bas.cpp:42-64, v4/comp.cu:99).
 //
-// Per round (one side, or both in lockstep; decided identically on every rank
-// from allreduced stats), each expanding side runs one level:
+// Per round (one side, or both in lockstep), each expanding side runs one level:
 //   sparse (top-down): owners expand their frontier vertices; neighbours they
 //     own are claimed on the spot, the rest become (v, parent) candidates
 //     (each remote vertex offered once per search) exchanged with ONE
 //     ncclAllGather; owners then claim the candidates addressed to them.
 //   dense (bottom-up): the owned frontier bitmap slices are allgathered into a
 //     full bitmap and every owner scans its unvisited vertices for a parent.
-//   In a lockstep round side S's exchange runs on a comm stream while side T
-//   expands on the compute stream.  The owner of a vertex holds both sides'
-//   visited bits and depths, so the meet test is local and exact; claimed
-//   counts / degree sums (ncclSum) and the meet key (ncclMin over
-//   length << 32 | vertex) are reduced in one grouped call per round.
+// The owner of a vertex holds both sides' visited bits and depths, so the
+// meet test is local and exact; claimed counts / degree sums (ncclSum) and
+// the meet key (ncclMin over length << 32 | vertex) are reduced in one
+// grouped call per round.
+// No host round trip per round: the round policy (sides, direction,
+// termination) is computed ON THE DEVICE from the reduced values, identically
+// on every rank, and the host enqueues K sparse rounds at a time with a
+// fixed-capacity exchange; kernels of a round that is not needed become
+// no-ops, and the host waits once per K rounds.  A round the speculative
+// shape cannot carry (a dense level, or a frontier larger than the enqueued
+// capacity) stalls the batch; the host then plans that round itself, sized
+// exactly.  The path comes back with ONE allgather of the
+// claimed (vertex, parent) pairs, walked on the device from an LDS table.
 // MPI is not needed at runtime: the communicator is bootstrapped from a
 // unique id distributed by MPI (mpi_bibfs), torch.distributed (bench.py) or
 // any other channel.
@@ -49,8 +56,25 @@ struct DistLevelStats {
   int rounds = 0, lockstep_rounds = 0;
   int sparse_levels = 0, dense_levels = 0, overflow_levels = 0;
   int count_syncs = 0;             // extra host round trips to size a candidate exchange
+  int host_syncs = 0;              // host waits on the device in this search (all causes)
+  int spec_rounds = 0;             // rounds enqueued speculatively (incl. no-op tails after the end)
+  int host_rounds = 0;             // rounds planned on the host (dense levels, oversized exchanges)
+  int collectives = 0;             // RCCL calls issued (allgather + allreduce)
   uint64_t exchanged_bytes = 0;    // bytes this rank received from allgathers
-  double comm_ms = 0.0;            // host wall time of the rounds (this rank)
+  double comm_ms = 0.0;            // host wall time of the round loop (this rank)
+  double device_ms = 0.0;          // device time from the first to the last op of the search (events)
+  int path_collectives = 0;        // collectives spent reconstructing the path
+};
+
+// Knobs of the partitioned engine (defaults are the production settings; the
+// small-capacity ones exist so tests can force every exchange branch).
+struct DistTuning {
+  int spec_rounds = 4;             // rounds enqueued per host wait (0 = plan every round on the host)
+  uint32_t spec_cap_max = 1u << 16;  // largest per-rank candidate block of a speculative round (pairs)
+  uint32_t cap = 0;                // per-rank candidate block of a host-planned round (0 = min(2^20, n))
+  uint64_t nosync_bytes = 1u << 20;  // host-planned round: size the exchange from host bounds up to this
+  double timeout_s = 120.0;        // a host wait longer than this aborts the communicator and throws
+  uint32_t walk_max = 8192;        // path from one gathered parent table when both sides claimed <= this
 };
 
 class DistBiBfs {
@@ -73,6 +97,14 @@ class DistBiBfs {
 
   void barrier();
   double allreduce_max(double x);
+  void release();  // free the graph shard and search state (the communicator stays)
+
+  void set_tuning(const DistTuning& t);
+  const DistTuning& tuning() const;
+  // Fault injection (tests): from the `at`-th enqueued round of a search on,
+  // this rank throws (mode 1) or stalls for 2 x timeout_s before throwing
+  // (mode 2).  mode 0 disarms.
+  void inject_fault(int at, int mode);
 
   int rank() const;
   int size() const;
@@ -93,9 +125,15 @@ class DistBiBfs {
 // sharing `device`, exchanging through the in-process local group instead of
 // RCCL.  Every rank loads `el` and answers `queries`; returns rank 0's results
 // after checking that every rank returned the same hop counts and paths.
+// `fault_rank` >= 0 arms inject_fault(fault_at, fault_mode) on that rank.
+struct DistLocalFault {
+  int rank = -1, at = 0, mode = 0;
+};
 std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& el,
                                          const std::vector<std::pair<vid_t, vid_t>>& queries,
-                                         const SearchOptions& opt = {});
+                                         const SearchOptions& opt = {}, const DistTuning& tuning = {},
+                                         const DistLocalFault& fault = {},
+                                         std::vector<DistLevelStats>* stats = nullptr);
 
 // Same harness, but every rank generates the graph on the device itself
 // (kind "gnp": arg = p; kind "rmat": arg = edge count) and keeps only its
@@ -111,6 +149,7 @@ struct DistLocalTiming {
 std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
                                                   double arg, uint64_t seed,
                                                   const std::vector<std::pair<vid_t, vid_t>>& queries,
-                                                  const SearchOptions& opt, DistLocalTiming* timing);
+                                                  const SearchOptions& opt, DistLocalTiming* timing,
+                                                  const DistTuning& tuning = {});
 
 }  // namespace bibfs

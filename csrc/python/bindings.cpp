@@ -68,8 +68,14 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["dense_levels"] = s.dense_levels;
   d["overflow_levels"] = s.overflow_levels;
   d["count_syncs"] = s.count_syncs;
+  d["host_syncs"] = s.host_syncs;
+  d["spec_rounds"] = s.spec_rounds;
+  d["host_rounds"] = s.host_rounds;
+  d["collectives"] = s.collectives;
+  d["path_collectives"] = s.path_collectives;
   d["exchanged_bytes"] = s.exchanged_bytes;
   d["comm_ms"] = s.comm_ms;
+  d["device_ms"] = s.device_ms;
   return d;
 }
 
@@ -299,6 +305,19 @@ PYBIND11_MODULE(_native, m) {
     auto id = dist_unique_id();
     return py::bytes(reinterpret_cast<const char*>(id.data()), id.size());
   });
+  py::class_<DistTuning>(m, "DistTuning")
+      .def(py::init<>())
+      .def_readwrite("spec_rounds", &DistTuning::spec_rounds)
+      .def_readwrite("spec_cap_max", &DistTuning::spec_cap_max)
+      .def_readwrite("cap", &DistTuning::cap)
+      .def_readwrite("nosync_bytes", &DistTuning::nosync_bytes)
+      .def_readwrite("timeout_s", &DistTuning::timeout_s)
+      .def_readwrite("walk_max", &DistTuning::walk_max);
+  py::class_<DistLocalFault>(m, "DistLocalFault")
+      .def(py::init<>())
+      .def_readwrite("rank", &DistLocalFault::rank)
+      .def_readwrite("at", &DistLocalFault::at)
+      .def_readwrite("mode", &DistLocalFault::mode);
   py::class_<DistBiBfs>(m, "DistBiBfs")
       .def(py::init([](int rank, int size, int device, py::bytes uid) {
              std::string s = uid;
@@ -325,19 +344,37 @@ PYBIND11_MODULE(_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("barrier", &DistBiBfs::barrier, py::call_guard<py::gil_scoped_release>())
       .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>())
+      .def("release", &DistBiBfs::release, py::call_guard<py::gil_scoped_release>())
+      .def("set_tuning", &DistBiBfs::set_tuning, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("tuning", &DistBiBfs::tuning)
+      .def("inject_fault", &DistBiBfs::inject_fault, py::arg("at"), py::arg("mode"))
       .def_property_readonly("backend", &DistBiBfs::backend)
       .def_property_readonly("last_stats", [](const DistBiBfs& e) { return dist_stats_dict(e.last_stats()); });
-  m.def("dist_local_run", &dist_local_run, py::arg("ranks"), py::arg("device"), py::arg("edges"),
-        py::arg("queries"), py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "dist_local_run",
+      [](int ranks, int device, const EdgeList& el, const std::vector<std::pair<vid_t, vid_t>>& queries,
+         const SearchOptions& opt, const DistTuning& tuning, const DistLocalFault& fault) {
+        std::vector<DistLevelStats> st;
+        std::vector<SearchResult> rs;
+        {
+          py::gil_scoped_release nogil;
+          rs = dist_local_run(ranks, device, el, queries, opt, tuning, fault, &st);
+        }
+        py::list stl;
+        for (const auto& x : st) stl.append(dist_stats_dict(x));
+        return py::make_tuple(rs, stl);
+      },
+      py::arg("ranks"), py::arg("device"), py::arg("edges"), py::arg("queries"),
+      py::arg("options") = SearchOptions{}, py::arg("tuning") = DistTuning{}, py::arg("fault") = DistLocalFault{});
   m.def(
       "dist_local_generate_run",
       [](int ranks, int device, const std::string& kind, uint32_t n, double arg, uint64_t seed,
-         const std::vector<std::pair<vid_t, vid_t>>& queries, const SearchOptions& opt) {
+         const std::vector<std::pair<vid_t, vid_t>>& queries, const SearchOptions& opt, const DistTuning& tuning) {
         DistLocalTiming t;
         std::vector<SearchResult> rs;
         {
           py::gil_scoped_release nogil;
-          rs = dist_local_generate_run(ranks, device, kind, n, arg, seed, queries, opt, &t);
+          rs = dist_local_generate_run(ranks, device, kind, n, arg, seed, queries, opt, &t, tuning);
         }
         py::dict d;
         d["build_ms"] = t.build_ms;
@@ -349,5 +386,5 @@ PYBIND11_MODULE(_native, m) {
         return py::make_tuple(rs, d);
       },
       py::arg("ranks"), py::arg("device"), py::arg("kind"), py::arg("n"), py::arg("arg"), py::arg("seed"),
-      py::arg("queries"), py::arg("options") = SearchOptions{});
+      py::arg("queries"), py::arg("options") = SearchOptions{}, py::arg("tuning") = DistTuning{});
 }

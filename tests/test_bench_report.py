@@ -33,3 +33,41 @@ def test_report_partitioned_is_strong_scaling_and_other_graph_has_no_baseline():
     out = bench.report(_args(mode="partitioned"), 2, _head(n=1000000), {}, {})
     assert out["scaling"] == "strong" and out["vs_baseline"] is None
     assert out["config"]["parallelism"] == "vertex-partition2" and out["config"]["global_batch"] == 1
+
+
+def test_spawn_path_forwards_rank0_line_and_status(capsys):
+    """`bench.py --gpus N` without a launcher runs the ranks as a child job
+    (mocked here by a child that prints a line) and forwards its status."""
+    import sys
+
+    line = json.dumps({"metric": "m", "value": 1.0, "n_gpus": 8})
+    ok = [sys.executable, "-c", f"print('noise'); print({line!r})"]
+    assert bench.spawn_ranks(8, [], cmd=ok) == 0
+    out = capsys.readouterr().out.strip().splitlines()
+    assert out == [line]
+    bad = [sys.executable, "-c", f"print({line!r}); raise SystemExit(3)"]
+    assert bench.spawn_ranks(8, [], cmd=bad) == 3
+    silent = [sys.executable, "-c", "pass"]
+    assert bench.spawn_ranks(8, [], cmd=silent) == 1
+
+
+def test_launcher_command_and_world_check(monkeypatch):
+    """The self-launch uses torch.distributed.run on 127.0.0.1 with one rank per
+    GPU; a launcher-provided WORLD_SIZE that disagrees with --gpus fails fast
+    (before torch is imported)."""
+    cmd = bench.launcher_cmd(4, ["--gpus", "4", "--steps", "3"])
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+    assert cmd[-5].endswith("bench.py")
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    assert bench.main(["--gpus", "4"]) == 2
+    monkeypatch.delenv("WORLD_SIZE")
+    called = {}
+
+    def fake_spawn(n, argv):
+        called["n"], called["argv"] = n, argv
+        return 0
+
+    monkeypatch.setattr(bench, "spawn_ranks", fake_spawn)
+    assert bench.main(["--gpus", "8", "--steps", "2"]) == 0
+    assert called == {"n": 8, "argv": ["--gpus", "8", "--steps", "2"]}

@@ -74,3 +74,84 @@ def test_local_group_device_generated_shards(ranks, spec):
         check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
     assert len(t["query_ms"]) == len(qs) and t["build_ms"] > 0
     assert len(t["local_nnz"]) == ranks and sum(t["local_nnz"]) == g.csr.nnz
+
+
+# ---- device-planned speculative rounds, exchange branches, failure paths ----
+
+def _check_all(g, qs, rs):
+    for (s, d), r in zip(qs, rs):
+        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+
+
+@pytest.mark.parametrize("spec_rounds", [0, 1, 4, 8])
+def test_speculative_rounds_match_oracle_and_cut_host_syncs(spec_rounds):
+    """spec_rounds = 0 plans every round on the host (one wait per round); K > 0
+    enqueues K device-planned rounds per wait."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    g = bb.from_spec("gnp:100000::6")
+    qs = _pairs(g.n, 12, 21)
+    rs, st = dist_local_run(2, g, qs, tuning=make_tuning(spec_rounds=spec_rounds), return_stats=True)
+    _check_all(g, qs, rs)
+    for (s, d), r, x in zip(qs, rs, st):
+        if s == d or not r.found:
+            continue
+        if spec_rounds == 0:
+            assert x["spec_rounds"] == 0 and x["host_rounds"] == x["rounds"]
+        else:
+            # one wait per batch of K rounds, + the path walk and the final cleanup wait
+            batches = -(-x["rounds"] // spec_rounds) + 1
+            assert x["host_syncs"] <= batches + 2 + x["host_rounds"], x
+            assert x["path_collectives"] == 1, x  # ONE allgather for the whole path
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 4])
+def test_tiny_capacities_force_count_sync_and_overflow(ranks):
+    """A 4-pair candidate block and no host-bound sizing: big sparse levels stall
+    the speculative batch, the host sizes the exchange with a count allreduce,
+    and counts above the block finish the level bottom-up."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    tune = make_tuning(cap=4, nosync_bytes=0, spec_cap_max=1024)
+    seen = {"host_rounds": 0, "count_syncs": 0, "overflow_levels": 0}
+    for spec in ("kron:14:16:3", "gnp:20000::6"):
+        g = bb.from_spec(spec)
+        qs = _pairs(g.n, 10, 5)
+        for kw in ({}, {"lockstep": False}, {"direction": "topdown"}):
+            rs, st = dist_local_run(ranks, g, qs, tuning=tune, return_stats=True, **kw)
+            _check_all(g, qs, rs)
+            for k in seen:
+                seen[k] += sum(x[k] for x in st)
+    assert seen["host_rounds"] > 0 and seen["count_syncs"] > 0, seen
+    if ranks > 1:  # one rank owns every vertex: nothing is ever offered, nothing overflows
+        assert seen["overflow_levels"] > 0, seen
+
+
+def test_path_walk_fallback_per_hop():
+    """Visited sets above walk_max: the path is rebuilt hop by hop (one
+    allreduce per hop) instead of from one gathered parent table."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    g = bb.from_spec("gnp:20000::6")
+    qs = _pairs(g.n, 8, 9)
+    rs, st = dist_local_run(3, g, qs, tuning=make_tuning(walk_max=1), return_stats=True)
+    _check_all(g, qs, rs)
+    assert any(x["path_collectives"] > 1 for x, r in zip(st, rs) if r.found and r.hops > 1)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_failing_rank_aborts_every_rank(mode):
+    """Rank 1 throws (mode 1) or hangs past the watchdog (mode 2) mid-search:
+    the group is torn down and the run reports the failure instead of hanging."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    g = bb.from_spec("gnp:20000::6")
+    qs = _pairs(g.n, 3, 2)
+    with pytest.raises(RuntimeError) as ei:
+        dist_local_run(3, g, qs, tuning=make_tuning(timeout_s=1.0), fault=(1, 2, mode))
+    msg = str(ei.value)
+    assert "injected fault" in msg or "timed out" in msg or "aborted" in msg, msg
