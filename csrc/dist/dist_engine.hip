@@ -276,7 +276,8 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
   pos = __shfl(pos, leader);
   if (mine) pick(V.queue, s)[pos + mbcnt64(mask)] = v;
   deg = wave_sum(deg);
-  if (lane == (uint32_t)leader) atomicAdd(&V.st->new_edges[s], deg);
+  if (lane == (uint32_t)leader) (void)__hip_atomic_fetch_add(&V.st->new_edges[s], deg, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Offer remote vertex v (parent u) to its owner -- at most once per search and
@@ -374,15 +375,16 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
 }
 
 // Last-block detection: true in exactly one block, after every block of the
-// grid has passed this point (its earlier global writes and atomics released).
+// grid has passed this point.  No fence: the last block reads only words the
+// other blocks updated with returning atomics (completed before their waves
+// reached the barrier, so before their arrival was counted) and reads them
+// with atomics; plain stores of other blocks are consumed only by the next
+// stream operation (kernel boundary).  A __threadfence here would cost
+// ~3.5 us per block (buffer_wbl2 + buffer_inv, MI355X_MICROARCH.md price list).
 __device__ __forceinline__ bool last_block(uint32_t* counter, uint32_t nblocks) {
   __shared__ int last;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(counter, 1u) == nblocks - 1;
-    if (last) __threadfence();
-  }
+  if (threadIdx.x == 0) last = atomicAdd(counter, 1u) == nblocks - 1;
   __syncthreads();
   return last != 0;
 }
@@ -864,16 +866,19 @@ __global__ void k_path_step(DView V, uint32_t* cur, uint32_t* pathS, uint32_t* p
 }
 
 // Reset the visited words of every vertex this search claimed (all of them are
-// in the queues): no O(N) clear per search.
-__global__ void k_cleanup(DView V) {
+// in the queues: no O(N) clear of the owned slices) and the `sent` bitmaps
+// (2 x N/8 bytes, streamed as 16-byte stores), in one launch.
+__global__ void k_cleanup(DView V, uint64_t sent_words) {
+  const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, nth = (uint64_t)gridDim.x * blockDim.x;
   for (int s = 0; s < 2; ++s) {
     const uint32_t qn = V.st->qtail[s];
     const uint32_t* q = pick(V.queue, s);
     uint32_t* vis = pick(V.vis, s);
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < qn;
-         i += (uint64_t)gridDim.x * blockDim.x)
-      vis[(q[i] - V.lo) >> 5] = 0u;
+    for (uint64_t i = tid; i < qn; i += nth) vis[(q[i] - V.lo) >> 5] = 0u;
   }
+  uint4* sw = reinterpret_cast<uint4*>(V.sent[0]);  // both sides, contiguous, 256-B aligned
+  for (uint64_t i = tid; i < sent_words / 4; i += nth) sw[i] = make_uint4(0, 0, 0, 0);
+  for (uint64_t i = sent_words / 4 * 4 + tid; i < sent_words; i += nth) V.sent[0][i] = 0u;
 }
 
 unsigned blocks_for(uint64_t work, int cus) {
@@ -1103,6 +1108,8 @@ struct DistBiBfs::Impl {
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt);
   void host_round(uint32_t it, const Policy& pol, SearchResult& r);
   bool walk_path(uint64_t key, SearchResult& r);
+  void finish_walk(SearchResult& r);
+  void cleanup_enqueue(const Ctl& h);
   void walk_path_per_hop(uint64_t key, uint32_t it, SearchResult& r);
 };
 
@@ -1311,20 +1318,19 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   r.stats.edges_inspected = h.einsp;
   r.stats.visited = h.vis[0] + h.vis[1];
   stats.comm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  bool path_pending = false;  // the gathered-table walk is enqueued, not yet read
   if (h.state == kDone) {
     const uint64_t key = h.key;
     r.found = true;
     r.meet = (uint32_t)(key & 0xffffffffull);
     r.hops = (int64_t)(key >> 32);
-    if (opt.want_path) {
-      if (!walk_path(key, r)) walk_path_per_hop(key, it, r);
-    }
+    if (opt.want_path && !(path_pending = walk_path(key, r))) walk_path_per_hop(key, it, r);
   }
-  k_cleanup<<<blocks_for(std::max<uint64_t>(h.vis[0] + h.vis[1], 1), cus), kThreads, 0, cs>>>(V);
-  HIP_CHECK(hipMemsetAsync(sent_base, 0, (size_t)gwords * 4 * 2, cs));
-  HIP_CHECK(hipGetLastError());
+  if (path_pending) cleanup_enqueue(h);  // behind the walk: one host wait for both
+  if (!path_pending) cleanup_enqueue(h);
   HIP_CHECK(hipEventRecord(ev_t1, cs));
   wait(cs);
+  if (path_pending) finish_walk(r);
   float dms = 0.f;
   HIP_CHECK(hipEventElapsedTime(&dms, ev_t0, ev_t1));
   stats.device_ms = dms;
@@ -1362,12 +1368,22 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_walk), h_walk_cap * 4, hipHostMallocDefault));
   }
   HIP_CHECK(hipMemcpyAsync(h_walk, d_walk, words * 4, hipMemcpyDeviceToHost, cs));
-  wait(cs);
+  return true;  // read by finish_walk after the search's last wait
+}
+
+void DistBiBfs::Impl::finish_walk(SearchResult& r) {
+  const uint32_t hops = (uint32_t)r.hops;
   BIBFS_REQUIRE(h_walk[0] == 0, "dist: parent chains from the meet vertex do not add up to the path length (" +
                                     std::to_string(h_walk[1]) + " + " + std::to_string(h_walk[2]) +
                                     " != " + std::to_string(hops) + ")");
   r.path.assign(h_walk + 4, h_walk + 4 + hops + 1);
-  return true;
+}
+
+void DistBiBfs::Impl::cleanup_enqueue(const Ctl& h) {
+  const uint64_t sent_words = (uint64_t)gwords * 2;
+  const uint64_t work = std::max<uint64_t>(h.vis[0] + h.vis[1], sent_words / 4);
+  k_cleanup<<<blocks_for(std::max<uint64_t>(work, 1), cus), kThreads, 0, cstream>>>(V, sent_words);
+  HIP_CHECK(hipGetLastError());
 }
 
 // Fallback: one allreduce per hop (visited sets too large to gather).
