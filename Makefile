@@ -3,6 +3,9 @@
 #   make -j8            -> build/lib/libbibfs.so, build/lib/libbibfs_mpi.so,
 #                          build/bin/* CLI tools, bidirectional_bfs_amd/_native*.so
 #   make cpu            -> host-only pieces (no hipcc needed)
+#   make asan           -> host-only pieces + MPI engines with AddressSanitizer +
+#                          UBSan in build-asan/ (scripts/asan_check.sh runs the
+#                          CLI / MPI test subset against them)
 #   make clean
 #
 # The reference builds each engine with its own Makefile (v1..v4/Makefile) and
@@ -16,7 +19,7 @@ HIPCC     ?= $(ROCM)/bin/hipcc
 CXX       ?= g++
 PYTHON    ?= python3
 
-BUILD     := build
+BUILD     ?= build
 OBJ       := $(BUILD)/obj
 LIB       := $(BUILD)/lib
 BIN       := $(BUILD)/bin
@@ -24,7 +27,9 @@ PKG       := bidirectional_bfs_amd
 
 CXXSTD    := -std=c++17
 INC       := -Icsrc/include -Icsrc/hip
-CXXFLAGS  += -O3 -fPIC $(CXXSTD) -Wall -Wextra -Wno-unused-parameter $(INC) -pthread
+OPT       ?= -O3
+SANFLAGS  ?=
+CXXFLAGS  += $(OPT) -fPIC $(CXXSTD) -Wall -Wextra -Wno-unused-parameter $(INC) -pthread $(SANFLAGS)
 HIPFLAGS  := -O3 -fPIC $(CXXSTD) $(INC) --offload-arch=$(ARCH) -mcode-object-version=5 \
              -Wno-unused-result -munsafe-fp-atomics
 MPI_INC   := -I$(MPI_HOME)/include
@@ -54,7 +59,7 @@ GPU_TOOLS := $(BIN)/bibfs_selftest $(BIN)/bibfs_hip $(BIN)/mpi_bibfs $(BIN)/bibf
 
 NATIVE_PY := $(PKG)/_native$(PY_EXT)
 
-.PHONY: all cpu gpu mpi python micro clean
+.PHONY: all cpu gpu mpi python micro clean asan
 all: cpu mpi gpu python micro
 cpu: $(LIB)/libbibfs_core.so $(CPU_TOOLS)
 mpi: $(LIB)/libbibfs_mpi.so $(MPI_TOOLS)
@@ -80,7 +85,7 @@ $(OBJ)/%.o: csrc/%.hip $(HEADERS)
 
 $(LIB)/libbibfs_core.so: $(CORE_OBJ)
 	@mkdir -p $(LIB)
-	$(CXX) -shared -o $@ $^ -pthread
+	$(CXX) -shared -o $@ $^ -pthread $(SANFLAGS)
 
 $(LIB)/libbibfs.so: $(CORE_OBJ) $(HIP_OBJ)
 	@mkdir -p $(LIB)
@@ -88,7 +93,7 @@ $(LIB)/libbibfs.so: $(CORE_OBJ) $(HIP_OBJ)
 
 $(LIB)/libbibfs_mpi.so: $(MPI_OBJ) $(LIB)/libbibfs_core.so
 	@mkdir -p $(LIB)
-	$(CXX) -shared -o $@ $(MPI_OBJ) -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN' $(MPI_LD) -pthread
+	$(CXX) -shared -o $@ $(MPI_OBJ) -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN' $(MPI_LD) -pthread $(SANFLAGS)
 
 # --- CLI tools ---------------------------------------------------------------
 TOOL_CXX = $(CXX) $(CXXFLAGS)
@@ -126,7 +131,13 @@ $(NATIVE_PY): csrc/python/bindings.cpp $(HEADERS) $(LIB)/libbibfs.so
 	  -Wl,-rpath,'$$ORIGIN/../$(LIB)' $(HIP_LD)
 
 clean:
-	rm -rf $(BUILD) $(PKG)/_native*.so
+	rm -rf $(BUILD) build-asan $(PKG)/_native*.so
+
+# Host code under AddressSanitizer + UndefinedBehaviorSanitizer (the GPU code
+# is not instrumented: GPU ASan is not available on this pool).
+asan:
+	$(MAKE) BUILD=build-asan OPT="-O1 -g -fno-omit-frame-pointer" \
+	  SANFLAGS="-fsanitize=address,undefined -fno-sanitize-recover=undefined" cpu mpi
 
 $(BIN)/bibfs_selftest: tools/bibfs_selftest.cpp tools/cli_common.hpp $(LIB)/libbibfs.so
 	@mkdir -p $(BIN)

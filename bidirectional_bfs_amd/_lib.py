@@ -29,8 +29,11 @@ def repo_root() -> str:
 
 
 def tool_path(name: str) -> str:
-    """Absolute path of a native CLI tool in build/bin (bibfs_serial, second_try, ...)."""
-    p = os.path.join(_REPO, "build", "bin", name)
+    """Absolute path of a native CLI tool in build/bin (bibfs_serial, second_try, ...).
+
+    ``BIBFS_BIN_DIR`` overrides the directory (e.g. ``build-asan/bin`` for the
+    sanitizer build, ``make asan``)."""
+    p = os.path.join(os.environ.get("BIBFS_BIN_DIR") or os.path.join(_REPO, "build", "bin"), name)
     if not os.path.exists(p):
         raise FileNotFoundError(f"{p} missing; run `make -j8` in {_REPO}")
     return p

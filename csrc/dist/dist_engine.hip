@@ -67,6 +67,7 @@ constexpr uint64_t kHubDeg = 512;
 constexpr uint64_t kNoHubs = ~0ull;
 constexpr int kHubTile = 1024;                  // hubs staged in LDS per pass
 constexpr uint32_t kSpecHubCap = 4096;          // speculative blocks up to this size skip the hub pass
+constexpr uint32_t kTraceCap = 4096;            // rounds recorded with SearchOptions::trace
 
 // Search control state: identical on every rank (computed from reduced
 // values only).  Double-buffered by round parity: round `it` reads
@@ -113,6 +114,15 @@ struct Reduced {
   uint32_t pad[2];
 };
 
+// One accounted round (SearchOptions::trace): the frontiers it expanded and
+// what they discovered -- the same record on every rank.
+struct RoundRec {
+  uint32_t sides, modes, depth[2];
+  unsigned long long cnt[2], fed[2];  // expanded frontiers (vertices, degree sum)
+  unsigned long long sums[4];         // discovered: [2s] vertices, [2s+1] their degree sum
+  unsigned long long meetkey;
+};
+
 struct DState {
   uint32_t fbeg[2], fend[2], qtail[2];  // queue[s][fbeg, fend) = frontier; qtail = append cursor
   uint32_t send_count[2];               // candidates this rank emitted for side s this level
@@ -140,6 +150,8 @@ struct DView {
   int P;
   DState* st;
   Ctl* ctl;                   // [2]
+  struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
+  uint32_t trace_cap;
   Reduced* red;               // [2]
 };
 
@@ -247,6 +259,23 @@ __device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, u
       c.einsp += c.fed[s];
       if (!((wm >> s) & 1)) c.sparse_levels += 1;
     }
+}
+
+// Publish round `p`'s plan; with tracing on, also record the round it accounted.
+__device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& rd, const Ctl& c) {
+  V.ctl[p] = c;
+  if (V.trace && prev.sides && !(prev.sides & kSeedBit) && c.rounds >= 1 && c.rounds <= V.trace_cap) {
+    RoundRec& t = V.trace[c.rounds - 1];
+    t.sides = prev.sides;
+    t.modes = prev.modes;
+    for (int s = 0; s < 2; ++s) {
+      t.depth[s] = prev.depth[s];
+      t.cnt[s] = prev.cnt[s];
+      t.fed[s] = prev.fed[s];
+    }
+    for (int k = 0; k < 4; ++k) t.sums[k] = rd.sums[k];
+    t.meetkey = rd.meetkey;
+  }
 }
 
 // Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
@@ -400,7 +429,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   if (threadIdx.x == 0) plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, cap, flags, c);
   __syncthreads();
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    V.ctl[p] = c;
+    publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
     V.red[p].meetkey = kNoKey;
   }
   const int s = blockIdx.y;
@@ -587,7 +616,7 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags) 
   const int p = it & 1;
   Ctl c;
   plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, flags, c);
-  V.ctl[p] = c;
+  publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
   *host = c;
   __threadfence_system();
 }
@@ -600,7 +629,7 @@ __global__ void k_plan_force(DView V, uint32_t it, Policy pol) {
   const int p = it & 1;
   Ctl c;
   plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, kPlanForce, c);
-  V.ctl[p] = c;
+  publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
   V.red[p].meetkey = kNoKey;
 }
 
@@ -917,6 +946,7 @@ struct DistBiBfs::Impl {
   uint32_t* d_pathS = nullptr;
   uint32_t* d_pathT = nullptr;
   uint32_t* d_walk = nullptr;  // k_walk output
+  RoundRec* d_trace = nullptr;
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
   uint32_t* h_walk = nullptr;  // pinned
@@ -1000,7 +1030,8 @@ struct DistBiBfs::Impl {
     const size_t o_sent = take((size_t)gwords * 4 * 2);
     const size_t o_st = take(sizeof(DState)), o_ctl = take(2 * sizeof(Ctl)), o_red = take(2 * sizeof(Reduced)),
                  o_cur = take(64), o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4),
-                 o_walk = take(((size_t)n + 8) * 4), o_sc = take(64);
+                 o_walk = take(((size_t)n + 8) * 4), o_sc = take(64),
+                 o_tr = take((size_t)kTraceCap * sizeof(RoundRec));
     HIP_CHECK(hipMalloc(&state, off));
     char* b = static_cast<char*>(state);
     V.n = n;
@@ -1034,6 +1065,9 @@ struct DistBiBfs::Impl {
     d_pathT = reinterpret_cast<uint32_t*>(b + o_pt);
     d_walk = reinterpret_cast<uint32_t*>(b + o_walk);
     d_scalar = reinterpret_cast<double*>(b + o_sc);
+    d_trace = reinterpret_cast<RoundRec*>(b + o_tr);
+    V.trace = nullptr;
+    V.trace_cap = kTraceCap;
     HIP_CHECK(hipMemsetAsync(V.st, 0, sizeof(DState), stream));
     HIP_CHECK(hipMemsetAsync(d_scalar, 0, 64, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
@@ -1230,6 +1264,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   hipStream_t cs = cstream;
   const Policy pol = policy(opt);
   V.cap = cap();
+  V.trace = opt.trace ? d_trace : nullptr;
 
   HIP_CHECK(hipEventRecord(ev_t0, cs));
   k_seed<<<1, 64, 0, cs>>>(V, src, dst);
@@ -1331,6 +1366,22 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   HIP_CHECK(hipEventRecord(ev_t1, cs));
   wait(cs);
   if (path_pending) finish_walk(r);
+  if (opt.trace && h.rounds) {
+    std::vector<RoundRec> tr(std::min<uint32_t>(h.rounds, kTraceCap));
+    HIP_CHECK(hipMemcpy(tr.data(), d_trace, tr.size() * sizeof(RoundRec), hipMemcpyDeviceToHost));
+    for (const RoundRec& t : tr)
+      for (int s = 0; s < 2; ++s) {
+        if (!((t.sides >> s) & 1)) continue;
+        LevelTrace lt;
+        lt.side = s;
+        lt.depth = (int)t.depth[s];
+        lt.frontier = t.cnt[s];
+        lt.edges = t.fed[s];
+        lt.discovered = t.sums[2 * s];
+        lt.mode = ((t.modes >> s) & 1) ? 5 : 4;
+        r.stats.trace.push_back(lt);
+      }
+  }
   float dms = 0.f;
   HIP_CHECK(hipEventElapsedTime(&dms, ev_t0, ev_t1));
   stats.device_ms = dms;

@@ -1,11 +1,11 @@
-"""Partitioned bidirectional BFS over ``torch.distributed`` collectives.
+"""Reference MODEL of the native partitioned engine's round protocol (test-only).
 
-This is the same per-level protocol as the RCCL engine
-(``csrc/dist/dist_engine.hip``, ``DistBiBfs``) written against
-``torch.distributed`` so that it runs on ANY backend: ``gloo`` on CPU
-processes (how the protocol is tested without GPUs, ``tests/test_dist_protocol.py``)
-or ``nccl`` (= RCCL) with device tensors.  It is the portable multi-process
-path; the native engine is the fast one.
+``csrc/dist/dist_engine.hip`` (``DistBiBfs``) is the only multi-GPU engine of
+the framework.  This file re-states its round semantics with plain numpy and
+``torch.distributed`` collectives so the protocol can be exercised by CPU
+processes over ``gloo`` (``tests/test_dist_protocol.py``); it is not a
+product path and is never run on GPUs.  Both this model and the native engine
+are checked round by round against ``tests/dist_round_spec.py``.
 
 Protocol (reference capability: v4/mpi_bas.cpp:79-132 and the v2 draft's
 frontier exchange, v2/main-v2.cpp:59-83):

@@ -1,9 +1,11 @@
-"""The partitioned multi-process protocol (same per-level collectives as the
-RCCL engine, csrc/dist/dist_engine.hip) on CPU processes over gloo, against
-the serial oracle: top-down candidate exchange, overflow to bottom-up, Beamer
-switching, unreachable pairs and path reconstruction by MIN-allreduce."""
+"""The partitioned engine's round protocol on CPU processes over gloo: the
+test-only model (tests/dist_protocol_model.py) against the serial oracle AND
+round by round against the protocol spec (tests/dist_round_spec.py) that the
+native engine's GPU tests assert too: top-down candidate exchange, overflow
+to bottom-up, Beamer switching, unreachable pairs, path reconstruction."""
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -21,7 +23,8 @@ def _free_port():
 def _worker(rank, world, port, specs, queue):
     import torch.distributed as dist
 
-    from bidirectional_bfs_amd.parallel.torch_dist import TorchDistBiBfs
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from dist_protocol_model import TorchDistBiBfs
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -33,7 +36,8 @@ def _worker(rank, world, port, specs, queue):
             eng = TorchDistBiBfs(g.edge_array(), g.n, candidate_cap=cap)
             for s, d in pairs:
                 r = eng.search(s, d, **kw)
-                out.append((spec, s, d, r.found, r.hops, list(r.path), r.sparse_levels, r.dense_levels))
+                out.append((spec, s, d, r.found, r.hops, list(r.path), r.sparse_levels, r.dense_levels,
+                            [tuple(int(x) for x in t) for t in r.trace], kw))
         if rank == 0:
             queue.put(out)
     finally:
@@ -74,10 +78,14 @@ def test_partitioned_protocol_matches_oracle(world):
     out = _run(world, specs)
     graphs = {}
     dense = 0
-    for spec, s, d, found, hops, path, sparse_l, dense_l in out:
+    from dist_round_spec import round_trace
+
+    for spec, s, d, found, hops, path, sparse_l, dense_l, trace, kw in out:
         g = graphs.setdefault(spec, bb.from_spec(spec))
         o = native.bfs_oracle(g.csr, s, d)
         assert found == o.found and hops == o.hops, (spec, s, d, hops, o.hops)
+        want, whops = round_trace(g.csr, s, d, side=kw.get("side", "edges"), lockstep=kw.get("lockstep", True))
+        assert trace == want and (whops if whops >= 0 else -1) == (hops if found else -1), (spec, s, d, kw)
         if found:
             ok, why = native.validate_path(g.csr, s, d, hops, path)
             assert ok, (spec, s, d, why)

@@ -155,3 +155,32 @@ def test_failing_rank_aborts_every_rank(mode):
         dist_local_run(3, g, qs, tuning=make_tuning(timeout_s=1.0), fault=(1, 2, mode))
     msg = str(ei.value)
     assert "injected fault" in msg or "timed out" in msg or "aborted" in msg, msg
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 3])
+@pytest.mark.parametrize("spec_rounds", [0, 4])
+def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
+    """Round by round, the native engine expands the sides the protocol spec
+    says and discovers what the BFS levels say (tests/dist_round_spec.py --
+    the same spec the CPU model is held to in tests/test_dist_protocol.py),
+    whether rounds are planned on the device or on the host, and through
+    tiny exchange blocks (count syncs, overflow to bottom-up)."""
+    import torch  # noqa: F401
+    from dist_round_spec import round_trace
+
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    for spec in ("gnp:20000::6", "rmat:16384:262144:3"):
+        g = bb.from_spec(spec)
+        qs = _pairs(g.n, 6, 13)
+        for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False},
+                   {"direction": "bottomup"}):
+            for tune in (make_tuning(spec_rounds=spec_rounds), make_tuning(spec_rounds=spec_rounds, cap=4,
+                                                                          nosync_bytes=0)):
+                rs = dist_local_run(ranks, g, qs, tuning=tune, trace=True, **kw)
+                for (s, d), r in zip(qs, rs):
+                    want, hops = round_trace(g.csr, s, d, side=kw.get("side", "edges"),
+                                             lockstep=kw.get("lockstep", True))
+                    got = [(t["side"], t["depth"], t["frontier"], t["edges"], t["discovered"]) for t in r.stats["trace"]]
+                    assert got == [w[:5] for w in want], (spec, s, d, kw)
+                    assert r.hops == hops, (spec, s, d, r.hops, hops)
