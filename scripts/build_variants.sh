@@ -6,7 +6,7 @@ ROOT="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
 cd "$ROOT"
 make -s -j8 gpu >/dev/null
 OBJS=$(ls build/obj/{io,gen,csr,cpu}/*.o | grep -v mpi_) 
-OTHER="build/obj/hip/capi.o build/obj/hip/csr_device.o build/obj/hip/hip_engine.o build/obj/dist/dist_engine.o"
+OTHER=$(ls build/obj/hip/*.o build/obj/dist/*.o | grep -v engine_kernels)
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   mkdir -p build/var/$name

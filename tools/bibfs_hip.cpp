@@ -17,6 +17,7 @@ static const char* bibfs_mode_name(int m) {
     case 4: return "grid-topdown";
     case 5: return "grid-bottomup";
     case 6: return "lds-lean";
+    case 7: return "reg-lockstep";
     default: return "cpu";
   }
 }
@@ -84,7 +85,12 @@ int main(int argc, char** argv) {
       std::printf("GPU BFS: %s\n", r.found ? "PATH FOUND" : "NO PATH");
       if (opt.trace && std::getenv("BIBFS_STAMP")) {
         for (auto& t : r.stats.trace) {
-          if (t.mode == 1 || t.mode == 2)  // wave rounds: phase split of wave 0 / the working wave
+          if (t.mode == 7)  // register-frontier lockstep round
+            std::printf("Stamp cycles: reg round=%d edges=%llu load=%d claim+meet=%llu book+scan=%llu redistribute=%llu\n",
+                        t.side, (unsigned long long)(t.edges & 0xffffffffu), t.depth,
+                        (unsigned long long)(t.frontier & 0xffff), (unsigned long long)(t.frontier >> 16),
+                        (unsigned long long)(t.edges >> 32));
+          else if (t.mode == 1 || t.mode == 2)  // wave rounds: phase split of wave 0 / the working wave
             std::printf("Stamp cycles: %s round=%d barrier_wait=%d rec+col=%llu row_off=%llu claim=%llu append=%llu\n",
                         bibfs_mode_name(t.mode), t.side, t.depth, (unsigned long long)(t.edges & 0xffff),
                         (unsigned long long)((t.edges >> 16) & 0xffff), (unsigned long long)((t.edges >> 32) & 0xffff),
