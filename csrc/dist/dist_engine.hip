@@ -44,6 +44,7 @@
 
 #include "bibfs/dist_engine.hpp"
 #include "bibfs/io.hpp"
+#include "bibfs/trace.hpp"
 #include "comm.hpp"
 #include "device.hpp"
 
@@ -1151,6 +1152,7 @@ struct DistBiBfs::Impl {
 // level, or a sparse level too big for the speculative block).  Sizes come
 // from the read-back Ctl; one host wait at the end (k_final).
 void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r) {
+  TraceRange range("dist:host_round");
   const Ctl h = *h_ctl;
   hipStream_t ps = stream, cs = cstream;
   const int P = size;
@@ -1244,6 +1246,7 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
 }
 
 SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& opt) {
+  TraceRange range("dist:search");
   const auto t0 = std::chrono::steady_clock::now();
   BIBFS_REQUIRE(n > 0, "no graph loaded");
   BIBFS_REQUIRE(src < n && dst < n, "src/dst out of range");
@@ -1307,6 +1310,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       }
     }
     // ---- K speculative sparse rounds, then one host wait
+    TraceRange batch_range("dist:speculative_batch");
     const unsigned bx = std::min<unsigned>(
         (unsigned)cus * 2, std::max<unsigned>(1, (unsigned)((uint64_t)spec_cap / P / kThreads) + 1));
     const unsigned cx = std::min<unsigned>((unsigned)cus * 2, std::max<unsigned>(1, spec_cap / kThreads / 4 + 1));
@@ -1395,6 +1399,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
 // claimed, ONE allgather, and a one-workgroup kernel walks both parent chains
 // from LDS tables.  False when the visited sets are too large for that.
 bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
+  TraceRange range("dist:path_gather");
   const Ctl& h = *h_ctl;
   const uint64_t vS = h.vis[0], vT = h.vis[1];
   if (vS + vT > tune.walk_max) return false;
@@ -1439,6 +1444,7 @@ void DistBiBfs::Impl::cleanup_enqueue(const Ctl& h) {
 
 // Fallback: one allreduce per hop (visited sets too large to gather).
 void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult& r) {
+  TraceRange range("dist:path_per_hop");
   hipStream_t cs = cstream;
   const uint32_t meet = (uint32_t)(key & 0xffffffffull);
   k_meet_depth<<<1, 64, 0, cs>>>(V, meet, it);
@@ -1504,6 +1510,7 @@ DistBiBfs::~DistBiBfs() {
 }
 
 void DistBiBfs::load_edges(const EdgeList& el) {
+  TraceRange range("dist:build");
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
   I.free_all();
@@ -1520,6 +1527,7 @@ void DistBiBfs::load_edges(const EdgeList& el) {
 }
 
 void DistBiBfs::load_bin(const std::string& path) {
+  TraceRange range("dist:build");
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
   I.free_all();
@@ -1538,6 +1546,7 @@ void DistBiBfs::load_bin(const std::string& path) {
 }
 
 void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
+  TraceRange range("dist:build");
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
   I.free_all();
@@ -1550,6 +1559,7 @@ void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
 }
 
 void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c) {
+  TraceRange range("dist:build");
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
   I.free_all();

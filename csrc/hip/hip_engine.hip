@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "bibfs/hip_engine.hpp"
+#include "bibfs/trace.hpp"
 #include "device.hpp"
 
 namespace bibfs {
@@ -531,6 +532,7 @@ HipBiBfs::~HipBiBfs() {
 }
 
 void HipBiBfs::load_csr(const Csr& g) {
+  TraceRange range("bibfs:build");
   HIP_CHECK(hipSetDevice(p_->device));
   p_->free_graph();
   auto& I = *p_;
@@ -553,6 +555,7 @@ void HipBiBfs::load_csr(const Csr& g) {
 
 
 void HipBiBfs::load_edges(const EdgeList& el) {
+  TraceRange range("bibfs:build");
   HIP_CHECK(hipSetDevice(p_->device));
   p_->free_graph();
   auto& I = *p_;
@@ -574,6 +577,7 @@ void HipBiBfs::load_edges(const EdgeList& el) {
 }
 
 void HipBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
+  TraceRange range("bibfs:build");
   HIP_CHECK(hipSetDevice(p_->device));
   p_->free_graph();
   auto& I = *p_;
@@ -594,6 +598,7 @@ void HipBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
 }
 
 void HipBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c) {
+  TraceRange range("bibfs:build");
   HIP_CHECK(hipSetDevice(p_->device));
   p_->free_graph();
   auto& I = *p_;
@@ -784,6 +789,7 @@ DeviceInfo HipBiBfs::info() const {
 }
 
 SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
+  TraceRange range("bibfs:search");
   auto& I = *p_;
   const auto t0 = std::chrono::steady_clock::now();
   BIBFS_REQUIRE(I.n > 0, "no graph loaded");
@@ -839,6 +845,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   }
   uint32_t pub_seq = seq;
   if (grid) {
+    TraceRange grange("bibfs:grid_levels");
     I.grid_loop(opt, stats);
     pub_seq = ++I.seq == 0 ? ++I.seq : I.seq;
     launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
