@@ -150,6 +150,7 @@ struct HostSide {
   dev::HostResult* res;  // pinned, device-visible
   uint32_t* path;        // pinned
   uint32_t path_cap;
+  dev::DevState* state = nullptr;  // pinned DevState mirror (the LDS hand-off publishes into it)
 };
 
 // csr_device.hip
@@ -188,13 +189,18 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
 void batch_global(const GraphView& g, uint32_t words, const uint32_t* qidx, uint32_t k, const uint32_t* src,
                   const uint32_t* dst, uint32_t* slots, uint32_t* bits, dev::BatchOut* out, uint32_t* path,
                   uint32_t path_cap, unsigned long long edge_cap, int threads, hipStream_t s);
+// One top-down level; the LAST workgroup finishes it, publishes the mirror
+// (seq) and, when the search ended, walks the path and publishes the result
+// (res_seq).  hub_pass: also enqueue the edge-parallel hub pass (graphs with
+// vertices above the hub degree), which then finishes the level instead.
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
-                  dev::DevState* mirror, uint32_t seq, int trace, hipStream_t s);
-void grid_hubs(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t hubs, hipStream_t s);
+                  dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
+                  bool hub_pass, hipStream_t s);
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
 void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);
 void finish_level(const SearchBuffers& b, int side, int mode, int trace, dev::DevState* mirror, uint32_t seq,
-                  hipStream_t s);
+                  const HostSide& h, uint32_t res_seq, uint32_t n, hipStream_t s);
+uint32_t grid_hub_degree();
 void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
                uint32_t n, hipStream_t s);

@@ -1194,6 +1194,27 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         st->fedges[q] = x.fed;
         st->vedges[q] = x.ved;
       }
+      if (DevState* m = P.h.state) {  // the host continues from this mirror: no copy + sync
+        auto put = [](auto* p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
+        put(&m->status, (uint32_t)kRunning);
+        put(&m->meet, kEmpty);
+        put(&m->meet_side, 0u);
+        put(&m->levels, levels);
+        put(&m->hub_count, 0u);
+        put(&m->chunk, 0u);
+        put(&m->nedges, 0ull);
+        put(&m->einsp, einsp);
+        put(&m->pad[1], 0u);
+        for (int q = 0; q < 2; ++q) {
+          const SideState x = sel(q, s0, s1);
+          put(&m->depth[q], (int32_t)x.depth);
+          put(&m->fbeg[q], x.fbeg);
+          put(&m->fend[q], x.qend);
+          put(&m->qtail[q], x.qend);
+          put(&m->fedges[q], x.fed);
+          put(&m->vedges[q], x.ved);
+        }
+      }
     }
     if (tid == 0) {  // write-through (system-scope) stores: no L2 writeback needed for the host
       auto put = [](auto* p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
@@ -1409,10 +1430,13 @@ struct GridParams {
   DevState* mirror;  // fused level end: pinned state mirror (nullptr = separate finish kernel)
   uint32_t seq;
   int trace;
+  launch::HostSide h;  // fused publish of a finished search (path + result)
+  uint32_t res_seq;
+  uint32_t hub_deg;    // frontier vertices above this degree go to k_grid_hubs (~0u: never)
 };
 
-__device__ void fused_finish(const launch::SearchBuffers& b, int s, int mode, int trace, DevState* mirror,
-                             uint32_t seq);
+template <typename OffT>
+__device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass);
 
 // Claim v for side s from parent u; wave-uniform call (every lane calls it,
 // `valid` masks lanes with no edge).  Appends claimed vertices to the queue
@@ -1431,7 +1455,9 @@ __device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid
   const int leader = __ffsll((long long)mask) - 1;
   uint32_t deg = 0;
   if (mine) {
-    P.b.parent[s][v] = u;
+    // write-through (sc1): the level's last workgroup may walk this parent
+    // chain in the same kernel, from another XCD, with sc1 loads
+    __hip_atomic_store(&P.b.parent[s][v], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     deg = (uint32_t)(P.row_off[v + 1] - P.row_off[v]);
     if (P.b.vis[o][w] & bit) {
       if (atomicCAS(&st->meet, kEmpty, v) == kEmpty) st->meet_side = (uint32_t)s;
@@ -1469,7 +1495,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
       u = P.b.queue[s][fbase + i];
       b = P.row_off[u];
       deg = (uint32_t)(P.row_off[u + 1] - b);
-      if (deg > kHubDegree) {
+      if (deg > P.hub_deg) {
         P.b.hub_list[atomicAdd(&st->hub_count, 1u)] = u;
         deg = 0;
       }
@@ -1497,7 +1523,10 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     sEb[tid] = x - deg + wsum[wid];
     __syncthreads();
     const uint32_t Ec = stotal;
-    for (uint32_t base = 0; base < Ec; base += kGridThreads) {
+    for (uint32_t base = 0, it = 0; base < Ec; base += kGridThreads, ++it) {
+      // a meet ends the level (single-side level: every meet has the same
+      // length): check it every 16 batches, wave-uniformly
+      if ((it & 15) == 15 && __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty) break;
       const uint32_t e = base + tid;
       const bool valid = e < Ec;
       uint32_t uu = 0, v = 0;
@@ -1515,33 +1544,88 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     }
     __syncthreads();
   }
-  if (P.mirror) fused_finish(P.b, P.side, 1, P.trace, P.mirror, P.seq);
+  if (P.mirror) fused_finish(P, 1, false);
 }
 
-// Hub vertices (degree > kHubDegree) deferred by k_grid_topdown: every
-// workgroup takes 256-edge chunks of every hub round-robin.
+// Hub vertices (degree > hub_deg) deferred by k_grid_topdown, expanded
+// edge-parallel: every workgroup stages a tile of up to 1024 hubs with the
+// exclusive prefix of their degrees in LDS and walks the tile's flattened edge
+// range with a grid stride (binary search for the hub of an edge), so each
+// hub's edges spread over every CU (the previous kernel walked the hub list
+// in order in every workgroup).  Enqueued right behind the top-down kernel;
+// a no-op when that level deferred nothing (its finisher reset hub_count),
+// otherwise its last workgroup finishes the level.
+constexpr int kHubTile = 1024;
 template <typename OffT>
 __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) {
-  const int s = P.side;
+  __shared__ uint32_t hu[kHubTile];
+  __shared__ OffT hb[kHubTile];
+  __shared__ unsigned long long hp[kHubTile + 1];
+  __shared__ unsigned long long wsum[kGridThreads / kWave];
   DevState* st = P.b.st;
-  const uint32_t nh = st->hub_count;
-  uint64_t g = 0;  // global chunk index across hubs
-  for (uint32_t h = 0; h < nh; ++h) {
-    if (load_agent(&st->meet) != kEmpty) return;
-    const uint32_t u = P.b.hub_list[h];
-    const OffT b = P.row_off[u], e = P.row_off[u + 1];
-    const uint64_t nch = ((uint64_t)(e - b) + kGridThreads - 1) / kGridThreads;
-    // chunks g .. g+nch-1 of this hub; this block handles those == blockIdx mod grid
-    uint64_t first = (blockIdx.x >= g % gridDim.x) ? blockIdx.x - g % gridDim.x
-                                                  : blockIdx.x + gridDim.x - g % gridDim.x;
-    for (uint64_t c = first; c < nch; c += gridDim.x) {
-      const OffT k = b + (OffT)(c * kGridThreads + threadIdx.x);
-      const bool valid = k < e;
-      grid_claim(P, valid, u, valid ? P.col[k] : 0u);
+  const uint32_t H = st->hub_count;
+  if (H == 0) return;  // grid-uniform: the top-down finisher completed the level
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  for (uint32_t t0 = 0; t0 < H; t0 += kHubTile) {
+    const uint32_t nt = min((uint32_t)kHubTile, H - t0);
+    constexpr int kPer = kHubTile / kGridThreads;
+    unsigned long long d[kPer], run = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const uint32_t j = tid * kPer + k;
+      d[k] = 0;
+      if (j < nt) {
+        const uint32_t u = P.b.hub_list[t0 + j];
+        const OffT b = P.row_off[u];
+        d[k] = (unsigned long long)(P.row_off[u + 1] - b);
+        hu[j] = u;
+        hb[j] = b;
+      }
+      run += d[k];
     }
-    g += nch;
+    unsigned long long x = run;  // inclusive wave scan of per-thread sums
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const unsigned long long y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    if (lane == kWave - 1) wsum[wid] = x;
+    __syncthreads();
+    unsigned long long pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kGridThreads / kWave; ++k) {
+      pre += k < wid ? wsum[k] : 0ull;
+      tot += wsum[k];
+    }
+    unsigned long long e0 = pre + x - run;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      hp[tid * kPer + k] = e0;
+      e0 += d[k];
+    }
+    __syncthreads();
+    uint32_t it = 0;
+    for (unsigned long long base = (unsigned long long)blockIdx.x * kGridThreads; base < tot;
+         base += (unsigned long long)gridDim.x * kGridThreads, ++it) {
+      if ((it & 15) == 15 && __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty) break;
+      const unsigned long long e = base + tid;
+      const bool valid = e < tot;
+      uint32_t uu = 0, v = 0;
+      if (valid) {
+        uint32_t a = 0, z = nt;  // last hub whose edge range starts at or before e
+        while (z - a > 1) {
+          const uint32_t mid = (a + z) >> 1;
+          if (hp[mid] <= e) a = mid;
+          else z = mid;
+        }
+        uu = hu[a];
+        v = P.col[hb[a] + (OffT)(e - hp[a])];
+      }
+      grid_claim(P, valid, uu, v);
+    }
+    __syncthreads();
   }
-  (void)s;
+  fused_finish(P, 1, true);
 }
 
 // Bottom-up level for side s: every unvisited vertex looks for a parent in the
@@ -1649,8 +1733,11 @@ __device__ void publish_state(const DevState& v, DevState* mirror, uint32_t seq,
   if (lane == 0) __hip_atomic_store(&mirror->pad[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+__device__ void publish_result(const launch::SearchBuffers& b, const launch::HostSide& h, const DevState& sv,
+                               uint32_t res_seq, uint32_t n);
+
 __global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int trace, DevState* mirror,
-                               uint32_t seq) {
+                               uint32_t seq, launch::HostSide h, uint32_t res_seq, uint32_t n) {
   __shared__ DevState sv;
   if (blockIdx.x != 0) return;
   if (threadIdx.x == 0) {
@@ -1658,7 +1745,41 @@ __global__ void k_finish_level(launch::SearchBuffers b, int s, int mode, int tra
     sv = *b.st;
   }
   __syncthreads();
+  if (res_seq && sv.status != kRunning) publish_result(b, h, sv, res_seq, n);
   if (mirror && threadIdx.x < 64) publish_state(sv, mirror, seq, threadIdx.x);
+}
+
+// A finished search, published by the workgroup that finished its last level:
+// two waves walk the two parent chains (sc1 loads) into pinned host memory,
+// then one lane writes the result record, `seq` last (system-scope release).
+// Needs >= 2 waves.
+__device__ void publish_result(const launch::SearchBuffers& b, const launch::HostSide& h, const DevState& sv,
+                               uint32_t res_seq, uint32_t n) {
+  const int tid = threadIdx.x;
+  const uint32_t status = sv.status == kFound ? kFound : kNoPath;
+  const int d0 = sv.depth[0], d1 = sv.depth[1];
+  const uint32_t hops = (uint32_t)(d0 + d1);
+  uint32_t* out = (hops + 1 <= h.path_cap) ? h.path : b.dpath;
+  if (status == kFound && (tid == 0 || tid == kWave)) {
+    walk_side(b.parent[tid ? 1 : 0], n, sv.meet, tid ? 1 : 0, d0, d1, out);
+    __threadfence_system();
+  }
+  __syncthreads();
+  if (tid == 0) {
+    HostResult* Rr = h.res;
+    Rr->status = status;
+    Rr->hops = status == kFound ? (int32_t)hops : -1;
+    Rr->meet = sv.meet;
+    Rr->levels = sv.levels;
+    Rr->visited = sv.qtail[0] + sv.qtail[1];
+    Rr->einsp = sv.einsp;
+    Rr->depth[0] = d0;
+    Rr->depth[1] = d1;
+    Rr->path_len = status == kFound ? hops + 1 : 0u;
+    Rr->path_on_device = (status == kFound && hops + 1 > h.path_cap) ? 1u : 0u;
+    __threadfence_system();
+    __hip_atomic_store(&Rr->seq, res_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // End-of-level bookkeeping of the grid engine on a DevState (device memory
@@ -1699,17 +1820,19 @@ __device__ void finish_state(DevState& sref, const launch::SearchBuffers& b, int
 // DevState word is read with a device-scope atomic (the counters were updated
 // by atomics from every XCD; a plain load could see a stale L2 line), the
 // bookkeeping runs on an LDS copy, the words go back with plain stores (the
-// next level is a new launch) and the pinned mirror is published.  With hubs
-// deferred, the mirror says so (pad[1] = 1) and the host runs the hub kernel
-// and the separate finish kernel instead.
-__device__ void fused_finish(const launch::SearchBuffers& b, int s, int mode, int trace, DevState* mirror,
-                             uint32_t seq) {
+// next level is a new launch), and the pinned mirror is published; when the
+// level ended the search, the same workgroup walks the path (the parents
+// were stored write-through) and publishes the result.  A top-down level that
+// deferred hubs leaves the finish to k_grid_hubs (hub_pass), which runs next.
+template <typename OffT>
+__device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass) {
   __shared__ DevState sv;
   __shared__ uint32_t slast;
   constexpr uint32_t kWords = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
   static_assert(kWords <= 64, "one lane per word");
+  const launch::SearchBuffers& b = P.b;
   const uint32_t tid = threadIdx.x;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's atomics have completed
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's atomics and sc1 stores have completed
   __syncthreads();
   if (tid == 0) slast = atomicAdd(&b.st->pad[1], 1u) == gridDim.x - 1;
   __syncthreads();
@@ -1717,28 +1840,19 @@ __device__ void fused_finish(const launch::SearchBuffers& b, int s, int mode, in
   uint32_t* w = reinterpret_cast<uint32_t*>(b.st);
   if (tid < kWords) reinterpret_cast<uint32_t*>(&sv)[tid] = atomicAdd(&w[tid], 0u);
   __syncthreads();
-  const bool hubs = sv.hub_count != 0;
+  const bool defer = !hub_pass && sv.hub_count != 0;  // the hub pass finishes this level
   if (tid == 0) {
-    sv.pad[1] = 0;  // done counter, for the next level
-    if (!hubs) finish_state(sv, b, s, mode, trace);
+    sv.pad[1] = 0;  // done counter, for the next kernel
+    if (!defer) finish_state(sv, b, P.side, mode, P.trace);
   }
   __syncthreads();
-  if (hubs) {
-    if (tid == 0) {
-      atomicExch(&b.st->pad[1], 0u);
-      if (mirror) {
-        __hip_atomic_store(&mirror->pad[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(&mirror->pad[0], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-    }
+  if (defer) {
+    if (tid == 0) atomicExch(&b.st->pad[1], 0u);
     return;
   }
   if (tid < kWords) w[tid] = reinterpret_cast<const uint32_t*>(&sv)[tid];
-  if (mirror && tid < 64) {
-    if (tid == 0) __hip_atomic_store(&mirror->pad[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    publish_state(sv, mirror, seq, tid);
-  }
+  if (P.res_seq && sv.status != kRunning) publish_result(b, P.h, sv, P.res_seq, P.n);
+  if (P.mirror && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
 }
 
 // Seed a search for the grid engine / step-wise API.
@@ -1834,6 +1948,9 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.mirror = nullptr;
   P.seq = 0;
   P.trace = 0;
+  P.h = launch::HostSide{nullptr, nullptr, 0, nullptr};
+  P.res_seq = 0;
+  P.hub_deg = kHubDegree;
   return P;
 }
 
@@ -1911,39 +2028,26 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
   HIP_CHECK(hipGetLastError());
 }
 
+uint32_t grid_hub_degree() { return kHubDegree; }
+
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
-                  dev::DevState* mirror, uint32_t seq, int trace, hipStream_t s) {
+                  dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
+                  bool hub_pass, hipStream_t s) {
   // Dynamic chunks of 256 frontier vertices; never more blocks than chunks:
   // every block takes at least one ticket from ONE counter, and 1024 blocks
-  // contending on it cost ~12 us even for a 3-vertex frontier.  Hubs: one
-  // block per deferred vertex at most.
+  // contending on it cost ~12 us even for a 3-vertex frontier.
   const uint64_t chunks = (frontier + kGridThreads - 1) / kGridThreads;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, chunks));
-  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier));
-  if (g.row_off32) {
-    auto P = gp<uint32_t>(g, b, side);
-    P.mirror = mirror, P.seq = seq, P.trace = trace;
-    k_grid_topdown<uint32_t><<<blocks, kGridThreads, 0, s>>>(P);
-    if (!mirror) k_grid_hubs<uint32_t><<<hblocks, kGridThreads, 0, s>>>(P);
-  } else {
-    auto P = gp<uint64_t>(g, b, side);
-    P.mirror = mirror, P.seq = seq, P.trace = trace;
-    k_grid_topdown<uint64_t><<<blocks, kGridThreads, 0, s>>>(P);
-    if (!mirror) k_grid_hubs<uint64_t><<<hblocks, kGridThreads, 0, s>>>(P);
-  }
-  HIP_CHECK(hipGetLastError());
-}
-
-// Hubs deferred by a fused top-down level (the host saw pad[1] in the mirror).
-void grid_hubs(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t hubs, hipStream_t s) {
-  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, hubs));
-  if (g.row_off32) {
-    auto P = gp<uint32_t>(g, b, side);
-    k_grid_hubs<uint32_t><<<hblocks, kGridThreads, 0, s>>>(P);
-  } else {
-    auto P = gp<uint64_t>(g, b, side);
-    k_grid_hubs<uint64_t><<<hblocks, kGridThreads, 0, s>>>(P);
-  }
+  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
+  auto launch_one = [&](auto P) {
+    using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
+    P.mirror = mirror, P.seq = seq, P.trace = trace, P.h = h, P.res_seq = res_seq;
+    P.hub_deg = hub_pass ? kHubDegree : ~0u;
+    k_grid_topdown<OffT><<<blocks, kGridThreads, 0, s>>>(P);
+    if (hub_pass) k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
+  };
+  if (g.row_off32) launch_one(gp<uint32_t>(g, b, side));
+  else launch_one(gp<uint64_t>(g, b, side));
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1971,8 +2075,8 @@ void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, h
 }
 
 void finish_level(const SearchBuffers& b, int side, int mode, int trace, DevState* mirror, uint32_t seq,
-                  hipStream_t s) {
-  k_finish_level<<<1, 64, 0, s>>>(b, side, mode, trace, mirror, seq);
+                  const HostSide& h, uint32_t res_seq, uint32_t n, hipStream_t s) {
+  k_finish_level<<<1, 128, 0, s>>>(b, side, mode, trace, mirror, seq, h, res_seq, n);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -145,7 +145,7 @@ struct HipBiBfs::Impl {
     if (dbg()) std::fprintf(stderr, "[server] launch seq %u pin %d\n", srv_launch_seq, pin);
     __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
     const uint32_t last = __atomic_load_n(&h_box->seq, __ATOMIC_ACQUIRE);
-    launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap}, h_box, srv_launch_seq, last, pin,
+    launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box, srv_launch_seq, last, pin,
                        d_flag + 4, srv_idle_ticks, sstream);
     srv_running = true;
   }
@@ -199,7 +199,7 @@ struct HipBiBfs::Impl {
           const uint32_t pending = qseq;
           srv_launch_seq = ++seq == 0 ? ++seq : seq;
           __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
-          launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap}, h_box, srv_launch_seq,
+          launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box, srv_launch_seq,
                              pending - 1, pin_xcc, d_flag + 4, srv_idle_ticks, sstream);
           srv_running = true;
         } else if (e != hipErrorNotReady) {
@@ -363,31 +363,29 @@ struct HipBiBfs::Impl {
     HIP_CHECK(hipStreamSynchronize(stream));
   }
 
-  // one grid level of side s; mode 1 = top-down, 2 = bottom-up
+  // one grid level of side s; mode 1 = top-down, 2 = bottom-up.  The level's
+  // last workgroup finishes it and publishes the pinned mirror; when the level
+  // ends the search it also walks the path and publishes the result with
+  // res_seq (0 = leave that to the caller: step-wise API).
+  uint32_t res_seq = 0;
   void grid_level(int s, int mode, int trace) {
     const auto g = view();
+    const launch::HostSide hs{h_res, h_path, h_path_cap, h_state};
+    const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
     if (mode == 2) {
       if (!fbits_valid[s]) launch::build_frontier_bits(g, buf, s, stream);
       launch::grid_bottomup(g, buf, s, cus, stream);
       std::swap(buf.fbits[s], buf.nbits[s]);
       fbits_valid[s] = true;
+      launch::finish_level(buf, s, mode, trace, h_state, ls, hs, res_seq, n, stream);
     } else {
-      // fused: the kernel's last workgroup finishes the level and publishes
-      // the mirror; hub vertices (if any) need the hub kernel + finish
-      const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
-      launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), h_state, ls, trace,
-                           stream);
+      // a vertex above the hub degree can only be in a frontier with that many edges
+      const bool hub_pass = h_state->fedges[s] > launch::grid_hub_degree();
+      launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), h_state, ls, trace, hs,
+                           res_seq, hub_pass, stream);
       fbits_valid[s] = false;
-      wait_level();
-      if (h_state->pad[1]) {
-        launch::grid_hubs(g, buf, s, cus, (uint64_t)h_state->hub_count, stream);
-        const uint32_t l2 = ++level_seq == 0 ? ++level_seq : level_seq;
-        launch::finish_level(buf, s, mode, trace, h_state, l2, stream);
-      }
-      return;
     }
-    const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
-    launch::finish_level(buf, s, mode, trace, h_state, ls, stream);
+    wait_level();
   }
 
   int choose_mode(int s, const SearchOptions& opt) {
@@ -415,14 +413,15 @@ struct HipBiBfs::Impl {
   }
 
   // Runs grid levels until the search ends; returns #grid levels and #bottom-up levels.
+  // mirror_valid: the LDS hand-off already published DevState into h_state.
+  bool mirror_valid = false;
   void grid_loop(const SearchOptions& opt, SearchStats& stats) {
     dir[0] = dir[1] = 1;
     fbits_valid[0] = fbits_valid[1] = false;
     int turn = 0;
     const int trace = opt.trace ? 1 : 0;
     for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
-      if (guard == 0) sync_state();  // state left by the seed / the LDS hand-off
-      else wait_level();             // pinned mirror of the level just finished
+      if (guard == 0 && !mirror_valid) sync_state();  // state left by the seed
       if (h_state->status != kRunning || h_state->meet != kEmpty) break;
       const int s = choose_side(opt, turn);
       const int mode = choose_mode(s, opt);
@@ -807,7 +806,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   HIP_CHECK(hipSetDevice(I.device));
   const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
   const auto g = I.view();
-  launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap};
+  launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap, I.h_state};
   SearchStats stats;
   bool grid = opt.force_grid;
   double lds_ms = 0.0;
@@ -838,6 +837,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     if (I.h_res->status == kHandoff) {
       grid = true;
       stats.handoff = true;
+      I.mirror_valid = true;  // the LDS kernel published the hand-off state
       HIP_CHECK(hipEventRecord(I.ev0, I.stream));
     }
   } else {
@@ -846,10 +846,15 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   uint32_t pub_seq = seq;
   if (grid) {
     TraceRange grange("bibfs:grid_levels");
-    I.grid_loop(opt, stats);
     pub_seq = ++I.seq == 0 ? ++I.seq : I.seq;
-    launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
-    I.wait_seq(pub_seq);
+    I.res_seq = pub_seq;  // the level that ends the search publishes the path + result
+    I.grid_loop(opt, stats);
+    I.res_seq = 0;
+    I.mirror_valid = false;
+    if (I.h_res->seq != pub_seq) {  // ended before any grid level ran (meet at hand-off / seed)
+      launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
+      I.wait_seq(pub_seq);
+    }
   }
   if (grid) HIP_CHECK(hipEventRecord(I.ev1, I.stream));
   SearchResult r = I.collect(pub_seq, opt, std::move(stats));
@@ -891,7 +896,6 @@ uint64_t HipBiBfs::expand(int side, bool* met, Direction dir) {
     return 0;
   }
   I.grid_level(side, dir == Direction::kBottomUp ? 2 : 1, 0);
-  I.sync_state();
   if (met) *met = I.h_state->meet != kEmpty;
   return I.h_state->qtail[side] - before;
 }
@@ -915,7 +919,7 @@ SearchResult HipBiBfs::finish() {
     r.path = {I.step_src};
   } else {
     const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
-    launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap};
+    launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap, I.h_state};
     launch::walk_path(I.buf, hs, I.step_src, I.step_dst, seq, I.n, I.stream);
     I.wait_seq(seq);
     SearchOptions opt;
