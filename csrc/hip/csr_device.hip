@@ -239,6 +239,33 @@ void build_padj(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, uint
   HIP_CHECK(hipGetLastError());
 }
 
+// Largest degree of the CSR (wave max, one atomic per wave).
+__global__ void k_max_degree(const uint64_t* __restrict__ row_off, uint32_t n, unsigned long long* out) {
+  unsigned long long m = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long d = row_off[i + 1] - row_off[i];
+    m = d > m ? d : m;
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned long long y = __shfl_xor(m, o);
+    m = y > m ? y : m;
+  }
+  if (__lane_id() == 0 && m) atomicMax(out, m);
+}
+
+uint64_t max_degree(const uint64_t* d_row_off, uint32_t n, hipStream_t s) {
+  unsigned long long* d = nullptr;
+  HIP_CHECK(hipMalloc(&d, 8));
+  HIP_CHECK(hipMemsetAsync(d, 0, 8, s));
+  k_max_degree<<<(unsigned)std::min<uint64_t>(grid_for(n, 256), 2048), 256, 0, s>>>(d_row_off, n, d);
+  HIP_CHECK(hipGetLastError());
+  unsigned long long h = 0;
+  HIP_CHECK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipFree(d));
+  return h;
+}
+
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s) {
   k_row32<<<grid_for(n + 1ULL, 256), 256, 0, s>>>(d_row_off, n + 1, d_row_off32);
   HIP_CHECK(hipGetLastError());

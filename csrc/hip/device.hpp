@@ -167,6 +167,7 @@ void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, c
                    uint64_t* d_cursor, uint32_t* d_col, hipStream_t s);
 void build_padj(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, uint4* padj, hipStream_t s);
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s);
+uint64_t max_degree(const uint64_t* d_row_off, uint32_t n, hipStream_t s);  // synchronous
 uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);
 void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,
                      uint32_t* d_uv, hipStream_t s);

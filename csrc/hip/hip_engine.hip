@@ -37,6 +37,7 @@ struct HipBiBfs::Impl {
   uint32_t* d_row_off32 = nullptr;
   uint32_t* d_col = nullptr;
   uint4* d_padj = nullptr;   // packed adjacency (LDS engine), when it fits the budget
+  uint64_t max_deg = 0;      // largest degree: no hub pass when it is below the hub degree
   uint32_t* d_uv = nullptr;  // last generated edge list (kept for small graphs / tests)
   uint64_t uv_m = 0;
   double build_ms = 0.0;
@@ -295,6 +296,7 @@ struct HipBiBfs::Impl {
       HIP_CHECK(hipMalloc(&d_padj, nnz * 16));
       launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
     }
+    max_deg = launch::max_degree(d_row_off, n, stream);
     alloc_state();
     build_ms = ms;
   }
@@ -380,7 +382,7 @@ struct HipBiBfs::Impl {
       launch::finish_level(buf, s, mode, trace, h_state, ls, hs, res_seq, n, stream);
     } else {
       // a vertex above the hub degree can only be in a frontier with that many edges
-      const bool hub_pass = h_state->fedges[s] > launch::grid_hub_degree();
+      const bool hub_pass = max_deg > launch::grid_hub_degree() && h_state->fedges[s] > launch::grid_hub_degree();
       launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), h_state, ls, trace, hs,
                            res_seq, hub_pass, stream);
       fbits_valid[s] = false;
