@@ -186,6 +186,7 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks
             "query_ms": round(head["ms_per_step"], 6),
             "device_ms_per_query": round(head["device_ms_per_query"], 6),
             "cpu_serial_ms": head.get("cpu_serial_ms"),
+            "cpu_serial_query_ms": head.get("cpu_serial_query_ms"),
             "baseline_best_100k_ms": BASELINE_100K_MS,
             "gteps_inspected": head["gteps_inspected"],
             "mean_hops": head["mean_hops"],
@@ -202,20 +203,26 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks
 
 
 def cpu_serial_ms(spec: str, pairs, reps: int = 20):
-    """Median search time of this repo's -O3 serial engine (v1 parity) on the same graph and pairs."""
+    """This repo's -O3 serial engine (v1 parity) on the same graph and pairs:
+    (median engine-internal search ms, mean of it, mean end-to-end query ms
+    through the same Python call + path access as the GPU loop)."""
     from bidirectional_bfs_amd import native
 
     kind, n, arg, seed = parse_spec(spec)
     el = native.gen_gnp(n, arg, seed) if kind == "gnp" else native.gen_rmat(n, int(arg), seed, 0.57, 0.19, 0.19)
     eng = native.SerialBiBfs(native.build_csr(el))
     ts = []
-    for i in range(reps * len(pairs)):
+    q = reps * len(pairs)
+    t0 = time.perf_counter()
+    for i in range(q):
         s, d, h = pairs[i % len(pairs)]
         r = eng.search(s, d)
-        assert r.hops == h, (s, d, r.hops, h)
+        path = r.path
+        assert r.found and r.hops == h and len(path) == h + 1, (s, d, r.hops, h)
         ts.append(r.search_ms)
+    e2e = (time.perf_counter() - t0) * 1e3 / q
     ts.sort()
-    return ts[len(ts) // 2], sum(ts) / len(ts)
+    return ts[len(ts) // 2], sum(ts) / len(ts), e2e
 
 
 def main(argv=None) -> int:
@@ -342,9 +349,10 @@ def main(argv=None) -> int:
         }
         eng.release()  # free HBM before the next config
         if cpu_ref and not a.no_cpu_ref:
-            med, mean = cpu_serial_ms(spec, pairs)
+            med, mean, e2e = cpu_serial_ms(spec, pairs)
             out["cpu_serial_ms"] = round(med, 6)
             out["cpu_serial_mean_ms"] = round(mean, 6)
+            out["cpu_serial_query_ms"] = round(e2e, 6)
         return out
 
     def dist_engine():
