@@ -807,7 +807,11 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
                                                uint32_t hops, uint32_t* out) {
   extern __shared__ uint32_t lds[];
   uint32_t* keys[2] = {lds, lds + 2 * slotsS};
-  const uint32_t mask[2] = {slotsS - 1, slotsT - 1};
+  const uint32_t nslot[2] = {slotsS, slotsT};
+  // multiply-shift range reduction: any table size, so a ~0.77 load factor
+  // fits ~15k (vertex, parent) pairs in 160 KB of LDS
+  auto home = [&](int s, uint32_t v) { return (uint32_t)(((uint64_t)(v * 2654435761u) * nslot[s]) >> 32); };
+  auto next = [&](int s, uint32_t h) { return h + 1 == nslot[s] ? 0u : h + 1; };
   for (uint32_t i = threadIdx.x; i < slotsS + slotsT; i += blockDim.x) {
     const uint32_t s = i < slotsS ? 0 : 1, k = s ? i - slotsS : i;
     keys[s][2 * k] = kEmpty;
@@ -821,11 +825,11 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
     for (uint32_t i = threadIdx.x; i < c0 + c1; i += blockDim.x) {
       const int s = i < c0 ? 0 : 1;
       const uint2 x = pr[s ? capS + (i - c0) : i];
-      uint32_t h = (x.x * 2654435761u) & mask[s];
+      uint32_t h = home(s, x.x);
       while (true) {
         const uint32_t prev = atomicCAS(&keys[s][2 * h], kEmpty, x.x);
         if (prev == kEmpty || prev == x.x) break;
-        h = (h + 1) & mask[s];
+        h = next(s, h);
       }
       keys[s][2 * h + 1] = x.y;
     }
@@ -833,12 +837,12 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
   __syncthreads();
   if (threadIdx.x != 0) return;
   auto parent_of = [&](int s, uint32_t v, bool& ok) -> uint32_t {
-    uint32_t h = (v * 2654435761u) & mask[s];
-    for (uint32_t probe = 0; probe <= mask[s]; ++probe) {
+    uint32_t h = home(s, v);
+    for (uint32_t probe = 0; probe < nslot[s]; ++probe) {
       const uint32_t k = keys[s][2 * h];
       if (k == v) return keys[s][2 * h + 1];
       if (k == kEmpty) break;
-      h = (h + 1) & mask[s];
+      h = next(s, h);
     }
     ok = false;
     return kEmpty;
@@ -1404,7 +1408,7 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   const uint64_t vS = h.vis[0], vT = h.vis[1];
   if (vS + vT > tune.walk_max) return false;
   const uint32_t capS = (uint32_t)std::max<uint64_t>(vS, 1), capT = (uint32_t)std::max<uint64_t>(vT, 1);
-  const uint32_t slotsS = next_pow2(2 * (uint64_t)capS), slotsT = next_pow2(2 * (uint64_t)capT);
+  const uint32_t slotsS = capS + capS / 3 + 1, slotsT = capT + capT / 3 + 1;  // load factor <= 0.75
   const size_t lds = (size_t)(slotsS + slotsT) * 8;
   if (lds > 160 * 1024) return false;
   const uint32_t meet = (uint32_t)(key & 0xffffffffull), hops = (uint32_t)(key >> 32);

@@ -74,7 +74,7 @@ struct DistTuning {
   uint32_t cap = 0;                // per-rank candidate block of a host-planned round (0 = min(2^20, n))
   uint64_t nosync_bytes = 1u << 20;  // host-planned round: size the exchange from host bounds up to this
   double timeout_s = 120.0;        // a host wait longer than this aborts the communicator and throws
-  uint32_t walk_max = 8192;        // path from one gathered parent table when both sides claimed <= this
+  uint32_t walk_max = 15000;       // path from one gathered parent table when both sides claimed <= this
 };
 
 class DistBiBfs {
