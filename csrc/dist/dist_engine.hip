@@ -151,6 +151,7 @@ struct DView {
   int P;
   DState* st;
   Ctl* ctl;                   // [2]
+  uint32_t* plan_word;        // pinned: ((it + 1) << 8) | state << 2 | sides of the latest planned round
   struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
   uint32_t trace_cap;
   Reduced* red;               // [2]
@@ -432,6 +433,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
     V.red[p].meetkey = kNoKey;
+    // one 4-byte write-through store: the host paces its enqueueing on it
+    __hip_atomic_store(V.plan_word, ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int s = blockIdx.y;
   if ((c.sides >> s) & 1)
@@ -954,6 +958,7 @@ struct DistBiBfs::Impl {
   RoundRec* d_trace = nullptr;
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
+  uint32_t* h_plan = nullptr;  // pinned plan word (k_spec_expand)
   uint32_t* h_walk = nullptr;  // pinned
   size_t h_walk_cap = 0;
   double* d_scalar = nullptr;
@@ -980,6 +985,9 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipEventCreate(&ev_t1));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl), sizeof(Ctl), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), 64, hipHostMallocDefault));
+    *h_plan = 0;
+    V.plan_word = h_plan;
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
@@ -1120,6 +1128,33 @@ struct DistBiBfs::Impl {
                       " s for a round (peer failure or hang); communicator aborted");
         }
         if (now - t0 > std::chrono::milliseconds(2)) std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
+  }
+
+  // Spin until the device has planned round `need` (the pinned plan word);
+  // returns the word.  Same watchdog as wait().
+  uint32_t wait_plan(uint32_t need, hipStream_t s) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto deadline = t0 + std::chrono::duration<double>(tune.timeout_s);
+    for (uint64_t spin = 0;; ++spin) {
+      const uint32_t w = __atomic_load_n(h_plan, __ATOMIC_ACQUIRE);
+      if ((w >> 8) >= need + 1) return w;
+      if ((spin & 1023) == 1023) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) {  // drained without planning that round: it was never enqueued
+          const uint32_t w2 = __atomic_load_n(h_plan, __ATOMIC_ACQUIRE);
+          if ((w2 >> 8) >= need + 1) return w2;
+          throw Error("dist: stream drained before round " + std::to_string(need) + " was planned");
+        }
+        if (e != hipErrorNotReady) HIP_CHECK(e);
+        comm->check();
+        const auto now = std::chrono::steady_clock::now();
+        if (now > deadline) {
+          comm->abort();
+          throw Error("dist: rank " + std::to_string(rank) + " waited " + std::to_string(tune.timeout_s) +
+                      " s for round " + std::to_string(need) + " (peer failure or hang); communicator aborted");
+        }
       }
     }
   }
@@ -1273,6 +1308,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
 
+  __atomic_store_n(h_plan, 0u, __ATOMIC_RELEASE);  // round numbers restart per search
   HIP_CHECK(hipEventRecord(ev_t0, cs));
   k_seed<<<1, 64, 0, cs>>>(V, src, dst);
   comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
@@ -1323,7 +1359,18 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
     const bool hubs = spec_cap > kSpecHubCap;
     const unsigned hx = std::min<unsigned>((unsigned)cus, spec_cap / kThreads + 1);
-    for (int k = 0; k < K; ++k) {
+    // Rolling lookahead: round `it` is enqueued once the plan of round it - K
+    // is visible in pinned memory (no stream sync); enqueueing stops at the
+    // first observed plan that is not "run" (done, no path or stalled), so at
+    // most ~K no-op rounds trail the end of a search.
+    const uint32_t first = it;
+    for (int k = 0;; ++k) {
+      if (k >= K) {
+        const uint32_t w = wait_plan(it - (uint32_t)K, cs);
+        stats.plan_polls++;
+        if (((w >> 2) & 3u) != kRun) break;
+      }
+      if ((uint64_t)(it - first) > 4ull * n + 16) break;  // safety net
       maybe_fault((int)it);
       k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, spec_cap, k == 0 ? flags : 0,
                                                       hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1);
@@ -1504,6 +1551,7 @@ DistBiBfs::~DistBiBfs() {
   p_->comm.reset();
   (void)hipHostFree(p_->h_red);
   (void)hipHostFree(p_->h_ctl);
+  (void)hipHostFree(p_->h_plan);
   if (p_->h_walk) (void)hipHostFree(p_->h_walk);
   for (auto e : p_->ev_pre) (void)hipEventDestroy(e);
   (void)hipEventDestroy(p_->ev_round);

@@ -58,6 +58,7 @@ struct DistLevelStats {
   int count_syncs = 0;             // extra host round trips to size a candidate exchange
   int host_syncs = 0;              // host waits on the device in this search (all causes)
   int spec_rounds = 0;             // rounds enqueued speculatively (incl. no-op tails after the end)
+  int plan_polls = 0;              // lookahead waits on the pinned plan word (no stream sync)
   int host_rounds = 0;             // rounds planned on the host (dense levels, oversized exchanges)
   int collectives = 0;             // RCCL calls issued (allgather + allreduce)
   uint64_t exchanged_bytes = 0;    // bytes this rank received from allgathers
@@ -69,7 +70,7 @@ struct DistLevelStats {
 // Knobs of the partitioned engine (defaults are the production settings; the
 // small-capacity ones exist so tests can force every exchange branch).
 struct DistTuning {
-  int spec_rounds = 4;             // rounds enqueued per host wait (0 = plan every round on the host)
+  int spec_rounds = 3;             // lookahead: rounds enqueued ahead of the last plan the host saw (0 = host plans every round)
   uint32_t spec_cap_max = 1u << 16;  // largest per-rank candidate block of a speculative round (pairs)
   uint32_t cap = 0;                // per-rank candidate block of a host-planned round (0 = min(2^20, n))
   uint64_t nosync_bytes = 1u << 20;  // host-planned round: size the exchange from host bounds up to this

@@ -70,6 +70,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["count_syncs"] = s.count_syncs;
   d["host_syncs"] = s.host_syncs;
   d["spec_rounds"] = s.spec_rounds;
+  d["plan_polls"] = s.plan_polls;
   d["host_rounds"] = s.host_rounds;
   d["collectives"] = s.collectives;
   d["path_collectives"] = s.path_collectives;
