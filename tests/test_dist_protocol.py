@@ -91,3 +91,22 @@ def test_partitioned_protocol_matches_oracle(world):
             assert ok, (spec, s, d, why)
         dense += dense_l
     assert dense > 0  # the bottom-up exchange was exercised
+
+
+def test_round_spec_hops_match_oracle():
+    """The protocol spec itself: its hop count is the BFS distance, every
+    policy, including unreachable pairs and src == dst."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from dist_round_spec import round_trace
+
+    for spec in ("gnp:3000::3", "rmat:4096:40000:2"):
+        g = bb.from_spec(spec)
+        for s, d in _pairs(g.n, 12, 9) + [(5, 5)]:
+            o = native.bfs_oracle(g.csr, s, d)
+            for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False}):
+                trace, hops = round_trace(g.csr, s, d, **kw)
+                assert hops == (o.hops if o.found else -1), (spec, s, d, kw)
+                if s != d:
+                    assert trace and trace[0][1] == 0  # first expansion starts at depth 0
