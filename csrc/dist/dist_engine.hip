@@ -38,6 +38,7 @@
 // In a host-planned lockstep round side S's exchange + post run on the comm
 // stream while side T's pre runs on the compute stream.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <thread>
@@ -69,6 +70,7 @@ constexpr uint64_t kNoHubs = ~0ull;
 constexpr int kHubTile = 1024;                  // hubs staged in LDS per pass
 constexpr uint32_t kSpecHubCap = 4096;          // speculative blocks up to this size skip the hub pass
 constexpr uint32_t kTraceCap = 4096;            // rounds recorded with SearchOptions::trace
+constexpr uint32_t kPlanRing = 64;              // pinned per-round plan words (lookahead < this)
 
 // Search control state: identical on every rank (computed from reduced
 // values only).  Double-buffered by round parity: round `it` reads
@@ -151,7 +153,7 @@ struct DView {
   int P;
   DState* st;
   Ctl* ctl;                   // [2]
-  uint32_t* plan_word;        // pinned: ((it + 1) << 8) | state << 2 | sides of the latest planned round
+  uint32_t* plan_ring;        // pinned [kPlanRing]: slot it % kPlanRing = ((it + 1) << 8) | state << 2 | sides
   struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
   uint32_t trace_cap;
   Reduced* red;               // [2]
@@ -433,9 +435,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
     V.red[p].meetkey = kNoKey;
-    // one 4-byte write-through store: the host paces its enqueueing on it
-    __hip_atomic_store(V.plan_word, ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+    // one 4-byte write-through store per round: the host paces its enqueueing on it
+    __hip_atomic_store(&V.plan_ring[it % kPlanRing], ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int s = blockIdx.y;
   if ((c.sides >> s) & 1)
@@ -958,7 +960,7 @@ struct DistBiBfs::Impl {
   RoundRec* d_trace = nullptr;
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
-  uint32_t* h_plan = nullptr;  // pinned plan word (k_spec_expand)
+  uint32_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
   uint32_t* h_walk = nullptr;  // pinned
   size_t h_walk_cap = 0;
   double* d_scalar = nullptr;
@@ -985,9 +987,9 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipEventCreate(&ev_t1));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl), sizeof(Ctl), hipHostMallocDefault));
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), 64, hipHostMallocDefault));
-    *h_plan = 0;
-    V.plan_word = h_plan;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 4, hipHostMallocDefault));
+    std::memset(h_plan, 0, kPlanRing * 4);
+    V.plan_ring = h_plan;
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
@@ -1132,19 +1134,21 @@ struct DistBiBfs::Impl {
     }
   }
 
-  // Spin until the device has planned round `need` (the pinned plan word);
-  // returns the word.  Same watchdog as wait().
+  // Spin until the device has planned round `need` and return ITS plan word
+  // (the per-round ring slot, so every rank stops enqueueing after the same
+  // round however far its GPU has progressed).  Same watchdog as wait().
   uint32_t wait_plan(uint32_t need, hipStream_t s) {
     const auto t0 = std::chrono::steady_clock::now();
     const auto deadline = t0 + std::chrono::duration<double>(tune.timeout_s);
+    const uint32_t* slot = &h_plan[need % kPlanRing];
     for (uint64_t spin = 0;; ++spin) {
-      const uint32_t w = __atomic_load_n(h_plan, __ATOMIC_ACQUIRE);
-      if ((w >> 8) >= need + 1) return w;
+      const uint32_t w = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+      if ((w >> 8) == need + 1) return w;
       if ((spin & 1023) == 1023) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) {  // drained without planning that round: it was never enqueued
-          const uint32_t w2 = __atomic_load_n(h_plan, __ATOMIC_ACQUIRE);
-          if ((w2 >> 8) >= need + 1) return w2;
+          const uint32_t w2 = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+          if ((w2 >> 8) == need + 1) return w2;
           throw Error("dist: stream drained before round " + std::to_string(need) + " was planned");
         }
         if (e != hipErrorNotReady) HIP_CHECK(e);
@@ -1308,7 +1312,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
 
-  __atomic_store_n(h_plan, 0u, __ATOMIC_RELEASE);  // round numbers restart per search
+  std::memset(h_plan, 0, kPlanRing * 4);  // round numbers restart per search
+  std::atomic_thread_fence(std::memory_order_seq_cst);
   HIP_CHECK(hipEventRecord(ev_t0, cs));
   k_seed<<<1, 64, 0, cs>>>(V, src, dst);
   comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
@@ -1317,7 +1322,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   uint32_t spec_cap = kSpecCapMin;
   int flags = 0;
   bool have_ctl = false;  // h_ctl describes the current device state
-  const int K = std::max(0, tune.spec_rounds);
+  const int K = std::min<int>(std::max(0, tune.spec_rounds), (int)kPlanRing - 1);
   const bool host_only = K == 0;  // A/B mode: every round planned on the host
   const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
   if (host_only) {
