@@ -153,7 +153,7 @@ struct DView {
   int P;
   DState* st;
   Ctl* ctl;                   // [2]
-  uint32_t* plan_ring;        // pinned [kPlanRing]: slot it % kPlanRing = ((it + 1) << 8) | state << 2 | sides
+  uint64_t* plan_ring;        // pinned [kPlanRing]: slot it % kPlanRing = fed_max << 32 | (it + 1) << 8 | state << 2 | sides
   struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
   uint32_t trace_cap;
   Reduced* red;               // [2]
@@ -435,9 +435,13 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
     V.red[p].meetkey = kNoKey;
-    // one 4-byte write-through store per round: the host paces its enqueueing on it
-    __hip_atomic_store(&V.plan_ring[it % kPlanRing], ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // one 8-byte write-through store per round: the host paces its enqueueing
+    // on the plan and sizes the rounds it enqueues from the frontier (larger
+    // side's edge count, clamped to 32 bits)
+    const unsigned long long fm = min(max(c.fed[0], c.fed[1]), 0xffffffffull);
+    __hip_atomic_store(&V.plan_ring[it % kPlanRing],
+                       (uint64_t)fm << 32 | ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int s = blockIdx.y;
   if ((c.sides >> s) & 1)
@@ -960,7 +964,7 @@ struct DistBiBfs::Impl {
   RoundRec* d_trace = nullptr;
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
-  uint32_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
+  uint64_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
   uint32_t* h_walk = nullptr;  // pinned
   size_t h_walk_cap = 0;
   double* d_scalar = nullptr;
@@ -987,8 +991,8 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipEventCreate(&ev_t1));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl), sizeof(Ctl), hipHostMallocDefault));
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 4, hipHostMallocDefault));
-    std::memset(h_plan, 0, kPlanRing * 4);
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 8, hipHostMallocDefault));
+    std::memset(h_plan, 0, kPlanRing * 8);
     V.plan_ring = h_plan;
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
@@ -1137,18 +1141,19 @@ struct DistBiBfs::Impl {
   // Spin until the device has planned round `need` and return ITS plan word
   // (the per-round ring slot, so every rank stops enqueueing after the same
   // round however far its GPU has progressed).  Same watchdog as wait().
-  uint32_t wait_plan(uint32_t need, hipStream_t s) {
+  uint64_t wait_plan(uint32_t need, hipStream_t s) {
     const auto t0 = std::chrono::steady_clock::now();
     const auto deadline = t0 + std::chrono::duration<double>(tune.timeout_s);
-    const uint32_t* slot = &h_plan[need % kPlanRing];
+    const uint64_t* slot = &h_plan[need % kPlanRing];
+    const uint64_t tag = (need + 1u) & 0xffffffu;
     for (uint64_t spin = 0;; ++spin) {
-      const uint32_t w = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
-      if ((w >> 8) == need + 1) return w;
+      const uint64_t w = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+      if (((w >> 8) & 0xffffffu) == tag) return w;
       if ((spin & 1023) == 1023) {
         const hipError_t e = hipStreamQuery(s);
         if (e == hipSuccess) {  // drained without planning that round: it was never enqueued
-          const uint32_t w2 = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
-          if ((w2 >> 8) == need + 1) return w2;
+          const uint64_t w2 = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
+          if (((w2 >> 8) & 0xffffffu) == tag) return w2;
           throw Error("dist: stream drained before round " + std::to_string(need) + " was planned");
         }
         if (e != hipErrorNotReady) HIP_CHECK(e);
@@ -1312,7 +1317,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
 
-  std::memset(h_plan, 0, kPlanRing * 4);  // round numbers restart per search
+  std::memset(h_plan, 0, kPlanRing * 8);  // round numbers restart per search
   std::atomic_thread_fence(std::memory_order_seq_cst);
   HIP_CHECK(hipEventRecord(ev_t0, cs));
   k_seed<<<1, 64, 0, cs>>>(V, src, dst);
@@ -1354,46 +1359,65 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         continue;
       }
     }
-    // ---- K speculative sparse rounds, then one host wait
+    // ---- speculative sparse rounds with a rolling lookahead
     TraceRange batch_range("dist:speculative_batch");
-    const unsigned bx = std::min<unsigned>(
-        (unsigned)cus * 2, std::max<unsigned>(1, (unsigned)((uint64_t)spec_cap / P / kThreads) + 1));
-    const unsigned cx = std::min<unsigned>((unsigned)cus * 2, std::max<unsigned>(1, spec_cap / kThreads / 4 + 1));
-    const uint64_t gather_bytes = 2 * block_words(spec_cap) * 4;
-    // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
-    // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
-    const bool hubs = spec_cap > kSpecHubCap;
-    const unsigned hx = std::min<unsigned>((unsigned)cus, spec_cap / kThreads + 1);
     // Rolling lookahead: round `it` is enqueued once the plan of round it - K
     // is visible in pinned memory (no stream sync); enqueueing stops at the
-    // first observed plan that is not "run" (done, no path or stalled), so at
-    // most ~K no-op rounds trail the end of a search.
+    // first such plan that is not "run" (done, no path or stalled), so about K
+    // no-op rounds trail the end of a search.  Each round's block capacity is
+    // predicted from the frontier sizes of the plans seen so far (growth per
+    // round, extrapolated K rounds), so a growing frontier rarely stalls the
+    // lookahead.  Plans and frontier sizes are reduced values, identical on
+    // every rank: every rank enqueues the same rounds with the same sizes.
     const uint32_t first = it;
+    uint32_t cap_it = spec_cap;
+    uint64_t f_prev = 0;
     for (int k = 0;; ++k) {
       if (k >= K) {
-        const uint32_t w = wait_plan(it - (uint32_t)K, cs);
+        const uint32_t need = it - (uint32_t)K;
+        const uint64_t w = wait_plan(need, cs);
         stats.plan_polls++;
         if (((w >> 2) & 3u) != kRun) break;
+        const uint64_t f = w >> 32;
+        uint64_t g = 2;  // growth per round; x2 until two plans are seen
+        if (f_prev) g = std::min<uint64_t>(8, std::max<uint64_t>(1, (f + f_prev - 1) / f_prev));
+        uint64_t pred = f;
+        for (int j = 0; j < K && pred < spec_max; ++j) pred *= g;
+        cap_it = std::max<uint32_t>(cap_it, std::min<uint32_t>(spec_max, next_pow2(std::min<uint64_t>(pred + pred / 2, spec_max))));
+        f_prev = f;
       }
       if ((uint64_t)(it - first) > 4ull * n + 16) break;  // safety net
+      const unsigned bx = std::min<unsigned>(
+          (unsigned)cus * 2, std::max<unsigned>(1, (unsigned)((uint64_t)cap_it / P / kThreads) + 1));
+      const unsigned cx = std::min<unsigned>((unsigned)cus * 2, std::max<unsigned>(1, cap_it / kThreads / 4 + 1));
+      const uint64_t gather_bytes = 2 * block_words(cap_it) * 4;
+      // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
+      // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
+      const bool hubs = cap_it > kSpecHubCap;
+      const unsigned hx = std::min<unsigned>((unsigned)cus, cap_it / kThreads + 1);
       maybe_fault((int)it);
-      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, spec_cap, k == 0 ? flags : 0,
+      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
                                                       hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1);
-      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, spec_cap);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it);
       HIP_CHECK(hipGetLastError());
-      comm->allgather(V.sendbuf, V.recvbuf, gather_bytes, cs);
-      k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, spec_cap);
+      if (P > 1) {  // one rank owns every vertex: expand claimed them all, the blocks are empty
+        comm->allgather(V.sendbuf, V.recvbuf, gather_bytes, cs);
+        k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, cap_it);
+      }
       k_meet_end<<<std::min<unsigned>(bx, 64), kThreads, 0, cs>>>(V, it);
       HIP_CHECK(hipGetLastError());
-      comm->group_begin();
-      comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
-      comm->allreduce(&V.red[it & 1].meetkey, 1, DType::kU64, ROp::kMin, cs);
-      comm->group_end();
-      stats.collectives += 3;
-      stats.exchanged_bytes += gather_bytes * P;
+      if (P > 1) {  // a one-rank reduction is the identity
+        comm->group_begin();
+        comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
+        comm->allreduce(&V.red[it & 1].meetkey, 1, DType::kU64, ROp::kMin, cs);
+        comm->group_end();
+        stats.collectives += 3;
+        stats.exchanged_bytes += gather_bytes * P;
+      }
       stats.spec_rounds++;
       ++it;
     }
+    spec_cap = cap_it;
     flags = 0;
     k_final<<<1, 64, 0, cs>>>(V, it++, pol, h_ctl, kPlanAccountOnly);
     HIP_CHECK(hipGetLastError());

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -84,6 +85,12 @@ constexpr bool kRegRounds = BIBFS_KNOB_REG_ROUNDS;
 #define BIBFS_KNOB_REG_SLOTS 1
 #endif
 constexpr uint32_t kRegSlots = BIBFS_KNOB_REG_SLOTS;
+// 1 = lockstep rounds of up to kLdsThreads frontier edges run on EVERY wave
+// with one LDS-only barrier per round (wave_rounds); 0 = the wave-0 rounds.
+#ifndef BIBFS_KNOB_WAVE_ROUNDS
+#define BIBFS_KNOB_WAVE_ROUNDS 1
+#endif
+constexpr bool kWaveRounds = BIBFS_KNOB_WAVE_ROUNDS;
 // Resident server: the mailbox diagnostics (stage / seen / poll latency) are
 // system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
 // issued them, its first global load of the search would wait for their PCIe
@@ -920,9 +927,173 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
   };
 
+  // ---- all-wave lockstep rounds (bitmap mode, 32-bit offsets, packed
+  // adjacency; both frontiers together <= kLdsThreads edges).  Every lane takes
+  // one edge -- side 0's on the first waves, side 1's from the next wave
+  // boundary, so each wave serves one side and the side is a scalar: one
+  // packed-adjacency load, the bitmap claim with the opposite-side word read
+  // in flight beside it, then a DPP degree scan and ONE packed LDS atomic per
+  // wave that places its new vertices and their edge records.  One barrier per round, LDS-only: the
+  // parent / queue stores to global memory are never waited for inside the
+  // rounds (vmcnt), only before the path walk.  The round counters rotate over
+  // three slots, so the barrier that publishes slot r also orders the reset of
+  // slot r + 2 after every read of it (round r - 1's).  The search state is
+  // replicated: every thread reads the same counters and applies the same
+  // update, and the state is written back to s0/s1 for the wave-0 schedule
+  // when the phase ends (meet, dead side, a round above kLdsThreads edges or
+  // a record buffer overflow).
+  __shared__ unsigned long long wctr[3][2];  // [slot][side]: (count << 32) | edge sum
+  __shared__ unsigned long long wmeet[3];    // [slot]: min (len << 32 | side << 31 | vertex)
+  auto wave_rounds = [&]() {
+    if constexpr (!std::is_same<OffT, uint32_t>::value || !kBm || !kWaveRounds) {
+      return;
+    } else {
+      if (!P.padj || !P.lockstep || (P.trace && !kStamp) || s0.ovf || s1.ovf) return;  // uniform
+      uint32_t E0 = (uint32_t)s0.fed, E1 = (uint32_t)s1.fed;
+      uint32_t d0 = (uint32_t)s0.depth, d1 = (uint32_t)s1.depth;
+      uint32_t qe0 = s0.qend, qe1 = s1.qend, c0 = s0.cnt, c1 = s1.cnt, h0 = s0.hcnt, h1 = s1.hcnt;
+      unsigned long long v0 = s0.ved, v1 = s1.ved;
+      uint32_t a0 = s0.cur, o0 = s0.off, a1 = s1.cur, o1 = s1.off;  // current records
+      uint32_t* const par0 = P.b.parent[0];
+      uint32_t* const par1 = P.b.parent[1];
+      uint32_t* const que0 = P.b.queue[0];
+      uint32_t* const que1 = P.b.queue[1];
+      unsigned long long* const W0 = W(0);
+      unsigned long long* const W1 = W(1);
+      const uint4* const padj = P.padj;
+      if (tid < 6) wctr[tid >> 1][tid & 1] = 0;
+      if (tid < 3) wmeet[tid] = ~0ull;
+      __syncthreads();
+      uint32_t slot = 0, rounds_done = 0;
+      bool ovf = false;
+      for (;;) {
+        const uint32_t ET = E0 + E1;
+        const uint32_t S1 = (E0 + kWave - 1) & ~(uint32_t)(kWave - 1);
+        if (status != kRunning || ovf || E0 == 0 || E1 == 0 || S1 + E1 > (uint32_t)kLdsThreads) break;
+        unsigned long long lt0 = 0, lt1 = 0, lsub = 0;  // kStamp: round start / work done / sub-phases
+        if constexpr (kStamp) lt0 = stamp();
+        auto sub = [&](int k) {  // kStamp: cycles since the previous mark into 16-bit field k
+          if constexpr (kStamp) {
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+            const unsigned long long t = stamp();
+            lsub |= min(t - (k ? lt1 : lt0), 0xffffull) << (16 * k);
+            lt1 = t;
+          }
+        };
+        const uint32_t used = (1u << a0) | (1u << a1);
+        const uint32_t nb0 = (uint32_t)__builtin_ctz(~used & 0xfu);
+        const uint32_t nb1 = (uint32_t)__builtin_ctz(~(used | (1u << nb0)) & 0xfu);
+        // side 0's edges on threads [0, E0), side 1's from the next wave boundary
+        // S1: every wave works for ONE side, so the side is a scalar and a
+        // wave needs one ballot, one scan and one counter atomic
+        const uint32_t wv = uni((uint32_t)tid >> 6);
+        const bool sd = wv * kWave >= S1;
+        const uint32_t Es = sd ? E1 : E0;
+        const uint32_t first = wv * kWave - (sd ? S1 : 0u);  // this wave's first edge of its side
+        if (first < Es) {  // wave-uniform: waves past the lists only join the barrier
+          const uint32_t e = first + lane;
+          const bool ok = e < Es;
+          const Rec r = (sd ? &R[a1][o1] : &R[a0][o0])[ok ? e : 0u];
+          sub(0);
+          const uint4 pq = padj[min(r.y, P.nnz_m1)];
+          const uint32_t v = pq.x, dg = pq.y, ob = pq.z;
+          sub(1);
+          const uint32_t a = (sd ? d1 : d0) + 1;  // claim depth on this side
+          const uint32_t bo = sd ? d0 : d1;       // opposite frontier depth (lockstep: parity rule)
+          const uint32_t bit = v & 31u;
+          unsigned long long old = ~0ull;
+          if (ok) old = atomicOr(&(sd ? W1 : W0)[v >> 5], 1ull << (bit + ((a & 1u) << 5)));
+          const unsigned long long w = (sd ? W0 : W1)[v >> 5];  // in flight with the claim
+          const bool isnew = ((old >> bit) & 0x100000001ull) == 0;
+          const uint32_t f = (uint32_t)((w >> bit) & 1ull) | ((uint32_t)((w >> (32 + bit)) & 1ull) << 1);
+          unsigned long long best = ~0ull;
+          if (isnew && f != 0) {
+            const uint32_t dob = (f == 3 || (f - 1) == (bo & 1u)) ? bo : bo + 1;
+            best = ((unsigned long long)(a + dob) << 32) | ((sd ? 1ull : 0ull) << 31) | v;
+          }
+          sub(2);
+          if (__ballot(best != ~0ull)) {  // the meeting round only
+            unsigned long long m = best;
+            for (int off = 32; off >= 1; off >>= 1) {
+              const unsigned long long y = __shfl_xor(m, off);
+              m = y < m ? y : m;
+            }
+            if (lane == 0) atomicMin(&wmeet[slot], m);
+          }
+          const unsigned long long mask = __ballot(isnew);
+          if (mask) {
+            const uint32_t dc = isnew ? min(dg, kDegClamp) : 0u;
+            const uint32_t incl = wave_incl_scan(dc);
+            const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+            unsigned long long pos = 0;
+            if (lane == 0) pos = atomicAdd(&wctr[slot][sd ? 1 : 0], ((unsigned long long)__popcll(mask) << 32) | tot);
+            const uint32_t be = __builtin_amdgcn_readlane((uint32_t)pos, 0);
+            const uint32_t bn = __builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0);
+            const uint32_t eb = be + incl - dc;
+            sub(3);
+            if (isnew) {
+              const uint32_t qi = (sd ? qe1 : qe0) + bn + mbcnt64(mask);
+              (sd ? par1 : par0)[v] = r.x;
+              if (qi < P.n) (sd ? que1 : que0)[qi] = v;
+            }
+            append_records(sd ? R[nb1] : R[nb0], isnew && eb + dg <= CAP ? dg : 0u, eb, v, ob);
+          }
+        }
+        if constexpr (kStamp) lt1 = stamp();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS-only: stores stay in flight
+        const unsigned long long p0 = wctr[slot][0], p1 = wctr[slot][1], mk = wmeet[slot];
+        const uint32_t sn = slot == 2 ? 0u : slot + 1, sr = sn == 2 ? 0u : sn + 1;
+        if (tid < 2) wctr[sr][tid] = 0;
+        if (tid == 2) wmeet[sr] = ~0ull;
+        const uint32_t n0 = uni((uint32_t)(p0 >> 32)), l0 = uni((uint32_t)p0);
+        const uint32_t n1 = uni((uint32_t)(p1 >> 32)), l1 = uni((uint32_t)p1);
+        const uint32_t mk_hi = uni((uint32_t)(mk >> 32)), mk_lo = uni((uint32_t)mk);
+        if (mk_hi != 0xffffffffu && (meet == kEmpty || mk_hi < md0 + md1)) {
+          const uint32_t side = mk_lo >> 31;
+          const uint32_t a = (side ? d1 : d0) + 1;
+          meet = mk_lo & kIdMask;
+          md0 = side ? mk_hi - a : a;
+          md1 = side ? a : mk_hi - a;
+        }
+        if constexpr (kStamp) {
+          if (tid == 0 && levels + 1 < P.b.trace_cap) {
+            LevelTraceDev& t = P.b.trace[levels + 1];
+            const unsigned long long lt2 = stamp();
+            t.side = (uint32_t)(lt2 - lt0);
+            t.depth = (uint32_t)(lt1 - lt0);
+            t.frontier = (uint32_t)(lt2 - lt1);
+            t.mode = 8;
+            t.edges = ET;
+            t.discovered = lsub;
+          }
+        }
+        levels += 2;
+        einsp += ET;
+        ++rounds_done;
+        ++d0, ++d1;
+        qe0 += n0, qe1 += n1;
+        h0 += n0, h1 += n1;
+        c0 = n0, c1 = n1;
+        v0 += l0, v1 += l1;
+        E0 = l0, E1 = l1;
+        a0 = nb0, o0 = 0, a1 = nb1, o1 = 0;
+        ovf = l0 > CAP || l1 > CAP;
+        if (meet != kEmpty) status = kFound;
+        else if (n0 == 0 || n1 == 0) status = kNoPath;
+        slot = sn;
+      }
+      if (rounds_done == 0) return;
+      s0.cur = a0, s0.off = o0, s0.fed = E0, s0.depth = (int)d0, s0.fbeg = qe0 - c0, s0.qend = qe0;
+      s0.cnt = c0, s0.hcnt = h0, s0.ved = v0, s0.ovf = E0 > CAP ? 1u : 0u;
+      s1.cur = a1, s1.off = o1, s1.fed = E1, s1.depth = (int)d1, s1.fbeg = qe1 - c1, s1.qend = qe1;
+      s1.cnt = c1, s1.hcnt = h1, s1.ved = v1, s1.ovf = E1 > CAP ? 1u : 0u;
+    }
+  };
+
   unsigned long long clk0 = 0;
   const unsigned long long rt0 = tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
+  wave_rounds();  // every wave; the replicated state continues below
   uint32_t fstatus = kRunning;
   for (;;) {
     if (wid == 0) {
@@ -1322,7 +1493,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_batch(LdsParams<OffT> P,
 // stop word, or `idle_ticks` of s_memrealtime (100 MHz) without a request --
 // every wave reaches the exit through the same barrier, so the grid drains
 // even if the host process is gone.
-template <typename OffT, bool kBm>
+template <typename OffT, bool kBm, bool kStamp = false>
 __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P, ServerBox* box,
                                                               uint32_t last_seq, unsigned long long idle_ticks) {
   // Every branch that encloses a barrier is made provably wave-uniform
@@ -1402,10 +1573,10 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
     Q.dst = min(uni(cmd[3]), P.n - 1);
     Q.side_policy = (int)uni(cmd[4]);
     Q.lockstep = (int)uni(cmd[5]);
-    Q.trace = 0;
+    Q.trace = kStamp ? 2 : 0;  // kStamp: BIBFS_STAMP_SERVER profiling build of the server
     last_seq = Q.seq;
     __syncthreads();  // every wave has read cmd before thread 0 may overwrite it
-    lds_search_body<OffT, false, kBm>(Q, true);
+    lds_search_body<OffT, kStamp, kBm>(Q, true);
     if (tid == kDiagTid) __hip_atomic_store(&box->stage, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (tid == 0) {
@@ -1998,7 +2169,10 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, d
   BIBFS_REQUIRE(g.row_off32 != nullptr, "resident server: 32-bit row offsets required");
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
-  if (g.n <= kBmMaxN)
+  static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
+  if (g.n <= kBmMaxN && stamp)
+    k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
+  else if (g.n <= kBmMaxN)
     k_lds_server<uint32_t, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
   else
     k_lds_server<uint32_t, false><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);

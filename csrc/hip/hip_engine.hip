@@ -819,7 +819,9 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   if (!grid) {
     const int tr = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
     const int lock = (opt.lockstep && I.n <= 0x7fffffffu) ? 1 : 0;
-    if (I.resident && !opt.trace && I.server_usable()) {
+    // BIBFS_STAMP_SERVER: the server's profiling build answers traced queries too
+    static const bool stamp_srv = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
+    if (I.resident && (!opt.trace || stamp_srv) && I.server_usable()) {
       I.server_query(src, dst, opt, seq);
       if (I.dbg())
         std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",

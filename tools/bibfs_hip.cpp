@@ -18,6 +18,7 @@ static const char* bibfs_mode_name(int m) {
     case 5: return "grid-bottomup";
     case 6: return "lds-lean";
     case 7: return "reg-lockstep";
+    case 8: return "wave-lockstep";
     default: return "cpu";
   }
 }
@@ -90,6 +91,13 @@ int main(int argc, char** argv) {
                         t.side, (unsigned long long)(t.edges & 0xffffffffu), t.depth,
                         (unsigned long long)(t.frontier & 0xffff), (unsigned long long)(t.frontier >> 16),
                         (unsigned long long)(t.edges >> 32));
+          else if (t.mode == 8)  // all-wave lockstep round
+            std::printf("Stamp cycles: wave round=%d edges=%llu work=%d barrier+book=%llu | rec=%llu load=%llu "
+                        "claim=%llu scan+place=%llu\n", t.side, (unsigned long long)t.edges, t.depth,
+                        (unsigned long long)t.frontier, (unsigned long long)(t.discovered & 0xffff),
+                        (unsigned long long)((t.discovered >> 16) & 0xffff),
+                        (unsigned long long)((t.discovered >> 32) & 0xffff),
+                        (unsigned long long)(t.discovered >> 48));
           else if (t.mode == 1 || t.mode == 2)  // wave rounds: phase split of wave 0 / the working wave
             std::printf("Stamp cycles: %s round=%d barrier_wait=%d rec+col=%llu row_off=%llu claim=%llu append=%llu\n",
                         bibfs_mode_name(t.mode), t.side, t.depth, (unsigned long long)(t.edges & 0xffff),
