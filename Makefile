@@ -67,6 +67,11 @@ gpu: $(LIB)/libbibfs.so $(GPU_TOOLS) $(BIN)/bibfs_cuda_only
 python: $(NATIVE_PY)
 micro: $(BIN)/lat_probe $(BIN)/mailbox_rtt
 
+# The LDS engine's counter atomics are already issued by one lane per wave:
+# the compiler's wave-reduction rewrite of them only adds instructions to the
+# latency-bound rounds.
+$(OBJ)/hip/engine_kernels.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+
 $(BIN)/mailbox_rtt: benchmarks/micro/mailbox_rtt.hip
 	@mkdir -p $(BIN)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 $< -o $@

@@ -91,6 +91,11 @@ constexpr uint32_t kRegSlots = BIBFS_KNOB_REG_SLOTS;
 #define BIBFS_KNOB_WAVE_ROUNDS 1
 #endif
 constexpr bool kWaveRounds = BIBFS_KNOB_WAVE_ROUNDS;
+// batches of 64 edges per wave in those rounds (1: frontiers up to 1024 edges, 2: 2048)
+#ifndef BIBFS_KNOB_WAVE_B
+#define BIBFS_KNOB_WAVE_B 2
+#endif
+constexpr uint32_t kWaveB = BIBFS_KNOB_WAVE_B;
 // Resident server: the mailbox diagnostics (stage / seen / poll latency) are
 // system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
 // issued them, its first global load of the search would wait for their PCIe
@@ -123,6 +128,10 @@ constexpr uint32_t kSmallEdges = BIBFS_KNOB_SMALL_EDGES;  // a level this small 
 constexpr uint32_t kDualEdges = BIBFS_KNOB_DUAL_EDGES;    // both sides together this small: one lockstep round
 constexpr uint32_t kDualBigEdges = 4096;                  // balanced sides up to this many edges: lockstep big level
 constexpr uint32_t kDegClamp = 65535;               // per-lane edge contribution to the packed counter
+// Bitmap mode with the all-wave rounds: smaller record buffers make room for
+// the LDS queue (vertex + parent's queue index per side) the path is walked on.
+constexpr uint32_t kCapBm = 1900;
+constexpr uint32_t kQCap = 2048;
 constexpr uint32_t kParity = 0x80000000u;           // depth-parity bit of a hash key
 constexpr uint32_t kIdMask = 0x7fffffffu;
 
@@ -281,9 +290,16 @@ struct LevelPlan {
 template <typename OffT, bool kStamp, bool kBm>
 __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool elected) {
   using Rec = typename LdsRec<OffT>::type;
-  constexpr uint32_t CAP = LdsRec<OffT>::cap;
+  constexpr bool kLq = kBm && kWaveRounds && std::is_same<OffT, uint32_t>::value;  // LDS queue + walk
+  constexpr uint32_t CAP = kLq ? kCapBm : LdsRec<OffT>::cap;
   __shared__ uint32_t H[2][kHashSize];
   __shared__ Rec R[4][CAP];
+  // kLq: per side, the vertices in claim (queue) order and each one's parent's
+  // queue index; a search that ends inside the all-wave rounds walks its path
+  // here instead of along the global parent arrays
+  __shared__ uint32_t LQ[kLq ? 2 : 1][kLq ? kQCap : 1];
+  __shared__ uint32_t LP[kLq ? 2 : 1][kLq ? kQCap : 1];
+  __shared__ uint32_t lq_meet[2];
   __shared__ unsigned long long ctr[2][2];  // big levels [slot][side]: (count << 32) | clamped edge sum
   __shared__ unsigned long long meetk[2];   // big levels [slot]: min (len << 32 | side << 31 | vertex)
   __shared__ LevelPlan plan;
@@ -341,7 +357,11 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
   };
   uint32_t* Hflat = &H[0][0];
-  for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) Hflat[i] = kBm ? 0u : kEmpty;
+  {
+    const uint32_t fill = kBm ? 0u : kEmpty;
+    uint4* H4 = reinterpret_cast<uint4*>(Hflat);
+    for (uint32_t i = tid; i < 2 * kHashSize / 4; i += kLdsThreads) H4[i] = make_uint4(fill, fill, fill, fill);
+  }
   // side q's bitmap view of the same LDS (kBm)
   auto W = [&](int q) { return reinterpret_cast<unsigned long long*>(q ? H[1] : H[0]); };
   if (tid < 4) ctr[tid >> 1][tid & 1] = 0;
@@ -369,10 +389,14 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     x.ved = one ? b.ved : a.ved;
     return x;
   };
+  // both endpoints' row offsets in flight together (the stores below would
+  // otherwise order side 1's loads after side 0's)
+  const OffT rb0 = P.row_off[P.src], re0 = P.row_off[P.src + 1];
+  const OffT rb1 = P.row_off[P.dst], re1 = P.row_off[P.dst + 1];
   auto init_side = [&](int q) {
     SideState x;
     const uint32_t r = q ? P.dst : P.src;
-    const OffT b = P.row_off[r], e = P.row_off[r + 1];
+    const OffT b = q ? rb1 : rb0, e = q ? re1 : re0;
     x.cur = (uint32_t)q;
     x.off = 0;
     x.cnt = 1;
@@ -401,14 +425,16 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   unsigned long long einsp = 0;
   int turn = 0;
   if (tid == 0) won = elected || ticket_old < P.seq;
-  __syncthreads();
+  // LDS-only barrier: the two global stores above are never read back in LDS
+  // mode before the final drain (a full __syncthreads waits for their acks)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (!uni(won)) return;  // uniform: a divergent-looking exit around barriers can be mis-structurized
   if (kStamp && tid == 0) e1 = __builtin_amdgcn_s_memtime();
   if (tid < 2) {  // depth 0: parity 0
     if constexpr (kBm) bm_claim(W(tid), tid ? P.dst : P.src, 0);
     else hash_insert(H[tid], tid ? P.dst : P.src, tid ? P.dst : P.src);
   }
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   auto fits = [&](const SideState& x) {
     return !x.ovf && (kBm || (unsigned long long)x.hcnt + x.fed <= kHashLimit);
@@ -928,24 +954,29 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   };
 
   // ---- all-wave lockstep rounds (bitmap mode, 32-bit offsets, packed
-  // adjacency; both frontiers together <= kLdsThreads edges).  Every lane takes
-  // one edge -- side 0's on the first waves, side 1's from the next wave
-  // boundary, so each wave serves one side and the side is a scalar: one
-  // packed-adjacency load, the bitmap claim with the opposite-side word read
-  // in flight beside it, then a DPP degree scan and ONE packed LDS atomic per
-  // wave that places its new vertices and their edge records.  One barrier per round, LDS-only: the
-  // parent / queue stores to global memory are never waited for inside the
-  // rounds (vmcnt), only before the path walk.  The round counters rotate over
-  // three slots, so the barrier that publishes slot r also orders the reset of
-  // slot r + 2 after every read of it (round r - 1's).  The search state is
-  // replicated: every thread reads the same counters and applies the same
-  // update, and the state is written back to s0/s1 for the wave-0 schedule
-  // when the phase ends (meet, dead side, a round above kLdsThreads edges or
-  // a record buffer overflow).
+  // adjacency; both frontiers together <= 2 x kLdsThreads edges).  The edges
+  // are cut into batches of 64, side 0's batches first; wave w takes batches
+  // w and w + 16, so every batch serves ONE side and the side is a scalar.
+  // Per batch: one packed-adjacency load, the bitmap claim with the
+  // opposite-side word read in flight beside it, then a DPP degree scan and
+  // ONE packed LDS atomic that places the batch's new vertices and their edge
+  // records.  One barrier per round, LDS-only.  The round
+  // counters rotate over three slots, so the barrier that publishes slot r
+  // also orders the reset of slot r + 2 after every read of it (round r - 1's).
+  // The search state is replicated: every thread reads the same counters and
+  // applies the same update.
+  // Records carry the PARENT'S QUEUE INDEX (not its id) and a claim lands only
+  // in the LDS queue (LQ: vertex, LP: parent's queue index) -- no global store
+  // at all -- so a search that ends here walks its path in LDS.  A phase that
+  // ends with the search still running (a round above 2 x kLdsThreads edges, a
+  // record or LDS-queue bound) writes the global queue and parent arrays from
+  // the LDS queue, rewrites the current records to vertex ids and hands the
+  // state to the wave-0 schedule through s0/s1.
   __shared__ unsigned long long wctr[3][2];  // [slot][side]: (count << 32) | edge sum
   __shared__ unsigned long long wmeet[3];    // [slot]: min (len << 32 | side << 31 | vertex)
+  bool lq_done = false;                      // replicated: the search ended inside wave_rounds
   auto wave_rounds = [&]() {
-    if constexpr (!std::is_same<OffT, uint32_t>::value || !kBm || !kWaveRounds) {
+    if constexpr (!kLq) {
       return;
     } else {
       if (!P.padj || !P.lockstep || (P.trace && !kStamp) || s0.ovf || s1.ovf) return;  // uniform
@@ -963,13 +994,19 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       const uint4* const padj = P.padj;
       if (tid < 6) wctr[tid >> 1][tid & 1] = 0;
       if (tid < 3) wmeet[tid] = ~0ull;
-      __syncthreads();
+      if (tid < 2) {  // depth 0: the endpoints at queue index 0
+        LQ[tid][0] = tid ? P.dst : P.src;
+        LP[tid][0] = kEmpty;
+      }
+      for (uint32_t i = tid; i < E0 + E1; i += kLdsThreads) {  // seed records: parent = queue index 0
+        if (i < E0) R[a0][o0 + i].x = 0u;
+        else R[a1][o1 + i - E0].x = 0u;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       uint32_t slot = 0, rounds_done = 0;
       bool ovf = false;
-      for (;;) {
-        const uint32_t ET = E0 + E1;
-        const uint32_t S1 = (E0 + kWave - 1) & ~(uint32_t)(kWave - 1);
-        if (status != kRunning || ovf || E0 == 0 || E1 == 0 || S1 + E1 > (uint32_t)kLdsThreads) break;
+      auto round = [&](auto bc, uint32_t nb0, uint32_t nbt, uint32_t x0, uint32_t x1) {
+        constexpr int B = decltype(bc)::value;
         unsigned long long lt0 = 0, lt1 = 0, lsub = 0;  // kStamp: round start / work done / sub-phases
         if constexpr (kStamp) lt0 = stamp();
         auto sub = [&](int k) {  // kStamp: cycles since the previous mark into 16-bit field k
@@ -980,66 +1017,101 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
             lt1 = t;
           }
         };
-        const uint32_t used = (1u << a0) | (1u << a1);
-        const uint32_t nb0 = (uint32_t)__builtin_ctz(~used & 0xfu);
-        const uint32_t nb1 = (uint32_t)__builtin_ctz(~(used | (1u << nb0)) & 0xfu);
-        // side 0's edges on threads [0, E0), side 1's from the next wave boundary
-        // S1: every wave works for ONE side, so the side is a scalar and a
-        // wave needs one ballot, one scan and one counter atomic
         const uint32_t wv = uni((uint32_t)tid >> 6);
-        const bool sd = wv * kWave >= S1;
-        const uint32_t Es = sd ? E1 : E0;
-        const uint32_t first = wv * kWave - (sd ? S1 : 0u);  // this wave's first edge of its side
-        if (first < Es) {  // wave-uniform: waves past the lists only join the barrier
-          const uint32_t e = first + lane;
-          const bool ok = e < Es;
-          const Rec r = (sd ? &R[a1][o1] : &R[a0][o0])[ok ? e : 0u];
-          sub(0);
+        if (wv >= nbt) return lsub;  // wave-uniform: no batch this round, only the barrier
+        bool act[B], sd[B], ok[B], isnew[B];
+        uint32_t u[B], v[B], dg[B], ob[B];
+        unsigned long long old[B], w[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {  // records -> packed adjacency loads, all in flight
+          const uint32_t bt = wv + (uint32_t)k * (kLdsThreads / kWave);
+          act[k] = bt < nbt;  // scalar
+          sd[k] = bt >= nb0;  // scalar
+          const uint32_t e = (bt - (sd[k] ? nb0 : 0u)) * kWave + lane;
+          ok[k] = act[k] && e < (sd[k] ? E1 : E0);
+          const Rec r = (sd[k] ? &R[a1][o1] : &R[a0][o0])[ok[k] ? e : 0u];
+          u[k] = r.x;
           const uint4 pq = padj[min(r.y, P.nnz_m1)];
-          const uint32_t v = pq.x, dg = pq.y, ob = pq.z;
-          sub(1);
-          const uint32_t a = (sd ? d1 : d0) + 1;  // claim depth on this side
-          const uint32_t bo = sd ? d0 : d1;       // opposite frontier depth (lockstep: parity rule)
-          const uint32_t bit = v & 31u;
-          unsigned long long old = ~0ull;
-          if (ok) old = atomicOr(&(sd ? W1 : W0)[v >> 5], 1ull << (bit + ((a & 1u) << 5)));
-          const unsigned long long w = (sd ? W0 : W1)[v >> 5];  // in flight with the claim
-          const bool isnew = ((old >> bit) & 0x100000001ull) == 0;
-          const uint32_t f = (uint32_t)((w >> bit) & 1ull) | ((uint32_t)((w >> (32 + bit)) & 1ull) << 1);
-          unsigned long long best = ~0ull;
-          if (isnew && f != 0) {
+          v[k] = pq.x;
+          dg[k] = pq.y;
+          ob[k] = pq.z;
+        }
+        sub(0);
+#pragma unroll
+        for (int k = 0; k < B; ++k) {  // claims, the opposite words beside them
+          const uint32_t a = (sd[k] ? d1 : d0) + 1;
+          const uint32_t bit = v[k] & 31u;
+          old[k] = ~0ull;
+          if (ok[k]) old[k] = atomicOr(&(sd[k] ? W1 : W0)[v[k] >> 5], 1ull << (bit + ((a & 1u) << 5)));
+          w[k] = (sd[k] ? W0 : W1)[v[k] >> 5];
+        }
+        unsigned long long best = ~0ull;
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          const uint32_t a = (sd[k] ? d1 : d0) + 1;
+          const uint32_t bo = sd[k] ? d0 : d1;  // opposite frontier depth (lockstep: parity rule)
+          const uint32_t bit = v[k] & 31u;
+          isnew[k] = ((old[k] >> bit) & 0x100000001ull) == 0;
+          const uint32_t f = (uint32_t)((w[k] >> bit) & 1ull) | ((uint32_t)((w[k] >> (32 + bit)) & 1ull) << 1);
+          if (isnew[k] && f != 0) {
             const uint32_t dob = (f == 3 || (f - 1) == (bo & 1u)) ? bo : bo + 1;
-            best = ((unsigned long long)(a + dob) << 32) | ((sd ? 1ull : 0ull) << 31) | v;
-          }
-          sub(2);
-          if (__ballot(best != ~0ull)) {  // the meeting round only
-            unsigned long long m = best;
-            for (int off = 32; off >= 1; off >>= 1) {
-              const unsigned long long y = __shfl_xor(m, off);
-              m = y < m ? y : m;
-            }
-            if (lane == 0) atomicMin(&wmeet[slot], m);
-          }
-          const unsigned long long mask = __ballot(isnew);
-          if (mask) {
-            const uint32_t dc = isnew ? min(dg, kDegClamp) : 0u;
-            const uint32_t incl = wave_incl_scan(dc);
-            const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
-            unsigned long long pos = 0;
-            if (lane == 0) pos = atomicAdd(&wctr[slot][sd ? 1 : 0], ((unsigned long long)__popcll(mask) << 32) | tot);
-            const uint32_t be = __builtin_amdgcn_readlane((uint32_t)pos, 0);
-            const uint32_t bn = __builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0);
-            const uint32_t eb = be + incl - dc;
-            sub(3);
-            if (isnew) {
-              const uint32_t qi = (sd ? qe1 : qe0) + bn + mbcnt64(mask);
-              (sd ? par1 : par0)[v] = r.x;
-              if (qi < P.n) (sd ? que1 : que0)[qi] = v;
-            }
-            append_records(sd ? R[nb1] : R[nb0], isnew && eb + dg <= CAP ? dg : 0u, eb, v, ob);
+            const unsigned long long key = ((unsigned long long)(a + dob) << 32) | ((sd[k] ? 1ull : 0ull) << 31) | v[k];
+            best = key < best ? key : best;
           }
         }
-        if constexpr (kStamp) lt1 = stamp();
+        sub(1);
+        if (__ballot(best != ~0ull)) {  // the meeting round only
+          unsigned long long m = best;
+          for (int off = 32; off >= 1; off >>= 1) {
+            const unsigned long long y = __shfl_xor(m, off);
+            m = y < m ? y : m;
+          }
+          if (lane == 0) atomicMin(&wmeet[slot], m);
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+          const unsigned long long mask = __ballot(isnew[k]);
+          if (!mask) continue;  // wave-uniform
+          const uint32_t dc = isnew[k] ? min(dg[k], kDegClamp) : 0u;
+          const uint32_t incl = wave_incl_scan(dc);
+          const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+          unsigned long long pos = 0;
+          if (lane == 0)
+            pos = atomicAdd(&wctr[slot][sd[k] ? 1 : 0], ((unsigned long long)__popcll(mask) << 32) | tot);
+          const uint32_t be = __builtin_amdgcn_readlane((uint32_t)pos, 0);
+          const uint32_t bn = __builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0);
+          const uint32_t eb = be + incl - dc;
+          const uint32_t qi = (sd[k] ? qe1 : qe0) + bn + mbcnt64(mask);  // < kQCap (round bound)
+          if (isnew[k]) {
+            (sd[k] ? LP[1] : LP[0])[qi] = u[k];
+            (sd[k] ? LQ[1] : LQ[0])[qi] = v[k];
+          }
+          append_records(sd[k] ? R[x1] : R[x0], isnew[k] && eb + dg[k] <= CAP ? dg[k] : 0u, eb, qi, ob[k]);
+        }
+        if constexpr (kStamp) {
+          sub(2);
+          lt0 = lt1;
+        }
+        return lsub;
+      };
+      for (;;) {
+        const uint32_t ET = E0 + E1;
+        const uint32_t nb0 = (E0 + kWave - 1) / kWave, nbt = nb0 + (E1 + kWave - 1) / kWave;
+        // every claim of the round must fit the LDS queue (a side claims at most E new vertices)
+        if (status != kRunning || ovf || E0 == 0 || E1 == 0 || nbt > kWaveB * (kLdsThreads / kWave) ||
+            qe0 + E0 > kQCap || qe1 + E1 > kQCap)
+          break;
+        const uint32_t used = (1u << a0) | (1u << a1);
+        const uint32_t x0 = (uint32_t)__builtin_ctz(~used & 0xfu);
+        const uint32_t x1 = (uint32_t)__builtin_ctz(~(used | (1u << x0)) & 0xfu);
+        unsigned long long rt0r = 0, lsub = 0;
+        if constexpr (kStamp) rt0r = stamp();
+        if (kWaveB == 1 || nbt <= (uint32_t)(kLdsThreads / kWave))
+          lsub = round(std::integral_constant<int, 1>{}, nb0, nbt, x0, x1);
+        else
+          lsub = round(std::integral_constant<int, (kWaveB > 1 ? 2 : 1)>{}, nb0, nbt, x0, x1);
+        unsigned long long rt1r = 0;
+        if constexpr (kStamp) rt1r = stamp();
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS-only: stores stay in flight
         const unsigned long long p0 = wctr[slot][0], p1 = wctr[slot][1], mk = wmeet[slot];
         const uint32_t sn = slot == 2 ? 0u : slot + 1, sr = sn == 2 ? 0u : sn + 1;
@@ -1058,10 +1130,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         if constexpr (kStamp) {
           if (tid == 0 && levels + 1 < P.b.trace_cap) {
             LevelTraceDev& t = P.b.trace[levels + 1];
-            const unsigned long long lt2 = stamp();
-            t.side = (uint32_t)(lt2 - lt0);
-            t.depth = (uint32_t)(lt1 - lt0);
-            t.frontier = (uint32_t)(lt2 - lt1);
+            const unsigned long long rt2r = stamp();
+            t.side = (uint32_t)(rt2r - rt0r);
+            t.depth = (uint32_t)(rt1r - rt0r);
+            t.frontier = (uint32_t)(rt2r - rt1r);
             t.mode = 8;
             t.edges = ET;
             t.discovered = lsub;
@@ -1076,11 +1148,34 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         c0 = n0, c1 = n1;
         v0 += l0, v1 += l1;
         E0 = l0, E1 = l1;
-        a0 = nb0, o0 = 0, a1 = nb1, o1 = 0;
+        a0 = x0, o0 = 0, a1 = x1, o1 = 0;
         ovf = l0 > CAP || l1 > CAP;
         if (meet != kEmpty) status = kFound;
         else if (n0 == 0 || n1 == 0) status = kNoPath;
         slot = sn;
+      }
+      if (status != kRunning) {
+        lq_done = true;  // the path is walked in LDS
+      } else {
+        // the wave-0 schedule continues: it needs the global queue and parent
+        // arrays (the hand-off, the global path walk) and records that carry
+        // parent ids -- both materialised here from the LDS queue
+        for (uint32_t i = tid; i < qe0 + qe1; i += kLdsThreads) {
+          const int q = i >= qe0;
+          const uint32_t j = q ? i - qe0 : i;
+          if (j == 0) continue;  // the endpoints: written by init_side
+          const uint32_t x = LQ[q][j];
+          (q ? par1 : par0)[x] = LQ[q][LP[q][j]];
+          if (j < P.n) (q ? que1 : que0)[j] = x;
+        }
+        for (uint32_t i = tid; i < E0 + E1; i += kLdsThreads) {
+          if (i < E0) {
+            if (o0 + i < CAP) R[a0][o0 + i].x = LQ[0][R[a0][o0 + i].x];
+          } else if (o1 + i - E0 < CAP) {
+            R[a1][o1 + i - E0].x = LQ[1][R[a1][o1 + i - E0].x];
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
       if (rounds_done == 0) return;
       s0.cur = a0, s0.off = o0, s0.fed = E0, s0.depth = (int)d0, s0.fbeg = qe0 - c0, s0.qend = qe0;
@@ -1321,9 +1416,18 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
 
   // search state is valid in wave 0; fstatus (from the final plan) in every wave
   HostResult* Rr = P.h.res;
-  // Parent stores of every wave must have reached L2 before the walkers'
-  // L1-bypassing loads read them.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (kLq && lq_done && status == kFound) {
+    // the meet vertex's queue index on each side: one parallel LDS search
+    for (uint32_t i = tid; i < s0.qend + s1.qend; i += kLdsThreads) {
+      const int q = i >= s0.qend;
+      const uint32_t j = q ? i - s0.qend : i;
+      if (j < kQCap && LQ[q][j] == meet) lq_meet[q] = j;
+    }
+  } else {
+    // Parent stores of every wave must have reached L2 before the walkers'
+    // L1-bypassing loads read them.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   __syncthreads();
   if (wid == 0) {
     const uint32_t hops = md0 + md1;
@@ -1336,9 +1440,24 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     uint32_t* pbuf = reinterpret_cast<uint32_t*>(&R[0][0]);
     constexpr uint32_t kPbufCap = sizeof(R) / sizeof(uint32_t);
     const bool staged = !path_dev && !path_skip && path_len <= kPbufCap;
-    if (status == kFound && !path_skip && tid < 2)
-      walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1,
-                staged ? pbuf : (path_dev ? P.b.dpath : P.h.path));
+    if (status == kFound && !path_skip && tid < 2) {
+      uint32_t* const out = staged ? pbuf : (path_dev ? P.b.dpath : P.h.path);
+      if (kLq && lq_done) {
+        // LDS walk: lane 0 from the meet back to the source (positions md0 .. 0),
+        // lane 1 on to the target (md0 .. md0 + md1), one LDS load per hop
+        uint32_t i = lq_meet[tid];
+        int pos = (int)md0;
+        for (int remain = tid ? (int)md1 : (int)md0;; --remain) {
+          out[pos] = LQ[tid][i];
+          if (remain == 0) break;
+          i = LP[tid][i];
+          if (i >= kQCap) break;  // never: every claim's parent index is in the queue
+          pos += tid ? 1 : -1;
+        }
+      } else {
+        walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1, out);
+      }
+    }
     if (staged) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       for (uint32_t i = lane; i < path_len; i += kWave)

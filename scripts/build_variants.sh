@@ -11,7 +11,7 @@ while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   mkdir -p build/var/$name
   /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -mcode-object-version=5 -munsafe-fp-atomics \
-    -Icsrc/include -Icsrc/hip $flags -c csrc/hip/engine_kernels.hip -o build/var/$name/engine_kernels.o &
+    -mllvm -amdgpu-atomic-optimizer-strategy=None -Icsrc/include -Icsrc/hip $flags -c csrc/hip/engine_kernels.hip -o build/var/$name/engine_kernels.o &
 done
 wait
 for d in build/var/*/; do
