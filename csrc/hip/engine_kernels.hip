@@ -1075,23 +1075,27 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           const uint32_t dc = isnew[k] ? min(dg[k], kDegClamp) : 0u;
           const uint32_t incl = wave_incl_scan(dc);
           const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+          // a side served by one batch owns its counter: a plain store, no atomic round trip
+          const bool alone = sd[k] ? nbt - nb0 == 1 : nb0 == 1;  // scalar
+          const unsigned long long add = ((unsigned long long)__popcll(mask) << 32) | tot;
           unsigned long long pos = 0;
-          if (lane == 0)
-            pos = atomicAdd(&wctr[slot][sd[k] ? 1 : 0], ((unsigned long long)__popcll(mask) << 32) | tot);
-          const uint32_t be = __builtin_amdgcn_readlane((uint32_t)pos, 0);
-          const uint32_t bn = __builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0);
+          if (alone) {
+            if (lane == 0) wctr[slot][sd[k] ? 1 : 0] = add;
+          } else if (lane == 0) {
+            pos = atomicAdd(&wctr[slot][sd[k] ? 1 : 0], add);
+          }
+          const uint32_t be = alone ? 0u : __builtin_amdgcn_readlane((uint32_t)pos, 0);
+          const uint32_t bn = alone ? 0u : __builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0);
           const uint32_t eb = be + incl - dc;
           const uint32_t qi = (sd[k] ? qe1 : qe0) + bn + mbcnt64(mask);  // < kQCap (round bound)
           if (isnew[k]) {
             (sd[k] ? LP[1] : LP[0])[qi] = u[k];
             (sd[k] ? LQ[1] : LQ[0])[qi] = v[k];
           }
+          if (k == 0) sub(2);
           append_records(sd[k] ? R[x1] : R[x0], isnew[k] && eb + dg[k] <= CAP ? dg[k] : 0u, eb, qi, ob[k]);
         }
-        if constexpr (kStamp) {
-          sub(2);
-          lt0 = lt1;
-        }
+        sub(3);
         return lsub;
       };
       for (;;) {
@@ -1676,7 +1680,9 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
         cmd[5] = (rq.w & kReqLockstep) ? 1u : 0u;
       }
     }
-    __syncthreads();
+    // LDS-only barriers around the request: the diagnostic stores to host
+    // memory (last wave) drain during the search instead of holding it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     if (tid == kDiagTid) {
       __hip_atomic_store(&box->stage, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&box->seen, diag[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1694,7 +1700,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
     Q.lockstep = (int)uni(cmd[5]);
     Q.trace = kStamp ? 2 : 0;  // kStamp: BIBFS_STAMP_SERVER profiling build of the server
     last_seq = Q.seq;
-    __syncthreads();  // every wave has read cmd before thread 0 may overwrite it
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave has read cmd
     lds_search_body<OffT, kStamp, kBm>(Q, true);
     if (tid == kDiagTid) __hip_atomic_store(&box->stage, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }

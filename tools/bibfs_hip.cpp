@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
                         (unsigned long long)(t.edges >> 32));
           else if (t.mode == 8)  // all-wave lockstep round
             std::printf("Stamp cycles: wave round=%d edges=%llu work=%d barrier+book=%llu | rec+load=%llu claim=%llu "
-                        "place=%llu (%llu)\n", t.side, (unsigned long long)t.edges, t.depth,
+                        "scan+place=%llu records=%llu\n", t.side, (unsigned long long)t.edges, t.depth,
                         (unsigned long long)t.frontier, (unsigned long long)(t.discovered & 0xffff),
                         (unsigned long long)((t.discovered >> 16) & 0xffff),
                         (unsigned long long)((t.discovered >> 32) & 0xffff),
