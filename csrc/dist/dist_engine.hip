@@ -85,6 +85,7 @@ enum : int { kPlanAccountOnly = 1, kPlanResume = 2, kPlanForce = 4, kPlanStall =
 struct Ctl {
   unsigned long long cnt[2];   // current frontier sizes (vertices)
   unsigned long long fed[2];   // current frontier degree sums
+  unsigned long long fmax[2];  // the largest share of fed[s] on one rank (bounds a rank's candidate block)
   unsigned long long ved[2];   // degree sum of everything side s claimed
   unsigned long long vis[2];   // vertices side s claimed (incl. the root)
   unsigned long long key;      // (length << 32) | meet vertex, once found
@@ -112,6 +113,7 @@ struct Policy {
 struct Reduced {
   unsigned long long sums[4];  // [2s] vertices side s claimed this round, [2s+1] their degree sum (sum)
   unsigned long long meetkey;  // (path length << 32) | meet vertex (min)
+  unsigned long long nfmax[2]; // ~(this rank's degree sum of side s's new frontier): min = ~max over ranks
   uint32_t maxsend[2];         // candidates of side s on this rank (max; host-planned rounds)
   uint32_t md[2];              // depth of the meet vertex from each root (owner contributes; min)
   uint32_t pad[2];
@@ -185,6 +187,7 @@ __device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, u
       for (int s = 0; s < 2; ++s) {
         c.cnt[s] = rd.sums[2 * s];
         c.fed[s] = rd.sums[2 * s + 1];
+        c.fmax[s] = c.fed[s];  // one owner per root
         c.ved[s] = c.fed[s];
         c.vis[s] = c.cnt[s];
       }
@@ -197,6 +200,7 @@ __device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, u
         c.levels += 1;
         c.cnt[s] = rd.sums[2 * s];
         c.fed[s] = rd.sums[2 * s + 1];
+        c.fmax[s] = ~rd.nfmax[s];
         c.ved[s] += c.fed[s];
         c.vis[s] += c.cnt[s];
       }
@@ -247,7 +251,7 @@ __device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, u
   if (!(flags & kPlanForce)) {
     bool fits = wm == 0;
     for (int s = 0; s < 2; ++s)
-      if (((want >> s) & 1) && c.fed[s] > spec_cap) fits = false;
+      if (((want >> s) & 1) && c.fmax[s] > spec_cap) fits = false;  // a rank's block holds its share
     if (!fits || (flags & kPlanStall)) {
       c.state = kStall;
       c.stall = (flags & kPlanStall) ? kStallHost : (wm ? kStallDense : kStallCap);
@@ -438,7 +442,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     // one 8-byte write-through store per round: the host paces its enqueueing
     // on the plan and sizes the rounds it enqueues from the frontier (larger
     // side's edge count, clamped to 32 bits)
-    const unsigned long long fm = min(max(c.fed[0], c.fed[1]), 0xffffffffull);
+    const unsigned long long fm = min(max(c.fmax[0], c.fmax[1]), 0xffffffffull);
     __hip_atomic_store(&V.plan_ring[it % kPlanRing],
                        (uint64_t)fm << 32 | ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
@@ -610,6 +614,7 @@ __global__ __launch_bounds__(kThreads) void k_meet_end(DView V, uint32_t it) {
       const unsigned long long ne = atomicExch(&st->new_edges[s], 0ull);
       V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - st->fend[s]) : 0ull;
       V.red[p].sums[2 * s + 1] = on ? ne : 0ull;
+      V.red[p].nfmax[s] = on ? ~ne : ~0ull;
       if (on) {
         st->fbeg[s] = st->fend[s];
         st->fend[s] = qt;
@@ -1288,7 +1293,7 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
   HIP_CHECK(hipGetLastError());
   comm->group_begin();
   comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
-  comm->allreduce(&V.red[it & 1].meetkey, 1, DType::kU64, ROp::kMin, cs);
+  comm->allreduce(&V.red[it & 1].meetkey, 3, DType::kU64, ROp::kMin, cs);  // meet key, ~per-rank frontier max
   comm->group_end();
   stats.collectives += 2;
 }
@@ -1343,7 +1348,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       const Ctl& h = *h_ctl;
       uint64_t need = 0;
       for (int s = 0; s < 2; ++s)
-        if ((h.want >> s) & 1) need = std::max<uint64_t>(need, h.fed[s]);
+        if ((h.want >> s) & 1) need = std::max<uint64_t>(need, h.fmax[s]);
       if (!host_only && h.stall == kStallCap && need <= spec_max) {
         spec_cap = std::max<uint32_t>(spec_cap, next_pow2(need));
         flags = kPlanResume;  // re-run the stalled plan speculatively with a bigger block
@@ -1354,7 +1359,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         HIP_CHECK(hipGetLastError());
         it += 2;
         wait(cs);
-        const uint64_t fm = std::max(h_ctl->fed[0], h_ctl->fed[1]);
+        const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
         spec_cap = std::min(spec_max, std::max<uint32_t>(kSpecCapMin, next_pow2(4 * fm)));
         continue;
       }
@@ -1387,8 +1392,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         f_prev = f;
       }
       if ((uint64_t)(it - first) > 4ull * n + 16) break;  // safety net
-      const unsigned bx = std::min<unsigned>(
-          (unsigned)cus * 2, std::max<unsigned>(1, (unsigned)((uint64_t)cap_it / P / kThreads) + 1));
+      const unsigned bx = std::min<unsigned>((unsigned)cus * 2, cap_it / kThreads + 1);  // ~ this rank's edges
       const unsigned cx = std::min<unsigned>((unsigned)cus * 2, std::max<unsigned>(1, cap_it / kThreads / 4 + 1));
       const uint64_t gather_bytes = 2 * block_words(cap_it) * 4;
       // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
@@ -1409,7 +1413,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       if (P > 1) {  // a one-rank reduction is the identity
         comm->group_begin();
         comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
-        comm->allreduce(&V.red[it & 1].meetkey, 1, DType::kU64, ROp::kMin, cs);
+        comm->allreduce(&V.red[it & 1].meetkey, 3, DType::kU64, ROp::kMin, cs);  // + ~per-rank frontier max
         comm->group_end();
         stats.collectives += 3;
         stats.exchanged_bytes += gather_bytes * P;
@@ -1424,7 +1428,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     wait(cs);
     have_ctl = true;
     if (h_ctl->state == kRun) {  // size the next batch for the frontier we have now
-      const uint64_t fm = std::max(h_ctl->fed[0], h_ctl->fed[1]);
+      const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
       spec_cap = std::min(spec_max, std::max<uint32_t>(spec_cap, next_pow2(4 * fm)));
     }
   }

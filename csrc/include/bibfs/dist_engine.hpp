@@ -70,7 +70,7 @@ struct DistLevelStats {
 // Knobs of the partitioned engine (defaults are the production settings; the
 // small-capacity ones exist so tests can force every exchange branch).
 struct DistTuning {
-  int spec_rounds = 2;             // lookahead: rounds enqueued ahead of the last plan the host saw (0 = host plans every round)
+  int spec_rounds = 1;             // lookahead: rounds enqueued ahead of the last plan the host saw (0 = host plans every round)
   uint32_t spec_cap_max = 1u << 16;  // largest per-rank candidate block of a speculative round (pairs)
   uint32_t cap = 0;                // per-rank candidate block of a host-planned round (0 = min(2^20, n))
   uint64_t nosync_bytes = 1u << 20;  // host-planned round: size the exchange from host bounds up to this
