@@ -192,11 +192,11 @@ void batch_global(const GraphView& g, uint32_t words, const uint32_t* qidx, uint
                   uint32_t path_cap, unsigned long long edge_cap, int threads, hipStream_t s);
 // One top-down level; the LAST workgroup finishes it, publishes the mirror
 // (seq) and, when the search ended, walks the path and publishes the result
-// (res_seq).  hub_pass: also enqueue the edge-parallel hub pass (graphs with
-// vertices above the hub degree), which then finishes the level instead.
+// (res_seq).  hub_deg != ~0u: frontier vertices above that degree are deferred
+// to the edge-parallel hub pass enqueued behind, which then finishes the level.
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
                   dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
-                  bool hub_pass, hipStream_t s);
+                  uint32_t hub_deg, hipStream_t s);
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
 void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);
 void finish_level(const SearchBuffers& b, int side, int mode, int trace, dev::DevState* mirror, uint32_t seq,

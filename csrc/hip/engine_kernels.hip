@@ -2331,7 +2331,7 @@ uint32_t grid_hub_degree() { return kHubDegree; }
 
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
                   dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
-                  bool hub_pass, hipStream_t s) {
+                  uint32_t hub_deg, hipStream_t s) {
   // Dynamic chunks of 256 frontier vertices; never more blocks than chunks:
   // every block takes at least one ticket from ONE counter, and 1024 blocks
   // contending on it cost ~12 us even for a 3-vertex frontier.
@@ -2341,9 +2341,9 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   auto launch_one = [&](auto P) {
     using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
     P.mirror = mirror, P.seq = seq, P.trace = trace, P.h = h, P.res_seq = res_seq;
-    P.hub_deg = hub_pass ? kHubDegree : ~0u;
+    P.hub_deg = hub_deg;  // ~0u: no hub pass
     k_grid_topdown<OffT><<<blocks, kGridThreads, 0, s>>>(P);
-    if (hub_pass) k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
+    if (hub_deg != ~0u) k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
   };
   if (g.row_off32) launch_one(gp<uint32_t>(g, b, side));
   else launch_one(gp<uint64_t>(g, b, side));

@@ -381,10 +381,19 @@ struct HipBiBfs::Impl {
       fbits_valid[s] = true;
       launch::finish_level(buf, s, mode, trace, h_state, ls, hs, res_seq, n, stream);
     } else {
-      // a vertex above the hub degree can only be in a frontier with that many edges
-      const bool hub_pass = max_deg > launch::grid_hub_degree() && h_state->fedges[s] > launch::grid_hub_degree();
-      launch::grid_topdown(g, buf, s, cus, (uint64_t)(h_state->fend[s] - h_state->fbeg[s]), h_state, ls, trace, hs,
-                           res_seq, hub_pass, stream);
+      // Vertices above the hub degree go to the edge-parallel hub pass (a
+      // vertex that big can only be in a frontier with that many edges).  The
+      // top-down kernel gives each workgroup 256 frontier VERTICES, so a small
+      // frontier of heavy vertices (Kronecker levels after the hand-off: a few
+      // hundred vertices, 10^5 edges) would run on a handful of workgroups:
+      // then every vertex above 64 edges goes edge-parallel over all CUs (at
+      // most a few hub tiles: every workgroup stages each tile, so a frontier
+      // of tens of thousands of vertices stays with the chunked kernel).
+      const uint64_t F = h_state->fend[s] - h_state->fbeg[s], fe = h_state->fedges[s];
+      uint32_t hub_deg = ~0u;
+      if (max_deg > launch::grid_hub_degree() && fe > launch::grid_hub_degree()) hub_deg = launch::grid_hub_degree();
+      if (F <= 4096 && fe > 16384 && max_deg > 64) hub_deg = 64;
+      launch::grid_topdown(g, buf, s, cus, F, h_state, ls, trace, hs, res_seq, hub_deg, stream);
       fbits_valid[s] = false;
     }
     wait_level();
