@@ -329,8 +329,10 @@ def main(argv=None) -> int:
             barrier()
             reps = max(3, steps // 40)
             tb = time.perf_counter()
+            fallbacks = 0
             for _ in range(reps):
                 bh, boff, _paths = eng.search_batch_arrays(bs, bd)
+                fallbacks += eng.last_batch_fallbacks
                 assert (bh >= 0).all() and (boff[1:] - boff[:-1] == bh + 1).all()
             barrier()
             bdt = max_over_ranks(time.perf_counter() - tb)
@@ -338,7 +340,9 @@ def main(argv=None) -> int:
             bq = reps * a.batch * world
             batched = {"batch": a.batch, "launches": reps, "ms_per_batch": bdt * 1e3 / reps,
                        "us_per_query": bdt * 1e6 / (reps * a.batch), "queries_per_s": bq / bdt,
-                       "gteps": m * bq / bdt / 1e9}
+                       "gteps": m * bq / bdt / 1e9,
+                       # queries re-run one by one (level above the batch edge cap / long path)
+                       "fallback_queries_per_batch": fallbacks / reps}
         out = {
             "n": n, "m": m, "seed": seed, "wall_s": dt, "ms_per_step": dt * 1e3 / steps,
             "gteps": m * queries / dt / 1e9,

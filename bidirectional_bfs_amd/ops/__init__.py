@@ -115,6 +115,13 @@ class HipEngine:
     def batch_edge_cap(self, edges: int) -> None:
         self._e.batch_edge_cap = int(edges)
 
+    @property
+    def last_batch_fallbacks(self) -> int:
+        """Queries of the last batched call that were re-run one by one through
+        ``search`` (a level above ``batch_edge_cap``, a path longer than the
+        batch path slot)."""
+        return self._e.last_batch_fallbacks
+
     def set_batch_tuning(self, lds_first: int = -1, threads: int = 0) -> "HipEngine":
         """Batched serving knobs: LDS pass first (1), HBM-bitmap pass only (0) or
         auto by graph size (-1); HBM-pass workgroup size 256/1024 (0 = auto)."""

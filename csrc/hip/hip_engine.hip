@@ -66,6 +66,7 @@ struct HipBiBfs::Impl {
   uint32_t* h_bq = nullptr;       // pinned staging for src/dst
   uint32_t bcap = 0;              // slots allocated
   uint64_t bedge_cap = 1ull << 20;  // batch_global: larger levels go to search()
+  uint64_t batch_fallbacks = 0;     // last search_batch: queries re-run through search()
   int blds = -1;                    // batch: LDS pass first (1), never (0), auto (-1)
   int bthreads = 0;                 // batch_global workgroup size (256 / 1024), 0 = auto
   uint32_t* d_bbits = nullptr;    // per slot 2 visited bitmaps (batch_global), all-zero between launches
@@ -645,6 +646,7 @@ void HipBiBfs::set_batch_tuning(int lds_first, int threads) {
   p_->bthreads = threads;
 }
 uint64_t HipBiBfs::batch_edge_cap() const { return p_->bedge_cap; }
+uint64_t HipBiBfs::last_batch_fallbacks() const { return p_->batch_fallbacks; }
 
 std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, const std::vector<vid_t>& dst,
                                                  const SearchOptions& opt) {
@@ -654,10 +656,12 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
   HIP_CHECK(hipSetDevice(I.device));
   const size_t K = src.size();
   std::vector<SearchResult> out(K);
+  I.batch_fallbacks = 0;
   if (K == 0) return out;
   for (size_t i = 0; i < K; ++i) BIBFS_REQUIRE(src[i] < I.n && dst[i] < I.n, "src/dst out of range");
   if (opt.force_grid || opt.trace || !I.server_usable()) {  // the batch kernel is the LDS engine only
     for (size_t i = 0; i < K; ++i) out[i] = search(src[i], dst[i], opt);
+    I.batch_fallbacks = K;
     return out;
   }
   // slots: up to 1024 per launch.  Per-slot state (parent + queue, 16n B) is
@@ -733,6 +737,7 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
         const BatchOut& G = I.h_bout[i];
         if (G.status != kFound && G.status != kNoPath) {
           r = search(s, d, opt);  // a level above the edge cap / path longer than the slot
+          ++I.batch_fallbacks;
           continue;
         }
         r.found = G.status == kFound;
@@ -750,6 +755,7 @@ std::vector<SearchResult> HipBiBfs::search_batch(const std::vector<vid_t>& src, 
       }
       if (R.status == kHandoff || R.path_on_device == 2 || (R.status != kFound && R.status != kNoPath)) {
         r = search(s, d, opt);  // path longer than the slot: single-query engines
+        ++I.batch_fallbacks;
         continue;
       }
       r.found = R.status == kFound;

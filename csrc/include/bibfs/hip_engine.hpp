@@ -63,6 +63,9 @@ class HipBiBfs {
                                          const SearchOptions& opt = {});
   void set_batch_edge_cap(uint64_t edges);
   uint64_t batch_edge_cap() const;
+  // Queries of the last search_batch call that fell back to search() (a level
+  // above batch_edge_cap, a path longer than the slot, or a failed pass).
+  uint64_t last_batch_fallbacks() const;
   // lds_first: 1 = LDS pass first, 0 = HBM-bitmap pass only, -1 = auto (by n);
   // threads: HBM-pass workgroup size 256 / 1024, 0 = auto (by query count)
   void set_batch_tuning(int lds_first, int threads);

@@ -280,6 +280,7 @@ PYBIND11_MODULE(_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("resident", &HipBiBfs::resident)
       .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
+      .def_property_readonly("last_batch_fallbacks", &HipBiBfs::last_batch_fallbacks)
       .def("set_batch_tuning", &HipBiBfs::set_batch_tuning, py::arg("lds_first") = -1, py::arg("threads") = 0)
       .def("begin", &HipBiBfs::begin, py::call_guard<py::gil_scoped_release>())
       .def(

@@ -249,6 +249,7 @@ def test_search_batch_global_pass(gpu_engine, spec):
         rs = gpu_engine.search_batch(pairs[:40])
         for (s, d), r, h in zip(pairs[:40], rs, truth[:40]):
             check_result(g.csr, s, d, r.hops, r.path, h)
+        assert gpu_engine.last_batch_fallbacks > 0
     finally:
         gpu_engine.batch_edge_cap = cap0
         gpu_engine.set_batch_tuning(-1, 0)
