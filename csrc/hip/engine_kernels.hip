@@ -171,6 +171,9 @@ struct LdsParams {
   int batch;          // batched search: no hand-off state / device path (the host re-runs those queries)
   launch::SearchBuffers b;
   launch::HostSide h;
+  // 0: fresh LDS (one-shot / batch kernels); resident server: 1 = its first
+  // search, 2 = a later one (LDS kept from the previous search in this launch)
+  int resident = 0;
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -357,7 +360,12 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
   };
   uint32_t* Hflat = &H[0][0];
-  {
+  // Visited sets start empty.  A resident search that ended inside the
+  // all-wave rounds cleared the bitmap words it set after publishing (sparse,
+  // off the critical path), so the 64 KB clear -- >= 512 cycles of LDS write
+  // bandwidth -- is skipped when the previous search left it clean.
+  __shared__ uint32_t bm_dirty;
+  if (!kBm || P.resident < 2 || bm_dirty) {
     const uint32_t fill = kBm ? 0u : kEmpty;
     uint4* H4 = reinterpret_cast<uint4*>(Hflat);
     for (uint32_t i = tid; i < 2 * kHashSize / 4; i += kLdsThreads) H4[i] = make_uint4(fill, fill, fill, fill);
@@ -1566,6 +1574,22 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
     __hip_atomic_store(&Rr->seq, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if constexpr (kLq) {
+    if (P.resident) {
+      // after the publish: leave the bitmaps clean for the next search.  Every
+      // set bit belongs to a vertex of a side's LDS queue (a losing claim only
+      // re-marks a vertex that side already holds), so zeroing those words
+      // clears everything; otherwise the next search clears it all.
+      if (lq_done) {
+        for (uint32_t i = tid; i < s0.qend + s1.qend; i += kLdsThreads) {
+          const int q = i >= s0.qend;
+          const uint32_t j = q ? i - s0.qend : i;
+          W(q)[LQ[q][j] >> 5] = 0ull;
+        }
+      }
+      if (tid == 0) bm_dirty = lq_done ? 0u : 1u;  // read after the server loop's barriers
+    }
+  }
 }
 
 template <typename OffT, bool kStamp, bool kBm>
@@ -1634,6 +1658,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
   if (!uni(srv_won)) return;
   if (tid == 0) __hip_atomic_store(&box->alive, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __shared__ uint32_t diag[3];  // seen, poll latency, polls
+  bool first = true;           // the first search of this launch: LDS holds nothing of ours
   __shared__ unsigned long long diag_t;
   constexpr int kDiagTid = kDiagOffWave0 ? kLdsThreads - kWave : 0;  // lane 0 of the last wave
   for (;;) {
@@ -1699,6 +1724,8 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
     Q.side_policy = (int)uni(cmd[4]);
     Q.lockstep = (int)uni(cmd[5]);
     Q.trace = kStamp ? 2 : 0;  // kStamp: BIBFS_STAMP_SERVER profiling build of the server
+    Q.resident = first ? 1 : 2;
+    first = false;
     last_seq = Q.seq;
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // every wave has read cmd
     lds_search_body<OffT, kStamp, kBm>(Q, true);
