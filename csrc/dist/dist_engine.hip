@@ -61,6 +61,11 @@ constexpr int kThreads = 256;
 constexpr unsigned long long kNoKey = ~0ull;
 constexpr uint64_t kCapMax = 1u << 20;          // host-planned round: candidate pairs per rank per level
 constexpr uint64_t kLockstepEdges = 1u << 16;   // both frontiers at most this many edges: always lockstep
+// Balanced frontiers (within 2x) go lockstep only up to this size: beyond it a
+// lockstep round doubles the work of the meeting level (Kronecker hub levels,
+// 10^7 edges a side), while a single-side level does the smaller half and
+// stops at its first meet (every meet of a single-side level has one length).
+constexpr uint64_t kLockstepMaxEdges = 1u << 20;
 constexpr uint32_t kSpecCapMin = 1024;          // smallest speculative candidate block (pairs)
 // A frontier vertex with more edges than this is not expanded by the block
 // that holds it: it is deferred to a hub list whose edges the whole grid then
@@ -135,6 +140,8 @@ struct DState {
   uint32_t hub_count[2];                // deferred hubs of side s this level
   uint32_t pad;
   unsigned long long new_edges[2];      // degree sum of the vertices side s claimed this level
+  uint32_t meet_found;                  // a single-side level claimed a vertex the other side holds
+  uint32_t pad2;
 };
 
 struct DView {
@@ -220,7 +227,8 @@ __device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, u
       return;
     }
     const unsigned long long flo = min(c.fed[0], c.fed[1]), fhi = max(c.fed[0], c.fed[1]);
-    if (pol.lockstep && pol.side != (int)SidePolicy::kAlternate && (fhi <= kLockstepEdges || fhi <= 2 * flo)) {
+    if (pol.lockstep && pol.side != (int)SidePolicy::kAlternate &&
+        (fhi <= kLockstepEdges || (fhi <= 2 * flo && fhi <= kLockstepMaxEdges))) {
       want = 3;
     } else if (pol.side == (int)SidePolicy::kAlternate) {
       want = 1u << c.turn;
@@ -289,14 +297,21 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
 // Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
 // every lane of the wave calls it, `want` masks lanes.  One queue append and
 // one degree-sum atomic per wave.
+// flag_meet (single-side levels): a claim of a vertex the other side already
+// holds raises DState::meet_found, so the expansion loops stop early -- in a
+// single-side level every meet has the same length (the other side's
+// frontier depth), so the first one is as good as the minimum; the exact key
+// still comes from k_meet_end over the vertices claimed.
 __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uint32_t v, uint32_t u,
-                                           uint32_t dnew) {
+                                           uint32_t dnew, bool flag_meet = false) {
   const uint32_t li = v - V.lo;
   uint32_t* vis = pick(V.vis, s);
   bool mine = false;
   if (want) {
     const uint32_t bit = 1u << (li & 31);
     if (!(vis[li >> 5] & bit)) mine = !(atomicOr(&vis[li >> 5], bit) & bit);
+    if (flag_meet && mine && (pick(V.vis, s ^ 1)[li >> 5] & bit))
+      __hip_atomic_store(&V.st->meet_found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const unsigned long long mask = __ballot(mine);
   if (!mask) return;  // wave-uniform
@@ -343,15 +358,26 @@ __device__ __forceinline__ void wave_emit(const DView& V, int s, bool want, uint
 // LDS and walks the chunk's edges one per lane (binary search for the owning
 // vertex), so a hub costs the same per edge as a leaf and no lane idles on a
 // short row.  Block-uniform control flow (it contains barriers).
+__device__ __forceinline__ bool meet_seen(const DView& V) {
+  return __hip_atomic_load(&V.st->meet_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+// exit_on_meet: a single-side level, which stops once a meet is claimed.
 __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pairs, uint32_t cap, uint32_t b0,
-                               uint32_t nb, uint64_t hub_deg) {
+                               uint32_t nb, uint64_t hub_deg, bool exit_on_meet) {
   __shared__ uint32_t su[kThreads];
   __shared__ unsigned long long sb[kThreads], se[kThreads];
   __shared__ unsigned long long wsum[kThreads / kWave];
+  __shared__ uint32_t sstop;
   const uint32_t fb = V.st->fbeg[s], F = V.st->fend[s] - fb;
   const uint32_t* q = pick(V.queue, s);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   for (uint64_t c0 = (uint64_t)b0 * kThreads; c0 < F; c0 += (uint64_t)nb * kThreads) {
+    if (exit_on_meet) {  // block-uniform: the flag goes through LDS between barriers
+      if (tid == 0) sstop = meet_seen(V) ? 1u : 0u;
+      __syncthreads();
+      if (sstop) break;
+    }
     const uint64_t i = c0 + tid;
     unsigned long long deg = 0, b = 0;
     uint32_t u = 0;
@@ -389,7 +415,10 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
     }
     se[tid] = pre + x - deg;
     __syncthreads();
-    for (unsigned long long base = 0; base < tot; base += kThreads) {
+    uint32_t iter = 0;
+    for (unsigned long long base = 0; base < tot; base += kThreads, ++iter) {
+      // wave-uniform exit (no barrier in this loop)
+      if (exit_on_meet && (iter & 15) == 15 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
       const unsigned long long e = base + tid;
       const bool valid = e < tot;
       uint32_t uu = 0, v = 0;
@@ -404,7 +433,7 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
         v = V.col[sb[a] + (e - se[a])];
       }
       const bool own = valid && v >= V.lo && v < V.hi;
-      wave_claim(V, s, own, v, uu, dnew);
+      wave_claim(V, s, own, v, uu, dnew, exit_on_meet);
       wave_emit(V, s, valid && !own, v, uu, pairs, cap);
     }
     __syncthreads();
@@ -450,7 +479,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   const int s = blockIdx.y;
   if ((c.sides >> s) & 1)
     td_expand_side(V, s, c.depth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
-                   blockIdx.x, gridDim.x, hub_deg);
+                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u);
   if (!header) return;  // k_td_hubs runs next and writes the headers
   if (last_block(&V.st->done_blocks[0], gridDim.x * gridDim.y) && threadIdx.x < 2) {
     const int ss = threadIdx.x;
@@ -467,7 +496,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
 // of hubs with their degree prefix in LDS and walks the tile's flattened edge
 // range with a grid stride, so each hub's edges spread over all CUs.
 __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int side, uint32_t dnew_fixed,
-                                                      uint32_t cap) {
+                                                      uint32_t cap, int single) {
   __shared__ uint32_t hu[kHubTile];
   __shared__ unsigned long long hb[kHubTile], hp[kHubTile + 1];
   __shared__ unsigned long long wsum[kThreads / kWave];
@@ -481,8 +510,15 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   const uint32_t H = V.st->hub_count[s];
   uint2* pairs = reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const bool exit_on_meet = side < 0 ? sides != 3u : single != 0;
+  __shared__ uint32_t sstop;
   if ((sides >> s) & 1) {
     for (uint32_t t0 = 0; t0 < H; t0 += kHubTile) {
+      if (exit_on_meet) {  // block-uniform
+        if (tid == 0) sstop = meet_seen(V) ? 1u : 0u;
+        __syncthreads();
+        if (sstop) break;
+      }
       const uint32_t nt = min((uint32_t)kHubTile, H - t0);
       constexpr int kPer = kHubTile / kThreads;  // hubs per thread for the scan
       unsigned long long d[kPer], run = 0;
@@ -521,8 +557,10 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
       }
       if (tid == 0) hp[kHubTile] = tot;
       __syncthreads();
+      uint32_t iter = 0;
       for (unsigned long long base = (unsigned long long)blockIdx.x * kThreads; base < tot;
-           base += (unsigned long long)gridDim.x * kThreads) {
+           base += (unsigned long long)gridDim.x * kThreads, ++iter) {
+        if (exit_on_meet && (iter & 15) == 15 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
         const unsigned long long e = base + tid;
         const bool valid = e < tot;
         uint32_t uu = 0, v = 0;
@@ -537,7 +575,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
           v = V.col[hb[a] + (e - hp[a])];
         }
         const bool own = valid && v >= V.lo && v < V.hi;
-        wave_claim(V, s, own, v, uu, dnew);
+        wave_claim(V, s, own, v, uu, dnew, exit_on_meet);
         wave_emit(V, s, valid && !own, v, uu, pairs, cap);
       }
       __syncthreads();
@@ -649,9 +687,10 @@ __global__ void k_plan_force(DView V, uint32_t it, Policy pol) {
   V.red[p].meetkey = kNoKey;
 }
 
-__global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t dnew, uint64_t hub_deg) {
+__global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t dnew, uint64_t hub_deg,
+                                                        int single) {
   td_expand_side(V, s, dnew, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(V.cap)) + 1, V.cap, blockIdx.x,
-                 gridDim.x, hub_deg);
+                 gridDim.x, hub_deg, single != 0);
 }
 
 __global__ void k_send_header(DView V, int s, uint32_t it) {
@@ -769,6 +808,7 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     st->done_blocks[2] = 0;
     st->hub_count[s] = 0;
     st->new_edges[s] = 0;
+    st->meet_found = 0;
     r.sums[2 * s] = r.sums[2 * s + 1] = 0;
     const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
@@ -1227,10 +1267,10 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
     const unsigned fblocks = blocks_for(h.cnt[s] / (uint64_t)P + kThreads, cus);
     if (!((h.want_modes >> s) & 1)) {
       const bool hubs = h.fed[s] > kHubDeg;
-      k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, hubs ? kHubDeg : kNoHubs);
+      k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, hubs ? kHubDeg : kNoHubs, ns == 1);
       if (hubs)
         k_td_hubs<<<blocks_for(std::min<uint64_t>(h.fed[s], (uint64_t)cus * 8 * kThreads), cus), kThreads, 0, ps>>>(
-            V, it, s, dnew, capr);
+            V, it, s, dnew, capr, ns == 1);
       k_send_header<<<1, 64, 0, ps>>>(V, s, it);
     } else {
       HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
@@ -1402,7 +1442,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       maybe_fault((int)it);
       k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
                                                       hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1);
-      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0);
       HIP_CHECK(hipGetLastError());
       if (P > 1) {  // one rank owns every vertex: expand claimed them all, the blocks are empty
         comm->allgather(V.sendbuf, V.recvbuf, gather_bytes, cs);

@@ -40,6 +40,7 @@ import numpy as np
 NONE = np.uint32(0xFFFFFFFF)
 NO_KEY = 1 << 62          # meet key (length << 32 | vertex) when no meet
 LOCKSTEP_EDGES = 1 << 16  # both frontiers this small (edges): lockstep round (native: kLockstepEdges)
+LOCKSTEP_MAX_EDGES = 1 << 20  # balanced frontiers above this: single-side rounds (native: kLockstepMaxEdges)
 
 
 @dataclass
@@ -203,7 +204,8 @@ class TorchDistBiBfs:
         while True:
             # rounds: both sides in lockstep while their frontiers are comparable
             flo, fhi = min(fed), max(fed)
-            if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or fhi <= 2 * flo):
+            if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or
+                                                      (fhi <= 2 * flo and fhi <= LOCKSTEP_MAX_EDGES)):
                 sides = [0, 1]
             elif side == "alternate":
                 sides, turn = [turn], turn ^ 1

@@ -17,6 +17,7 @@ gloo model (tests/dist_protocol_model.py) in ``result.trace``.
 import numpy as np
 
 LOCKSTEP_EDGES = 1 << 16  # dist_engine.hip kLockstepEdges
+LOCKSTEP_MAX_EDGES = 1 << 20  # dist_engine.hip kLockstepMaxEdges
 
 
 def round_trace(csr, src: int, dst: int, side: str = "edges", lockstep: bool = True):
@@ -35,7 +36,7 @@ def round_trace(csr, src: int, dst: int, side: str = "edges", lockstep: bool = T
     trace = []
     while True:
         flo, fhi = min(fed), max(fed)
-        if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or fhi <= 2 * flo):
+        if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or (fhi <= 2 * flo and fhi <= LOCKSTEP_MAX_EDGES)):
             sides = [0, 1]
         elif side == "alternate":
             sides, turn = [turn], turn ^ 1
