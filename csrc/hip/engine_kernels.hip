@@ -96,6 +96,15 @@ constexpr bool kWaveRounds = BIBFS_KNOB_WAVE_ROUNDS;
 #define BIBFS_KNOB_WAVE_B 2
 #endif
 constexpr uint32_t kWaveB = BIBFS_KNOB_WAVE_B;
+// 1 = the all-wave rounds also run with LDS hash visited sets (graphs above
+// 131072 vertices); 0 = bitmap graphs only.  A/B (profiles/r2_wave_hash_ab.txt):
+// 1M G(n,p) 28.9 -> 27.4 us, but 10M 110 -> 122 us -- the LDS queue costs
+// record capacity (2976 -> 1900 per buffer), so big graphs hand off to the
+// grid engine a level earlier.  Off by default.
+#ifndef BIBFS_KNOB_WAVE_HASH
+#define BIBFS_KNOB_WAVE_HASH 0
+#endif
+constexpr bool kWaveHash = BIBFS_KNOB_WAVE_HASH;
 // Resident server: the mailbox diagnostics (stage / seen / poll latency) are
 // system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
 // issued them, its first global load of the search would wait for their PCIe
@@ -293,7 +302,7 @@ struct LevelPlan {
 template <typename OffT, bool kStamp, bool kBm>
 __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool elected) {
   using Rec = typename LdsRec<OffT>::type;
-  constexpr bool kLq = kBm && kWaveRounds && std::is_same<OffT, uint32_t>::value;  // LDS queue + walk
+  constexpr bool kLq = (kBm || kWaveHash) && kWaveRounds && std::is_same<OffT, uint32_t>::value;  // LDS queue + walk
   constexpr uint32_t CAP = kLq ? kCapBm : LdsRec<OffT>::cap;
   __shared__ uint32_t H[2][kHashSize];
   __shared__ Rec R[4][CAP];
@@ -1048,19 +1057,33 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
 #pragma unroll
         for (int k = 0; k < B; ++k) {  // claims, the opposite words beside them
           const uint32_t a = (sd[k] ? d1 : d0) + 1;
-          const uint32_t bit = v[k] & 31u;
           old[k] = ~0ull;
-          if (ok[k]) old[k] = atomicOr(&(sd[k] ? W1 : W0)[v[k] >> 5], 1ull << (bit + ((a & 1u) << 5)));
-          w[k] = (sd[k] ? W0 : W1)[v[k] >> 5];
+          if constexpr (kBm) {
+            const uint32_t bit = v[k] & 31u;
+            if (ok[k]) old[k] = atomicOr(&(sd[k] ? W1 : W0)[v[k] >> 5], 1ull << (bit + ((a & 1u) << 5)));
+            w[k] = (sd[k] ? W0 : W1)[v[k] >> 5];
+          } else {
+            // hash sets: insert (key = id | parity of the claim depth), then
+            // the opposite table's key; old/w carry "new" and that key
+            const bool ins = ok[k] && hash_insert(sd[k] ? H[1] : H[0], v[k], v[k] | ((a & 1u) ? kParity : 0u));
+            old[k] = ins ? 0ull : ~0ull;
+            w[k] = ins ? hash_find(sd[k] ? H[0] : H[1], v[k]) : kEmpty;
+          }
         }
         unsigned long long best = ~0ull;
 #pragma unroll
         for (int k = 0; k < B; ++k) {
           const uint32_t a = (sd[k] ? d1 : d0) + 1;
           const uint32_t bo = sd[k] ? d0 : d1;  // opposite frontier depth (lockstep: parity rule)
-          const uint32_t bit = v[k] & 31u;
-          isnew[k] = ((old[k] >> bit) & 0x100000001ull) == 0;
-          const uint32_t f = (uint32_t)((w[k] >> bit) & 1ull) | ((uint32_t)((w[k] >> (32 + bit)) & 1ull) << 1);
+          uint32_t f;  // opposite state: 0 absent, else 1 + parity (3 = an older claim)
+          if constexpr (kBm) {
+            const uint32_t bit = v[k] & 31u;
+            isnew[k] = ((old[k] >> bit) & 0x100000001ull) == 0;
+            f = (uint32_t)((w[k] >> bit) & 1ull) | ((uint32_t)((w[k] >> (32 + bit)) & 1ull) << 1);
+          } else {
+            isnew[k] = old[k] == 0ull;
+            f = w[k] == kEmpty ? 0u : 1u + (uint32_t)(w[k] >> 31);
+          }
           if (isnew[k] && f != 0) {
             const uint32_t dob = (f == 3 || (f - 1) == (bo & 1u)) ? bo : bo + 1;
             const unsigned long long key = ((unsigned long long)(a + dob) << 32) | ((sd[k] ? 1ull : 0ull) << 31) | v[k];
@@ -1111,7 +1134,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         const uint32_t nb0 = (E0 + kWave - 1) / kWave, nbt = nb0 + (E1 + kWave - 1) / kWave;
         // every claim of the round must fit the LDS queue (a side claims at most E new vertices)
         if (status != kRunning || ovf || E0 == 0 || E1 == 0 || nbt > kWaveB * (kLdsThreads / kWave) ||
-            qe0 + E0 > kQCap || qe1 + E1 > kQCap)
+            qe0 + E0 > kQCap || qe1 + E1 > kQCap || (!kBm && (h0 + E0 > kHashLimit || h1 + E1 > kHashLimit)))
           break;
         const uint32_t used = (1u << a0) | (1u << a1);
         const uint32_t x0 = (uint32_t)__builtin_ctz(~used & 0xfu);
@@ -1574,7 +1597,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
     __hip_atomic_store(&Rr->seq, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if constexpr (kLq) {
+  if constexpr (kLq && kBm) {
     if (P.resident) {
       // after the publish: leave the bitmaps clean for the next search.  Every
       // set bit belongs to a vertex of a side's LDS queue (a losing claim only

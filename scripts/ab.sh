@@ -6,7 +6,7 @@ set -o pipefail
 mkdir -p gpurun_out
 out=gpurun_out/ab.txt
 : > $out
-for g in "gnp:100000::6 0 99999" "gnp:1000000::2 0 999999"; do
+for g in "gnp:100000::6 0 99999" "gnp:1000000::2 0 999999" "gnp:10000000::1 0 9999999"; do
   for rep in 1 2; do
     for d in build/var/*/; do
       v=$(basename $d)
