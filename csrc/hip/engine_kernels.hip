@@ -74,17 +74,6 @@ using namespace dev;
 #endif
 constexpr bool kWidUniform = BIBFS_KNOB_WID_UNIFORM;
 constexpr bool kAppendBallot = BIBFS_KNOB_APPEND_BALLOT;
-// 1 = small lockstep rounds keep the frontier in registers (reg_rounds); 0 =
-// the per-edge LDS record rounds (lean_rounds), for A/B.
-#ifndef BIBFS_KNOB_REG_ROUNDS
-#define BIBFS_KNOB_REG_ROUNDS 1
-#endif
-constexpr bool kRegRounds = BIBFS_KNOB_REG_ROUNDS;
-// register slots per lane of those rounds: frontiers up to 64 x this many edges
-#ifndef BIBFS_KNOB_REG_SLOTS
-#define BIBFS_KNOB_REG_SLOTS 1
-#endif
-constexpr uint32_t kRegSlots = BIBFS_KNOB_REG_SLOTS;
 // 1 = lockstep rounds of up to kLdsThreads frontier edges run on EVERY wave
 // with one LDS-only barrier per round (wave_rounds); 0 = the wave-0 rounds.
 #ifndef BIBFS_KNOB_WAVE_ROUNDS
@@ -263,17 +252,6 @@ __device__ __forceinline__ unsigned long long stamp() {
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-
-// Inclusive wave64 prefix MAX, same DPP pattern as the sum below.
-__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false));
-  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false));
-  return x;
-}
 
 // Inclusive wave64 prefix sum on the VALU via DPP (row_shr 1/2/4/8 inside
 // each 16-lane row, then row_bcast15 / row_bcast31 across rows) -- no LDS
@@ -630,346 +608,6 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     return out;
   };
 
-  // ---- lean lockstep rounds (bitmap mode, both sides together <= 64 edges):
-  // the common early phase of a query, written for a short instruction
-  // stream -- one edge per lane, both sides' records read from and written to
-  // one buffer each round, the state held in a few scalars and written back
-  // to s0/s1 when the phase ends (round too big, meet, dead side, overflow).
-  auto lean_rounds = [&]() {
-    uint32_t E0 = (uint32_t)s0.fed, E1 = (uint32_t)s1.fed;
-    const Rec* rp0 = &R[s0.cur][s0.off];
-    const Rec* rp1 = &R[s1.cur][s1.off];
-    uint32_t d0 = (uint32_t)s0.depth, d1 = (uint32_t)s1.depth;
-    uint32_t qe0 = s0.qend, qe1 = s1.qend, c0 = s0.cnt, c1 = s1.cnt, h0 = s0.hcnt, h1 = s1.hcnt;
-    unsigned long long v0 = s0.ved, v1 = s1.ved;
-    uint32_t nb = free_buf(), cb = kEmpty;
-    uint32_t rounds_done = 0;
-    bool ovf = false;
-    uint32_t* const par0 = P.b.parent[0];
-    uint32_t* const par1 = P.b.parent[1];
-    uint32_t* const que0 = P.b.queue[0];
-    uint32_t* const que1 = P.b.queue[1];
-    unsigned long long* const W0 = W(0);
-    unsigned long long* const W1 = W(1);
-    for (;;) {
-      const uint32_t ET = E0 + E1;
-      if (ET > (uint32_t)kWave || E0 == 0 || E1 == 0 || status != kRunning || ovf) break;
-      unsigned long long lt0 = 0;
-      if constexpr (kStamp) lt0 = stamp();
-      Rec* Nb = R[nb];
-      const uint32_t e = lane;
-      const bool ok = e < ET;
-      const bool sd = e >= E0;
-      const Rec r = sd ? rp1[ok ? e - E0 : 0u] : rp0[e];
-      const uint32_t u = r.x;
-      const OffT k = min(rec_k(r), P.nnz_m1);
-      uint32_t v;
-      OffT ob, oe;
-      if (P.padj) {
-        const uint4 pq = P.padj[k];
-        v = pq.x;
-        ob = (OffT)((uint64_t)pq.z | ((uint64_t)pq.w << 32));
-        oe = ob + (OffT)pq.y;
-      } else {
-        v = P.col[k];
-        ob = P.row_off[v];
-        oe = P.row_off[v + 1];
-      }
-      const uint32_t a = (sd ? d1 : d0) + 1;
-      const uint32_t bit = v & 31u;
-      const unsigned long long old = atomicOr(&(sd ? W1 : W0)[v >> 5], 1ull << (bit + ((a & 1u) << 5)));
-      const bool isnew = ok && ((old >> bit) & 0x100000001ull) == 0;
-      uint32_t hl = kEmpty, hv = 0, hd = 0;
-      if (isnew) {
-        const unsigned long long w = (sd ? W0 : W1)[v >> 5];
-        const uint32_t f = (uint32_t)((w >> bit) & 1ull) | ((uint32_t)((w >> (32 + bit)) & 1ull) << 1);
-        if (f != 0) {
-          const uint32_t bo = sd ? d0 : d1;
-          const uint32_t dob = (f == 3 || (f - 1) == (bo & 1u)) ? bo : bo + 1;
-          hl = a + dob;
-          hv = v;
-          hd = sd ? dob | (a << 16) : a | (dob << 16);
-        }
-      }
-      unsigned long long hm = __ballot(hl != kEmpty);
-      while (hm) {  // the meeting round only
-        const int l = __ffsll((long long)hm) - 1;
-        hm &= hm - 1;
-        const uint32_t len = __builtin_amdgcn_readlane(hl, l);
-        if (meet == kEmpty || len < md0 + md1) {
-          meet = __builtin_amdgcn_readlane(hv, l);
-          const uint32_t dd = __builtin_amdgcn_readlane(hd, l);
-          md0 = dd & 0xffffu;
-          md1 = dd >> 16;
-        }
-      }
-      const unsigned long long mask = __ballot(isnew);
-      const unsigned long long m1 = __ballot(isnew && sd);
-      uint32_t l0 = 0, l1 = 0;
-      if (mask) {
-        const OffT d = isnew ? oe - ob : (OffT)0;
-        const uint32_t dc = (uint32_t)min(d, (OffT)kDegClamp);
-        const uint32_t incl = wave_incl_scan(dc);
-        const uint32_t eb = incl - dc;
-        if (isnew) {
-          if (sd) {
-            par1[v] = u;
-            const uint32_t i = qe1 + mbcnt64(m1);
-            if (i < P.n) que1[i] = v;
-          } else {
-            par0[v] = u;
-            const uint32_t i = qe0 + mbcnt64(mask);
-            if (i < P.n) que0[i] = v;
-          }
-        }
-        append_records(Nb, isnew && (OffT)eb + d <= (OffT)CAP ? (uint32_t)d : 0u, eb, v, ob);
-        const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
-        l0 = __builtin_amdgcn_readlane(incl, E0 - 1);  // side-0 lanes are [0, E0)
-        l1 = tot - l0;
-      }
-      const uint32_t n1 = (uint32_t)__popcll(m1), n0 = (uint32_t)__popcll(mask) - n1;
-      if constexpr (kStamp) {
-        if (lane == 0 && levels + 1 < P.b.trace_cap) {
-          LevelTraceDev& t = P.b.trace[levels + 1];
-          t.side = (uint32_t)(stamp() - lt0);
-          t.depth = t.frontier = 0;
-          t.mode = 6;
-          t.edges = ET;
-        }
-      }
-      levels += 2;
-      einsp += ET;
-      ++rounds_done;
-      ++d0, ++d1;
-      qe0 += n0, qe1 += n1;
-      h0 += n0, h1 += n1;
-      c0 = n0, c1 = n1;
-      v0 += l0, v1 += l1;
-      ovf = (unsigned long long)l0 + l1 > CAP;
-      E0 = l0, E1 = l1;
-      rp0 = Nb;
-      rp1 = Nb + l0;
-      cb = nb;
-      if (meet != kEmpty) status = kFound;
-      else if (n0 == 0 || n1 == 0) status = kNoPath;
-      // next output: the buffer no side reads any more (the old current ones are free)
-      nb = (uint32_t)__builtin_ctz(~(1u << cb) & 0xfu);
-    }
-    if (rounds_done == 0) return false;
-    s0.cur = cb, s0.off = 0, s0.fed = E0, s0.depth = (int)d0, s0.fbeg = qe0 - c0, s0.qend = qe0;
-    s0.cnt = c0, s0.hcnt = h0, s0.ved = v0, s0.ovf = E0 > CAP ? 1u : 0u;
-    s1.cur = cb, s1.off = E0, s1.fed = E1, s1.depth = (int)d1, s1.fbeg = qe1 - c1, s1.qend = qe1;
-    s1.cnt = c1, s1.hcnt = h1, s1.ved = v1, s1.ovf = (unsigned long long)E0 + E1 > CAP ? 1u : 0u;
-    return true;
-  };
-
-
-  // ---- register-frontier lockstep rounds (bitmap mode, 32-bit CSR offsets,
-  // both sides together <= 256 frontier edges): the frontier's edges live in
-  // wave 0's REGISTERS -- edge e of the virtual list (side 0's edges, then
-  // side 1's) is slot e / 64 of lane e % 64 as {parent u, CSR index k} -- so a
-  // round needs no record reads and no per-edge record writes.  A round is:
-  // one packed-adjacency load per edge, the bitmap claim + opposite-side test,
-  // and the new frontier's redistribution onto lanes: exclusive degree scan,
-  // each new vertex scatters {start marker, id, row base - start} at its first
-  // edge slot in LDS, a prefix-max over the markers tells every lane the
-  // vertex its edge belongs to, two LDS gathers finish it.  One wave's LDS ops
-  // execute in order, so no barrier is needed.  Replaces the per-edge record
-  // rounds (lean_rounds): ~3x fewer instructions per round on the critical
-  // wave (rocprof: the 100k query is instruction-bound, L2 hit 93%).
-  auto reg_rounds = [&]() -> bool {
-    if constexpr (!std::is_same<OffT, uint32_t>::value || !kBm) {
-      return false;
-    } else {
-      constexpr uint32_t kSlots = kRegSlots;
-      uint32_t E0 = (uint32_t)s0.fed, E1 = (uint32_t)s1.fed;
-      if (!P.padj || E0 == 0 || E1 == 0 || E0 + E1 > kSlots * kWave || status != kRunning) return false;
-      uint32_t d0 = (uint32_t)s0.depth, d1 = (uint32_t)s1.depth;
-      uint32_t qe0 = s0.qend, qe1 = s1.qend, c0 = s0.cnt, c1 = s1.cnt, h0 = s0.hcnt, h1 = s1.hcnt;
-      unsigned long long v0 = s0.ved, v1 = s1.ved;
-      uint32_t u[kSlots], kx[kSlots];
-      {
-        const Rec* rp0 = &R[s0.cur][s0.off];
-        const Rec* rp1 = &R[s1.cur][s1.off];
-        const uint32_t E = E0 + E1;
-#pragma unroll
-        for (uint32_t q = 0; q < kSlots; ++q) {
-          const uint32_t e = q * kWave + lane;
-          const Rec r = e < E0 ? rp0[e] : rp1[e < E ? e - E0 : 0u];
-          u[q] = r.x;
-          kx[q] = r.y;
-        }
-      }
-      // scratch in record buffer 3 (its records, if any, are in registers now):
-      // MK[e] = round tag << 9 | (e + 1) at the first edge slot e of each new
-      // vertex (tagged, so no clearing: stale markers of earlier rounds lose
-      // every prefix max), VK[e] = {vertex id, row base - e}.  A frontier that
-      // outgrows the registers is materialised into record buffer 0.
-      uint32_t* const MK = reinterpret_cast<uint32_t*>(&R[3][0]);
-      uint2* const VK = reinterpret_cast<uint2*>(MK + kSlots * kWave);
-      uint32_t* const par0 = P.b.parent[0];
-      uint32_t* const par1 = P.b.parent[1];
-      uint32_t* const que0 = P.b.queue[0];
-      uint32_t* const que1 = P.b.queue[1];
-      unsigned long long* const W0 = W(0);
-      unsigned long long* const W1 = W(1);
-      const uint4* const padj = P.padj;
-      bool spilled = false;
-      uint32_t tag = 1;
-      // buffer 3 may hold records (or markers of another query): zero the markers once
-#pragma unroll
-      for (uint32_t q = 0; q < kSlots; ++q) MK[q * kWave + lane] = 0u;
-      auto round = [&](auto bc) {
-        constexpr uint32_t B = decltype(bc)::value;
-        unsigned long long lt0 = 0, lt1 = 0, lt2 = 0, lt3 = 0;
-        if constexpr (kStamp) lt0 = stamp();
-        const uint32_t E = E0 + E1;
-        uint32_t v[B], ob[B], dg[B], up[B];
-        bool ok[B], sd[B], isnew[B];
-#pragma unroll
-        for (uint32_t q = 0; q < B; ++q) {  // every load in flight before the first use
-          const uint32_t e = q * kWave + lane;
-          up[q] = u[q];  // the parent of whatever this edge claims
-          ok[q] = e < E;
-          sd[q] = e >= E0;
-          const uint4 pq = padj[min(kx[q], P.nnz_m1)];
-          v[q] = pq.x;
-          dg[q] = pq.y;
-          ob[q] = pq.z;
-        }
-        if constexpr (kStamp) {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          lt1 = stamp();
-        }
-        // claim on this side's bitmap at the parity of the new depth, then the
-        // opposite side's word (a meet candidate of exact length, parity rule)
-        uint32_t hl = kEmpty, hv = 0, hd = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < B; ++q) {
-          const uint32_t a = (sd[q] ? d1 : d0) + 1;
-          const uint32_t bit = v[q] & 31u;
-          unsigned long long* const Wm = sd[q] ? W1 : W0;
-          unsigned long long old = ~0ull;
-          if (ok[q]) old = atomicOr(&Wm[v[q] >> 5], 1ull << (bit + ((a & 1u) << 5)));
-          isnew[q] = ((old >> bit) & 0x100000001ull) == 0;
-          const unsigned long long w = (sd[q] ? W0 : W1)[v[q] >> 5];
-          const uint32_t f = (uint32_t)((w >> bit) & 1ull) | ((uint32_t)((w >> (32 + bit)) & 1ull) << 1);
-          const uint32_t bo = sd[q] ? d0 : d1;
-          const uint32_t dob = (f == 3 || (f - 1) == (bo & 1u)) ? bo : bo + 1;
-          if (isnew[q] && f != 0 && a + dob < hl) {
-            hl = a + dob;
-            hv = v[q];
-            hd = sd[q] ? dob | (a << 16) : a | (dob << 16);
-          }
-        }
-        unsigned long long hm = __ballot(hl != kEmpty);
-        while (hm) {  // the meeting round only
-          const int l = __ffsll((long long)hm) - 1;
-          hm &= hm - 1;
-          const uint32_t len = __builtin_amdgcn_readlane(hl, l);
-          if (meet == kEmpty || len < md0 + md1) {
-            meet = __builtin_amdgcn_readlane(hv, l);
-            const uint32_t dd = __builtin_amdgcn_readlane(hd, l);
-            md0 = dd & 0xffffu;
-            md1 = dd >> 16;
-          }
-        }
-        if constexpr (kStamp) lt2 = stamp();
-        // queue slots and the new frontier's degree scan (e order = queue order per side)
-        uint32_t n0 = 0, n1 = 0, carry = 0, l0 = 0;
-        uint32_t p[B], dl[B], qi[B];
-        const uint32_t qb = E0 / kWave, lb = E0 % kWave;  // the first side-1 edge: slot qb, lane lb
-#pragma unroll
-        for (uint32_t q = 0; q < B; ++q) {
-          const unsigned long long m1 = __ballot(isnew[q] && sd[q]);
-          const unsigned long long m0 = __ballot(isnew[q] && !sd[q]);
-          qi[q] = sd[q] ? qe1 + n1 + mbcnt64(m1) : qe0 + n0 + mbcnt64(m0);
-          n0 += (uint32_t)__popcll(m0);
-          n1 += (uint32_t)__popcll(m1);
-          dl[q] = isnew[q] ? min(dg[q], kDegClamp) : 0u;
-          const uint32_t incl = wave_incl_scan(dl[q]);
-          p[q] = carry + incl - dl[q];
-          if (q == qb) l0 = __builtin_amdgcn_readlane(p[q], lb);
-          carry += __builtin_amdgcn_readlane(incl, 63);
-        }
-        const uint32_t tot = carry;
-        if constexpr (kStamp) lt3 = stamp();
-        levels += 2;
-        einsp += E;
-        ++d0, ++d1;
-        qe0 += n0, qe1 += n1;
-        h0 += n0, h1 += n1;
-        c0 = n0, c1 = n1;
-        v0 += l0, v1 += tot - l0;
-        E0 = l0, E1 = tot - l0;
-        if (meet != kEmpty) status = kFound;
-        else if (n0 == 0 || n1 == 0) status = kNoPath;
-        if (status == kRunning) {
-          if (tot > kSlots * kWave) {
-            // the next frontier needs the record engine: materialise it
-#pragma unroll
-            for (uint32_t q = 0; q < B; ++q)
-              append_records(R[0], isnew[q] && p[q] + dl[q] <= CAP ? dl[q] : 0u, p[q], v[q], (OffT)ob[q]);
-            spilled = true;
-          } else {
-            ++tag;
-#pragma unroll
-            for (uint32_t q = 0; q < B; ++q)
-              if (dl[q]) {
-                MK[p[q]] = (tag << 9) | (p[q] + 1u);
-                VK[p[q]] = make_uint2(v[q], ob[q] - p[q]);
-              }
-            const uint32_t Bn = (tot + kWave - 1) / kWave;
-            uint32_t mcarry = 0;
-#pragma unroll
-            for (uint32_t q = 0; q < kSlots; ++q)
-              if (q < Bn) {
-                const uint32_t mx = max(mcarry, wave_incl_max(MK[q * kWave + lane]));
-                mcarry = __builtin_amdgcn_readlane(mx, 63);
-                const uint2 x = VK[(mx & 511u) - 1u];  // this lane's vertex: its first edge slot
-                u[q] = x.x;
-                kx[q] = x.y + q * kWave + lane;
-              }
-          }
-        }
-        // global bookkeeping last: nothing of this round waits on these stores
-        // (vmcnt counts stores; issued earlier they would stretch every wait)
-#pragma unroll
-        for (uint32_t q = 0; q < B; ++q)
-          if (isnew[q]) {
-            (sd[q] ? par1 : par0)[v[q]] = up[q];
-            if (qi[q] < P.n) (sd[q] ? que1 : que0)[qi[q]] = v[q];
-          }
-        if constexpr (kStamp) {
-          const unsigned long long lt4 = stamp();
-          if (lane == 0 && levels - 1 < P.b.trace_cap) {
-            LevelTraceDev& t = P.b.trace[levels - 1];
-            t.side = (uint32_t)(lt4 - lt0);
-            t.depth = (uint32_t)(lt1 - lt0);
-            t.frontier = (uint32_t)min(lt2 - lt1, 0xffffull) | ((uint32_t)min(lt3 - lt2, 0xffffull) << 16);
-            t.mode = 7;
-            t.edges = (unsigned long long)E | ((lt4 - lt3) << 32);
-          }
-        }
-      };
-      uint32_t rounds_done = 0;
-      for (;;) {
-        const uint32_t E = E0 + E1;
-        if (status != kRunning || spilled || E0 == 0 || E1 == 0 || E > kSlots * kWave) break;
-        if (E <= kWave) round(std::integral_constant<uint32_t, 1>{});
-        else if (kSlots == 1 || E <= 2 * kWave) round(std::integral_constant<uint32_t, (kSlots < 2 ? kSlots : 2)>{});
-        else round(std::integral_constant<uint32_t, kSlots>{});
-        ++rounds_done;
-      }
-      if (rounds_done == 0) return false;
-      s0.cur = 0, s0.off = 0, s0.fed = E0, s0.depth = (int)d0, s0.fbeg = qe0 - c0, s0.qend = qe0;
-      s0.cnt = c0, s0.hcnt = h0, s0.ved = v0, s0.ovf = E0 > CAP ? 1u : 0u;
-      s1.cur = 0, s1.off = E0, s1.fed = E1, s1.depth = (int)d1, s1.fbeg = qe1 - c1, s1.qend = qe1;
-      s1.cnt = c1, s1.hcnt = h1, s1.ved = v1, s1.ovf = (unsigned long long)E0 + E1 > CAP ? 1u : 0u;
-      return true;
-    }
-  };
-
   // ---- all-wave lockstep rounds (bitmap mode, 32-bit offsets, packed
   // adjacency; both frontiers together <= 2 x kLdsThreads edges).  The edges
   // are cut into batches of 64, side 0's batches first; wave w takes batches
@@ -1242,14 +880,6 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         if (!dual && (!fq || eq > kSmallEdges)) {
           if (!fq) status = kHandoff;
           break;  // big level (all waves) or hand-off
-        }
-        if constexpr (kBm) {
-          if (dual && (!P.trace || kStamp) && s0.fed && s1.fed) {
-            if constexpr (std::is_same<OffT, uint32_t>::value) {
-              if (kRegRounds && reg_rounds()) continue;  // state written back; re-decide
-            }
-            if (s0.fed + s1.fed <= (unsigned long long)kWave && lean_rounds()) continue;
-          }
         }
         unsigned long long ts0 = 0;
         if (kStamp && tid == 0) ts0 = stamp();
