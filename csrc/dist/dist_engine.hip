@@ -294,24 +294,52 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
   }
 }
 
+// Meet detection at claim time (speculative rounds): `meetkey` non-null.
+// Every vertex that becomes held by both sides in a round is seen by at least
+// one of its two claims: each claim's atomicOr completes (its result decides
+// `mine`) before the same thread's device-scope load of the other side's
+// word, and device-scope atomics are coherent across XCDs -- so of two
+// same-round claims the later one sees the earlier.  The other side's depth
+// of v is read the same way; kEmpty there (depth arrays are kEmpty outside a
+// search) means that side claimed v in THIS round and its store is not
+// visible yet, so the depth is its frontier depth + 1.  single: a
+// single-side level, where every meet has the same length, so the first one
+// also raises DState::meet_found and the expansion loops stop early.
+struct ClaimMeet {
+  unsigned long long* meetkey = nullptr;
+  uint32_t dother = 0;  // the other side's frontier depth this round
+  bool single = false;
+};
+
 // Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
 // every lane of the wave calls it, `want` masks lanes.  One queue append and
 // one degree-sum atomic per wave.
-// flag_meet (single-side levels): a claim of a vertex the other side already
-// holds raises DState::meet_found, so the expansion loops stop early -- in a
-// single-side level every meet has the same length (the other side's
-// frontier depth), so the first one is as good as the minimum; the exact key
-// still comes from k_meet_end over the vertices claimed.
 __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uint32_t v, uint32_t u,
-                                           uint32_t dnew, bool flag_meet = false) {
+                                           uint32_t dnew, const ClaimMeet& cm = ClaimMeet{}) {
   const uint32_t li = v - V.lo;
   uint32_t* vis = pick(V.vis, s);
   bool mine = false;
+  unsigned long long best = kNoKey;
   if (want) {
     const uint32_t bit = 1u << (li & 31);
     if (!(vis[li >> 5] & bit)) mine = !(atomicOr(&vis[li >> 5], bit) & bit);
-    if (flag_meet && mine && (pick(V.vis, s ^ 1)[li >> 5] & bit))
-      __hip_atomic_store(&V.st->meet_found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((cm.meetkey || cm.single) && mine &&
+        (__hip_atomic_load(&pick(V.vis, s ^ 1)[li >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) {
+      if (cm.meetkey) {
+        uint32_t dd = __hip_atomic_load(&pick(V.depth, s ^ 1)[li], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dd == kEmpty) dd = cm.dother + 1;
+        best = ((unsigned long long)(dnew + dd) << 32) | v;
+      }
+      if (cm.single) __hip_atomic_store(&V.st->meet_found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (cm.meetkey && __ballot(best != kNoKey)) {  // rare: the meeting round
+#pragma unroll
+    for (int o = kWave / 2; o >= 1; o >>= 1) {
+      const unsigned long long y = __shfl_xor(best, o);
+      best = y < best ? y : best;
+    }
+    if (__lane_id() == 0) atomicMin(cm.meetkey, best);
   }
   const unsigned long long mask = __ballot(mine);
   if (!mask) return;  // wave-uniform
@@ -364,7 +392,7 @@ __device__ __forceinline__ bool meet_seen(const DView& V) {
 
 // exit_on_meet: a single-side level, which stops once a meet is claimed.
 __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pairs, uint32_t cap, uint32_t b0,
-                               uint32_t nb, uint64_t hub_deg, bool exit_on_meet) {
+                               uint32_t nb, uint64_t hub_deg, bool exit_on_meet, const ClaimMeet& cm) {
   __shared__ uint32_t su[kThreads];
   __shared__ unsigned long long sb[kThreads], se[kThreads];
   __shared__ unsigned long long wsum[kThreads / kWave];
@@ -433,12 +461,41 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
         v = V.col[sb[a] + (e - se[a])];
       }
       const bool own = valid && v >= V.lo && v < V.hi;
-      wave_claim(V, s, own, v, uu, dnew, exit_on_meet);
+      wave_claim(V, s, own, v, uu, dnew, cm);
       wave_emit(V, s, valid && !own, v, uu, pairs, cap);
     }
     __syncthreads();
   }
 }
+
+// End of a speculative round on this rank, by the last workgroup of the
+// round's last claiming kernel: the per-side counts for the reduction, the
+// frontiers advanced, and the NEXT round's meet key reset (this round's plan
+// -- every workgroup of its first kernel -- has read that buffer).  `sides`
+// comes from the caller's own copy of the plan: inside the planning kernel
+// ctl[p] is block 0's plain store, not yet visible to the other workgroups.
+__device__ void spec_round_end(const DView& V, uint32_t it, uint32_t sides) {
+  const int p = it & 1;
+  DState* st = V.st;
+  for (int s = 0; s < 2; ++s) {
+    const bool on = (sides >> s) & 1;
+    const uint32_t qt = atomicAdd(&st->qtail[s], 0u);
+    const unsigned long long ne = atomicExch(&st->new_edges[s], 0ull);
+    V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - st->fend[s]) : 0ull;
+    V.red[p].sums[2 * s + 1] = on ? ne : 0ull;
+    V.red[p].nfmax[s] = on ? ~ne : ~0ull;
+    if (on) {
+      st->fbeg[s] = st->fend[s];
+      st->fend[s] = qt;
+    }
+    st->hub_count[s] = 0;
+  }
+  V.red[p ^ 1].meetkey = kNoKey;
+}
+
+// A block's claims (returning and non-returning atomics) complete before it
+// counts itself in for the last-block test of a round-ending kernel.
+__device__ __forceinline__ void drain_atomics() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Last-block detection: true in exactly one block, after every block of the
 // grid has passed this point.  No fence: the last block reads only words the
@@ -459,15 +516,16 @@ __device__ __forceinline__ bool last_block(uint32_t* counter, uint32_t nblocks) 
 
 // Plan (every block computes the same plan; block 0 publishes it) + top-down
 // pre phase of both sides (blockIdx.y = side) into blocks of `cap` pairs.
+// header = 0: k_td_hubs runs next (it writes the headers); finish: this
+// kernel ends the round's claims on this rank (one rank, no hub pass).
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
-                                                          int flags, uint64_t hub_deg, int header) {
+                                                          int flags, uint64_t hub_deg, int header, int finish) {
   const int p = it & 1;
   __shared__ Ctl c;
   if (threadIdx.x == 0) plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, cap, flags, c);
   __syncthreads();
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
-    V.red[p].meetkey = kNoKey;
     // one 8-byte write-through store per round: the host paces its enqueueing
     // on the plan and sizes the rounds it enqueues from the frontier (larger
     // side's edge count, clamped to 32 bits)
@@ -477,15 +535,24 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
   const int s = blockIdx.y;
-  if ((c.sides >> s) & 1)
+  if ((c.sides >> s) & 1) {
+    ClaimMeet cm;
+    cm.meetkey = &V.red[p].meetkey;
+    cm.dother = c.depth[s ^ 1];
+    cm.single = c.sides != 3u;
     td_expand_side(V, s, c.depth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
-                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u);
+                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u, cm);
+  }
   if (!header) return;  // k_td_hubs runs next and writes the headers
-  if (last_block(&V.st->done_blocks[0], gridDim.x * gridDim.y) && threadIdx.x < 2) {
-    const int ss = threadIdx.x;
-    const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
-    V.sendbuf[ss * block_words(cap)] = ((c.sides >> ss) & 1) ? min(cnt, cap) : 0u;
-    if (ss == 0) atomicExch(&V.st->done_blocks[0], 0u);
+  if (finish) drain_atomics();
+  if (last_block(&V.st->done_blocks[0], gridDim.x * gridDim.y)) {
+    if (threadIdx.x < 2) {
+      const int ss = threadIdx.x;
+      const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
+      V.sendbuf[ss * block_words(cap)] = ((c.sides >> ss) & 1) ? min(cnt, cap) : 0u;
+      if (ss == 0) atomicExch(&V.st->done_blocks[0], 0u);
+    }
+    if (finish && threadIdx.x == kWave) spec_round_end(V, it, c.sides);  // another wave: the header atomics are independent
   }
 }
 
@@ -496,7 +563,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
 // of hubs with their degree prefix in LDS and walks the tile's flattened edge
 // range with a grid stride, so each hub's edges spread over all CUs.
 __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int side, uint32_t dnew_fixed,
-                                                      uint32_t cap, int single) {
+                                                      uint32_t cap, int single, int finish) {
   __shared__ uint32_t hu[kHubTile];
   __shared__ unsigned long long hb[kHubTile], hp[kHubTile + 1];
   __shared__ unsigned long long wsum[kThreads / kWave];
@@ -511,6 +578,12 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   uint2* pairs = reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const bool exit_on_meet = side < 0 ? sides != 3u : single != 0;
+  ClaimMeet cm;  // speculative rounds detect meets at claim time; host rounds in k_meet_end
+  cm.single = exit_on_meet;
+  if (side < 0) {
+    cm.meetkey = &V.red[it & 1].meetkey;
+    cm.dother = V.ctl[it & 1].depth[s ^ 1];
+  }
   __shared__ uint32_t sstop;
   if ((sides >> s) & 1) {
     for (uint32_t t0 = 0; t0 < H; t0 += kHubTile) {
@@ -575,29 +648,38 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
           v = V.col[hb[a] + (e - hp[a])];
         }
         const bool own = valid && v >= V.lo && v < V.hi;
-        wave_claim(V, s, own, v, uu, dnew, exit_on_meet);
+        wave_claim(V, s, own, v, uu, dnew, cm);
         wave_emit(V, s, valid && !own, v, uu, pairs, cap);
       }
       __syncthreads();
     }
   }
   if (side >= 0) return;
-  if (last_block(&V.st->done_blocks[2], gridDim.x * gridDim.y) && threadIdx.x < 2) {
-    const int ss = threadIdx.x;
-    const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
-    V.sendbuf[ss * block_words(cap)] = ((sides >> ss) & 1) ? min(cnt, cap) : 0u;
-    if (ss == 0) atomicExch(&V.st->done_blocks[2], 0u);
+  if (finish) drain_atomics();
+  if (last_block(&V.st->done_blocks[2], gridDim.x * gridDim.y)) {
+    if (threadIdx.x < 2) {
+      const int ss = threadIdx.x;
+      const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
+      V.sendbuf[ss * block_words(cap)] = ((sides >> ss) & 1) ? min(cnt, cap) : 0u;
+      if (ss == 0) atomicExch(&V.st->done_blocks[2], 0u);
+    }
+    if (finish && threadIdx.x == kWave) spec_round_end(V, it, sides);
   }
 }
 
 // Post phase of both sides: owners claim the candidates addressed to them
 // (rank r's side-s block is recvbuf[(2r + s) * block_words(cap)]).
+// (more than one rank: this kernel ends the round's claims; its last
+// workgroup closes the round)
 __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap) {
   const Ctl& c = V.ctl[it & 1];
   const int s = blockIdx.y;
-  if (!((c.sides >> s) & 1)) return;  // block-uniform
   const uint32_t dnew = c.depth[s] + 1;
-  for (int r = 0; r < V.P; ++r) {
+  ClaimMeet cm;
+  cm.meetkey = &V.red[it & 1].meetkey;
+  cm.dother = c.depth[s ^ 1];
+  cm.single = c.sides != 3u;
+  for (int r = 0; ((c.sides >> s) & 1) && r < V.P; ++r) {  // block-uniform
     const uint32_t* b = V.recvbuf + (2 * (uint64_t)r + s) * block_words(cap);
     const uint32_t cnt = min(b[0], cap);
     const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
@@ -611,8 +693,13 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
         u = x.y;
         want = v >= V.lo && v < V.hi;
       }
-      wave_claim(V, s, want, v, u, dnew);
+      wave_claim(V, s, want, v, u, dnew, cm);
     }
+  }
+  drain_atomics();
+  if (last_block(&V.st->done_blocks[1], gridDim.x * gridDim.y) && threadIdx.x == 0) {
+    spec_round_end(V, it, c.sides);
+    atomicExch(&V.st->done_blocks[1], 0u);
   }
 }
 
@@ -671,6 +758,7 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags) 
   Ctl c;
   plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, flags, c);
   publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
+  V.red[p ^ 1].meetkey = kNoKey;  // read; it is the buffer of the next round (it + 1)
   *host = c;
   __threadfence_system();
 }
@@ -689,8 +777,10 @@ __global__ void k_plan_force(DView V, uint32_t it, Policy pol) {
 
 __global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t dnew, uint64_t hub_deg,
                                                         int single) {
+  ClaimMeet cm;  // host rounds: keys from k_meet_end; the flag only stops a single-side level early
+  cm.single = single != 0;
   td_expand_side(V, s, dnew, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(V.cap)) + 1, V.cap, blockIdx.x,
-                 gridDim.x, hub_deg, single != 0);
+                 gridDim.x, hub_deg, single != 0, cm);
 }
 
 __global__ void k_send_header(DView V, int s, uint32_t it) {
@@ -823,6 +913,7 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     }
   }
   r.meetkey = kNoKey;
+  V.red[0].meetkey = kNoKey;  // round 0 detects its meets into red[0]
   Ctl c = {};
   c.dir[0] = c.dir[1] = 1;
   c.state = kRun;
@@ -963,7 +1054,12 @@ __global__ void k_cleanup(DView V, uint64_t sent_words) {
     const uint32_t qn = V.st->qtail[s];
     const uint32_t* q = pick(V.queue, s);
     uint32_t* vis = pick(V.vis, s);
-    for (uint64_t i = tid; i < qn; i += nth) vis[(q[i] - V.lo) >> 5] = 0u;
+    uint32_t* dep = pick(V.depth, s);
+    for (uint64_t i = tid; i < qn; i += nth) {
+      const uint32_t li = q[i] - V.lo;
+      vis[li >> 5] = 0u;
+      dep[li] = kEmpty;  // claim-time meet detection reads kEmpty as "not visible yet"
+    }
   }
   uint4* sw = reinterpret_cast<uint4*>(V.sent[0]);  // both sides, contiguous, 256-B aligned
   for (uint64_t i = tid; i < sent_words / 4; i += nth) sw[i] = make_uint4(0, 0, 0, 0);
@@ -1115,6 +1211,7 @@ struct DistBiBfs::Impl {
       V.gbits[s] = reinterpret_cast<uint32_t*>(b + o_gb[s]);
       V.sent[s] = sent_base + (size_t)s * gwords;
       HIP_CHECK(hipMemsetAsync(V.vis[s], 0, words * 4, stream));
+      HIP_CHECK(hipMemsetAsync(V.depth[s], 0xff, (size_t)chunk * 4, stream));  // kEmpty
     }
     V.sendbuf = reinterpret_cast<uint32_t*>(b + o_send);
     V.recvbuf = reinterpret_cast<uint32_t*>(b + o_recv);
@@ -1270,7 +1367,7 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
       k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, hubs ? kHubDeg : kNoHubs, ns == 1);
       if (hubs)
         k_td_hubs<<<blocks_for(std::min<uint64_t>(h.fed[s], (uint64_t)cus * 8 * kThreads), cus), kThreads, 0, ps>>>(
-            V, it, s, dnew, capr, ns == 1);
+            V, it, s, dnew, capr, ns == 1, 0);
       k_send_header<<<1, 64, 0, ps>>>(V, s, it);
     } else {
       HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
@@ -1440,15 +1537,18 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       const bool hubs = cap_it > kSpecHubCap;
       const unsigned hx = std::min<unsigned>((unsigned)cus, cap_it / kThreads + 1);
       maybe_fault((int)it);
+      // The round's last claiming kernel closes it (meets were detected at
+      // claim time): the claim kernel with more than one rank, else the hub
+      // pass or the expansion itself -- no separate meet / round-end kernel.
+      const int end_in_expand = (P == 1 && !hubs) ? 1 : 0;
       k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
-                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1);
-      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0);
+                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0);
       HIP_CHECK(hipGetLastError());
       if (P > 1) {  // one rank owns every vertex: expand claimed them all, the blocks are empty
         comm->allgather(V.sendbuf, V.recvbuf, gather_bytes, cs);
         k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, cap_it);
       }
-      k_meet_end<<<std::min<unsigned>(bx, 64), kThreads, 0, cs>>>(V, it);
       HIP_CHECK(hipGetLastError());
       if (P > 1) {  // a one-rank reduction is the identity
         comm->group_begin();
