@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Per-pair device search time of the resident server on the bench's 100k
+pairs (bench.py pick_pairs), median over repeats, with levels and edges.
+Shows which queries dominate the headline mean.
+
+    python benchmarks/pair_latency.py [--graph gnp:100000::6] [--pairs 64] [--reps 20]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--graph", default="gnp:100000::6")
+    ap.add_argument("--pairs", type=int, default=64)
+    ap.add_argument("--reps", type=int, default=20)
+    a = ap.parse_args()
+    import torch  # noqa: F401  (HIP runtime first)
+    import bench
+    from bidirectional_bfs_amd.ops import HipEngine
+
+    _, n, _, _ = bench.parse_spec(a.graph)
+    eng = bench.generate(HipEngine(0), a.graph)
+    eng.set_resident(True)
+    pairs = bench.pick_pairs(eng, n, a.pairs, 12345)
+    for s, d, h in pairs:
+        dev, tot = [], []
+        for _ in range(a.reps):
+            r = eng.search(s, d)
+            assert r.hops == h
+            dev.append(r.search_ms)
+            tot.append(r.total_ms)
+        print(json.dumps({"src": s, "dst": d, "hops": h, "search_us": round(statistics.median(dev) * 1e3, 2),
+                          "query_us": round(statistics.median(tot) * 1e3, 2), "levels": r.levels,
+                          "edges": r.edges_inspected, "visited": r.visited}), flush=True)
+    eng.set_resident(False)
+
+
+if __name__ == "__main__":
+    main()

@@ -80,6 +80,12 @@ constexpr bool kAppendBallot = BIBFS_KNOB_APPEND_BALLOT;
 #define BIBFS_KNOB_WAVE_ROUNDS 1
 #endif
 constexpr bool kWaveRounds = BIBFS_KNOB_WAVE_ROUNDS;
+// 1 = an all-wave round that cannot carry both frontiers expands the smaller
+// side alone (while it fits) instead of leaving the all-wave rounds.
+#ifndef BIBFS_KNOB_WAVE_SINGLE
+#define BIBFS_KNOB_WAVE_SINGLE 1
+#endif
+constexpr bool kWaveSingle = BIBFS_KNOB_WAVE_SINGLE;
 // batches of 64 edges per wave in those rounds (1: frontiers up to 1024 edges, 2: 2048)
 #ifndef BIBFS_KNOB_WAVE_B
 #define BIBFS_KNOB_WAVE_B 2
@@ -659,7 +665,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       uint32_t slot = 0, rounds_done = 0;
-      bool ovf = false;
+      uint32_t X0 = 0, X1 = 0;  // edges each side expands this round (0: the side idles)
       auto round = [&](auto bc, uint32_t nb0, uint32_t nbt, uint32_t x0, uint32_t x1) {
         constexpr int B = decltype(bc)::value;
         unsigned long long lt0 = 0, lt1 = 0, lsub = 0;  // kStamp: round start / work done / sub-phases
@@ -683,7 +689,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           act[k] = bt < nbt;  // scalar
           sd[k] = bt >= nb0;  // scalar
           const uint32_t e = (bt - (sd[k] ? nb0 : 0u)) * kWave + lane;
-          ok[k] = act[k] && e < (sd[k] ? E1 : E0);
+          ok[k] = act[k] && e < (sd[k] ? X1 : X0);
           const Rec r = (sd[k] ? &R[a1][o1] : &R[a0][o0])[ok[k] ? e : 0u];
           u[k] = r.x;
           const uint4 pq = padj[min(r.y, P.nnz_m1)];
@@ -767,13 +773,29 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         sub(3);
         return lsub;
       };
+      constexpr uint32_t kMaxBatches = kWaveB * (kLdsThreads / kWave);
       for (;;) {
-        const uint32_t ET = E0 + E1;
-        const uint32_t nb0 = (E0 + kWave - 1) / kWave, nbt = nb0 + (E1 + kWave - 1) / kWave;
-        // every claim of the round must fit the LDS queue (a side claims at most E new vertices)
-        if (status != kRunning || ovf || E0 == 0 || E1 == 0 || nbt > kWaveB * (kLdsThreads / kWave) ||
-            qe0 + E0 > kQCap || qe1 + E1 > kQCap || (!kBm && (h0 + E0 > kHashLimit || h1 + E1 > kHashLimit)))
-          break;
+        if (status != kRunning || E0 == 0 || E1 == 0) break;
+        // A side can expand here when its records are all in LDS (E <= CAP),
+        // its batches fit the waves and every claim fits the LDS queue (a side
+        // claims at most E new vertices).  Both sides when both fit together
+        // (lockstep: one round per two levels); otherwise the side with fewer
+        // edges alone while it fits -- an unbalanced pair (one frontier past the
+        // queue or record bound) then still ends in LDS instead of handing the
+        // search to the wave-0 schedule.  The meet rule covers an idle side.
+        const uint32_t nb0e = (E0 + kWave - 1) / kWave, nb1e = (E1 + kWave - 1) / kWave;
+        const bool f0 = E0 <= CAP && nb0e <= kMaxBatches && qe0 + E0 <= kQCap && (kBm || h0 + E0 <= kHashLimit);
+        const bool f1 = E1 <= CAP && nb1e <= kMaxBatches && qe1 + E1 <= kQCap && (kBm || h1 + E1 <= kHashLimit);
+        bool run0 = f0, run1 = f1;
+        if (!(f0 && f1 && nb0e + nb1e <= kMaxBatches)) {
+          if (!kWaveSingle || !(f0 || f1)) break;
+          run0 = f0 && (!f1 || E0 <= E1);
+          run1 = !run0;
+        }
+        X0 = run0 ? E0 : 0u;
+        X1 = run1 ? E1 : 0u;
+        const uint32_t ET = X0 + X1;
+        const uint32_t nb0 = run0 ? nb0e : 0u, nbt = nb0 + (run1 ? nb1e : 0u);
         const uint32_t used = (1u << a0) | (1u << a1);
         const uint32_t x0 = (uint32_t)__builtin_ctz(~used & 0xfu);
         const uint32_t x1 = (uint32_t)__builtin_ctz(~(used | (1u << x0)) & 0xfu);
@@ -801,8 +823,9 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           md1 = side ? a : mk_hi - a;
         }
         if constexpr (kStamp) {
-          if (tid == 0 && levels + 1 < P.b.trace_cap) {
-            LevelTraceDev& t = P.b.trace[levels + 1];
+          const uint32_t lv = levels + (run0 && run1 ? 1u : 0u);
+          if (tid == 0 && lv < P.b.trace_cap) {
+            LevelTraceDev& t = P.b.trace[lv];
             const unsigned long long rt2r = stamp();
             t.side = (uint32_t)(rt2r - rt0r);
             t.depth = (uint32_t)(rt1r - rt0r);
@@ -812,19 +835,17 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
             t.discovered = lsub;
           }
         }
-        levels += 2;
+        levels += (run0 ? 1u : 0u) + (run1 ? 1u : 0u);
         einsp += ET;
         ++rounds_done;
-        ++d0, ++d1;
-        qe0 += n0, qe1 += n1;
-        h0 += n0, h1 += n1;
-        c0 = n0, c1 = n1;
-        v0 += l0, v1 += l1;
-        E0 = l0, E1 = l1;
-        a0 = x0, o0 = 0, a1 = x1, o1 = 0;
-        ovf = l0 > CAP || l1 > CAP;
+        if (run0) {  // an idle side keeps its frontier, records and counts
+          ++d0, qe0 += n0, h0 += n0, c0 = n0, v0 += l0, E0 = l0, a0 = x0, o0 = 0;
+        }
+        if (run1) {
+          ++d1, qe1 += n1, h1 += n1, c1 = n1, v1 += l1, E1 = l1, a1 = x1, o1 = 0;
+        }
         if (meet != kEmpty) status = kFound;
-        else if (n0 == 0 || n1 == 0) status = kNoPath;
+        else if ((run0 && n0 == 0) || (run1 && n1 == 0)) status = kNoPath;
         slot = sn;
       }
       if (status != kRunning) {
