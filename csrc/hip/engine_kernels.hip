@@ -91,6 +91,7 @@ constexpr bool kWaveSingle = BIBFS_KNOB_WAVE_SINGLE;
 #define BIBFS_KNOB_WAVE_B 2
 #endif
 constexpr uint32_t kWaveB = BIBFS_KNOB_WAVE_B;
+static_assert(kWaveB == 1 || kWaveB == 2 || kWaveB == 4, "batches per wave: 1, 2 or 4");
 // 1 = the all-wave rounds also run with LDS hash visited sets (graphs above
 // 131072 vertices); 0 = bitmap graphs only.  A/B (profiles/r2_wave_hash_ab.txt):
 // 1M G(n,p) 28.9 -> 27.4 us, but 10M 110 -> 122 us -- the LDS queue costs
@@ -803,8 +804,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         if constexpr (kStamp) rt0r = stamp();
         if (kWaveB == 1 || nbt <= (uint32_t)(kLdsThreads / kWave))
           lsub = round(std::integral_constant<int, 1>{}, nb0, nbt, x0, x1);
-        else
+        else if (kWaveB == 2 || nbt <= 2u * (kLdsThreads / kWave))
           lsub = round(std::integral_constant<int, (kWaveB > 1 ? 2 : 1)>{}, nb0, nbt, x0, x1);
+        else
+          lsub = round(std::integral_constant<int, (kWaveB > 2 ? 4 : 1)>{}, nb0, nbt, x0, x1);
         unsigned long long rt1r = 0;
         if constexpr (kStamp) rt1r = stamp();
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // LDS-only: stores stay in flight
