@@ -253,3 +253,33 @@ def test_search_batch_global_pass(gpu_engine, spec):
     finally:
         gpu_engine.batch_edge_cap = cap0
         gpu_engine.set_batch_tuning(-1, 0)
+
+
+def _lollipop(n_path, n_blob, p_blob, seed):
+    """A long path glued to a dense G(n, p) blob: a query from the path's far
+    end into the blob has one tiny frontier and one that grows fast -- the
+    unbalanced shape the all-wave rounds serve one side at a time."""
+    blob = native.gen_gnp(n_blob, p_blob, seed).edges().astype(np.int64) + n_path
+    path = [[i, i + 1] for i in range(n_path - 1)] + [[n_path - 1, n_path]]
+    return Graph.from_edges(n_path + n_blob, np.concatenate([np.asarray(path, dtype=np.int64), blob]))
+
+
+@pytest.mark.parametrize("resident", [False, True])
+def test_unbalanced_frontiers_in_lds(gpu_engine, resident):
+    """Bitmap-mode graphs (n <= 131072) whose two frontiers outgrow the
+    lockstep round unevenly: single-side all-wave rounds, meets right after a
+    switch, empty frontiers (no path), all against the oracle."""
+    rnd = random.Random(11)
+    graphs = [gnp(100000, 3.2 / 100000, 9),          # fast-growing frontiers
+              gnp(120000, 1.6 / 120000, 4),          # many small components: no-path pairs
+              rmat(65536, 400000, 7),                # hubs next to leaves
+              _lollipop(40, 60000, 6.0 / 60000, 3)]  # tiny side vs big side
+    for g in graphs:
+        gpu_engine.load(g)
+        gpu_engine.set_resident(resident)
+        n = g.n
+        pairs = [(0, n - 1), (n - 1, 0)] + [(rnd.randrange(n), rnd.randrange(n)) for _ in range(40)]
+        if g.n == 60040:
+            pairs += [(rnd.randrange(40), 40 + rnd.randrange(60000)) for _ in range(20)]
+        assert_engine(gpu_engine, g, pairs)
+        gpu_engine.set_resident(False)
