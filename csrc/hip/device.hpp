@@ -72,13 +72,19 @@ struct HostResult {
 // The request is ONE 16-byte word, read by the server with a single PCIe
 // load per poll (a poll of pinned host memory costs ~1 us): {seq, src, dst,
 // tag} with tag = flags | (seq & 0xffffff) << 8, so a torn read is detected.
-struct alignas(16) ServerBox {
+// The request owns the first 64-byte line and the server's status words the
+// second: the server's per-query diagnostic stores then never invalidate the
+// host's copy of the request line, and the host's post never has to re-fetch
+// a line the GPU just wrote.
+struct alignas(64) ServerBox {
   uint32_t seq, src, dst, tag;  // host -> server
+  uint32_t req_pad[12];
   uint32_t alive;  // server -> host: its launch seq while running, ~launch seq after exit
   uint32_t stage;  // server -> host (diagnostics): 1 polling, 2 request taken, 3 answered
   uint32_t seen;   // last request seq the server took
-  uint32_t pad[9];
+  uint32_t pad[13];
 };
+static_assert(sizeof(ServerBox) == 128, "request line + status line");
 constexpr uint32_t kReqStop = 1u, kReqLockstep = 2u;  // tag flags; side policy in bits 2..3
 __host__ __device__ inline uint32_t req_tag(uint32_t seq, uint32_t flags) { return (flags & 0xffu) | (seq << 8); }
 
