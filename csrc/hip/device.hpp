@@ -201,7 +201,7 @@ void batch_global(const GraphView& g, uint32_t words, const uint32_t* qidx, uint
 // (res_seq).  hub_deg != ~0u: frontier vertices above that degree are deferred
 // to the edge-parallel hub pass enqueued behind, which then finishes the level.
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
-                  dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
+                  uint64_t frontier_edges, dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
                   uint32_t hub_deg, hipStream_t s);
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
 void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);

@@ -1419,6 +1419,10 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
 // ============================================================================
 constexpr int kGridThreads = 256;
 constexpr uint32_t kHubDegree = 4096;  // deferred to k_grid_hubs
+#ifndef BIBFS_KNOB_GRID_CHUNK_MIN
+#define BIBFS_KNOB_GRID_CHUNK_MIN 64
+#endif
+constexpr uint64_t kGridChunkMin = BIBFS_KNOB_GRID_CHUNK_MIN;  // smallest chunk (vertices) of k_grid_topdown
 
 template <typename OffT>
 struct GridParams {
@@ -1433,6 +1437,7 @@ struct GridParams {
   launch::HostSide h;  // fused publish of a finished search (path + result)
   uint32_t res_seq;
   uint32_t hub_deg;    // frontier vertices above this degree go to k_grid_hubs (~0u: never)
+  uint32_t chunk_v;    // k_grid_topdown: frontier vertices per chunk ticket (<= kGridThreads)
 };
 
 template <typename OffT>
@@ -1487,11 +1492,12 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     if (tid == 0) schunk = (load_agent(&st->meet) != kEmpty) ? kEmpty : atomicAdd(&st->chunk, 1u);
     __syncthreads();
     const uint32_t c = schunk;
-    if (c == kEmpty || (uint64_t)c * kGridThreads >= F) break;
-    const uint32_t i = c * kGridThreads + tid;
+    const uint32_t cv = P.chunk_v;
+    if (c == kEmpty || (uint64_t)c * cv >= F) break;
+    const uint32_t i = c * cv + tid;
     uint32_t deg = 0, u = 0;
     OffT b = 0;
-    if (i < F) {
+    if ((uint32_t)tid < cv && i < F) {
       u = P.b.queue[s][fbase + i];
       b = P.row_off[u];
       deg = (uint32_t)(P.row_off[u + 1] - b);
@@ -1951,6 +1957,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.h = launch::HostSide{nullptr, nullptr, 0, nullptr};
   P.res_seq = 0;
   P.hub_deg = kHubDegree;
+  P.chunk_v = kGridThreads;
   return P;
 }
 
@@ -2034,18 +2041,28 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
 uint32_t grid_hub_degree() { return kHubDegree; }
 
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
-                  dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
+                  uint64_t frontier_edges, dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
                   uint32_t hub_deg, hipStream_t s) {
-  // Dynamic chunks of 256 frontier vertices; never more blocks than chunks:
+  // Dynamic chunks of frontier vertices; never more blocks than chunks:
   // every block takes at least one ticket from ONE counter, and 1024 blocks
-  // contending on it cost ~12 us even for a 3-vertex frontier.
-  const uint64_t chunks = (frontier + kGridThreads - 1) / kGridThreads;
+  // contending on it cost ~12 us even for a 3-vertex frontier.  A chunk is
+  // sized to about one 256-edge batch of the frontier's mean degree (64..256
+  // vertices): a block walks its chunk's edges in serial batches, each a chain
+  // of dependent loads and atomics, so a mid-size frontier (10^3-10^5
+  // vertices, degree ~2) spreads over 4x the blocks instead of running ~3
+  // batches back to back on a few CUs.  Frontiers that fill every block keep
+  // 256-vertex chunks (fewer ticket atomics).
+  uint64_t cv = kGridThreads;
+  if ((frontier + kGridThreads - 1) / kGridThreads < (uint64_t)cus * 4 && frontier_edges > 0)
+    cv = std::min<uint64_t>(kGridThreads, std::max<uint64_t>(kGridChunkMin, kGridThreads * frontier / frontier_edges));
+  const uint64_t chunks = (frontier + cv - 1) / cv;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, chunks));
   const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
   auto launch_one = [&](auto P) {
     using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
     P.mirror = mirror, P.seq = seq, P.trace = trace, P.h = h, P.res_seq = res_seq;
     P.hub_deg = hub_deg;  // ~0u: no hub pass
+    P.chunk_v = (uint32_t)cv;
     k_grid_topdown<OffT><<<blocks, kGridThreads, 0, s>>>(P);
     if (hub_deg != ~0u) k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
   };

@@ -394,7 +394,7 @@ struct HipBiBfs::Impl {
       uint32_t hub_deg = ~0u;
       if (max_deg > launch::grid_hub_degree() && fe > launch::grid_hub_degree()) hub_deg = launch::grid_hub_degree();
       if (F <= 4096 && fe > 16384 && max_deg > 64) hub_deg = 64;
-      launch::grid_topdown(g, buf, s, cus, F, h_state, ls, trace, hs, res_seq, hub_deg, stream);
+      launch::grid_topdown(g, buf, s, cus, F, fe, h_state, ls, trace, hs, res_seq, hub_deg, stream);
       fbits_valid[s] = false;
     }
     wait_level();
