@@ -1423,6 +1423,15 @@ constexpr uint32_t kHubDegree = 4096;  // deferred to k_grid_hubs
 #define BIBFS_KNOB_GRID_CHUNK_MIN 64
 #endif
 constexpr uint64_t kGridChunkMin = BIBFS_KNOB_GRID_CHUNK_MIN;  // smallest chunk (vertices) of k_grid_topdown
+// Single-side grid levels stop at their first meet (every meet of such a level
+// has the same length).  The edge loops of k_grid_topdown / k_grid_hubs read
+// the meet word every (mask + 1) batches of 256 edges per workgroup: a
+// Kronecker hub level spans only a few grid-stride iterations, so a sparse
+// check never fires before the level has walked every hub edge.
+#ifndef BIBFS_KNOB_MEET_CHECK_MASK
+#define BIBFS_KNOB_MEET_CHECK_MASK 0
+#endif
+constexpr uint32_t kMeetCheckMask = BIBFS_KNOB_MEET_CHECK_MASK;
 
 template <typename OffT>
 struct GridParams {
@@ -1532,7 +1541,9 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     for (uint32_t base = 0, it = 0; base < Ec; base += kGridThreads, ++it) {
       // a meet ends the level (single-side level: every meet has the same
       // length): check it every 16 batches, wave-uniformly
-      if ((it & 15) == 15 && __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty) break;
+      if (it > 0 && (it & kMeetCheckMask) == kMeetCheckMask &&
+          __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty)
+        break;
       const uint32_t e = base + tid;
       const bool valid = e < Ec;
       uint32_t uu = 0, v = 0;
@@ -1613,7 +1624,9 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
     uint32_t it = 0;
     for (unsigned long long base = (unsigned long long)blockIdx.x * kGridThreads; base < tot;
          base += (unsigned long long)gridDim.x * kGridThreads, ++it) {
-      if ((it & 15) == 15 && __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty) break;
+      if (it > 0 && (it & kMeetCheckMask) == kMeetCheckMask &&
+          __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty)
+        break;
       const unsigned long long e = base + tid;
       const bool valid = e < tot;
       uint32_t uu = 0, v = 0;

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 out=gpurun_out/ab_grid.txt
 : > $out
 for rep in 1 2; do
-  for g in gnp:10000000::1 kron:22:16:1; do
+  for g in ${GRAPHS:-gnp:10000000::1 kron:22:16:1}; do
     for d in build/var/*/; do
       v=$(basename $d)
       r=$(LD_LIBRARY_PATH=$d timeout -k 5 120 python3 bench.py --graph $g --steps 200 --warmup 20 --extra-graph "" \
