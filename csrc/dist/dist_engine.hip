@@ -446,7 +446,7 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
     uint32_t iter = 0;
     for (unsigned long long base = 0; base < tot; base += kThreads, ++iter) {
       // wave-uniform exit (no barrier in this loop)
-      if (exit_on_meet && (iter & 15) == 15 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
+      if (exit_on_meet && iter > 0 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
       const unsigned long long e = base + tid;
       const bool valid = e < tot;
       uint32_t uu = 0, v = 0;
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
       uint32_t iter = 0;
       for (unsigned long long base = (unsigned long long)blockIdx.x * kThreads; base < tot;
            base += (unsigned long long)gridDim.x * kThreads, ++iter) {
-        if (exit_on_meet && (iter & 15) == 15 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
+        if (exit_on_meet && iter > 0 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
         const unsigned long long e = base + tid;
         const bool valid = e < tot;
         uint32_t uu = 0, v = 0;
