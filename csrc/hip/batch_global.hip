@@ -144,6 +144,10 @@ __global__ __launch_bounds__(kBgThreads) void k_batch_global(BgArgs A) {
       __syncthreads();
       einsp += total;
       for (uint32_t e = tid; e < total; e += kBgThreads) {
+        // every meet of this level has the same length (see above): the
+        // first one ends the level (a Kronecker hub level would otherwise
+        // walk all its edges on this one CU)
+        if (__hip_atomic_load(&meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != kEmpty) break;
         // owner vertex: last j with pre[j] <= e
         uint32_t lo = 0, hi = kBgThreads;
         while (hi - lo > 1) {
@@ -162,6 +166,7 @@ __global__ __launch_bounds__(kBgThreads) void k_batch_global(BgArgs A) {
         if (ld_agent(&bt[wi]) & bit) atomicMin(&meet, v);
       }
       __syncthreads();  // pre/rowb/vtx are rewritten by the next chunk
+      if (meet != kEmpty) break;  // block-uniform: read after the barrier
     }
     // plain stores of parent/queue become visible to every lane of the block
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
