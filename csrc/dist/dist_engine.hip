@@ -981,8 +981,11 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
     }
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  auto parent_of = [&](int s, uint32_t v, bool& ok) -> uint32_t {
+  // lanes 0 and 1 of wave 0 walk one side each: the chain lengths, then (with
+  // the meet's position known) each side's half of the path
+  if (threadIdx.x >= 2) return;
+  const int s = (int)threadIdx.x;
+  auto parent_of = [&](uint32_t v, bool& ok) -> uint32_t {
     uint32_t h = home(s, v);
     for (uint32_t probe = 0; probe < nslot[s]; ++probe) {
       const uint32_t k = keys[s][2 * h];
@@ -994,29 +997,34 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
     return kEmpty;
   };
   bool ok = true;
-  uint32_t d[2] = {0, 0};
-  for (int s = 0; s < 2 && ok; ++s)  // chain lengths
-    for (uint32_t v = meet, u; ok && (u = parent_of(s, v, ok)) != kEmpty && d[s] <= hops; v = u) ++d[s];
-  if (!ok || d[0] + d[1] != hops) {
-    out[0] = 1;
-    out[1] = d[0];
-    out[2] = d[1];
+  uint32_t d = 0;
+  for (uint32_t v = meet, u; ok && (u = parent_of(v, ok)) != kEmpty && d <= hops; v = u) ++d;
+  const uint32_t dx = (uint32_t)__shfl_xor((int)d, 1), okx = (uint32_t)__shfl_xor(ok ? 1 : 0, 1);
+  const uint32_t d0 = s ? dx : d, d1 = s ? d : dx;
+  if (!ok || !okx || d0 + d1 != hops) {
+    if (s == 0) {
+      out[0] = 1;
+      out[1] = d0;
+      out[2] = d1;
+    }
     return;
   }
-  uint32_t* path = out + 4;  // src .. meet .. dst
+  uint32_t* path = out + 4;  // src .. meet .. dst; both lanes write the meet at d0
   uint32_t v = meet;
-  for (int i = (int)d[0]; i >= 0; --i) {
-    path[i] = v;
-    v = parent_of(0, v, ok);
+  if (s == 0) {
+    for (int i = (int)d0; i >= 0; --i) {
+      path[i] = v;
+      v = parent_of(v, ok);
+    }
+    out[0] = 0;
+    out[1] = d0;
+    out[2] = d1;
+  } else {
+    for (uint32_t i = d0; i <= hops; ++i) {
+      path[i] = v;
+      v = parent_of(v, ok);
+    }
   }
-  v = meet;
-  for (uint32_t i = d[0]; i <= hops; ++i) {
-    path[i] = v;
-    v = parent_of(1, v, ok);
-  }
-  out[0] = 0;
-  out[1] = d[0];
-  out[2] = d[1];
 }
 
 // Fallback for very large visited sets: the owner of the meet vertex
