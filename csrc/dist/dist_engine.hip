@@ -752,7 +752,9 @@ __global__ __launch_bounds__(kThreads) void k_meet_end(DView V, uint32_t it) {
 
 // Account the last enqueued round and publish Ctl to the host (pinned).
 // flags = kPlanAccountOnly, or kPlanStall to also plan the next round for the host.
-__global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags) {
+// Writes the accounted Ctl to pinned host memory, then `tag` into the pinned
+// word the host spins on (no stream query on the host side).
+__global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags, uint32_t* fin, uint32_t tag) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int p = it & 1;
   Ctl c;
@@ -761,6 +763,15 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags) 
   V.red[p ^ 1].meetkey = kNoKey;  // read; it is the buffer of the next round (it + 1)
   *host = c;
   __threadfence_system();
+  __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// End-of-stream marker for DistBiBfs::Impl::wait: everything before it in the
+// stream has completed (and its writes are visible) once the host sees `tag`.
+__global__ void k_host_tag(uint32_t* fin, uint32_t tag) {
+  if (threadIdx.x != 0) return;
+  __threadfence_system();
+  __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- host-planned round kernels ---------------------------------------------
@@ -1113,6 +1124,8 @@ struct DistBiBfs::Impl {
   RoundRec* d_trace = nullptr;
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
+  uint32_t* h_fin = nullptr;   // pinned, k_final's tag (written after h_ctl)
+  uint32_t fin_seq = 0;
   uint64_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
   uint32_t* h_walk = nullptr;  // pinned
   size_t h_walk_cap = 0;
@@ -1140,6 +1153,8 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipEventCreate(&ev_t1));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl), sizeof(Ctl), hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_fin), 64, hipHostMallocDefault));
+    *h_fin = 0;
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 8, hipHostMallocDefault));
     std::memset(h_plan, 0, kPlanRing * 8);
     V.plan_ring = h_plan;
@@ -1264,18 +1279,32 @@ struct DistBiBfs::Impl {
     nnz = rows.nnz();
   }
 
-  // Host wait with a watchdog: poll the stream; an RCCL error reported by the
+  // Host wait with a watchdog.  A one-lane kernel at the end of the stream
+  // writes a tag into pinned memory and the host spins on it: it sees the
+  // stream drain one PCIe write after the last kernel instead of at the next
+  // hipStreamQuery poll (~10-20 us later on this stack; A/B in
+  // profiles/r2_dist_fintag_ab.txt).  An RCCL error reported by the
   // communicator, or no progress within timeout_s (a dead or hung peer leaves
   // our collective waiting forever), aborts the communicator and throws.
   void wait(hipStream_t s) {
+    fin_seq = fin_seq + 1 == 0 ? 1 : fin_seq + 1;
+    const uint32_t tag = fin_seq;
+    k_host_tag<<<1, 64, 0, s>>>(h_fin, tag);
+    HIP_CHECK(hipGetLastError());
     stats.host_syncs++;
+    spin_tag(tag, s);
+  }
+
+  void spin_tag(uint32_t tag, hipStream_t s) {
     const auto t0 = std::chrono::steady_clock::now();
     const auto deadline = t0 + std::chrono::duration<double>(tune.timeout_s);
     for (uint64_t spin = 0;; ++spin) {
-      const hipError_t e = hipStreamQuery(s);
-      if (e == hipSuccess) return;
-      if (e != hipErrorNotReady) HIP_CHECK(e);
-      if ((spin & 255) == 255) {
+      if (__atomic_load_n(h_fin, __ATOMIC_ACQUIRE) == tag) return;
+      if ((spin & 1023) == 1023) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e != hipSuccess && e != hipErrorNotReady) HIP_CHECK(e);
+        if (e == hipSuccess && __atomic_load_n(h_fin, __ATOMIC_ACQUIRE) != tag)
+          throw Error("dist: stream drained without its host tag");
         comm->check();
         const auto now = std::chrono::steady_clock::now();
         if (now > deadline) {
@@ -1286,6 +1315,19 @@ struct DistBiBfs::Impl {
         if (now - t0 > std::chrono::milliseconds(2)) std::this_thread::sleep_for(std::chrono::microseconds(50));
       }
     }
+  }
+
+  // Enqueue k_final and wait for it through its pinned tag: the host sees the
+  // accounted Ctl one PCIe write after the kernel ends instead of at the next
+  // hipStreamQuery poll.  k_final is the last work in the stream here, so
+  // this is a full host sync.  Same watchdog as wait().
+  void final_and_wait(uint32_t it, const Policy& pol, int flags, hipStream_t s) {
+    fin_seq = fin_seq + 1 == 0 ? 1 : fin_seq + 1;
+    const uint32_t tag = fin_seq;
+    k_final<<<1, 64, 0, s>>>(V, it, pol, h_ctl, flags, h_fin, tag);
+    HIP_CHECK(hipGetLastError());
+    stats.host_syncs++;
+    spin_tag(tag, s);
   }
 
   // Spin until the device has planned round `need` and return ITS plan word
@@ -1481,9 +1523,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   const bool host_only = K == 0;  // A/B mode: every round planned on the host
   const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
   if (host_only) {
-    k_final<<<1, 64, 0, cs>>>(V, it++, pol, h_ctl, kPlanStall);
-    HIP_CHECK(hipGetLastError());
-    wait(cs);
+    final_and_wait(it++, pol, kPlanStall, cs);
     have_ctl = true;
   }
   for (uint64_t guard = 0;; ++guard) {
@@ -1500,10 +1540,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       } else {
         maybe_fault((int)it);
         host_round(it, pol, r);
-        k_final<<<1, 64, 0, cs>>>(V, it + 1, pol, h_ctl, host_only ? kPlanStall : kPlanAccountOnly);
-        HIP_CHECK(hipGetLastError());
+        final_and_wait(it + 1, pol, host_only ? kPlanStall : kPlanAccountOnly, cs);
         it += 2;
-        wait(cs);
         const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
         spec_cap = std::min(spec_max, std::max<uint32_t>(kSpecCapMin, next_pow2(4 * fm)));
         continue;
@@ -1571,9 +1609,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     }
     spec_cap = cap_it;
     flags = 0;
-    k_final<<<1, 64, 0, cs>>>(V, it++, pol, h_ctl, kPlanAccountOnly);
-    HIP_CHECK(hipGetLastError());
-    wait(cs);
+    final_and_wait(it++, pol, kPlanAccountOnly, cs);
     have_ctl = true;
     if (h_ctl->state == kRun) {  // size the next batch for the frontier we have now
       const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
@@ -1619,6 +1655,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       }
   }
   float dms = 0.f;
+  // the host saw the stream's tag; the runtime may mark the event complete a moment later
+  HIP_CHECK(hipEventSynchronize(ev_t1));
   HIP_CHECK(hipEventElapsedTime(&dms, ev_t0, ev_t1));
   stats.device_ms = dms;
   r.stats.grid_levels = r.stats.levels;
@@ -1732,6 +1770,7 @@ DistBiBfs::~DistBiBfs() {
   p_->comm.reset();
   (void)hipHostFree(p_->h_red);
   (void)hipHostFree(p_->h_ctl);
+  (void)hipHostFree(p_->h_fin);
   (void)hipHostFree(p_->h_plan);
   if (p_->h_walk) (void)hipHostFree(p_->h_walk);
   for (auto e : p_->ev_pre) (void)hipEventDestroy(e);
