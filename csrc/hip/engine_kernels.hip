@@ -1796,6 +1796,9 @@ __device__ void publish_result(const launch::SearchBuffers& b, const launch::Hos
     Rr->depth[1] = d1;
     Rr->path_len = status == kFound ? hops + 1 : 0u;
     Rr->path_on_device = (status == kFound && hops + 1 > h.path_cap) ? 1u : 0u;
+    // end of a search that left LDS: rt_begin is the LDS kernel's stamp, so
+    // rt_end - rt_begin is the device-side span of the whole search
+    Rr->rt_end = __builtin_amdgcn_s_memrealtime();
     __threadfence_system();
     __hip_atomic_store(&Rr->seq, res_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }

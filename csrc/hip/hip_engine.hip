@@ -857,7 +857,6 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
       grid = true;
       stats.handoff = true;
       I.mirror_valid = true;  // the LDS kernel published the hand-off state
-      HIP_CHECK(hipEventRecord(I.ev0, I.stream));
     }
   } else {
     launch::seed_state(g, I.buf, src, dst, I.stream);
@@ -875,12 +874,18 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
       I.wait_seq(pub_seq);
     }
   }
-  if (grid) HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  // device time of a hand-off search: the grid publish stamps rt_end on the
+  // same 100 MHz clock as the LDS kernel's rt_begin (no events, no event sync
+  // on the query path); a search that never ran in LDS is timed with events
+  const bool timed_by_events = grid && !stats.handoff;
+  if (timed_by_events) HIP_CHECK(hipEventRecord(I.ev1, I.stream));
   SearchResult r = I.collect(pub_seq, opt, std::move(stats));
   r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   r.search_ms = lds_ms;
-  if (grid) {
-    launch::cleanup(I.buf, I.n, I.stream);  // async: next query is stream-ordered behind it
+  if (grid && !timed_by_events && I.h_res->seq == pub_seq)
+    r.search_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;
+  if (grid) launch::cleanup(I.buf, I.n, I.stream);  // async: next query is stream-ordered behind it
+  if (timed_by_events) {
     HIP_CHECK(hipEventSynchronize(I.ev1));
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
