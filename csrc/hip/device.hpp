@@ -211,7 +211,8 @@ uint32_t grid_hub_degree();
 void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
                uint32_t n, hipStream_t s);
-void cleanup(const SearchBuffers& b, uint32_t n, hipStream_t s);
+void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
+             bool if_done, hipStream_t s);
 
 }  // namespace launch
 }  // namespace bibfs

@@ -1940,13 +1940,28 @@ __global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t 
 // Reset the visited words of every vertex a grid search claimed (all of them
 // are in the queues), so the next search starts from all-zero bitmaps without
 // an O(N) memset.
-__global__ void k_cleanup(launch::SearchBuffers b) {
+// Clears the visited words of every queued vertex.  The last workgroup then
+// writes `tag` to pinned host memory: the resident server runs on another
+// stream, so the host checks the tag before a new search may hand off into
+// these bitmaps.
+// if_done: enqueued behind every grid level, it only runs once a level has
+// ended the search (then right behind that level, with no launch latency).
+__global__ void k_cleanup(launch::SearchBuffers b, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
+                          int if_done) {
   const DevState* st = b.st;
+  if (if_done && load_agent(&st->status) == kRunning) return;  // grid-uniform
   for (int s = 0; s < 2; ++s) {
     const uint32_t q = st->qtail[s];
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < q;
          i += (uint64_t)gridDim.x * blockDim.x)
       b.vis[s][b.queue[s][i] >> 5] = 0u;
+  }
+  __threadfence();  // this thread's clears are device-visible before the block counts itself done
+  __syncthreads();
+  if (threadIdx.x == 0 && atomicAdd(done_ctr, 1u) == gridDim.x - 1) {
+    *done_ctr = 0;
+    __threadfence_system();
+    __hip_atomic_store(host_tag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -2130,9 +2145,10 @@ void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t
   HIP_CHECK(hipGetLastError());
 }
 
-void cleanup(const SearchBuffers& b, uint32_t n, hipStream_t s) {
+void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
+             bool if_done, hipStream_t s) {
   (void)n;
-  k_cleanup<<<512, 256, 0, s>>>(b);
+  k_cleanup<<<64, 1024, 0, s>>>(b, done_ctr, host_tag, tag, if_done ? 1 : 0);  // few blocks: one done-counter atomic each
   HIP_CHECK(hipGetLastError());
 }
 

@@ -46,7 +46,33 @@ struct HipBiBfs::Impl {
   launch::SearchBuffers buf{};
   void* state_block = nullptr;  // one allocation holding every per-search array
   size_t state_bytes = 0;
-  uint32_t* d_flag = nullptr;
+  uint32_t* d_flag = nullptr;     // [0] bitmap-meet flag, [4] election ticket, [8] cleanup done counter
+  uint32_t* h_clean = nullptr;    // pinned: tag of the last finished k_cleanup
+  uint32_t clean_seq = 0, clean_pending = 0;
+  bool grid_cleaned = false;  // the search's last grid level enqueued the cleanup that ran
+
+  // async cleanup of the global visited words; its tag lets the host order
+  // the resident server's next hand-off (another stream) after it
+  void cleanup_async(bool if_done = false) {
+    clean_seq = clean_seq + 1 == 0 ? 1 : clean_seq + 1;
+    clean_pending = clean_seq;
+    launch::cleanup(buf, n, d_flag + 8, h_clean, clean_seq, if_done, stream);
+  }
+  void wait_cleanup() {
+    if (!clean_pending) return;
+    for (uint64_t it = 1; __atomic_load_n(h_clean, __ATOMIC_ACQUIRE) != clean_pending; ++it) {
+      if ((it & 8191) == 0) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess && __atomic_load_n(h_clean, __ATOMIC_ACQUIRE) != clean_pending)
+          throw Error("bibfs: cleanup finished without its tag");
+        if (e != hipSuccess && e != hipErrorNotReady)
+          throw Error(std::string("bibfs: cleanup failed: ") + hipGetErrorString(e));
+      } else {
+        _mm_pause();
+      }
+    }
+    clean_pending = 0;
+  }
 
   // pinned host memory
   HostResult* h_res = nullptr;
@@ -215,6 +241,7 @@ struct HipBiBfs::Impl {
 
   void free_graph() {
     stop_server();
+    clean_pending = 0;  // hipFree below synchronises the device: any cleanup has finished
     free_batch();
     if (d_row_off) HIP_CHECK(hipFree(d_row_off));
     if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
@@ -397,6 +424,9 @@ struct HipBiBfs::Impl {
       launch::grid_topdown(g, buf, s, cus, F, fe, h_state, ls, trace, hs, res_seq, hub_deg, stream);
       fbits_valid[s] = false;
     }
+    // the cleanup rides behind every level and runs behind the one that ends
+    // the search, so it is done about when the host has read the answer
+    if (res_seq) cleanup_async(true);
     wait_level();
   }
 
@@ -520,6 +550,8 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_state), sizeof(DevState),
                           hipHostMallocMapped | hipHostMallocCoherent));  // k_finish_level writes it
   std::memset(p_->h_res, 0, sizeof(HostResult));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_clean), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(p_->h_clean, 0, 64);
   HIP_CHECK(hipEventCreate(&p_->ev0));
   HIP_CHECK(hipEventCreate(&p_->ev1));
 }
@@ -535,6 +567,7 @@ HipBiBfs::~HipBiBfs() {
   (void)hipStreamDestroy(p_->sstream);
   (void)hipHostFree(p_->h_box);
   (void)hipHostFree(p_->h_res);
+  (void)hipHostFree(p_->h_clean);
   (void)hipHostFree(p_->h_path);
   (void)hipHostFree(p_->h_state);
   (void)hipEventDestroy(p_->ev0);
@@ -837,6 +870,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     // BIBFS_STAMP_SERVER: the server's profiling build answers traced queries too
     static const bool stamp_srv = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
     if (I.resident && (!opt.trace || stamp_srv) && I.server_usable()) {
+      I.wait_cleanup();  // the server (own stream) may hand off into the bitmaps the last cleanup clears
       I.server_query(src, dst, opt, seq);
       if (I.dbg())
         std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",
@@ -869,9 +903,11 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     I.grid_loop(opt, stats);
     I.res_seq = 0;
     I.mirror_valid = false;
+    I.grid_cleaned = stats.grid_levels > 0;
     if (I.h_res->seq != pub_seq) {  // ended before any grid level ran (meet at hand-off / seed)
       launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
       I.wait_seq(pub_seq);
+      I.grid_cleaned = false;
     }
   }
   // device time of a hand-off search: the grid publish stamps rt_end on the
@@ -884,7 +920,9 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   r.search_ms = lds_ms;
   if (grid && !timed_by_events && I.h_res->seq == pub_seq)
     r.search_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;
-  if (grid) launch::cleanup(I.buf, I.n, I.stream);  // async: next query is stream-ordered behind it
+  // the last grid level's predicated cleanup did the work (its tag is the
+  // pending one); a search that ended before any grid level cleans up here
+  if (grid && !I.grid_cleaned) I.cleanup_async();
   if (timed_by_events) {
     HIP_CHECK(hipEventSynchronize(I.ev1));
     float ms = 0;
@@ -949,8 +987,9 @@ SearchResult HipBiBfs::finish() {
     SearchOptions opt;
     r = I.collect(seq, opt, SearchStats{});
   }
-  launch::cleanup(I.buf, I.n, I.stream);
+  I.cleanup_async();
   HIP_CHECK(hipStreamSynchronize(I.stream));
+  I.clean_pending = 0;
   return r;
 }
 
