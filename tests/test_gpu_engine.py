@@ -283,3 +283,28 @@ def test_unbalanced_frontiers_in_lds(gpu_engine, resident):
             pairs += [(rnd.randrange(40), 40 + rnd.randrange(60000)) for _ in range(20)]
         assert_engine(gpu_engine, g, pairs)
         gpu_engine.set_resident(False)
+
+
+def test_resident_back_to_back_handoffs(gpu_engine):
+    """Back-to-back resident queries that all leave LDS: the server (own
+    stream) must not start the next search while the previous one's cleanup
+    (engine stream) still reads and clears the global visited words."""
+    g = kronecker(22, 16, 5)
+    gpu_engine.load(g)
+    rnd = random.Random(3)
+    pairs = []
+    while len(pairs) < 8:
+        s, d = rnd.randrange(g.n), rnd.randrange(g.n)
+        h = native.bfs_oracle(g.csr, s, d).hops
+        if h > 0:
+            pairs.append((s, d, h))
+    gpu_engine.set_resident(True)
+    try:
+        for i in range(600):
+            s, d, h = pairs[i % len(pairs)]
+            r = gpu_engine.search(s, d)
+            assert r.hops == h, (i, s, d, r.hops, h)
+            if i % 100 == 0:
+                check_result(g.csr, s, d, r.hops, r.path, h)
+    finally:
+        gpu_engine.set_resident(False)
