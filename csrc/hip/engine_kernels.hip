@@ -1950,11 +1950,21 @@ __global__ void k_cleanup(launch::SearchBuffers b, uint32_t* done_ctr, uint32_t*
                           int if_done) {
   const DevState* st = b.st;
   if (if_done && load_agent(&st->status) == kRunning) return;  // grid-uniform
-  for (int s = 0; s < 2; ++s) {
-    const uint32_t q = st->qtail[s];
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < q;
-         i += (uint64_t)gridDim.x * blockDim.x)
-      b.vis[s][b.queue[s][i] >> 5] = 0u;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (((uint64_t)st->qtail[0] + st->qtail[1]) * 32 > b.words) {
+    // a large visited set (a hub level): streaming every word beats one
+    // dependent queue load per cleared word
+    for (int s = 0; s < 2; ++s) {
+      uint4* w4 = reinterpret_cast<uint4*>(b.vis[s]);
+      const uint64_t n4 = b.words / 4;
+      for (uint64_t i = t0; i < n4; i += stride) w4[i] = make_uint4(0u, 0u, 0u, 0u);
+      for (uint64_t i = n4 * 4 + t0; i < b.words; i += stride) b.vis[s][i] = 0u;
+    }
+  } else {
+    for (int s = 0; s < 2; ++s) {
+      const uint32_t q = st->qtail[s];
+      for (uint64_t i = t0; i < q; i += stride) b.vis[s][b.queue[s][i] >> 5] = 0u;
+    }
   }
   __threadfence();  // this thread's clears are device-visible before the block counts itself done
   __syncthreads();
