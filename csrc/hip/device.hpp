@@ -86,6 +86,7 @@ struct alignas(64) ServerBox {
 };
 static_assert(sizeof(ServerBox) == 128, "request line + status line");
 constexpr uint32_t kReqStop = 1u, kReqLockstep = 2u;  // tag flags; side policy in bits 2..3
+constexpr uint32_t kReqAltBuf = 16u;                   // tag flag: search in the server's second state set
 __host__ __device__ inline uint32_t req_tag(uint32_t seq, uint32_t flags) { return (flags & 0xffu) | (seq << 8); }
 
 // Result of one query of the batched global-visited kernel (batch_global.hip).
@@ -184,8 +185,8 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
                 int lockstep, hipStream_t s);
 int lds_threads();
 size_t lds_bytes(bool wide);
-void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, dev::ServerBox* box,
-                uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
+void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers& b_alt, const HostSide& h,
+                dev::ServerBox* box, uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
                 unsigned long long idle_ticks, hipStream_t s);
 void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* h_src, uint32_t* h_dst,
                uint32_t k, uint32_t* d_slots, dev::HostResult* h_res, uint32_t* h_path, uint32_t path_cap,

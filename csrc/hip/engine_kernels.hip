@@ -179,6 +179,10 @@ struct LdsParams {
   // 0: fresh LDS (one-shot / batch kernels); resident server: 1 = its first
   // search, 2 = a later one (LDS kept from the previous search in this launch)
   int resident = 0;
+  // resident server: the second search-state set (request flag kReqAltBuf);
+  // the host alternates sets so a search never shares its global state with
+  // the previous search's still-running cleanup
+  launch::SearchBuffers b_alt{};
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -1324,7 +1328,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
   // (readfirstlane): with a lane-divergent-looking loop exit the structurizer
   // may keep lanes 1..63 of wave 0 looping over the barriers while lane 0
   // waits to poll -- a deadlock.  So the whole of wave 0 polls, uniformly.
-  __shared__ uint32_t cmd[6];  // stop, seq, src, dst, side_policy, lockstep
+  __shared__ uint32_t cmd[7];  // stop, seq, src, dst, side_policy, lockstep, state set
   __shared__ uint32_t srv_won;
   const int tid = threadIdx.x;
   const uint32_t wid = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
@@ -1380,6 +1384,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
         cmd[3] = rq.z;
         cmd[4] = (rq.w >> 2) & 3u;
         cmd[5] = (rq.w & kReqLockstep) ? 1u : 0u;
+        cmd[6] = (rq.w & kReqAltBuf) ? 1u : 0u;
       }
     }
     // LDS-only barriers around the request: the diagnostic stores to host
@@ -1401,6 +1406,7 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
     Q.side_policy = (int)uni(cmd[4]);
     Q.lockstep = (int)uni(cmd[5]);
     Q.trace = kStamp ? 2 : 0;  // kStamp: BIBFS_STAMP_SERVER profiling build of the server
+    if (uni(cmd[6])) Q.b = P.b_alt;
     Q.resident = first ? 1 : 2;
     first = false;
     last_seq = Q.seq;
@@ -2039,13 +2045,14 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   HIP_CHECK(hipGetLastError());
 }
 
-void lds_server(const GraphView& g, const SearchBuffers& b, const HostSide& h, dev::ServerBox* box,
-                uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
+void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers& b_alt, const HostSide& h,
+                dev::ServerBox* box, uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
                 unsigned long long idle_ticks, hipStream_t s) {
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   BIBFS_REQUIRE(g.row_off32 != nullptr, "resident server: 32-bit row offsets required");
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
+  P.b_alt = b_alt;
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);

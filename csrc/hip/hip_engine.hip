@@ -44,26 +44,35 @@ struct HipBiBfs::Impl {
 
   // search state
   launch::SearchBuffers buf{};
-  void* state_block = nullptr;  // one allocation holding every per-search array
+  void* state_block = nullptr;  // one allocation holding every per-search array (state set 0)
+  void* state_block_alt = nullptr;  // state set 1 (resident queries alternate)
+  size_t state_bytes_alt = 0;
   size_t state_bytes = 0;
   uint32_t* d_flag = nullptr;     // [0] bitmap-meet flag, [4] election ticket, [8] cleanup done counter
   uint32_t* h_clean = nullptr;    // pinned: tag of the last finished k_cleanup
   uint32_t clean_seq = 0, clean_pending = 0;
+  // two search-state sets: resident queries alternate between them, so a
+  // search never shares global state with the previous search's cleanup
+  launch::SearchBuffers bufs[2]{};
+  int cur = 0;
+  uint32_t clean_tag[2] = {0, 0};  // last cleanup enqueued on each set
   bool grid_cleaned = false;  // the search's last grid level enqueued the cleanup that ran
 
   // async cleanup of the global visited words; its tag lets the host order
   // the resident server's next hand-off (another stream) after it
+  // tags increase and cleanups finish in stream order, so "done" is h_clean >= tag
   void cleanup_async(bool if_done = false) {
     clean_seq = clean_seq + 1 == 0 ? 1 : clean_seq + 1;
     clean_pending = clean_seq;
+    clean_tag[cur] = clean_seq;
     launch::cleanup(buf, n, d_flag + 8, h_clean, clean_seq, if_done, stream);
   }
-  void wait_cleanup() {
-    if (!clean_pending) return;
-    for (uint64_t it = 1; __atomic_load_n(h_clean, __ATOMIC_ACQUIRE) != clean_pending; ++it) {
+  void wait_tag(uint32_t tag) {
+    if (!tag) return;
+    for (uint64_t it = 1; (int32_t)(__atomic_load_n(h_clean, __ATOMIC_ACQUIRE) - tag) < 0; ++it) {
       if ((it & 8191) == 0) {
         const hipError_t e = hipStreamQuery(stream);
-        if (e == hipSuccess && __atomic_load_n(h_clean, __ATOMIC_ACQUIRE) != clean_pending)
+        if (e == hipSuccess && (int32_t)(__atomic_load_n(h_clean, __ATOMIC_ACQUIRE) - tag) < 0)
           throw Error("bibfs: cleanup finished without its tag");
         if (e != hipSuccess && e != hipErrorNotReady)
           throw Error(std::string("bibfs: cleanup failed: ") + hipGetErrorString(e));
@@ -71,7 +80,19 @@ struct HipBiBfs::Impl {
         _mm_pause();
       }
     }
+  }
+  void wait_cleanup() {
+    wait_tag(clean_pending);
     clean_pending = 0;
+    clean_tag[0] = clean_tag[1] = 0;
+  }
+  // Resident query: switch to the other state set and wait only for the
+  // cleanup last enqueued on THAT set (two searches ago: normally long done).
+  void flip_state_set() {
+    cur ^= 1;
+    buf = bufs[cur];
+    wait_tag(clean_tag[cur]);
+    clean_tag[cur] = 0;
   }
 
   // pinned host memory
@@ -173,8 +194,8 @@ struct HipBiBfs::Impl {
     if (dbg()) std::fprintf(stderr, "[server] launch seq %u pin %d\n", srv_launch_seq, pin);
     __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
     const uint32_t last = __atomic_load_n(&h_box->seq, __ATOMIC_ACQUIRE);
-    launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box, srv_launch_seq, last, pin,
-                       d_flag + 4, srv_idle_ticks, sstream);
+    launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
+                       srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, sstream);
     srv_running = true;
   }
 
@@ -193,7 +214,7 @@ struct HipBiBfs::Impl {
     if (srv_running && __atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) == ~srv_launch_seq)
       srv_running = false;  // idled out (a relaunch queues behind its last instructions)
     if (!srv_running) launch_server(pin_xcc);
-    post(qseq, src, dst, (opt.lockstep ? kReqLockstep : 0u) | ((uint32_t)opt.side & 3u) << 2);
+    post(qseq, src, dst, (opt.lockstep ? kReqLockstep : 0u) | ((uint32_t)opt.side & 3u) << 2 | (cur ? kReqAltBuf : 0u));
     if (dbg()) std::fprintf(stderr, "[server] post %u (stage %u alive %u)\n", qseq, h_box->stage, h_box->alive);
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t it = 1;; ++it) {
@@ -227,8 +248,8 @@ struct HipBiBfs::Impl {
           const uint32_t pending = qseq;
           srv_launch_seq = ++seq == 0 ? ++seq : seq;
           __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
-          launch::lds_server(view(), buf, launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box, srv_launch_seq,
-                             pending - 1, pin_xcc, d_flag + 4, srv_idle_ticks, sstream);
+          launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
+                             srv_launch_seq, pending - 1, pin_xcc, d_flag + 4, srv_idle_ticks, sstream);
           srv_running = true;
         } else if (e != hipErrorNotReady) {
           throw Error(std::string("bibfs: resident server failed: ") + hipGetErrorString(e));
@@ -249,6 +270,9 @@ struct HipBiBfs::Impl {
     if (d_padj) HIP_CHECK(hipFree(d_padj));
     if (d_uv) HIP_CHECK(hipFree(d_uv));
     if (state_block) HIP_CHECK(hipFree(state_block));
+    if (state_block_alt) HIP_CHECK(hipFree(state_block_alt));
+    state_block_alt = nullptr;
+    state_bytes_alt = 0;
     d_row_off = nullptr;
     d_row_off32 = nullptr;
     d_col = nullptr;
@@ -262,6 +286,20 @@ struct HipBiBfs::Impl {
   // One allocation for every per-search array, sized for the 288 GB HBM of
   // the part: 3 bitmaps pairs (n/8 B each) + parent/queue (4n B each) per side.
   void alloc_state() {
+    const uint64_t words = ((uint64_t)n + 63) / 64 * 2 + 2;
+    // set 1 first (the same layout, its own block), then set 0 below as before
+    alloc_state_set();
+    bufs[1] = buf;
+    state_block_alt = state_block;
+    state_bytes_alt = state_bytes;
+    alloc_state_set();
+    bufs[0] = buf;
+    cur = 0;
+    clean_tag[0] = clean_tag[1] = 0;
+    (void)words;
+  }
+
+  void alloc_state_set() {
     const uint64_t words = ((uint64_t)n + 63) / 64 * 2 + 2;
     const uint64_t trace_cap = 4096;
     size_t off = 0;
@@ -821,7 +859,7 @@ size_t HipBiBfs::device_bytes() const {
   const auto& I = *p_;
   return ((size_t)I.n + 1) * 8 + (I.d_row_off32 ? ((size_t)I.n + 1) * 4 : 0) + I.nnz * 4 +
          (I.d_padj ? I.nnz * 16 : 0) +
-         (I.d_uv ? I.uv_m * 8 : 0) + I.state_bytes;
+         (I.d_uv ? I.uv_m * 8 : 0) + I.state_bytes + I.state_bytes_alt;
 }
 int HipBiBfs::device() const { return p_->device; }
 void* HipBiBfs::stream() const { return p_->stream; }
@@ -870,7 +908,7 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     // BIBFS_STAMP_SERVER: the server's profiling build answers traced queries too
     static const bool stamp_srv = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
     if (I.resident && (!opt.trace || stamp_srv) && I.server_usable()) {
-      I.wait_cleanup();  // the server (own stream) may hand off into the bitmaps the last cleanup clears
+      I.flip_state_set();  // the server (own stream) must not share state with a running cleanup
       I.server_query(src, dst, opt, seq);
       if (I.dbg())
         std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",
