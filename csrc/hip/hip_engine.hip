@@ -89,6 +89,7 @@ struct HipBiBfs::Impl {
   // Resident query: switch to the other state set and wait only for the
   // cleanup last enqueued on THAT set (two searches ago: normally long done).
   void flip_state_set() {
+    ensure_alt_set();
     cur ^= 1;
     buf = bufs[cur];
     wait_tag(clean_tag[cur]);
@@ -286,17 +287,32 @@ struct HipBiBfs::Impl {
   // One allocation for every per-search array, sized for the 288 GB HBM of
   // the part: 3 bitmaps pairs (n/8 B each) + parent/queue (4n B each) per side.
   void alloc_state() {
-    const uint64_t words = ((uint64_t)n + 63) / 64 * 2 + 2;
-    // set 1 first (the same layout, its own block), then set 0 below as before
     alloc_state_set();
+    bufs[0] = buf;
+    bufs[1] = launch::SearchBuffers{};  // allocated by the first resident query
+    cur = 0;
+    clean_tag[0] = clean_tag[1] = 0;
+  }
+
+  // State set 1 (same layout, its own block), on the first resident query:
+  // graph loads and one-shot use pay nothing for it.  The server takes both
+  // sets at launch, so a running server is stopped first (it relaunches on
+  // the query being posted).
+  void ensure_alt_set() {
+    if (state_block_alt) return;
+    stop_server();
+    void* const blk0 = state_block;
+    const size_t bytes0 = state_bytes;
+    uint32_t* const flag0 = d_flag;
+    const launch::SearchBuffers set0 = buf;
+    alloc_state_set();  // into buf / state_block / state_bytes / d_flag
     bufs[1] = buf;
     state_block_alt = state_block;
     state_bytes_alt = state_bytes;
-    alloc_state_set();
-    bufs[0] = buf;
-    cur = 0;
-    clean_tag[0] = clean_tag[1] = 0;
-    (void)words;
+    state_block = blk0;
+    state_bytes = bytes0;
+    d_flag = flag0;
+    buf = set0;
   }
 
   void alloc_state_set() {
