@@ -43,7 +43,7 @@ PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include()
 PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
 
 CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp
-HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/batch_global.hip csrc/hip/hip_engine.hip \
+HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/tiny_engine.hip csrc/hip/batch_global.hip csrc/hip/hip_engine.hip \
              csrc/hip/capi.hip csrc/dist/comm.hip csrc/dist/dist_engine.hip
 MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp
 
@@ -70,7 +70,7 @@ micro: $(BIN)/lat_probe $(BIN)/mailbox_rtt
 # The LDS engine's counter atomics are already issued by one lane per wave:
 # the compiler's wave-reduction rewrite of them only adds instructions to the
 # latency-bound rounds.
-$(OBJ)/hip/engine_kernels.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
+$(OBJ)/hip/engine_kernels.o $(OBJ)/hip/tiny_engine.o: HIPFLAGS += -mllvm -amdgpu-atomic-optimizer-strategy=None
 
 $(BIN)/mailbox_rtt: benchmarks/micro/mailbox_rtt.hip
 	@mkdir -p $(BIN)

@@ -72,6 +72,28 @@ class HipEngine:
             options = make_options(**kw) if kw else _DEFAULT_OPTIONS
         return self._e.search(int(src), int(dst), options)
 
+    def query(self, src: int, dst: int):
+        """Serving entry point: ``(hops, path)`` with hops = -1 when there is no
+        path.  With ``set_resident(True)`` a small graph (n <= 2^17) is answered
+        by the resident tiny server (csrc/hip/tiny_engine.hip: one launch for
+        the engine's lifetime, one mailbox round trip per query); everything
+        else goes through ``search``."""
+        return self._e.query(src, dst)
+
+    @property
+    def last_search_ms(self) -> float:
+        """Device time of the last ``query`` (request seen -> answer written)."""
+        return self._e.last_search_ms
+
+    @property
+    def last_edges_inspected(self) -> int:
+        return self._e.last_edges_inspected
+
+    @property
+    def tiny_engine(self) -> bool:
+        """The loaded graph carries the tiny server's packed adjacency."""
+        return self._e.tiny_engine
+
     def search_batch(self, pairs, options: Optional["native.SearchOptions"] = None, **kw):
         """Answer many queries with one launch, one CU per query (throughput serving)."""
         if options is None:

@@ -1847,6 +1847,11 @@ void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, d
 
 SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   auto& I = *p_;
+  // Input errors fail identically on every rank before any collective is
+  // enqueued: they must not abort the communicator (a bad query would
+  // otherwise poison every later search).
+  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
+  BIBFS_REQUIRE(src < I.n && dst < I.n, "src/dst out of range");
   try {
     return I.search(src, dst, opt);
   } catch (...) {
@@ -1958,6 +1963,22 @@ std::vector<SearchResult> dist_local_run(int ranks, int device, const EdgeList& 
                          [&](DistBiBfs& e, int r, std::vector<SearchResult>& out) {
                            e.load_edges(el);
                            for (const auto& q : queries) {
+                             // an out-of-range query fails on every rank before any
+                             // collective: reported as hops -2, the group keeps serving
+                             if (q.first >= el.n || q.second >= el.n) {
+                               bool threw = false;
+                               try {
+                                 e.search(q.first, q.second, opt);
+                               } catch (const Error&) {
+                                 threw = true;
+                               }
+                               BIBFS_REQUIRE(threw, "dist: an out-of-range query did not raise");
+                               SearchResult bad;
+                               bad.hops = -2;
+                               out.push_back(bad);
+                               if (r == 0 && stats) stats->push_back(DistLevelStats{});
+                               continue;
+                             }
                              out.push_back(e.search(q.first, q.second, opt));
                              if (r == 0 && stats) stats->push_back(e.last_stats());
                            }

@@ -22,7 +22,11 @@
 //     All meets found in the first meeting level have the same length
 //     d_s + 1 + d_t: a neighbour v of u (depth d_s) that the other side reached
 //     at depth < d_t would have been expanded by it, so u would already be on
-//     both sides.  Any meet vertex therefore gives a shortest path.
+//     both sides.  Any meet vertex therefore gives a shortest path.  The
+//     level stops at the first meet it sees, so WHICH shortest path a batch
+//     returns depends on scheduling (it may differ between runs and from
+//     search()); the hop count does not.  The contract is "any shortest path"
+//     (tie-breaking is unspecified in every reference engine).
 //   * A level whose frontier has more than `edge_cap` edges stops the query
 //     with kHandoff; the host answers it with the single-query engine, whose
 //     bottom-up levels suit hub-heavy frontiers better than one CU does.

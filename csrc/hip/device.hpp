@@ -89,6 +89,33 @@ constexpr uint32_t kReqStop = 1u, kReqLockstep = 2u;  // tag flags; side policy 
 constexpr uint32_t kReqAltBuf = 16u;                   // tag flag: search in the server's second state set
 __host__ __device__ inline uint32_t req_tag(uint32_t seq, uint32_t flags) { return (flags & 0xffu) | (seq << 8); }
 
+// ---- small-graph resident server (tiny_engine.hip) --------------------------
+// Graphs up to kTinyMaxN vertices keep both visited sets in LDS as bitmaps and
+// read a packed adjacency: one 8-byte word per directed edge holding the
+// neighbour id, its CSR base and its degree, so a level costs ONE dependent
+// global load.  Word layout: v[63:47] | base[46:20] | deg[19:0].
+constexpr uint32_t kTinyMaxN = 1u << 17;
+constexpr uint64_t kTinyMaxNnz = 1ull << 27;
+constexpr int kTinyB = 2;  // frontier edges per lane per round
+// per-wave edge sums are scanned as two 16-bit halves: 64 lanes x kTinyB x deg < 2^16
+constexpr uint32_t kTinyMaxDeg = 65535u / (64u * kTinyB);
+__host__ __device__ inline uint64_t tiny_pack(uint32_t v, uint64_t base, uint64_t deg) {
+  return (uint64_t)v << 47 | base << 20 | deg;
+}
+// The answer: 16-byte packets, each carrying the query's seq in its first
+// word and written by one 16-byte system-scope store, so the host checks every
+// packet by itself and no release fence orders them (a packet is read whole
+// by one 16-byte host load).
+//   packet 0: {seq, status | levels << 8, hops, meet}
+//   packet 1: {seq, device ticks (100 MHz, request seen -> answer), edges inspected, visited}
+//   packet 2+: {seq, path[3j], path[3j+1], path[3j+2]}
+struct alignas(16) TinyPkt {
+  uint32_t seq, a, b, c;
+};
+enum : uint32_t { kTinyFound = 1, kTinyNoPath = 2, kTinyOverflow = 3 };
+constexpr uint32_t kTinyQ = 4096;  // LDS queue capacity per side (12-bit queue indices)
+constexpr uint32_t kTinyPktCap = 2 + (2 * kTinyQ + 2) / 3 + 1;
+
 // Result of one query of the batched global-visited kernel (batch_global.hip).
 struct BatchOut {
   uint32_t status;
@@ -178,6 +205,24 @@ uint64_t max_degree(const uint64_t* d_row_off, uint32_t n, hipStream_t s);  // s
 uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);
 void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,
                      uint32_t* d_uv, hipStream_t s);
+
+// tiny_engine.hip
+struct TinyArgs {
+  const unsigned long long* tadj;   // nnz packed words
+  const unsigned long long* tinfo;  // n packed words (the vertex's own)
+  uint32_t n;
+  dev::ServerBox* box;
+  dev::TinyPkt* pkts;               // pinned, kTinyPktCap packets
+  uint32_t launch_seq, last_seq;
+  int pin_xcc;
+  uint32_t* ticket;
+  unsigned long long idle_ticks;
+  unsigned long long* stamps;       // device, 16 words (stamp build only)
+};
+bool tiny_supported(uint32_t n, uint64_t nnz, uint64_t max_deg);
+void build_tiny_adj(const uint64_t* row_off, const uint32_t* col, uint32_t n, uint64_t nnz,
+                    unsigned long long* tadj, unsigned long long* tinfo, hipStream_t s);
+void tiny_server(const TinyArgs& a, bool stamp, hipStream_t s);
 
 // engine_kernels.hip
 void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, uint32_t src,

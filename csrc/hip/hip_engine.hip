@@ -50,7 +50,7 @@ struct HipBiBfs::Impl {
   size_t state_bytes = 0;
   uint32_t* d_flag = nullptr;     // [0] bitmap-meet flag, [4] election ticket, [8] cleanup done counter
   uint32_t* h_clean = nullptr;    // pinned: tag of the last finished k_cleanup
-  uint32_t clean_seq = 0, clean_pending = 0;
+  uint32_t clean_seq = 0;
   // two search-state sets: resident queries alternate between them, so a
   // search never shares global state with the previous search's cleanup
   launch::SearchBuffers bufs[2]{};
@@ -63,7 +63,6 @@ struct HipBiBfs::Impl {
   // tags increase and cleanups finish in stream order, so "done" is h_clean >= tag
   void cleanup_async(bool if_done = false) {
     clean_seq = clean_seq + 1 == 0 ? 1 : clean_seq + 1;
-    clean_pending = clean_seq;
     clean_tag[cur] = clean_seq;
     launch::cleanup(buf, n, d_flag + 8, h_clean, clean_seq, if_done, stream);
   }
@@ -80,11 +79,6 @@ struct HipBiBfs::Impl {
         _mm_pause();
       }
     }
-  }
-  void wait_cleanup() {
-    wait_tag(clean_pending);
-    clean_pending = 0;
-    clean_tag[0] = clean_tag[1] = 0;
   }
   // Resident query: switch to the other state set and wait only for the
   // cleanup last enqueued on THAT set (two searches ago: normally long done).
@@ -159,13 +153,37 @@ struct HipBiBfs::Impl {
     bcap = k;
   }
 
-  // resident server (k_lds_server)
+  // resident server (k_lds_server, or k_tiny_server for small graphs)
   hipStream_t sstream = nullptr;
   ServerBox* h_box = nullptr;
   bool resident = false;         // user setting
   bool srv_running = false;      // a server kernel was launched and has not been seen to exit
+  int srv_kind = 0;              // kSrvLds / kSrvTiny: which server kernel is running
   uint32_t srv_launch_seq = 0;
   unsigned long long srv_idle_ticks = 20000000ull;  // 200 ms of s_memrealtime
+  static constexpr int kSrvLds = 1, kSrvTiny = 2;
+
+  // small-graph server (tiny_engine.hip): packed adjacency + self-tagged result packets
+  unsigned long long* d_tadj = nullptr;
+  unsigned long long* d_tinfo = nullptr;
+  unsigned long long* d_stamps = nullptr;
+  TinyPkt* h_pkts = nullptr;
+  bool tiny_ok = false;
+  // the last query answered (query() API)
+  double last_ms = 0.0;
+  uint64_t last_einsp = 0;
+  static bool tiny_stamp() {
+    static const bool on = std::getenv("BIBFS_TINY_STAMP") != nullptr;
+    return on;
+  }
+  static bool tiny_disabled() {
+    static const bool off = std::getenv("BIBFS_NO_TINY") != nullptr;
+    return off;
+  }
+  bool tiny_usable(const SearchOptions& opt) const {
+    return tiny_ok && resident && !opt.trace && !opt.force_grid && opt.lockstep &&
+           opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
+  }
 
   // step-wise API
   int dir[2] = {1, 1};
@@ -190,14 +208,126 @@ struct HipBiBfs::Impl {
     std::atomic_thread_fence(std::memory_order_seq_cst);
   }
 
-  void launch_server(int pin) {
+  // Launch a server kernel of `kind`; it serves requests whose seq != last.
+  void launch_kind(int kind, int pin, uint32_t last) {
     srv_launch_seq = ++seq == 0 ? ++seq : seq;
-    if (dbg()) std::fprintf(stderr, "[server] launch seq %u pin %d\n", srv_launch_seq, pin);
+    if (dbg()) std::fprintf(stderr, "[server] launch kind %d seq %u pin %d\n", kind, srv_launch_seq, pin);
+    HIP_CHECK(hipSetDevice(device));
     __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
-    const uint32_t last = __atomic_load_n(&h_box->seq, __ATOMIC_ACQUIRE);
-    launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
-                       srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, sstream);
+    if (kind == kSrvTiny) {
+      launch::TinyArgs a{d_tadj, d_tinfo, n, h_box, h_pkts, srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks,
+                         d_stamps};
+      launch::tiny_server(a, tiny_stamp(), sstream);
+    } else {
+      launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
+                         srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, sstream);
+    }
+    srv_kind = kind;
     srv_running = true;
+  }
+  void launch_server(int pin) { launch_kind(kSrvLds, pin, __atomic_load_n(&h_box->seq, __ATOMIC_ACQUIRE)); }
+
+  // Make a server of `kind` run (stopping the other kind first).
+  void ensure_server(int kind) {
+    if (srv_running && srv_kind != kind) stop_server();
+    if (srv_running && __atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) == ~srv_launch_seq)
+      srv_running = false;  // idled out (a relaunch queues behind its last instructions)
+    if (!srv_running) launch_kind(kind, pin_xcc, __atomic_load_n(&h_box->seq, __ATOMIC_ACQUIRE));
+  }
+
+  // Spin until done(); every 8192 spins check the deadline and that the
+  // server still runs -- relaunching it (unpinned if no block reached the
+  // pinned XCD) so the pending request qseq is served.
+  template <class Done>
+  void wait_server(int kind, uint32_t qseq, Done done) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t it = 1;; ++it) {
+      if (done()) return;
+      if ((it & 8191) == 0) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+          char msg[512];
+          std::snprintf(msg, sizeof msg,
+                        "bibfs: resident server (kind %d) did not answer query %u in 5 s (alive %u launch %u)", kind,
+                        qseq, h_box->alive, srv_launch_seq);
+          std::fprintf(stderr, "%s\n", msg);
+          post(++seq == 0 ? ++seq : seq, 0, 0, kReqStop);
+          throw Error(msg);
+        }
+        const hipError_t e = hipStreamQuery(sstream);
+        if (e == hipSuccess) {  // server gone: idle exit raced this query, or no block won the election
+          if (done()) return;
+          if (__atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) != ~srv_launch_seq) pin_xcc = -1;
+          srv_running = false;
+          launch_kind(kind, pin_xcc, qseq - 1);
+        } else if (e != hipErrorNotReady) {
+          throw Error(std::string("bibfs: resident server failed: ") + hipGetErrorString(e));
+        }
+      } else {
+        _mm_pause();
+      }
+    }
+  }
+
+  // One query through the small-graph server.  Returns kTinyFound /
+  // kTinyNoPath / kTinyOverflow (the caller re-runs those on the general
+  // engine); fills hops, meet, stats and, when path != nullptr, the path.
+  struct TinyAnswer {
+    uint32_t status = 0, levels = 0, hops = 0, meet = 0, ticks = 0, einsp = 0, visited = 0;
+  };
+  static bool read_pkt(const TinyPkt* p, uint32_t want, TinyPkt& out) {
+    asm volatile("" ::: "memory");
+    const __m128i v = _mm_load_si128(reinterpret_cast<const __m128i*>(p));  // one 16-byte load: a whole packet
+    _mm_storeu_si128(reinterpret_cast<__m128i*>(&out), v);
+    return out.seq == want;
+  }
+  void spin_pkt(const TinyPkt* p, uint32_t want, TinyPkt& out) {
+    for (uint64_t it = 1; !read_pkt(p, want, out); ++it) {
+      if ((it & 65535) == 0 && hipStreamQuery(sstream) == hipSuccess && !read_pkt(p, want, out))
+        throw Error("bibfs: tiny server exited with an answer half written");
+      _mm_pause();
+    }
+  }
+  uint32_t tiny_search(uint32_t src, uint32_t dst, std::vector<vid_t>* path, TinyAnswer& a) {
+    ensure_server(kSrvTiny);
+    const uint32_t qseq = ++seq == 0 ? ++seq : seq;
+    post(qseq, src, dst, 0u);
+    TinyPkt p0, p1;
+    wait_server(kSrvTiny, qseq, [&] { return read_pkt(h_pkts, qseq, p0); });
+    spin_pkt(h_pkts + 1, qseq, p1);
+    a.status = p0.a & 0xffu;
+    a.levels = p0.a >> 8;
+    a.hops = p0.b;
+    a.meet = p0.c;
+    a.ticks = p1.a;
+    a.einsp = p1.b;
+    a.visited = p1.c;
+    if (a.status == kTinyFound && path) {
+      const uint32_t plen = a.hops + 1;
+      path->resize(plen);
+      vid_t* out = path->data();
+      for (uint32_t j = 0; 3 * j < plen; ++j) {
+        TinyPkt pk;
+        spin_pkt(h_pkts + 2 + j, qseq, pk);
+        out[3 * j] = pk.a;
+        if (3 * j + 1 < plen) out[3 * j + 1] = pk.b;
+        if (3 * j + 2 < plen) out[3 * j + 2] = pk.c;
+      }
+    }
+    if (tiny_stamp()) {
+      unsigned long long s[16];
+      HIP_CHECK(hipMemcpy(s, d_stamps, sizeof s, hipMemcpyDeviceToHost));
+      std::fprintf(stderr,
+                   "[tiny] cycles: seed %llu rounds %llu (%llu rounds, %llu levels, %.0f/round) meet-scan %llu walk %llu "
+                   "publish %llu | device %.2f us\n",
+                   s[1] - s[0], s[2] - s[1], s[6], s[7], s[6] ? (double)(s[2] - s[1]) / (double)s[6] : 0.0,
+                   s[3] ? s[3] - s[2] : 0ull, s[3] ? s[4] - s[3] : 0ull, s[5] - s[4], a.ticks * 0.01);
+      const double r = s[6] ? (double)s[6] : 1.0;
+      std::fprintf(stderr,
+                   "[tiny] per round (wave 0): plan %.0f rec %.0f load %.0f claim %.0f scan+atomic %.0f place %.0f "
+                   "barrier %.0f book %.0f\n",
+                   s[8] / r, s[9] / r, s[10] / r, s[11] / r, s[12] / r, s[13] / r, s[14] / r, s[15] / r);
+    }
+    return a.status;
   }
 
   void stop_server() {
@@ -212,63 +342,31 @@ struct HipBiBfs::Impl {
 
   // Post one query to the server and wait for its answer.
   void server_query(uint32_t src, uint32_t dst, const SearchOptions& opt, uint32_t qseq) {
-    if (srv_running && __atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) == ~srv_launch_seq)
-      srv_running = false;  // idled out (a relaunch queues behind its last instructions)
-    if (!srv_running) launch_server(pin_xcc);
+    ensure_server(kSrvLds);
     post(qseq, src, dst, (opt.lockstep ? kReqLockstep : 0u) | ((uint32_t)opt.side & 3u) << 2 | (cur ? kReqAltBuf : 0u));
     if (dbg()) std::fprintf(stderr, "[server] post %u (stage %u alive %u)\n", qseq, h_box->stage, h_box->alive);
     const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t it = 1;; ++it) {
-      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq) {
-        if (dbg()) {
-          const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-          const double dev_us = (double)(h_res->rt_end - h_res->rt_pickup) * 0.01;
-          const double srch_us = (double)(h_res->rt_end - h_res->rt_begin) * 0.01;
-          std::fprintf(stderr, "[server] host round trip %.2f us, device pickup->result %.2f us (search %.2f)\n",
-                       host_us, dev_us, srch_us);
-        }
-        return;
-      }
-      if ((it & 8191) == 0) {
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-          char msg[512];
-          std::snprintf(msg, sizeof msg,
-                        "bibfs: resident server did not answer query %u in 5 s (alive %u launch %u stage %u seen %u "
-                        "result seq %u)",
-                        qseq, h_box->alive, srv_launch_seq, h_box->stage, h_box->seen, h_res->seq);
-          std::fprintf(stderr, "%s\n", msg);
-          post(++seq == 0 ? ++seq : seq, 0, 0, kReqStop);
-          throw Error(msg);
-        }
-        const hipError_t e = hipStreamQuery(sstream);
-        if (e == hipSuccess) {  // server gone: idle exit raced this query, or no block won the election
-          if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq) return;
-          if (__atomic_load_n(&h_box->alive, __ATOMIC_ACQUIRE) != srv_launch_seq) pin_xcc = -1;
-          // relaunch so the pending request (box seq != last) is served
-          srv_running = false;
-          const uint32_t pending = qseq;
-          srv_launch_seq = ++seq == 0 ? ++seq : seq;
-          __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
-          launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
-                             srv_launch_seq, pending - 1, pin_xcc, d_flag + 4, srv_idle_ticks, sstream);
-          srv_running = true;
-        } else if (e != hipErrorNotReady) {
-          throw Error(std::string("bibfs: resident server failed: ") + hipGetErrorString(e));
-        }
-      } else {
-        _mm_pause();
-      }
+    wait_server(kSrvLds, qseq, [&] { return __atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq; });
+    if (dbg()) {
+      const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+      const double dev_us = (double)(h_res->rt_end - h_res->rt_pickup) * 0.01;
+      const double srch_us = (double)(h_res->rt_end - h_res->rt_begin) * 0.01;
+      std::fprintf(stderr, "[server] host round trip %.2f us, device pickup->result %.2f us (search %.2f)\n", host_us,
+                   dev_us, srch_us);
     }
   }
 
   void free_graph() {
     stop_server();
-    clean_pending = 0;  // hipFree below synchronises the device: any cleanup has finished
     free_batch();
     if (d_row_off) HIP_CHECK(hipFree(d_row_off));
     if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
     if (d_col) HIP_CHECK(hipFree(d_col));
     if (d_padj) HIP_CHECK(hipFree(d_padj));
+    if (d_tadj) HIP_CHECK(hipFree(d_tadj));
+    if (d_tinfo) HIP_CHECK(hipFree(d_tinfo));
+    d_tadj = d_tinfo = nullptr;
+    tiny_ok = false;
     if (d_uv) HIP_CHECK(hipFree(d_uv));
     if (state_block) HIP_CHECK(hipFree(state_block));
     if (state_block_alt) HIP_CHECK(hipFree(state_block_alt));
@@ -379,6 +477,13 @@ struct HipBiBfs::Impl {
       launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
     }
     max_deg = launch::max_degree(d_row_off, n, stream);
+    // small graphs: the packed 8-byte adjacency of the tiny server (8 (nnz + n) B)
+    if (!tiny_disabled() && launch::tiny_supported(n, nnz, max_deg)) {
+      HIP_CHECK(hipMalloc(&d_tadj, std::max<uint64_t>(nnz, 1) * 8));
+      HIP_CHECK(hipMalloc(&d_tinfo, (size_t)n * 8));
+      launch::build_tiny_adj(d_row_off, d_col, n, nnz, d_tadj, d_tinfo, stream);
+      tiny_ok = true;
+    }
     alloc_state();
     build_ms = ms;
   }
@@ -606,6 +711,10 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
   std::memset(p_->h_res, 0, sizeof(HostResult));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_clean), 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(p_->h_clean, 0, 64);
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_pkts), kTinyPktCap * sizeof(TinyPkt),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(p_->h_pkts, 0, kTinyPktCap * sizeof(TinyPkt));
+  HIP_CHECK(hipMalloc(&p_->d_stamps, 16 * sizeof(unsigned long long)));
   HIP_CHECK(hipEventCreate(&p_->ev0));
   HIP_CHECK(hipEventCreate(&p_->ev1));
 }
@@ -622,6 +731,8 @@ HipBiBfs::~HipBiBfs() {
   (void)hipHostFree(p_->h_box);
   (void)hipHostFree(p_->h_res);
   (void)hipHostFree(p_->h_clean);
+  (void)hipHostFree(p_->h_pkts);
+  (void)hipFree(p_->d_stamps);
   (void)hipHostFree(p_->h_path);
   (void)hipHostFree(p_->h_state);
   (void)hipEventDestroy(p_->ev0);
@@ -891,7 +1002,62 @@ DeviceInfo HipBiBfs::info() const {
   return d;
 }
 
+int64_t HipBiBfs::query(vid_t src, vid_t dst, std::vector<vid_t>* path) {
+  auto& I = *p_;
+  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
+  BIBFS_REQUIRE(src < I.n && dst < I.n, "src/dst out of range");
+  if (src == dst) {
+    if (path) path->assign(1, src);
+    I.last_ms = 0.0;
+    I.last_einsp = 0;
+    return 0;
+  }
+  static const SearchOptions kDefault{};
+  if (I.tiny_usable(kDefault)) {
+    Impl::TinyAnswer a;
+    const uint32_t st = I.tiny_search(src, dst, path, a);
+    if (st != kTinyOverflow) {
+      I.last_ms = a.ticks * 1e-5;
+      I.last_einsp = a.einsp;
+      if (st == kTinyFound) return a.hops;
+      if (path) path->clear();
+      return -1;
+    }
+  }
+  SearchResult r = search_general(src, dst, kDefault);
+  I.last_ms = r.search_ms;
+  I.last_einsp = r.stats.edges_inspected;
+  if (path) *path = std::move(r.path);
+  return r.found ? r.hops : -1;
+}
+
+double HipBiBfs::last_search_ms() const { return p_->last_ms; }
+uint64_t HipBiBfs::last_edges_inspected() const { return p_->last_einsp; }
+bool HipBiBfs::tiny_engine() const { return p_->tiny_ok; }
+
 SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
+  auto& I = *p_;
+  if (src != dst && I.n > 0 && src < I.n && dst < I.n && I.tiny_usable(opt)) {
+    const auto t0 = std::chrono::steady_clock::now();
+    SearchResult r;
+    Impl::TinyAnswer a;
+    const uint32_t st = I.tiny_search(src, dst, opt.want_path ? &r.path : nullptr, a);
+    if (st != kTinyOverflow) {
+      r.found = st == kTinyFound;
+      r.hops = r.found ? (int64_t)a.hops : -1;
+      r.meet = r.found ? a.meet : kNoVertex;
+      r.stats.levels = (int)a.levels;
+      r.stats.edges_inspected = a.einsp;
+      r.stats.visited = a.visited;
+      r.search_ms = a.ticks * 1e-5;
+      r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      return r;
+    }
+  }
+  return search_general(src, dst, opt);
+}
+
+SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions& opt) {
   TraceRange range("bibfs:search");
   auto& I = *p_;
   const auto t0 = std::chrono::steady_clock::now();
@@ -923,7 +1089,9 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     const int lock = (opt.lockstep && I.n <= 0x7fffffffu) ? 1 : 0;
     // BIBFS_STAMP_SERVER: the server's profiling build answers traced queries too
     static const bool stamp_srv = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
-    if (I.resident && (!opt.trace || stamp_srv) && I.server_usable()) {
+    // with the tiny server resident for this graph, the queries it cannot take
+    // (non-default options, overflow) run one-shot beside it
+    if (I.resident && !I.tiny_ok && (!opt.trace || stamp_srv) && I.server_usable()) {
       I.flip_state_set();  // the server (own stream) must not share state with a running cleanup
       I.server_query(src, dst, opt, seq);
       if (I.dbg())
@@ -954,7 +1122,19 @@ SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
     TraceRange grange("bibfs:grid_levels");
     pub_seq = ++I.seq == 0 ? ++I.seq : I.seq;
     I.res_seq = pub_seq;  // the level that ends the search publishes the path + result
-    I.grid_loop(opt, stats);
+    try {
+      I.grid_loop(opt, stats);
+    } catch (...) {
+      // unwind: a failed level must not leave the set's visited words dirty or
+      // a stale predicated-cleanup tag that later flips would wait for forever
+      I.res_seq = 0;
+      I.mirror_valid = false;
+      try {
+        I.cleanup_async(false);
+      } catch (...) {
+      }
+      throw;
+    }
     I.res_seq = 0;
     I.mirror_valid = false;
     I.grid_cleaned = stats.grid_levels > 0;
@@ -1043,7 +1223,6 @@ SearchResult HipBiBfs::finish() {
   }
   I.cleanup_async();
   HIP_CHECK(hipStreamSynchronize(I.stream));
-  I.clean_pending = 0;
   return r;
 }
 

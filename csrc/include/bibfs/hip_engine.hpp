@@ -52,6 +52,14 @@ class HipBiBfs {
 
   // --- search ---------------------------------------------------------------
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
+  // Serving entry point: hop count (-1 = no path) and, when path != nullptr,
+  // the path src .. dst.  Small graphs (n <= 2^17) are answered by the
+  // resident tiny server (csrc/hip/tiny_engine.hip) when resident serving is
+  // on; everything else, and queries that outgrow it, by search().
+  int64_t query(vid_t src, vid_t dst, std::vector<vid_t>* path);
+  double last_search_ms() const;         // device time of the last query()
+  uint64_t last_edges_inspected() const;
+  bool tiny_engine() const;              // the loaded graph has the tiny server's packed adjacency
 
   // Throughput serving: answer K queries with one launch, one workgroup (one
   // CU) per query, up to 256 in flight.  Same results as K search() calls.
@@ -95,6 +103,7 @@ class HipBiBfs {
   void synchronize() const;
 
  private:
+  SearchResult search_general(vid_t src, vid_t dst, const SearchOptions& opt);
   struct Impl;
   std::unique_ptr<Impl> p_;
 };

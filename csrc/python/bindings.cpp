@@ -57,6 +57,14 @@ py::dict stats_dict(const SearchStats& s) {
   return d;
 }
 
+// (hops, [path]) -- the serving API's answer, built straight from the vector
+py::tuple hops_path(int64_t hops, const std::vector<vid_t>& p) {
+  PyObject* l = PyList_New((Py_ssize_t)p.size());
+  if (!l) throw py::error_already_set();
+  for (size_t i = 0; i < p.size(); ++i) PyList_SET_ITEM(l, (Py_ssize_t)i, PyLong_FromUnsignedLong(p[i]));
+  return py::make_tuple(hops, py::reinterpret_steal<py::list>(l));
+}
+
 }  // namespace
 
 static py::dict dist_stats_dict(const DistLevelStats& s) {
@@ -209,7 +217,13 @@ PYBIND11_MODULE(_native, m) {
   py::class_<SerialBiBfs>(m, "SerialBiBfs")
       .def(py::init<const Csr&>(), py::keep_alive<1, 2>())
       .def("search", &SerialBiBfs::search, py::arg("src"), py::arg("dst"),
-           py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>());
+           py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>())
+      // same lean answer as HipBiBfs.query, so the CPU / GPU serving comparison
+      // pays identical Python overhead
+      .def("query", [](SerialBiBfs& e, vid_t s, vid_t d) {
+        SearchResult r = e.search(s, d);
+        return hops_path(r.found ? r.hops : -1, r.path);
+      });
   m.def("bfs_oracle", &bfs_oracle, py::call_guard<py::gil_scoped_release>());
   m.def("bfs_distances", [](const Csr& g, vid_t src) { return to_numpy(bfs_distances(g, src)); });
   m.def("validate_path", [](const Csr& g, vid_t src, vid_t dst, int64_t hops, const std::vector<vid_t>& path) {
@@ -243,6 +257,15 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("device", &HipBiBfs::device)
       .def("search", &HipBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
            py::call_guard<py::gil_scoped_release>())
+      // serving entry point: (hops, path); the GIL is kept (a query is ~10 us)
+      .def("query", [](HipBiBfs& e, vid_t s, vid_t d) {
+        std::vector<vid_t> p;
+        const int64_t h = e.query(s, d, &p);
+        return hops_path(h, p);
+      })
+      .def_property_readonly("last_search_ms", &HipBiBfs::last_search_ms)
+      .def_property_readonly("last_edges_inspected", &HipBiBfs::last_edges_inspected)
+      .def_property_readonly("tiny_engine", &HipBiBfs::tiny_engine)
       .def("release", &HipBiBfs::release, py::call_guard<py::gil_scoped_release>())
       .def("search_batch", &HipBiBfs::search_batch, py::arg("src"), py::arg("dst"),
            py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>())

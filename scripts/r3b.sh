@@ -1,0 +1,8 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+BIBFS_TINY_STAMP=1 timeout -k 10 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999 --resident --repeat 6 > gpurun_out/r3b_stamp.txt 2>&1 || { echo STAMP_FAILED; tail gpurun_out/r3b_stamp.txt; exit 1; }
+tail -8 gpurun_out/r3b_stamp.txt
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_engine.py -k "tiny or resident or unbalanced" > gpurun_out/r3b_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/r3b_tests.log; exit 1; }
+tail -2 gpurun_out/r3b_tests.log
+timeout -k 10 200 python -u benchmarks/tiny_latency.py --reps 50 > gpurun_out/r3b_lat.jsonl 2> gpurun_out/r3b_lat.err || { echo LAT_FAILED; tail -20 gpurun_out/r3b_lat.err; exit 1; }
+cat gpurun_out/r3b_lat.jsonl

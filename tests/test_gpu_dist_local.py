@@ -190,3 +190,17 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
                         got, exp = got[:-1], exp[:-1]
                     assert got == exp, (spec, s, d, kw)
                     assert r.hops == hops, (spec, s, d, r.hops, hops)
+
+
+def test_out_of_range_query_keeps_group_serving():
+    """A bad query raises on every rank before any collective and does not
+    abort the communicator: the next valid query still gets the oracle's answer."""
+    import torch  # noqa: F401
+
+    g = bb.from_spec("gnp:20000::6")
+    qs = [(0, g.n - 1), (g.n + 5, 3), (3, g.n), (17, 4242), (0, g.n - 1)]
+    rs = dist_local_run(3, g, qs)
+    assert rs[1].hops == -2 and rs[2].hops == -2
+    for i in (0, 3, 4):
+        s, d = qs[i]
+        check_result(g.csr, s, d, rs[i].hops, rs[i].path, native.bfs_oracle(g.csr, s, d).hops)

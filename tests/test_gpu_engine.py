@@ -308,3 +308,82 @@ def test_resident_back_to_back_handoffs(gpu_engine):
                 check_result(g.csr, s, d, r.hops, r.path, h)
     finally:
         gpu_engine.set_resident(False)
+
+
+# ---------------------------------------------------------------- tiny server
+def test_tiny_server_query_vs_oracle(gpu_engine):
+    """Resident small-graph server (tiny_engine.hip): hops + path of query()
+    and search() against the oracle, connected and disconnected pairs, src ==
+    dst, interleaved with one-shot queries of non-default options."""
+    g = gnp(100000, seed=6)
+    gpu_engine.load(g)
+    assert gpu_engine.tiny_engine
+    pairs = pairs_for(g.n, 300, 41) + [(7, 7)]
+    gpu_engine.set_resident(True)
+    try:
+        for i, (s, d) in enumerate(pairs):
+            h, path = gpu_engine.query(s, d)
+            truth = native.bfs_oracle(g.csr, s, d).hops
+            check_result(g.csr, s, d, h, path, truth)
+            if h > 0:
+                assert gpu_engine.last_search_ms > 0
+            if i % 50 == 0:  # the general engine beside the resident server
+                r = gpu_engine.search(s, d, make_options(force_grid=True))
+                check_result(g.csr, s, d, r.hops, r.path, truth)
+                r = gpu_engine.search(s, d, make_options(trace=True))
+                check_result(g.csr, s, d, r.hops, r.path, truth)
+        assert_engine(gpu_engine, g, pairs[:40])
+        assert gpu_engine.query(0, 99999)[0] == 17
+    finally:
+        gpu_engine.set_resident(False)
+
+
+def test_tiny_server_overflow_falls_back(gpu_engine):
+    """Frontiers beyond the tiny server's LDS capacity (a round above 2048
+    edges, a queue above 4096 vertices): the query is re-run on the general
+    engine with the same answer."""
+    g = gnp(120000, 12.0 / 120000, 3)
+    gpu_engine.load(g)
+    assert gpu_engine.tiny_engine
+    gpu_engine.set_resident(True)
+    try:
+        for s, d in pairs_for(g.n, 40, 5):
+            h, path = gpu_engine.query(s, d)
+            check_result(g.csr, s, d, h, path, native.bfs_oracle(g.csr, s, d).hops)
+    finally:
+        gpu_engine.set_resident(False)
+
+
+def test_tiny_server_not_used_for_hubs(gpu_engine):
+    """A degree above the packed-word limit keeps the graph on the general server."""
+    star = Graph.from_edges(5001, [[0, i] for i in range(1, 5001)])
+    gpu_engine.load(star)
+    assert not gpu_engine.tiny_engine
+    gpu_engine.set_resident(True)
+    try:
+        h, path = gpu_engine.query(1, 4000)
+        assert h == 2 and path == [1, 0, 4000]
+    finally:
+        gpu_engine.set_resident(False)
+
+
+def test_tiny_server_relaunch_and_kind_switch(gpu_engine):
+    """Idle exit + relaunch of the tiny server, and a switch to a big graph
+    (general server) and back."""
+    import time
+
+    small = gnp(100000, seed=6)
+    gpu_engine.load(small)
+    gpu_engine.set_resident(True, idle_ms=5.0)
+    try:
+        for _ in range(3):
+            assert gpu_engine.query(0, 99999)[0] == 17
+            time.sleep(0.05)
+        gpu_engine.generate_gnp(1_000_000, 2.2000000001 / 1_000_000, 2)
+        assert not gpu_engine.tiny_engine
+        r = gpu_engine.search(0, 999_999)
+        assert r.found
+        gpu_engine.load(small)
+        assert gpu_engine.query(0, 99999)[0] == 17
+    finally:
+        gpu_engine.set_resident(False)
