@@ -105,6 +105,17 @@ class DistEngine:
     def local_nnz(self) -> int:
         return self._e.local_nnz
 
+    @property
+    def shard_bytes(self) -> int:
+        """Bytes of this rank's CSR shard (row offsets + columns)."""
+        return self._e.shard_bytes
+
+    @property
+    def gen_peak_bytes(self) -> int:
+        """Peak allocation of the last device generation on this rank: the
+        shard plus one cursor array (the edge list is never materialised)."""
+        return self._e.gen_peak_bytes
+
     def allreduce_max(self, x: float) -> float:
         return self._e.allreduce_max(float(x))
 

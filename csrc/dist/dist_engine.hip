@@ -1257,6 +1257,11 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipStreamSynchronize(stream));
   }
 
+  // bytes of the owned CSR shard (row offsets + columns) and the generator's
+  // peak allocation while building it (streamed generation: shard + cursor)
+  size_t gen_peak_bytes = 0;
+  size_t shard_bytes() const { return ((size_t)(hi - lo) + 1) * 8 + (size_t)nnz * 4; }
+
   void build_rows_from_device_edges(const uint32_t* d_uv, uint64_t m) {
     HIP_CHECK(hipMalloc(&d_row_off, ((size_t)(hi - lo) + 1) * 8));
     nnz = launch::count_csr_rows(d_uv, m, lo, hi, d_row_off, stream);
@@ -1823,10 +1828,12 @@ void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
   HIP_CHECK(hipSetDevice(I.device));
   I.free_all();
   I.set_partition(n);
-  uint32_t* d_uv = nullptr;
-  I.m_input = launch::gen_gnp_device(n, p, seed, &d_uv, I.stream);
-  I.build_rows_from_device_edges(d_uv, I.m_input);
-  HIP_CHECK(hipFree(d_uv));
+  // owned rows straight from the generator (no edge list on any rank)
+  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)(I.hi - I.lo) + 1) * 8));
+  uint64_t m = 0;
+  I.nnz = launch::gen_rows_gnp(n, p, seed, I.lo, I.hi, I.d_row_off, &I.d_col, &m, I.stream);
+  I.m_input = m;
+  I.gen_peak_bytes = I.shard_bytes() + ((size_t)(I.hi - I.lo) + 1) * 8;  // + the scatter cursor
   I.alloc_state();
 }
 
@@ -1836,12 +1843,11 @@ void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, d
   HIP_CHECK(hipSetDevice(I.device));
   I.free_all();
   I.set_partition(n);
-  uint32_t* d_uv = nullptr;
-  HIP_CHECK(hipMalloc(&d_uv, std::max<uint64_t>(2 * m, 2) * 4));
-  launch::gen_rmat_device(n, m, seed, a, b, c, d_uv, I.stream);
+  // owned rows straight from the generator (no edge list on any rank)
+  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)(I.hi - I.lo) + 1) * 8));
+  I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, I.lo, I.hi, I.d_row_off, &I.d_col, I.stream);
   I.m_input = m;
-  I.build_rows_from_device_edges(d_uv, m);
-  HIP_CHECK(hipFree(d_uv));
+  I.gen_peak_bytes = I.shard_bytes() + ((size_t)(I.hi - I.lo) + 1) * 8;  // + the scatter cursor
   I.alloc_state();
 }
 
@@ -1910,6 +1916,8 @@ int DistBiBfs::size() const { return p_->size; }
 uint32_t DistBiBfs::n() const { return p_->n; }
 uint64_t DistBiBfs::m_input() const { return p_->m_input; }
 uint64_t DistBiBfs::local_nnz() const { return p_->nnz; }
+size_t DistBiBfs::shard_bytes() const { return p_->shard_bytes(); }
+size_t DistBiBfs::gen_peak_bytes() const { return p_->gen_peak_bytes; }
 uint32_t DistBiBfs::lo() const { return p_->lo; }
 uint32_t DistBiBfs::hi() const { return p_->hi; }
 const DistLevelStats& DistBiBfs::last_stats() const { return p_->stats; }
@@ -1992,7 +2000,8 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
                                                   const DistTuning& tuning) {
   BIBFS_REQUIRE(kind == "gnp" || kind == "rmat", "dist_local_generate_run: kind must be gnp or rmat");
   std::vector<double> build_ms((size_t)std::max(ranks, 1), 0.0), qms;
-  std::vector<uint64_t> nnz((size_t)std::max(ranks, 1), 0);
+  std::vector<uint64_t> nnz((size_t)std::max(ranks, 1), 0), shard((size_t)std::max(ranks, 1), 0),
+      peak((size_t)std::max(ranks, 1), 0);
   std::vector<DistLevelStats> qstats;
   auto rs = run_local_ranks(
       "dist_local_generate_run", ranks, device, queries.size(), tuning, DistLocalFault{},
@@ -2001,9 +2010,11 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
         if (kind == "gnp")
           e.generate_gnp(n, arg, seed);
         else
-          e.generate_rmat(n, (uint64_t)arg, seed);  // ends with hipFree of the edge list: synchronous
+          e.generate_rmat(n, (uint64_t)arg, seed);  // synchronous (ends with the cursor's hipFree)
         build_ms[(size_t)r] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         nnz[(size_t)r] = e.local_nnz();
+        shard[(size_t)r] = e.shard_bytes();
+        peak[(size_t)r] = e.gen_peak_bytes();
         for (const auto& q : queries) {
           const auto q0 = std::chrono::steady_clock::now();
           out.push_back(e.search(q.first, q.second, opt));
@@ -2017,6 +2028,8 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
     timing->build_ms = *std::max_element(build_ms.begin(), build_ms.end());
     timing->query_ms = std::move(qms);
     timing->local_nnz = std::move(nnz);
+    timing->shard_bytes = std::move(shard);
+    timing->gen_peak_bytes = std::move(peak);
     timing->stats = std::move(qstats);
   }
   return rs;

@@ -197,9 +197,121 @@ __global__ void k_rmat(RmatParams P, uint64_t m, uint32_t* __restrict__ uv) {
   }
 }
 
+// ---- streamed generation of owned rows: the generators are pure functions of
+// (seed, edge or chunk index), so a rank builds its CSR rows [lo, hi) in two
+// passes over the stream -- degrees, then scatter -- and never materialises
+// the edge list.  Peak memory is the shard itself (row offsets + columns) plus
+// one cursor array, whatever the graph size (the reference broadcasts the
+// whole edge list to every rank, v4/mpi_bas.cpp:29-64).
+__device__ __forceinline__ void own_count(uint32_t x, uint32_t y, uint32_t lo, uint32_t hi, uint64_t* deg) {
+  if (x == y) return;  // self loops carry no BFS information
+  if (x >= lo && x < hi) atomicAdd(reinterpret_cast<unsigned long long*>(&deg[x - lo]), 1ULL);
+  if (y >= lo && y < hi) atomicAdd(reinterpret_cast<unsigned long long*>(&deg[y - lo]), 1ULL);
+}
+__device__ __forceinline__ void own_scatter(uint32_t x, uint32_t y, uint32_t lo, uint32_t hi,
+                                            unsigned long long* cursor, uint32_t* col) {
+  if (x == y) return;
+  if (x >= lo && x < hi) col[atomicAdd(&cursor[x - lo], 1ULL)] = y;
+  if (y >= lo && y < hi) col[atomicAdd(&cursor[y - lo], 1ULL)] = x;
+}
+
+__global__ void k_rmat_degree(RmatParams P, uint64_t m, uint32_t lo, uint32_t hi, uint64_t* __restrict__ deg) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t u, v;
+    rmat_edge(P, e, &u, &v);
+    own_count(u, v, lo, hi, deg);
+  }
+}
+__global__ void k_rmat_scatter(RmatParams P, uint64_t m, uint32_t lo, uint32_t hi,
+                               unsigned long long* __restrict__ cursor, uint32_t* __restrict__ col) {
+  for (uint64_t e = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; e < m; e += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t u, v;
+    rmat_edge(P, e, &u, &v);
+    own_scatter(u, v, lo, hi, cursor, col);
+  }
+}
+__global__ void k_gnp_degree(uint32_t n, double p, uint64_t seed, uint64_t nchunks, uint32_t lo, uint32_t hi,
+                             uint64_t* __restrict__ deg, unsigned long long* __restrict__ medges) {
+  unsigned long long mine = 0;
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchunks;
+       c += (uint64_t)gridDim.x * blockDim.x)
+    mine += gnp_walk_chunk(n, p, seed, nchunks, c, [&](uint32_t v, uint32_t w) { own_count(w, v, lo, hi, deg); });
+  if (mine) atomicAdd(medges, mine);
+}
+__global__ void k_gnp_scatter(uint32_t n, double p, uint64_t seed, uint64_t nchunks, uint32_t lo, uint32_t hi,
+                              unsigned long long* __restrict__ cursor, uint32_t* __restrict__ col) {
+  for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < nchunks;
+       c += (uint64_t)gridDim.x * blockDim.x)
+    gnp_walk_chunk(n, p, seed, nchunks, c, [&](uint32_t v, uint32_t w) { own_scatter(w, v, lo, hi, cursor, col); });
+}
+
+RmatParams rmat_params(uint32_t n, uint64_t seed, double a, double b, double c) {
+  RmatParams P;
+  P.n = n;
+  P.scale = ceil_log2_u64(n);
+  P.a = a;
+  P.b = b;
+  P.c = c;
+  P.seed = seed;
+  return P;
+}
+
 }  // namespace
 
 namespace launch {
+
+// Scan the degree array into row offsets, allocate the columns, run the
+// scatter pass (`scatter(cursor, col)`); returns nnz.
+template <class Scatter>
+uint64_t finish_rows(uint32_t rows, uint64_t* d_row_off, uint32_t** d_col_out, hipStream_t s, Scatter scatter) {
+  exclusive_scan_u64(d_row_off, rows + 1ULL, s);
+  uint64_t nnz = 0;
+  HIP_CHECK(hipMemcpyAsync(&nnz, d_row_off + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  uint32_t* col = nullptr;
+  HIP_CHECK(hipMalloc(&col, std::max<uint64_t>(nnz, 1) * 4));
+  uint64_t* cursor = nullptr;
+  HIP_CHECK(hipMalloc(&cursor, (rows + 1ULL) * 8));
+  k_copy_u64<<<grid_for(rows + 1ULL, 256), 256, 0, s>>>(d_row_off, rows + 1ULL, cursor);
+  scatter(reinterpret_cast<unsigned long long*>(cursor), col);
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(s));
+  HIP_CHECK(hipFree(cursor));
+  *d_col_out = col;
+  return nnz;
+}
+
+uint64_t gen_rows_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c, uint32_t lo, uint32_t hi,
+                       uint64_t* d_row_off, uint32_t** d_col_out, hipStream_t s) {
+  const RmatParams P = rmat_params(n, seed, a, b, c);
+  const uint32_t rows = hi - lo;
+  HIP_CHECK(hipMemsetAsync(d_row_off, 0, (rows + 1ULL) * 8, s));
+  if (m) k_rmat_degree<<<grid_for(m, 256), 256, 0, s>>>(P, m, lo, hi, d_row_off);
+  HIP_CHECK(hipGetLastError());
+  return finish_rows(rows, d_row_off, d_col_out, s, [&](unsigned long long* cur, uint32_t* col) {
+    if (m) k_rmat_scatter<<<grid_for(m, 256), 256, 0, s>>>(P, m, lo, hi, cur, col);
+  });
+}
+
+uint64_t gen_rows_gnp(uint32_t n, double p, uint64_t seed, uint32_t lo, uint32_t hi, uint64_t* d_row_off,
+                      uint32_t** d_col_out, uint64_t* m_out, hipStream_t s) {
+  const uint64_t K = gnp_num_chunks(n, p);
+  const uint32_t rows = hi - lo;
+  unsigned long long* dm = nullptr;
+  HIP_CHECK(hipMalloc(&dm, 8));
+  HIP_CHECK(hipMemsetAsync(dm, 0, 8, s));
+  HIP_CHECK(hipMemsetAsync(d_row_off, 0, (rows + 1ULL) * 8, s));
+  k_gnp_degree<<<grid_for(K, 256), 256, 0, s>>>(n, p, seed, K, lo, hi, d_row_off, dm);
+  HIP_CHECK(hipGetLastError());
+  unsigned long long m = 0;
+  HIP_CHECK(hipMemcpyAsync(&m, dm, 8, hipMemcpyDeviceToHost, s));
+  const uint64_t nnz = finish_rows(rows, d_row_off, d_col_out, s, [&](unsigned long long* cur, uint32_t* col) {
+    k_gnp_scatter<<<grid_for(K, 256), 256, 0, s>>>(n, p, seed, K, lo, hi, cur, col);
+  });
+  HIP_CHECK(hipFree(dm));
+  *m_out = m;
+  return nnz;
+}
 
 uint64_t count_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, uint64_t* d_row_off,
                         hipStream_t s) {
@@ -294,13 +406,7 @@ uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out
 
 void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,
                      uint32_t* d_uv, hipStream_t s) {
-  RmatParams P;
-  P.n = n;
-  P.scale = ceil_log2_u64(n);
-  P.a = a;
-  P.b = b;
-  P.c = c;
-  P.seed = seed;
+  const RmatParams P = rmat_params(n, seed, a, b, c);
   if (m) k_rmat<<<grid_for(m, 256), 256, 0, s>>>(P, m, d_uv);
   HIP_CHECK(hipGetLastError());
 }

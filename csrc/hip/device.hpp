@@ -205,6 +205,13 @@ uint64_t max_degree(const uint64_t* d_row_off, uint32_t n, hipStream_t s);  // s
 uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);
 void gen_rmat_device(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c,
                      uint32_t* d_uv, hipStream_t s);
+// Owned rows [lo, hi) of a device-generated graph straight from the generator
+// (two passes, no edge list): fills d_row_off (hi - lo + 1), allocates the
+// columns, returns nnz.  gen_rows_gnp also returns the undirected edge count.
+uint64_t gen_rows_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c, uint32_t lo, uint32_t hi,
+                       uint64_t* d_row_off, uint32_t** d_col_out, hipStream_t s);
+uint64_t gen_rows_gnp(uint32_t n, double p, uint64_t seed, uint32_t lo, uint32_t hi, uint64_t* d_row_off,
+                      uint32_t** d_col_out, uint64_t* m_out, hipStream_t s);
 
 // tiny_engine.hip
 struct TinyArgs {

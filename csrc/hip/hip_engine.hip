@@ -40,6 +40,10 @@ struct HipBiBfs::Impl {
   uint64_t max_deg = 0;      // largest degree: no hub pass when it is below the hub degree
   uint32_t* d_uv = nullptr;  // last generated edge list (kept for small graphs / tests)
   uint64_t uv_m = 0;
+  // graphs above this many undirected edges are generated straight into the
+  // CSR (two passes over the counter-based generator, no edge list in HBM)
+  static constexpr uint64_t kKeepEdges = 1ull << 26;
+  static bool force_stream_gen() { return std::getenv("BIBFS_STREAM_GEN") != nullptr; }  // tests
   double build_ms = 0.0;
 
   // search state
@@ -317,15 +321,15 @@ struct HipBiBfs::Impl {
       unsigned long long s[16];
       HIP_CHECK(hipMemcpy(s, d_stamps, sizeof s, hipMemcpyDeviceToHost));
       std::fprintf(stderr,
-                   "[tiny] cycles: seed %llu rounds %llu (%llu rounds, %llu levels, %.0f/round) meet-scan %llu walk %llu "
-                   "publish %llu | device %.2f us\n",
-                   s[1] - s[0], s[2] - s[1], s[6], s[7], s[6] ? (double)(s[2] - s[1]) / (double)s[6] : 0.0,
-                   s[3] ? s[3] - s[2] : 0ull, s[3] ? s[4] - s[3] : 0ull, s[5] - s[4], a.ticks * 0.01);
-      const double r = s[6] ? (double)s[6] : 1.0;
+                   "[tiny] cycles: seed %llu single-wave %llu all-wave %llu (%llu rounds, %.0f/round) meet-scan %llu "
+                   "walk %llu publish %llu | device %.2f us, %u levels\n",
+                   s[1] - s[0], s[2] - s[1], s[3] - s[2], s[7], s[7] ? (double)(s[3] - s[2]) / (double)s[7] : 0.0,
+                   s[4] ? s[4] - s[3] : 0ull, s[4] ? s[5] - s[4] : 0ull, s[6] - s[5], a.ticks * 0.01, a.levels);
+      const double r = s[7] ? (double)s[7] : 1.0;
       std::fprintf(stderr,
-                   "[tiny] per round (wave 0): plan %.0f rec %.0f load %.0f claim %.0f scan+atomic %.0f place %.0f "
-                   "barrier %.0f book %.0f\n",
-                   s[8] / r, s[9] / r, s[10] / r, s[11] / r, s[12] / r, s[13] / r, s[14] / r, s[15] / r);
+                   "[tiny] per all-wave round (wave 0): plan %.0f claim %.0f scan+atomic %.0f place %.0f barrier %.0f "
+                   "book %.0f\n",
+                   s[8] / r, s[11] / r, s[12] / r, s[13] / r, s[14] / r, s[15] / r);
     }
     return a.status;
   }
@@ -792,17 +796,25 @@ void HipBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
   auto& I = *p_;
   I.n = n;
   HIP_CHECK(hipEventRecord(I.ev0, I.stream));
-  uint32_t* d_uv = nullptr;
-  const uint64_t m = launch::gen_gnp_device(n, p, seed, &d_uv, I.stream);
-  I.m_input = m;
   HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)n + 1) * 8));
-  I.build_from_device_edges(d_uv, m);
+  const double expect_m = p * 0.5 * (double)n * (double)(n - 1);
+  if (expect_m > (double)Impl::kKeepEdges || Impl::force_stream_gen()) {
+    // large graph: CSR straight from the generator, no edge list in HBM
+    uint64_t m = 0;
+    I.nnz = launch::gen_rows_gnp(n, p, seed, 0, n, I.d_row_off, &I.d_col, &m, I.stream);
+    I.m_input = m;
+  } else {
+    uint32_t* d_uv = nullptr;
+    const uint64_t m = launch::gen_gnp_device(n, p, seed, &d_uv, I.stream);
+    I.m_input = m;
+    I.build_from_device_edges(d_uv, m);
+    I.d_uv = d_uv;  // kept for download_edges()
+    I.uv_m = m;
+  }
   HIP_CHECK(hipEventRecord(I.ev1, I.stream));
   HIP_CHECK(hipEventSynchronize(I.ev1));
   float ms = 0;
   HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
-  I.d_uv = d_uv;
-  I.uv_m = m;
   I.finish_graph(ms);
 }
 
@@ -815,17 +827,22 @@ void HipBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, do
   I.n = n;
   I.m_input = m;
   HIP_CHECK(hipEventRecord(I.ev0, I.stream));
-  uint32_t* d_uv = nullptr;
-  HIP_CHECK(hipMalloc(&d_uv, std::max<uint64_t>(2 * m, 2) * 4));
-  launch::gen_rmat_device(n, m, seed, a, b, c, d_uv, I.stream);
   HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)n + 1) * 8));
-  I.build_from_device_edges(d_uv, m);
+  if (m > Impl::kKeepEdges || Impl::force_stream_gen()) {
+    // large graph: CSR straight from the generator, no edge list in HBM
+    I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, 0, n, I.d_row_off, &I.d_col, I.stream);
+  } else {
+    uint32_t* d_uv = nullptr;
+    HIP_CHECK(hipMalloc(&d_uv, std::max<uint64_t>(2 * m, 2) * 4));
+    launch::gen_rmat_device(n, m, seed, a, b, c, d_uv, I.stream);
+    I.build_from_device_edges(d_uv, m);
+    I.d_uv = d_uv;  // kept for download_edges()
+    I.uv_m = m;
+  }
   HIP_CHECK(hipEventRecord(I.ev1, I.stream));
   HIP_CHECK(hipEventSynchronize(I.ev1));
   float ms = 0;
   HIP_CHECK(hipEventElapsedTime(&ms, I.ev0, I.ev1));
-  I.d_uv = d_uv;
-  I.uv_m = m;
   I.finish_graph(ms);
 }
 

@@ -102,14 +102,136 @@ __device__ __forceinline__ unsigned long long stamp() {
   return t;
 }
 
+// Per-round state every wave holds identically (SGPRs), handed from the
+// single-wave phase to the all-wave phase through LDS.
+struct TinyState {
+  uint32_t status, E0, E1, cb0, cb1, d0, d1, ql0, ql1, levels, x0, x1;
+  unsigned long long einsp, meet;
+};
+
+// One lane's share of a round: its NB frontier edges (items i0 + b * stride),
+// loaded, claimed and checked against the other side.
+template <int NB>
+struct LaneWork {
+  unsigned long long rec[NB], fat[NB], oth[NB];
+  bool act[NB], s1[NB], nw[NB];
+  uint32_t deg[NB], qpre[NB];
+  uint32_t ep;        // degrees of the new vertices, side 0 | side 1 << 16
+  uint32_t qt0, qt1;  // the wave's new vertices per side (uniform)
+};
+
+template <int NB>
+__device__ __forceinline__ void expand_claim(LaneWork<NB>& W, int nb, uint32_t i0, uint32_t stride, uint32_t x0,
+                                             uint32_t tot, uint32_t par0, uint32_t par1,
+                                             const unsigned long long* rb0, const unsigned long long* rb1,
+                                             const unsigned long long* __restrict__ tadj,
+                                             unsigned long long (*VIS)[kTW]) {
+  unsigned long long old[NB];
+  // Branch-free: an idle lane reads record 0, loads word 0 and claims with an
+  // empty mask, so each step is ONE wave instruction per batch and the loads /
+  // claims of all batches stay in flight together.
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint32_t i = i0 + (uint32_t)b * stride;
+    W.act[b] = i < tot;
+    W.s1[b] = i >= x0;
+    W.rec[b] = W.fat[b] = W.oth[b] = old[b] = 0ull;
+    if (b < nb) W.rec[b] = *((W.s1[b] ? rb1 : rb0) + (W.act[b] ? i : 0u));
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    if (b < nb) W.fat[b] = tadj[W.act[b] ? (uint32_t)W.rec[b] : 0u];
+  // claim, then read the other side's word: the LDS executes one wave's DS
+  // instructions in order, so of two same-round claims of a vertex by the two
+  // sides at least one sees the other
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b < nb) {
+      const uint32_t v = (uint32_t)(W.fat[b] >> 47);
+      const uint32_t sh = (v & 31) + ((W.s1[b] ? par1 : par0) << 5);
+      const unsigned long long m = W.act[b] ? 1ull << sh : 0ull;
+      unsigned long long* w = &VIS[W.s1[b] ? 1 : 0][v >> 5];
+      old[b] = __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      W.oth[b] = __hip_atomic_load(W.s1[b] ? w - kTW : w + kTW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  // new vertices: queue slots from ballots (no scan)
+  W.ep = 0;
+  W.qt0 = W.qt1 = 0;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    const uint32_t bt = (uint32_t)(W.fat[b] >> 47) & 31;
+    W.nw[b] = W.act[b] && ((old[b] >> bt) & 0x100000001ull) == 0;
+    W.deg[b] = W.nw[b] ? (uint32_t)(W.fat[b] & 0xFFFFFu) : 0u;
+    W.ep += W.s1[b] ? W.deg[b] << 16 : W.deg[b];
+    const unsigned long long m0 = __ballot(W.nw[b] && !W.s1[b]), m1 = __ballot(W.nw[b] && W.s1[b]);
+    W.qpre[b] = W.s1[b] ? W.qt1 + mbcnt64(m1) : W.qt0 + mbcnt64(m0);
+    W.qt0 += (uint32_t)__popcll(m0);
+    W.qt1 += (uint32_t)__popcll(m1);
+  }
+}
+
+// Queue entries and next-round records of the lane's new vertices; meet
+// candidates go to C.meet.  q0b/q1b: queue index of the wave's first new
+// vertex per side; e0p/e1p: the lane's first record slot per side.  Returns
+// true when a queue or record buffer would overflow.
+template <int NB>
+__device__ __forceinline__ bool place(const LaneWork<NB>& W, uint32_t q0b, uint32_t q1b, uint32_t e0p, uint32_t e1p,
+                                      uint32_t cb0, uint32_t cb1, uint32_t d0, uint32_t d1, uint32_t x0, uint32_t x1,
+                                      uint32_t (*QU)[kTinyQ], unsigned long long (*R)[2][kTRC],
+                                      unsigned long long* meet) {
+  bool ovf = false;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (!W.nw[b]) continue;
+    const bool s1 = W.s1[b];
+    const uint32_t v = (uint32_t)(W.fat[b] >> 47);
+    const uint32_t base_v = (uint32_t)((W.fat[b] >> 20) & 0x7FFFFFFu);
+    const uint32_t deg = W.deg[b];
+    const uint32_t q = (s1 ? q1b : q0b) + W.qpre[b];
+    const uint32_t e = s1 ? e1p : e0p;
+    if (s1) e1p += deg;
+    else e0p += deg;
+    if (q >= kTinyQ || e + deg > kTRC) {
+      ovf = true;
+      continue;
+    }
+    QU[s1 ? 1 : 0][q] = v << kQBits | (uint32_t)(W.rec[b] >> 32);
+    unsigned long long* out = &R[(s1 ? cb1 : cb0) ^ 1][s1 ? 1 : 0][e];
+    const unsigned long long hi = (unsigned long long)q << 32;
+    // the first kTinyUnroll records straight-line: past the degree a store
+    // rewrites the last record with its own value (deg >= 1: the edge back to
+    // the parent) instead of branching
+#pragma unroll
+    for (uint32_t j = 0; j < kTinyUnroll; ++j) {
+      const uint32_t jj = min(j, deg - 1);
+      out[jj] = hi | (base_v + jj);
+    }
+    for (uint32_t j = kTinyUnroll; j < deg; ++j) out[j] = hi | (base_v + j);
+    const uint32_t bt = v & 31;
+    const uint32_t ost = (uint32_t)((W.oth[b] >> bt) & 1ull) | (uint32_t)((W.oth[b] >> (bt + 32)) & 1ull) << 1;
+    if (ost) {  // a meet: the other side holds v at depth bo, or bo + 1 if it claimed v this round
+      const uint32_t bo = s1 ? d0 : d1;
+      const bool oexp = (s1 ? x0 : x1) != 0;
+      const uint32_t dov = (oexp && ost == (1u << ((bo + 1) & 1))) ? bo + 1 : bo;
+      const uint32_t len = (s1 ? d1 : d0) + 1 + dov;
+      atomicMin(meet, (unsigned long long)len << 32 | (unsigned long long)(s1 ? 1u : 0u) << 31 | q);
+    }
+  }
+  return ovf;
+}
+
 template <bool kStamp>
 __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
   constexpr int B = kTinyB;
-  constexpr uint32_t kCapR = (uint32_t)kTT * B;  // frontier edges one round expands
+  constexpr uint32_t kCapR = (uint32_t)kTT * B;  // frontier edges one all-wave round expands
+  constexpr int SB = 2;                          // batches per lane in the single-wave rounds
+  constexpr uint32_t kCapW = 64u * SB;           // frontier edges one single-wave round expands
   __shared__ unsigned long long VIS[2][kTW];
   __shared__ uint32_t QU[2][kTinyQ];
   __shared__ unsigned long long R[2][2][kTRC];  // [buffer][side][record]: parent queue index << 32 | CSR index
   __shared__ TinyCtl C;
+  __shared__ TinyState S;
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   const uint32_t wid = uni(tid >> 6);
@@ -134,11 +256,16 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
 
   uint32_t last_seq = P.last_seq;
   for (;;) {
-    // ---- wait for a request: wave 0 polls the pinned mailbox (one 16-byte
-    // system-scope load per poll; relaxed, so the XCD's L2 -- the graph -- is
-    // never invalidated); the other waves sleep in the barrier
     unsigned long long rt0 = 0;
+    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t seq = 0;
+    // ======== wave 0 alone: poll, seed, and the rounds small enough for one
+    // wave -- no barrier, the round state in SGPRs, the counters from the
+    // wave's own scan.  The other waves sleep in the barrier below.
     if (wid == 0) {
+      // wait for a request: one 16-byte system-scope load of the pinned
+      // mailbox per poll (relaxed: the XCD's L2 -- the graph -- is never
+      // invalidated)
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t stop = 0;
       u32x4 rq;
@@ -157,51 +284,96 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           break;
         }
       }
+      seq = rq.x;
       if (lane == 0) {
         C.cmd[0] = stop;
-        C.cmd[1] = rq.x;
-        C.cmd[2] = rq.y;
-        C.cmd[3] = rq.z;
+        C.cmd[1] = seq;
+      }
+      if (!stop) {
+        if (kStamp) st[0] = stamp();
+        // the host checked src/dst < n and src != dst; clamp anyway (a torn request never faults)
+        const uint32_t src = min(rq.y, P.n - 1), dst = min(rq.z, P.n - 1);
+        // ---- seed: both roots at depth 0, their edges as the first records
+        const unsigned long long fs = P.tinfo[src], fd = P.tinfo[dst];
+        TinyState T{};
+        T.E0 = (uint32_t)(fs & 0xFFFFFu);
+        T.E1 = (uint32_t)(fd & 0xFFFFFu);
+        T.ql0 = T.ql1 = 1;
+        T.meet = ~0ull;
+        {
+          const uint32_t b0 = (uint32_t)((fs >> 20) & 0x7FFFFFFu), b1 = (uint32_t)((fd >> 20) & 0x7FFFFFFu);
+          for (uint32_t j = lane; j < min(T.E0, kTRC); j += 64) R[0][0][j] = b0 + j;
+          for (uint32_t j = lane; j < min(T.E1, kTRC); j += 64) R[0][1][j] = b1 + j;
+          if (lane == 0) {
+            QU[0][0] = src << kQBits;
+            QU[1][0] = dst << kQBits;
+            VIS[0][src >> 5] = 1ull << (src & 31);
+            VIS[1][dst >> 5] = 1ull << (dst & 31);
+          }
+        }
+        if (T.E0 == 0 || T.E1 == 0) T.status = kTinyNoPath;  // an isolated endpoint
+        else if (T.E0 > kTRC || T.E1 > kTRC) T.status = kTinyOverflow;
+        if (kStamp) st[1] = stamp();
+        // ---- single-wave rounds
+        while (T.status == 0 && T.E0 + T.E1 <= kCapW) {
+          const uint32_t x0 = T.E0, x1 = T.E1, tot = x0 + x1;
+          const int nb = tot > 64 ? SB : 1;
+          LaneWork<SB> W;
+          expand_claim<SB>(W, nb, lane, 64, x0, tot, (T.d0 + 1) & 1, (T.d1 + 1) & 1, &R[T.cb0][0][0],
+                           &R[T.cb1][1][0] - x0, P.tadj, VIS);
+          const uint32_t ei = wave_scan(W.ep);
+          const uint32_t et = lane63(ei);
+          const uint32_t ex = ei - W.ep;
+          const bool ovf = place<SB>(W, T.ql0, T.ql1, ex & 0xffffu, ex >> 16, T.cb0, T.cb1, T.d0, T.d1, x0, x1, QU,
+                                     R, &C.meet);
+          const bool ovf_any = __ballot(ovf) != 0;
+          T.x0 = x0;
+          T.x1 = x1;
+          T.einsp += tot;
+          T.levels += (x0 != 0) + (x1 != 0);
+          if (ovf_any) {
+            T.status = kTinyOverflow;
+            break;
+          }
+          if (x0) T.ql0 += W.qt0;
+          if (x1) T.ql1 += W.qt1;
+          // the wave's own ds_min_u64 precede this read (one wave's LDS ops are in order)
+          const unsigned long long m = uni64(__hip_atomic_load(&C.meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          if (m != ~0ull) {
+            T.meet = m;
+            T.status = kTinyFound;
+            break;
+          }
+          if (x0) {
+            T.E0 = et & 0xffffu;
+            T.cb0 ^= 1;
+            ++T.d0;
+            if (!T.E0) T.status = kTinyNoPath;  // side 0 claimed nothing: its component is exhausted
+          }
+          if (x1) {
+            T.E1 = et >> 16;
+            T.cb1 ^= 1;
+            ++T.d1;
+            if (!T.E1) T.status = kTinyNoPath;
+          }
+        }
+        if (lane == 0) S = T;
       }
     }
     lds_barrier();
     if (uni(C.cmd[0])) break;
-    const uint32_t seq = uni(C.cmd[1]);
+    seq = uni(C.cmd[1]);
     last_seq = seq;
-    // the host checked src/dst < n and src != dst; clamp anyway (a torn request never faults)
-    const uint32_t src = min(uni(C.cmd[2]), P.n - 1), dst = min(uni(C.cmd[3]), P.n - 1);
-    unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (kStamp) st[0] = stamp();
+    if (kStamp) st[2] = stamp();
 
-    // ---- seed: both roots at depth 0, their edges as the first records
-    const unsigned long long fs = P.tinfo[src], fd = P.tinfo[dst];
-    uint32_t E0 = (uint32_t)(fs & 0xFFFFFu), E1 = (uint32_t)(fd & 0xFFFFFu);
-    {
-      const uint32_t b0 = (uint32_t)((fs >> 20) & 0x7FFFFFFu), b1 = (uint32_t)((fd >> 20) & 0x7FFFFFFu);
-      for (uint32_t j = tid; j < min(E0, kTRC); j += kTT) R[0][0][j] = b0 + j;
-      for (uint32_t j = tid; j < min(E1, kTRC); j += kTT) R[0][1][j] = b1 + j;
-      if (tid == 0) {
-        QU[0][0] = src << kQBits;
-        QU[1][0] = dst << kQBits;
-        VIS[0][src >> 5] = 1ull << (src & 31);
-        VIS[1][dst >> 5] = 1ull << (dst & 31);
-      }
-    }
-    uint32_t status = 0;
-    if (E0 == 0 || E1 == 0) status = kTinyNoPath;  // an isolated endpoint
-    else if (E0 > kTRC || E1 > kTRC) status = kTinyOverflow;
-    lds_barrier();
-    if (kStamp) st[1] = stamp();
-
-    // ---- rounds (uniform state, identical in every wave)
-    uint32_t cb0 = 0, cb1 = 0;  // current record buffer of each side
-    uint32_t d0 = 0, d1 = 0;    // depth of each side's current frontier
-    uint32_t ql0 = 1, ql1 = 1;  // queue lengths
-    uint32_t levels = 0, rnd = 0, slot = 0;
-    unsigned long long einsp = 0, meet = ~0ull, cnt = 0;
-    uint32_t x0 = 0, x1 = 0;
+    // ======== all-wave rounds (uniform state, identical in every wave)
+    uint32_t status = uni(S.status), E0 = uni(S.E0), E1 = uni(S.E1), cb0 = uni(S.cb0), cb1 = uni(S.cb1);
+    uint32_t d0 = uni(S.d0), d1 = uni(S.d1), ql0 = uni(S.ql0), ql1 = uni(S.ql1), levels = uni(S.levels);
+    uint32_t x0 = uni(S.x0), x1 = uni(S.x1), slot = 0;
+    unsigned long long einsp = uni64(S.einsp), meet = uni64(S.meet);
     // stamp build: wave 0's cycles per round phase (s_memtime, waits at each mark)
     unsigned long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tp = kStamp ? stamp() : 0;
+    uint32_t rnd = 0;
 #define TINY_PH(k)                         \
   if (kStamp && wid == 0) {                \
     const unsigned long long t_ = stamp(); \
@@ -225,109 +397,26 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       const uint32_t tot = x0 + x1;
       TINY_PH(0)
       if (wid * 64 < tot) {
-        const uint32_t par0 = (d0 + 1) & 1, par1 = (d1 + 1) & 1;
         // batches this wave holds at all (uniform): batch b covers lanes tid + b * kTT
         const int nb = (wid * 64 + kTT < tot) ? B : 1;
-        const unsigned long long* rb0 = &R[cb0][0][0];
-        const unsigned long long* rb1 = &R[cb1][1][0] - x0;
-        unsigned long long rec[B] = {}, fat[B] = {}, old[B] = {}, oth[B] = {};
-        bool act[B], s1[B];
-        // Branch-free: an idle lane reads record 0, loads word 0 and claims
-        // with an empty mask, so each step is ONE wave instruction per batch
-        // and the loads / claims of both batches stay in flight together.
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-          const uint32_t i = tid + (uint32_t)b * kTT;
-          act[b] = i < tot;
-          s1[b] = i >= x0;
-          if (b < nb) rec[b] = *((s1[b] ? rb1 : rb0) + (act[b] ? i : 0u));
-        }
-        TINY_PH(1)
-#pragma unroll
-        for (int b = 0; b < B; ++b)
-          if (b < nb) fat[b] = P.tadj[act[b] ? (uint32_t)rec[b] : 0u];
-        if (kStamp) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        TINY_PH(2)
-        // claim, then read the other side's word: the LDS executes one wave's
-        // DS instructions in order, so of two same-round claims of a vertex by
-        // the two sides at least one sees the other
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-          if (b < nb) {
-            const uint32_t v = (uint32_t)(fat[b] >> 47);
-            const uint32_t sh = (v & 31) + ((s1[b] ? par1 : par0) << 5);
-            const unsigned long long m = act[b] ? 1ull << sh : 0ull;
-            unsigned long long* w = &VIS[s1[b] ? 1 : 0][v >> 5];
-            old[b] = __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            oth[b] = __hip_atomic_load(s1[b] ? w - kTW : w + kTW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-        }
+        LaneWork<B> W;
+        expand_claim<B>(W, nb, tid, kTT, x0, tot, (d0 + 1) & 1, (d1 + 1) & 1, &R[cb0][0][0], &R[cb1][1][0] - x0,
+                        P.tadj, VIS);
         TINY_PH(3)
-        // new vertices: queue slots from ballots, record slots from one DPP
-        // scan of the degrees (both sides as 16-bit halves), ONE counter add
-        uint32_t ep = 0, deg[B], qpre[B];
-        bool nw[B];
-        uint32_t qt0 = 0, qt1 = 0;
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-          const uint32_t bt = (uint32_t)(fat[b] >> 47) & 31;
-          nw[b] = act[b] && ((old[b] >> bt) & 0x100000001ull) == 0;
-          deg[b] = nw[b] ? (uint32_t)(fat[b] & 0xFFFFFu) : 0u;
-          ep += s1[b] ? deg[b] << 16 : deg[b];
-          const unsigned long long m0 = __ballot(nw[b] && !s1[b]), m1 = __ballot(nw[b] && s1[b]);
-          qpre[b] = s1[b] ? qt1 + mbcnt64(m1) : qt0 + mbcnt64(m0);
-          qt0 += (uint32_t)__popcll(m0);
-          qt1 += (uint32_t)__popcll(m1);
-        }
-        if (qt0 | qt1) {  // uniform
-          const uint32_t ei = wave_scan(ep);
+        if (W.qt0 | W.qt1) {  // uniform
+          // record slots from one DPP scan of the degrees (both sides as 16-bit
+          // halves), both counters in ONE ds_add_rtn_u64 (TinyCtl field layout)
+          const uint32_t ei = wave_scan(W.ep);
           const uint32_t et = lane63(ei);
           unsigned long long base = 0;
           if (lane == 0)
             base = atomicAdd(&C.cnt[slot], (unsigned long long)(et & 0xffffu) | (unsigned long long)(et >> 16) << 20 |
-                                               (unsigned long long)qt0 << 40 | (unsigned long long)qt1 << 52);
+                                               (unsigned long long)W.qt0 << 40 | (unsigned long long)W.qt1 << 52);
           const uint32_t blo = lane0((uint32_t)base), bhi = lane0((uint32_t)(base >> 32));
           TINY_PH(4)
-          const uint32_t ex = ei - ep;  // exclusive, per 16-bit half
-          uint32_t e0p = (blo & 0xFFFFFu) + (ex & 0xffffu);
-          uint32_t e1p = ((blo >> 20) | (bhi << 12)) + (ex >> 16);
-          const uint32_t q0b = ql0 + ((bhi >> 8) & 0xFFFu), q1b = ql1 + (bhi >> 20);
-          bool ovf = false;
-#pragma unroll
-          for (int b = 0; b < B; ++b) {
-            if (!nw[b]) continue;
-            const uint32_t v = (uint32_t)(fat[b] >> 47);
-            const uint32_t base_v = (uint32_t)((fat[b] >> 20) & 0x7FFFFFFu);
-            const uint32_t q = (s1[b] ? q1b : q0b) + qpre[b];
-            const uint32_t e = s1[b] ? e1p : e0p;
-            if (s1[b]) e1p += deg[b];
-            else e0p += deg[b];
-            if (q >= kTinyQ || e + deg[b] > kTRC) {
-              ovf = true;
-              continue;
-            }
-            (s1[b] ? QU[1] : QU[0])[q] = v << kQBits | (uint32_t)(rec[b] >> 32);
-            unsigned long long* out = &R[(s1[b] ? cb1 : cb0) ^ 1][s1[b] ? 1 : 0][e];
-            const unsigned long long hi = (unsigned long long)q << 32;
-            // the first kTinyUnroll records straight-line: past the degree a
-            // store rewrites the last record with its own value (deg >= 1:
-            // the edge back to the parent) instead of branching
-#pragma unroll
-            for (uint32_t j = 0; j < kTinyUnroll; ++j) {
-              const uint32_t jj = min(j, deg[b] - 1);
-              out[jj] = hi | (base_v + jj);
-            }
-            for (uint32_t j = kTinyUnroll; j < deg[b]; ++j) out[j] = hi | (base_v + j);
-            const uint32_t bt = v & 31;
-            const uint32_t ost = (uint32_t)((oth[b] >> bt) & 1ull) | (uint32_t)((oth[b] >> (bt + 32)) & 1ull) << 1;
-            if (ost) {  // a meet: the other side holds v at depth bo, or bo + 1 if it claimed v this round
-              const uint32_t bo = s1[b] ? d0 : d1;
-              const bool oexp = (s1[b] ? x0 : x1) != 0;
-              const uint32_t dov = (oexp && ost == (1u << ((bo + 1) & 1))) ? bo + 1 : bo;
-              const uint32_t len = (s1[b] ? d1 : d0) + 1 + dov;
-              atomicMin(&C.meet, (unsigned long long)len << 32 | (unsigned long long)(s1[b] ? 1u : 0u) << 31 | q);
-            }
-          }
+          const uint32_t ex = ei - W.ep;  // exclusive, per 16-bit half
+          const bool ovf = place<B>(W, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20), (blo & 0xFFFFFu) + (ex & 0xffffu),
+                                    ((blo >> 20) | (bhi << 12)) + (ex >> 16), cb0, cb1, d0, d1, x0, x1, QU, R, &C.meet);
           if (ovf) atomicMin(&C.meet, 0ull);  // key 0 = overflow (a meet has length >= 1)
         }
       }
@@ -336,23 +425,23 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       TINY_PH(6)
       einsp += tot;
       levels += (x0 != 0) + (x1 != 0);
-      cnt = uni64(C.cnt[slot]);
+      const unsigned long long cnt = uni64(C.cnt[slot]);
       meet = uni64(C.meet);
       slot = slot == 2 ? 0 : slot + 1;
+      if (x0) ql0 += (uint32_t)(cnt >> 40) & 0xFFFu;
+      if (x1) ql1 += (uint32_t)(cnt >> 52);
       if (meet != ~0ull) {
         status = meet == 0 ? kTinyOverflow : kTinyFound;
         break;
       }
       if (x0) {
         E0 = (uint32_t)cnt & 0xFFFFFu;
-        ql0 += (uint32_t)(cnt >> 40) & 0xFFFu;
         cb0 ^= 1;
         ++d0;
         if (!E0) status = kTinyNoPath;  // side 0 claimed nothing: its component is exhausted
       }
       if (x1) {
         E1 = (uint32_t)(cnt >> 20) & 0xFFFFFu;
-        ql1 += (uint32_t)(cnt >> 52);
         cb1 ^= 1;
         ++d1;
         if (!E1) status = kTinyNoPath;
@@ -361,26 +450,25 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       TINY_PH(7)
     }
 #undef TINY_PH
-    if (kStamp) st[2] = stamp();
+    if (kStamp) st[3] = stamp();
 
     // ---- the path: find the meet vertex on the other side, walk both chains
-    uint32_t len = 0, mv = ~0u, visited = ql0 + ql1;
+    uint32_t len = 0, mv = ~0u;
+    const uint32_t visited = ql0 + ql1;
     uint32_t* PATH = reinterpret_cast<uint32_t*>(&R[0][0][0]);
     if (status == kTinyFound) {
       len = (uint32_t)(meet >> 32);
       const uint32_t s = (uint32_t)(meet >> 31) & 1u, qs = (uint32_t)meet & 0x7fffffffu;
       mv = QU[s][qs] >> kQBits;
-      const uint32_t nq0 = ql0 + (x0 ? (uint32_t)(cnt >> 40) & 0xFFFu : 0u), nq1 = ql1 + (x1 ? (uint32_t)(cnt >> 52) : 0u);
-      visited = nq0 + nq1;
-      const uint32_t o = s ^ 1, nqo = o ? nq1 : nq0;
+      const uint32_t o = s ^ 1, nqo = o ? ql1 : ql0;
       for (uint32_t i = tid; i < nqo; i += kTT)
         if ((QU[o][i] >> kQBits) == mv) C.other_q = i;
       lds_barrier();
-      if (kStamp) st[3] = stamp();
+      if (kStamp) st[4] = stamp();
       if (wid == 0 && lane < 2) {
         const uint32_t qo = C.other_q;
-        const uint32_t dsv = (s ? d1 : d0) + 1;     // depth of the meet vertex on the claiming side
-        const uint32_t d0v = s ? len - dsv : dsv;   // its distance from src = its path position
+        const uint32_t dsv = (s ? d1 : d0) + 1;    // depth of the meet vertex on the claiming side
+        const uint32_t d0v = s ? len - dsv : dsv;  // its distance from src = its path position
         const uint32_t side = lane;
         uint32_t idx = side == s ? qs : qo;
         const uint32_t hops = side ? len - d0v : d0v;
@@ -395,7 +483,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     }
     // ---- publish: self-tagged packets, one 16-byte store each
     if (wid == 0) {
-      if (kStamp) st[4] = stamp();
+      if (kStamp) st[5] = stamp();
       const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
       const uint32_t plen = status == kTinyFound ? len + 1 : 0u;
       const uint32_t npk = 2 + (plen + 2) / 3;
@@ -419,9 +507,8 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         store_sys16(P.pkts + j, pk);
       }
       if (kStamp && lane == 0) {
-        st[5] = stamp();
-        st[6] = rnd;
-        st[7] = levels;
+        st[6] = stamp();
+        st[7] = rnd;
         for (int k = 0; k < 8; ++k) P.stamps[k] = st[k];
         for (int k = 0; k < 8; ++k) P.stamps[8 + k] = ph[k];
       }

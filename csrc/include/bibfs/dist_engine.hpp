@@ -112,6 +112,8 @@ class DistBiBfs {
   uint32_t n() const;
   uint64_t m_input() const;
   uint64_t local_nnz() const;
+  size_t shard_bytes() const;     // owned CSR rows: row offsets + columns
+  size_t gen_peak_bytes() const;  // peak allocation of the last device generation (0: loaded, not generated)
   uint32_t lo() const;
   uint32_t hi() const;
   const DistLevelStats& last_stats() const;
@@ -145,6 +147,7 @@ struct DistLocalTiming {
   double build_ms = 0.0;
   std::vector<double> query_ms;
   std::vector<uint64_t> local_nnz;  // per rank
+  std::vector<uint64_t> shard_bytes, gen_peak_bytes;  // per rank
   std::vector<DistLevelStats> stats;  // rank 0, per query
 };
 std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,

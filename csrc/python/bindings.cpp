@@ -356,6 +356,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("n", &DistBiBfs::n)
       .def_property_readonly("m_input", &DistBiBfs::m_input)
       .def_property_readonly("local_nnz", &DistBiBfs::local_nnz)
+      .def_property_readonly("shard_bytes", &DistBiBfs::shard_bytes)
+      .def_property_readonly("gen_peak_bytes", &DistBiBfs::gen_peak_bytes)
       .def_property_readonly("lo", &DistBiBfs::lo)
       .def_property_readonly("hi", &DistBiBfs::hi)
       .def("load_edges", &DistBiBfs::load_edges, py::call_guard<py::gil_scoped_release>())
@@ -405,6 +407,8 @@ PYBIND11_MODULE(_native, m) {
         d["build_ms"] = t.build_ms;
         d["query_ms"] = t.query_ms;
         d["local_nnz"] = t.local_nnz;
+        d["shard_bytes"] = t.shard_bytes;
+        d["gen_peak_bytes"] = t.gen_peak_bytes;
         py::list st;
         for (const auto& x : t.stats) st.append(dist_stats_dict(x));
         d["stats"] = st;

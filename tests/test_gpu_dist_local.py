@@ -204,3 +204,25 @@ def test_out_of_range_query_keeps_group_serving():
     for i in (0, 3, 4):
         s, d = qs[i]
         check_result(g.csr, s, d, rs[i].hops, rs[i].path, native.bfs_oracle(g.csr, s, d).hops)
+
+
+@pytest.mark.parametrize("spec", ["gnp:40000::3", "kron:15:16:2"])
+def test_generated_shards_hold_only_their_rows(spec):
+    """Every rank generates its shard straight from the generator: its peak
+    allocation is its own rows (+ one cursor array), never the edge list."""
+    import torch  # noqa: F401
+
+    from bidirectional_bfs_amd.parallel import dist_local_generate_run
+
+    g = bb.from_spec(spec)
+    qs = _pairs(g.n, 6, 4)
+    rs, t = dist_local_generate_run(3, spec, qs)
+    for (s, d), r in zip(qs, rs):
+        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+    edge_list_bytes = 8 * g.m
+    for nnz, shard, peak in zip(t["local_nnz"], t["shard_bytes"], t["gen_peak_bytes"]):
+        rows = (g.n + 2) // 3 + 64
+        assert shard <= nnz * 4 + (rows + 1) * 8
+        assert peak <= shard + (rows + 1) * 8
+        assert peak < edge_list_bytes  # the old path held the whole edge list on every rank
+    assert sum(t["local_nnz"]) == g.csr.nnz

@@ -387,3 +387,27 @@ def test_tiny_server_relaunch_and_kind_switch(gpu_engine):
         assert gpu_engine.query(0, 99999)[0] == 17
     finally:
         gpu_engine.set_resident(False)
+
+
+@pytest.mark.parametrize("spec", ["gnp:30000:0.0002:9", "rmat:20000:150000:5"])
+def test_streamed_generation_equals_edge_list_csr(gpu_engine, spec, monkeypatch):
+    """Graphs generated straight into the CSR (two passes over the
+    counter-based generator, no edge list -- the large-graph path) have exactly
+    the rows of the CSR built from the materialised edge list."""
+    kind, n, arg, seed = spec.split(":")[0], int(spec.split(":")[1]), float(spec.split(":")[2]), int(spec.split(":")[3])
+    el = native.gen_gnp(n, arg, seed) if kind == "gnp" else native.gen_rmat(n, int(arg), seed)
+    h = native.build_csr(el)
+    monkeypatch.setenv("BIBFS_STREAM_GEN", "1")
+    if kind == "gnp":
+        gpu_engine.generate_gnp(n, arg, seed)
+    else:
+        gpu_engine.generate_rmat(n, int(arg), seed)
+    monkeypatch.delenv("BIBFS_STREAM_GEN")
+    d = gpu_engine.download_csr()
+    assert gpu_engine.m == el.m
+    assert np.array_equal(d.row_off, h.row_off)
+    for v in range(0, n, 37):
+        a, b = slice(h.row_off[v], h.row_off[v + 1]), slice(d.row_off[v], d.row_off[v + 1])
+        assert sorted(h.col[a]) == sorted(d.col[b])
+    r = gpu_engine.search(0, n - 1)
+    check_result(h, 0, n - 1, r.hops, r.path, native.bfs_oracle(h, 0, n - 1).hops)
