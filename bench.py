@@ -401,13 +401,27 @@ def main(argv=None) -> int:
         _, n, _, seed = parse_spec(spec)
         ref = generate(HipEngine(local), spec)
         pairs = pick_pairs(ref, n, min(a.pairs, steps + warmup), 12345)
+        assert pairs, f"no connected pairs found in {spec}"
+        # the single-GPU engine on the same graph and pairs (resident serving),
+        # so every partitioned entry states its speedup over one GPU
+        ref.set_resident(True)
+        for i in range(warmup):
+            ref.query(*pairs[i % len(pairs)][:2])
+        ts = time.perf_counter()
+        for i in range(steps):
+            s_, d_, h_ = pairs[(warmup + i) % len(pairs)]
+            assert ref.query(s_, d_)[0] == h_
+        single_ms = max_over_ranks((time.perf_counter() - ts) * 1e3 / steps)
+        ref.set_resident(False)
         ref.release()
         del ref
-        assert pairs, f"no connected pairs found in {spec}"
+        torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
         eng = generate(dist_engine(), spec)
         build_ms = max_over_ranks((time.perf_counter() - t0) * 1e3)
+        free_b, total_b = torch.cuda.mem_get_info(dev)
+        hbm_used = total_b - free_b
         m = eng.m
         wrong = []
 
@@ -435,7 +449,14 @@ def main(argv=None) -> int:
             "engine": f"DistBiBfs/{eng.backend}", "ranks": world, "rccl_ranks": eng.world,
             "n": n, "m": m, "seed": seed, "build_ms": round(build_ms, 3),
             "local_nnz_max": int(max_over_ranks(float(eng.local_nnz))),
+            # per-rank HBM: the CSR shard, and the generator's peak (shard + one
+            # cursor array: the edge list is never materialised on any rank)
+            "shard_bytes_max": int(max_over_ranks(float(eng.shard_bytes))),
+            "gen_peak_bytes_max": int(max_over_ranks(float(eng.gen_peak_bytes))),
+            "hbm_used_bytes_max": int(max_over_ranks(float(hbm_used))),
             "queries": steps, "ms_per_query": round(dt * 1e3 / steps, 5),
+            "single_gpu_ms": round(single_ms, 5),
+            "speedup_vs_single_gpu": round(single_ms / (dt * 1e3 / steps), 4),
             "gteps": m * steps / dt / 1e9,
             "device_ms_per_query": round(sum(r.search_ms for r, _ in done) / steps, 5),
             "mean_hops": sum(r.hops for r, _ in done) / steps,
@@ -443,6 +464,8 @@ def main(argv=None) -> int:
             "ms_per_round": round(dt * 1e3 / steps / max(rounds, 1e-9), 5),
             "host_syncs_per_query": sum(s["host_syncs"] for s in st) / steps,
             "exchanged_bytes_per_query": sum(s["exchanged_bytes"] for s in st) / steps,
+            "collectives_per_query": sum(s["collectives"] for s in st) / steps,
+            "collectives_per_round": sum(s["collectives"] for s in st) / max(1, sum(s["rounds"] for s in st)),
             "speculative_rounds_per_query": sum(s["spec_rounds"] for s in st) / steps,
             "dense_levels_per_query": sum(s["dense_levels"] for s in st) / steps,
             "verified": ok, "checked_queries": steps + warmup,
