@@ -379,6 +379,7 @@ def main(argv=None) -> int:
             "mean_hops": hops / steps, "device_ms_per_query": dev_ms / steps,
             "build_ms": build_s * 1e3, "server_launch_ms": round(launch_ms, 4),
             "tiny_server": bool(eng.tiny_engine and resident),
+            "tiny_overflows": eng.tiny_overflows,  # queries re-run on the general engine (cumulative)
             "end_to_end_first_query_ms": build_s * 1e3 + launch_ms,
             "queries": queries, "batched": batched,
         }

@@ -36,9 +36,12 @@ def main() -> int:
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--direction", default="auto", choices=["auto", "topdown", "bottomup"])
+    ap.add_argument("--alpha", type=float, default=14.0, help="Beamer top-down -> bottom-up: m_f > m_u / alpha")
+    ap.add_argument("--beta", type=float, default=24.0, help="Beamer bottom-up -> top-down: n_f < n / beta")
+    ap.add_argument("--force-grid", action="store_true", help="skip the LDS engine: every level on the grid engine")
     a = ap.parse_args()
     eng = HipEngine(a.device)
-    opt = make_options(direction=a.direction)
+    opt = make_options(direction=a.direction, alpha=a.alpha, beta=a.beta, force_grid=a.force_grid)
     for scale in [int(x) for x in a.scales.split(",") if x]:
         n, m = 1 << scale, a.ef << scale
         t0 = time.perf_counter()
@@ -73,6 +76,7 @@ def main() -> int:
             "gteps_inspected": round(insp / k / (med * 1e-3) / 1e9, 3), "mean_hops": hops / k,
             "mean_grid_levels": grid / k, "mean_bottomup_levels": bu / k,
             "device_gb": round(eng.device_bytes / 1e9, 2), "direction": a.direction,
+            "alpha": a.alpha, "beta": a.beta, "force_grid": a.force_grid,
         }), flush=True)
         eng.release()
     return 0

@@ -55,7 +55,8 @@ def main():
            "graph": a.graph, "queries": len(t_all),
            "query_us_mean": round(statistics.fmean(t_all) * 1e6, 3),
            "query_us_median": round(statistics.median(t_all) * 1e6, 3),
-           "device_us_mean": round(statistics.fmean(dev) * 1e3, 3)}
+           "device_us_mean": round(statistics.fmean(dev) * 1e3, 3),
+           "tiny_overflows": eng.tiny_overflows}
     print(json.dumps(gpu), flush=True)
     if a.per_pair:
         for i, (s, d, h) in enumerate(pairs):

@@ -90,6 +90,11 @@ class HipEngine:
         return self._e.last_edges_inspected
 
     @property
+    def tiny_overflows(self) -> int:
+        """Queries the tiny server could not hold (re-run on the general engine), cumulative."""
+        return self._e.tiny_overflows
+
+    @property
     def tiny_engine(self) -> bool:
         """The loaded graph carries the tiny server's packed adjacency."""
         return self._e.tiny_engine

@@ -92,15 +92,18 @@ __host__ __device__ inline uint32_t req_tag(uint32_t seq, uint32_t flags) { retu
 // ---- small-graph resident server (tiny_engine.hip) --------------------------
 // Graphs up to kTinyMaxN vertices keep both visited sets in LDS as bitmaps and
 // read a packed adjacency: one 8-byte word per directed edge holding the
-// neighbour id, its CSR base and its degree, so a level costs ONE dependent
-// global load.  Word layout: v[63:47] | base[46:20] | deg[19:0].
+// neighbour id, its CSR base and its degree.  Word layout (52 bits):
+// v[51:35] | base[34:9] | deg[8:0]; the server's records put the parent's
+// queue index in [63:52].
 constexpr uint32_t kTinyMaxN = 1u << 17;
-constexpr uint64_t kTinyMaxNnz = 1ull << 27;
+constexpr uint64_t kTinyMaxNnz = 1ull << 26;
 constexpr int kTinyB = 2;  // frontier edges per lane per round
-// per-wave edge sums are scanned as two 16-bit halves: 64 lanes x kTinyB x deg < 2^16
-constexpr uint32_t kTinyMaxDeg = 65535u / (64u * kTinyB);
+// 9-bit degree field; per-wave record sums are scanned as two 16-bit halves
+// (64 lanes x kTinyB x 511 < 2^16)
+constexpr uint32_t kTinyMaxDeg = 511;
+static_assert(64u * kTinyB * kTinyMaxDeg < 65536u, "per-wave record sums must fit 16 bits");
 __host__ __device__ inline uint64_t tiny_pack(uint32_t v, uint64_t base, uint64_t deg) {
-  return (uint64_t)v << 47 | base << 20 | deg;
+  return (uint64_t)v << 35 | base << 9 | deg;
 }
 // The answer: 16-byte packets, each carrying the query's seq in its first
 // word and written by one 16-byte system-scope store, so the host checks every

@@ -174,6 +174,7 @@ struct HipBiBfs::Impl {
   TinyPkt* h_pkts = nullptr;
   bool tiny_ok = false;
   // the last query answered (query() API)
+  uint64_t tiny_overflows = 0;  // queries the tiny server handed back (re-run on the general engine)
   double last_ms = 0.0;
   uint64_t last_einsp = 0;
   static bool tiny_stamp() {
@@ -305,6 +306,7 @@ struct HipBiBfs::Impl {
     a.ticks = p1.a;
     a.einsp = p1.b;
     a.visited = p1.c;
+    if (a.status == kTinyOverflow) ++tiny_overflows;
     if (a.status == kTinyFound && path) {
       const uint32_t plen = a.hops + 1;
       path->resize(plen);
@@ -322,9 +324,9 @@ struct HipBiBfs::Impl {
       HIP_CHECK(hipMemcpy(s, d_stamps, sizeof s, hipMemcpyDeviceToHost));
       std::fprintf(stderr,
                    "[tiny] cycles: seed %llu single-wave %llu all-wave %llu (%llu rounds, %.0f/round) meet-scan %llu "
-                   "walk %llu publish %llu | device %.2f us, %u levels\n",
+                   "walk %llu publish %llu | device %.2f us, %u levels, status %u\n",
                    s[1] - s[0], s[2] - s[1], s[3] - s[2], s[7], s[7] ? (double)(s[3] - s[2]) / (double)s[7] : 0.0,
-                   s[4] ? s[4] - s[3] : 0ull, s[4] ? s[5] - s[4] : 0ull, s[6] - s[5], a.ticks * 0.01, a.levels);
+                   s[4] ? s[4] - s[3] : 0ull, s[4] ? s[5] - s[4] : 0ull, s[6] - s[5], a.ticks * 0.01, a.levels, a.status);
       const double r = s[7] ? (double)s[7] : 1.0;
       std::fprintf(stderr,
                    "[tiny] per all-wave round (wave 0): plan %.0f claim %.0f scan+atomic %.0f place %.0f barrier %.0f "
@@ -1051,6 +1053,7 @@ int64_t HipBiBfs::query(vid_t src, vid_t dst, std::vector<vid_t>* path) {
 double HipBiBfs::last_search_ms() const { return p_->last_ms; }
 uint64_t HipBiBfs::last_edges_inspected() const { return p_->last_einsp; }
 bool HipBiBfs::tiny_engine() const { return p_->tiny_ok; }
+uint64_t HipBiBfs::tiny_overflows() const { return p_->tiny_overflows; }
 
 SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   auto& I = *p_;

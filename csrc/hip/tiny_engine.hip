@@ -42,9 +42,23 @@ using namespace dev;
 #endif
 constexpr int kTT = BIBFS_TINY_THREADS;
 constexpr uint32_t kTW = kTinyMaxN / 32;  // u64 visited words per side (low half even, high half odd)
-constexpr uint32_t kTRC = 2040;           // per-edge records per side per buffer
+constexpr uint32_t kTRC = 2008;           // per-edge records per side per buffer
 constexpr uint32_t kQBits = 12;
 constexpr uint32_t kTinyUnroll = 4;  // record stores per new vertex without a loop
+// Rounds whose two frontiers together exceed this many edges expand the side
+// with fewer edges alone (lockstep below it).
+#ifndef BIBFS_TINY_LOCK_MAX
+#define BIBFS_TINY_LOCK_MAX 2048
+#endif
+constexpr uint32_t kLockMax = BIBFS_TINY_LOCK_MAX;
+// All-wave rounds: 1 = fetch each neighbour's first edges speculatively at the
+// round's start (beside the claim), 0 = only for the vertices claimed, after
+// the claim (16 waves of speculative scattered loads queue on the address
+// unit; one wave's do not).
+#ifndef BIBFS_TINY_SPEC_ALL
+#define BIBFS_TINY_SPEC_ALL 0
+#endif
+constexpr bool kSpecAll = BIBFS_TINY_SPEC_ALL;
 static_assert(kTinyQ == 1u << kQBits, "queue index width");
 
 // Per-round counter (three slots, rotated): new records of side 0 [19:0] and
@@ -56,6 +70,7 @@ struct TinyCtl {
   unsigned long long cnt[3];
   unsigned long long meet;   // min over candidates of len << 32 | side << 31 | queue index; 0 = overflow
   uint32_t other_q;          // the meet vertex's queue index on the other side
+  uint32_t rovf;             // a record buffer overflowed (fatal only without a meet)
   uint32_t won;
   uint32_t cmd[4];           // stop, seq, src, dst
 };
@@ -109,113 +124,167 @@ struct TinyState {
   unsigned long long einsp, meet;
 };
 
-// One lane's share of a round: its NB frontier edges (items i0 + b * stride),
-// loaded, claimed and checked against the other side.
-template <int NB>
-struct LaneWork {
-  unsigned long long rec[NB], fat[NB], oth[NB];
-  bool act[NB], s1[NB], nw[NB];
-  uint32_t deg[NB], qpre[NB];
-  uint32_t ep;        // degrees of the new vertices, side 0 | side 1 << 16
-  uint32_t qt0, qt1;  // the wave's new vertices per side (uniform)
+// tiny word fields (device.hpp tiny_pack) and the record's parent index
+__device__ __forceinline__ uint32_t tw_v(unsigned long long w) { return (uint32_t)(w >> 35) & 0x1FFFFu; }
+__device__ __forceinline__ uint32_t tw_base(unsigned long long w) { return (uint32_t)(w >> 9) & 0x3FFFFFFu; }
+__device__ __forceinline__ uint32_t tw_deg(unsigned long long w) { return (uint32_t)w & 0x1FFu; }
+__device__ __forceinline__ uint32_t tw_pq(unsigned long long w) { return (uint32_t)(w >> 52); }
+
+// Uniform description of one round.
+struct RoundCtx {
+  uint32_t x0, tot;                  // items [0, x0) are side 0's records, [x0, tot) side 1's
+  const unsigned long long* rb0;     // side 0's current records
+  const unsigned long long* rb1x;    // side 1's current records, minus x0 (indexed by the item)
+  unsigned long long* nb[2];         // next-round record buffers
+  uint32_t par[2];                   // depth parity bit of this round's claims per side
+  uint32_t dep[2];                   // frontier depth per side before the round
+  bool exp[2];                       // the side expands this round
 };
 
+// One lane's NB items (frontier edges) of a round.
 template <int NB>
-__device__ __forceinline__ void expand_claim(LaneWork<NB>& W, int nb, uint32_t i0, uint32_t stride, uint32_t x0,
-                                             uint32_t tot, uint32_t par0, uint32_t par1,
-                                             const unsigned long long* rb0, const unsigned long long* rb1,
-                                             const unsigned long long* __restrict__ tadj,
-                                             unsigned long long (*VIS)[kTW]) {
+struct Work {
+  unsigned long long rec[NB];        // the record: the neighbour's tiny word | parent queue index << 52
+  unsigned long long nbw[NB][kTinyUnroll];  // the neighbour's first edges' words (speculative)
+  unsigned long long oth[NB];        // the other side's visited word of the neighbour
+  bool act[NB], s1[NB], nw[NB];
+  uint32_t deg[NB];                  // degree of the neighbour when this lane claimed it (else 0)
+};
+
+// Round step 1: read the records, and at once issue the loads of each
+// neighbour's first edges (the NEXT round's records, fetched speculatively
+// so their latency overlaps the claim) and the claims.  Branch-free: an idle
+// lane reads a harmless word and claims with an empty mask.
+template <int NB, bool kSpec>
+__device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint32_t i0, uint32_t stride, int nb,
+                                            const unsigned long long* __restrict__ tadj,
+                                            unsigned long long (*VIS)[kTW]) {
   unsigned long long old[NB];
-  // Branch-free: an idle lane reads record 0, loads word 0 and claims with an
-  // empty mask, so each step is ONE wave instruction per batch and the loads /
-  // claims of all batches stay in flight together.
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     const uint32_t i = i0 + (uint32_t)b * stride;
-    W.act[b] = i < tot;
-    W.s1[b] = i >= x0;
-    W.rec[b] = W.fat[b] = W.oth[b] = old[b] = 0ull;
-    if (b < nb) W.rec[b] = *((W.s1[b] ? rb1 : rb0) + (W.act[b] ? i : 0u));
+    W.act[b] = i < R.tot;
+    W.s1[b] = i >= R.x0;
+    W.rec[b] = 1ull;  // an idle lane: vertex 0, base 0, degree 1
+    if (b < nb && W.act[b]) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
   }
+  if (kSpec) {
 #pragma unroll
-  for (int b = 0; b < NB; ++b)
-    if (b < nb) W.fat[b] = tadj[W.act[b] ? (uint32_t)W.rec[b] : 0u];
+    for (int b = 0; b < NB; ++b) {
+      if (b >= nb) continue;
+      const uint32_t base = tw_base(W.rec[b]), deg = W.act[b] ? tw_deg(W.rec[b]) : 0u;
+#pragma unroll
+      for (uint32_t j = 0; j < kTinyUnroll; ++j)
+        if (j < deg) W.nbw[b][j] = tadj[base + j];  // exec-masked: no address for a missing edge
+    }
+  }
   // claim, then read the other side's word: the LDS executes one wave's DS
   // instructions in order, so of two same-round claims of a vertex by the two
   // sides at least one sees the other
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    if (b < nb) {
-      const uint32_t v = (uint32_t)(W.fat[b] >> 47);
-      const uint32_t sh = (v & 31) + ((W.s1[b] ? par1 : par0) << 5);
-      const unsigned long long m = W.act[b] ? 1ull << sh : 0ull;
-      unsigned long long* w = &VIS[W.s1[b] ? 1 : 0][v >> 5];
-      old[b] = __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      W.oth[b] = __hip_atomic_load(W.s1[b] ? w - kTW : w + kTW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    old[b] = W.oth[b] = 0ull;
+    if (b >= nb) continue;
+    const uint32_t v = tw_v(W.rec[b]);
+    const uint32_t par = W.s1[b] ? R.par[1] : R.par[0];
+    const unsigned long long m = W.act[b] ? 1ull << ((v & 31) + (par << 5)) : 0ull;
+    unsigned long long* own = &VIS[W.s1[b] ? 1 : 0][v >> 5];
+    old[b] = __hip_atomic_fetch_or(own, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    W.oth[b] = __hip_atomic_load(W.s1[b] ? own - kTW : own + kTW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  // new vertices: queue slots from ballots (no scan)
-  W.ep = 0;
-  W.qt0 = W.qt1 = 0;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const uint32_t bt = (uint32_t)(W.fat[b] >> 47) & 31;
-    W.nw[b] = W.act[b] && ((old[b] >> bt) & 0x100000001ull) == 0;
-    W.deg[b] = W.nw[b] ? (uint32_t)(W.fat[b] & 0xFFFFFu) : 0u;
-    W.ep += W.s1[b] ? W.deg[b] << 16 : W.deg[b];
-    const unsigned long long m0 = __ballot(W.nw[b] && !W.s1[b]), m1 = __ballot(W.nw[b] && W.s1[b]);
-    W.qpre[b] = W.s1[b] ? W.qt1 + mbcnt64(m1) : W.qt0 + mbcnt64(m0);
-    W.qt0 += (uint32_t)__popcll(m0);
-    W.qt1 += (uint32_t)__popcll(m1);
+    const uint32_t bt = tw_v(W.rec[b]) & 31;
+    W.nw[b] = b < nb && W.act[b] && ((((uint32_t)old[b] | (uint32_t)(old[b] >> 32)) >> bt) & 1u) == 0;
+    W.deg[b] = W.nw[b] ? tw_deg(W.rec[b]) : 0u;
   }
 }
 
-// Queue entries and next-round records of the lane's new vertices; meet
-// candidates go to C.meet.  q0b/q1b: queue index of the wave's first new
-// vertex per side; e0p/e1p: the lane's first record slot per side.  Returns
-// true when a queue or record buffer would overflow.
+// Per-lane and per-wave counts of the new vertices: queue slots from ballots,
+// record slots from ONE DPP scan of the degrees (side 0 [15:0], side 1 [31:16]).
 template <int NB>
-__device__ __forceinline__ bool place(const LaneWork<NB>& W, uint32_t q0b, uint32_t q1b, uint32_t e0p, uint32_t e1p,
-                                      uint32_t cb0, uint32_t cb1, uint32_t d0, uint32_t d1, uint32_t x0, uint32_t x1,
-                                      uint32_t (*QU)[kTinyQ], unsigned long long (*R)[2][kTRC],
-                                      unsigned long long* meet) {
-  bool ovf = false;
+struct Counts {
+  uint32_t qpre[NB];  // new vertices of this lane's side below this lane (in batches < b, then lanes < lane)
+  uint32_t qt[2];     // the wave's new vertices per side (uniform)
+  uint32_t ex, et;    // exclusive / total (uniform) record counts per side
+};
+template <int NB>
+__device__ __forceinline__ void round_count(Counts<NB>& K, const Work<NB>& W) {
+  uint32_t ep = 0;
+  K.qt[0] = K.qt[1] = 0;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    if (!W.nw[b]) continue;
-    const bool s1 = W.s1[b];
-    const uint32_t v = (uint32_t)(W.fat[b] >> 47);
-    const uint32_t base_v = (uint32_t)((W.fat[b] >> 20) & 0x7FFFFFFu);
-    const uint32_t deg = W.deg[b];
-    const uint32_t q = (s1 ? q1b : q0b) + W.qpre[b];
-    const uint32_t e = s1 ? e1p : e0p;
-    if (s1) e1p += deg;
-    else e0p += deg;
-    if (q >= kTinyQ || e + deg > kTRC) {
-      ovf = true;
-      continue;
-    }
-    QU[s1 ? 1 : 0][q] = v << kQBits | (uint32_t)(W.rec[b] >> 32);
-    unsigned long long* out = &R[(s1 ? cb1 : cb0) ^ 1][s1 ? 1 : 0][e];
-    const unsigned long long hi = (unsigned long long)q << 32;
-    // the first kTinyUnroll records straight-line: past the degree a store
-    // rewrites the last record with its own value (deg >= 1: the edge back to
-    // the parent) instead of branching
+    const unsigned long long m0 = __ballot(W.nw[b] && !W.s1[b]), m1 = __ballot(W.nw[b] && W.s1[b]);
+    K.qpre[b] = W.s1[b] ? K.qt[1] + mbcnt64(m1) : K.qt[0] + mbcnt64(m0);
+    K.qt[0] += (uint32_t)__popcll(m0);
+    K.qt[1] += (uint32_t)__popcll(m1);
+    ep += W.deg[b] << (W.s1[b] ? 16 : 0);
+  }
+  const uint32_t ei = wave_scan(ep);
+  K.ex = ei - ep;
+  K.et = lane63(ei);
+}
+
+// Round step 2: queue entries, next-round records (the speculatively loaded
+// words, tagged with the new vertex's queue index) and meet candidates.
+// q0b/q1b: queue index of the wave's first new vertex per side; e0b/e1b: its
+// first record slot per side.  Returns kOvfQueue when a queue would overflow
+// (fatal: the path walk needs every entry) and kOvfRec when a record buffer
+// would (fatal only if the round finds no meet: records feed the NEXT round).
+// A lane with nothing to store writes its own junk slot (no branch).
+constexpr uint32_t kOvfQueue = 1, kOvfRec = 2;
+template <int NB, bool kSpec>
+__device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K, const RoundCtx& R, int nb,
+                                                uint32_t q0b, uint32_t q1b, uint32_t e0b, uint32_t e1b, uint32_t lane,
+                                                const unsigned long long* __restrict__ tadj, uint32_t (*QU)[kTinyQ],
+                                                uint32_t* JQ, unsigned long long* JR, unsigned long long* meet) {
+  uint32_t ovf = 0;
+  uint32_t e0 = e0b + (K.ex & 0xffffu), e1 = e1b + (K.ex >> 16);
+  if (!kSpec) {  // the claimed vertices' first edges, fetched now
 #pragma unroll
-    for (uint32_t j = 0; j < kTinyUnroll; ++j) {
-      const uint32_t jj = min(j, deg - 1);
-      out[jj] = hi | (base_v + jj);
+    for (int b = 0; b < NB; ++b) {
+      if (b >= nb) continue;
+      const uint32_t base = tw_base(W.rec[b]);
+#pragma unroll
+      for (uint32_t j = 0; j < kTinyUnroll; ++j)
+        if (j < W.deg[b]) W.nbw[b][j] = tadj[base + j];
     }
-    for (uint32_t j = kTinyUnroll; j < deg; ++j) out[j] = hi | (base_v + j);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b >= nb) continue;
+    const bool s1 = W.s1[b], nw = W.nw[b];
+    const uint32_t v = tw_v(W.rec[b]);
+    const uint32_t deg = W.deg[b];
+    const uint32_t q = (s1 ? q1b : q0b) + K.qpre[b];
+    const uint32_t e = s1 ? e1 : e0;
+    if (s1) e1 += deg;
+    else e0 += deg;
+    const bool qok = nw && q < kTinyQ;
+    const bool rok = qok && e + deg <= kTRC;
+    if (nw && !qok) ovf |= kOvfQueue;
+    if (qok && !rok) ovf |= kOvfRec;
+    *(qok ? &QU[s1 ? 1 : 0][q] : JQ + lane) = v << kQBits | tw_pq(W.rec[b]);
+    unsigned long long* out = R.nb[s1 ? 1 : 0] + e;
+    unsigned long long* junk = JR + lane;
+    const uint32_t dd = rok ? deg : 0u;
+    const unsigned long long tag = (unsigned long long)q << 52;
+    // past the degree (or with nothing to store) a store goes to the lane's junk slot
+#pragma unroll
+    for (uint32_t j = 0; j < kTinyUnroll; ++j) *(j < dd ? out + j : junk) = W.nbw[b][j] | tag;
+    if (__ballot(rok && deg > kTinyUnroll)) {  // rare: a vertex of degree > 4
+      const uint32_t base = tw_base(W.rec[b]);
+      for (uint32_t j = kTinyUnroll; rok && j < deg; ++j) out[j] = tadj[base + j] | tag;
+    }
     const uint32_t bt = v & 31;
     const uint32_t ost = (uint32_t)((W.oth[b] >> bt) & 1ull) | (uint32_t)((W.oth[b] >> (bt + 32)) & 1ull) << 1;
-    if (ost) {  // a meet: the other side holds v at depth bo, or bo + 1 if it claimed v this round
-      const uint32_t bo = s1 ? d0 : d1;
-      const bool oexp = (s1 ? x0 : x1) != 0;
+    const bool cand = qok && ost;
+    if (__ballot(cand) && cand) {  // a meet: the other side holds v at depth bo, or bo + 1 if it claimed v now
+      const uint32_t bo = s1 ? R.dep[0] : R.dep[1];
+      const bool oexp = s1 ? R.exp[0] : R.exp[1];
       const uint32_t dov = (oexp && ost == (1u << ((bo + 1) & 1))) ? bo + 1 : bo;
-      const uint32_t len = (s1 ? d1 : d0) + 1 + dov;
-      atomicMin(meet, (unsigned long long)len << 32 | (unsigned long long)(s1 ? 1u : 0u) << 31 | q);
+      const uint32_t ds = s1 ? R.dep[1] : R.dep[0];
+      atomicMin(meet, (unsigned long long)(ds + 1 + dov) << 32 | (unsigned long long)(s1 ? 1u : 0u) << 31 | q);
     }
   }
   return ovf;
@@ -223,15 +292,16 @@ __device__ __forceinline__ bool place(const LaneWork<NB>& W, uint32_t q0b, uint3
 
 template <bool kStamp>
 __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
-  constexpr int B = kTinyB;
-  constexpr uint32_t kCapR = (uint32_t)kTT * B;  // frontier edges one all-wave round expands
-  constexpr int SB = 2;                          // batches per lane in the single-wave rounds
-  constexpr uint32_t kCapW = 64u * SB;           // frontier edges one single-wave round expands
+  static_assert(kTinyB == 2, "two items per lane");
+  constexpr uint32_t kCapR = (uint32_t)kTT * kTinyB;  // frontier edges one all-wave round expands
+  constexpr uint32_t kCapW = 64u * kTinyB;             // ... one single-wave round
   __shared__ unsigned long long VIS[2][kTW];
   __shared__ uint32_t QU[2][kTinyQ];
-  __shared__ unsigned long long R[2][2][kTRC];  // [buffer][side][record]: parent queue index << 32 | CSR index
+  __shared__ unsigned long long R[2][2][kTRC];  // [buffer][side][record]
   __shared__ TinyCtl C;
   __shared__ TinyState S;
+  __shared__ uint32_t JQ[64];  // junk slots of the branch-free stores
+  __shared__ unsigned long long JR[64];
   const uint32_t tid = threadIdx.x;
   const uint32_t lane = tid & 63;
   const uint32_t wid = uni(tid >> 6);
@@ -249,10 +319,30 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
 #pragma unroll 4
     for (uint32_t i = tid; i < 2 * kTW; i += kTT) V[i] = 0ull;
     if (tid < 3) C.cnt[tid] = 0ull;
-    if (tid == 0) C.meet = ~0ull;
+    if (tid == 0) {
+      C.meet = ~0ull;
+      C.rovf = 0u;
+    }
   };
   zero_state();
   lds_barrier();
+
+  auto make_ctx = [&](uint32_t x0, uint32_t x1, uint32_t cb0, uint32_t cb1, uint32_t d0, uint32_t d1) {
+    RoundCtx X;
+    X.x0 = x0;
+    X.tot = x0 + x1;
+    X.rb0 = &R[cb0][0][0];
+    X.rb1x = &R[cb1][1][0] - x0;
+    X.nb[0] = &R[cb0 ^ 1][0][0];
+    X.nb[1] = &R[cb1 ^ 1][1][0];
+    X.par[0] = (d0 + 1) & 1;
+    X.par[1] = (d1 + 1) & 1;
+    X.dep[0] = d0;
+    X.dep[1] = d1;
+    X.exp[0] = x0 != 0;
+    X.exp[1] = x1 != 0;
+    return X;
+  };
 
   uint32_t last_seq = P.last_seq;
   for (;;) {
@@ -261,7 +351,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     uint32_t seq = 0;
     // ======== wave 0 alone: poll, seed, and the rounds small enough for one
     // wave -- no barrier, the round state in SGPRs, the counters from the
-    // wave's own scan.  The other waves sleep in the barrier below.
+    // wave's own ballots and scan.  The other waves sleep in the barrier below.
     if (wid == 0) {
       // wait for a request: one 16-byte system-scope load of the pinned
       // mailbox per poll (relaxed: the XCD's L2 -- the graph -- is never
@@ -293,17 +383,18 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         if (kStamp) st[0] = stamp();
         // the host checked src/dst < n and src != dst; clamp anyway (a torn request never faults)
         const uint32_t src = min(rq.y, P.n - 1), dst = min(rq.z, P.n - 1);
-        // ---- seed: both roots at depth 0, their edges as the first records
+        // ---- seed: both roots at depth 0; their records are their
+        // neighbours' words (parent queue index 0 = the root)
         const unsigned long long fs = P.tinfo[src], fd = P.tinfo[dst];
         TinyState T{};
-        T.E0 = (uint32_t)(fs & 0xFFFFFu);
-        T.E1 = (uint32_t)(fd & 0xFFFFFu);
+        T.E0 = tw_deg(fs);
+        T.E1 = tw_deg(fd);
         T.ql0 = T.ql1 = 1;
         T.meet = ~0ull;
         {
-          const uint32_t b0 = (uint32_t)((fs >> 20) & 0x7FFFFFFu), b1 = (uint32_t)((fd >> 20) & 0x7FFFFFFu);
-          for (uint32_t j = lane; j < min(T.E0, kTRC); j += 64) R[0][0][j] = b0 + j;
-          for (uint32_t j = lane; j < min(T.E1, kTRC); j += 64) R[0][1][j] = b1 + j;
+          const uint32_t b0 = tw_base(fs), b1 = tw_base(fd);
+          for (uint32_t j = lane; j < T.E0; j += 64) R[0][0][j] = P.tadj[b0 + j];
+          for (uint32_t j = lane; j < T.E1; j += 64) R[0][1][j] = P.tadj[b1 + j];
           if (lane == 0) {
             QU[0][0] = src << kQBits;
             QU[1][0] = dst << kQBits;
@@ -312,31 +403,29 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           }
         }
         if (T.E0 == 0 || T.E1 == 0) T.status = kTinyNoPath;  // an isolated endpoint
-        else if (T.E0 > kTRC || T.E1 > kTRC) T.status = kTinyOverflow;
         if (kStamp) st[1] = stamp();
-        // ---- single-wave rounds
+        // ---- single-wave rounds: both frontiers together up to 128 edges
         while (T.status == 0 && T.E0 + T.E1 <= kCapW) {
-          const uint32_t x0 = T.E0, x1 = T.E1, tot = x0 + x1;
-          const int nb = tot > 64 ? SB : 1;
-          LaneWork<SB> W;
-          expand_claim<SB>(W, nb, lane, 64, x0, tot, (T.d0 + 1) & 1, (T.d1 + 1) & 1, &R[T.cb0][0][0],
-                           &R[T.cb1][1][0] - x0, P.tadj, VIS);
-          const uint32_t ei = wave_scan(W.ep);
-          const uint32_t et = lane63(ei);
-          const uint32_t ex = ei - W.ep;
-          const bool ovf = place<SB>(W, T.ql0, T.ql1, ex & 0xffffu, ex >> 16, T.cb0, T.cb1, T.d0, T.d1, x0, x1, QU,
-                                     R, &C.meet);
-          const bool ovf_any = __ballot(ovf) != 0;
+          const uint32_t x0 = T.E0, x1 = T.E1;
+          const RoundCtx X = make_ctx(x0, x1, T.cb0, T.cb1, T.d0, T.d1);
+          const int nb = x0 + x1 > 64 ? 2 : 1;
+          Work<2> W;
+          round_issue<2, true>(W, X, lane, 64, nb, P.tadj, VIS);
+          Counts<2> K;
+          round_count<2>(K, W);
+          const uint32_t ovf =
+              round_place<2, true>(W, K, X, nb, T.ql0, T.ql1, 0u, 0u, lane, P.tadj, QU, JQ, JR, &C.meet);
+          const bool qovf = __ballot(ovf & kOvfQueue) != 0, rovf = __ballot(ovf & kOvfRec) != 0;
           T.x0 = x0;
           T.x1 = x1;
-          T.einsp += tot;
-          T.levels += (x0 != 0) + (x1 != 0);
-          if (ovf_any) {
+          T.einsp += x0 + x1;
+          T.levels += 2;
+          T.ql0 += K.qt[0];
+          T.ql1 += K.qt[1];
+          if (qovf) {
             T.status = kTinyOverflow;
             break;
           }
-          if (x0) T.ql0 += W.qt0;
-          if (x1) T.ql1 += W.qt1;
           // the wave's own ds_min_u64 precede this read (one wave's LDS ops are in order)
           const unsigned long long m = uni64(__hip_atomic_load(&C.meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
           if (m != ~0ull) {
@@ -344,18 +433,17 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
             T.status = kTinyFound;
             break;
           }
-          if (x0) {
-            T.E0 = et & 0xffffu;
-            T.cb0 ^= 1;
-            ++T.d0;
-            if (!T.E0) T.status = kTinyNoPath;  // side 0 claimed nothing: its component is exhausted
+          if (rovf) {  // the next round's records do not fit
+            T.status = kTinyOverflow;
+            break;
           }
-          if (x1) {
-            T.E1 = et >> 16;
-            T.cb1 ^= 1;
-            ++T.d1;
-            if (!T.E1) T.status = kTinyNoPath;
-          }
+          T.E0 = K.et & 0xffffu;
+          T.E1 = K.et >> 16;
+          T.cb0 ^= 1;
+          T.cb1 ^= 1;
+          ++T.d0;
+          ++T.d1;
+          if (!T.E0 || !T.E1) T.status = kTinyNoPath;  // a side claimed nothing: its component is exhausted
         }
         if (lane == 0) S = T;
       }
@@ -383,7 +471,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     while (status == 0) {
       x0 = E0;
       x1 = E1;
-      if (x0 + x1 > kCapR) {  // both do not fit one round: the side with fewer edges alone
+      if (x0 + x1 > kCapR || x0 + x1 > kLockMax) {  // the side with fewer edges alone
         if (x0 <= x1) x1 = 0;
         else x0 = 0;
         if (x0 + x1 > kCapR) {
@@ -394,36 +482,35 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       // the counter slot of the NEXT round was last read two barriers ago; the
       // last wave (idle in small rounds) clears it
       if (tid == kTT - 64) C.cnt[slot == 2 ? 0 : slot + 1] = 0ull;
-      const uint32_t tot = x0 + x1;
+      const RoundCtx X = make_ctx(x0, x1, cb0, cb1, d0, d1);
       TINY_PH(0)
-      if (wid * 64 < tot) {
-        // batches this wave holds at all (uniform): batch b covers lanes tid + b * kTT
-        const int nb = (wid * 64 + kTT < tot) ? B : 1;
-        LaneWork<B> W;
-        expand_claim<B>(W, nb, tid, kTT, x0, tot, (d0 + 1) & 1, (d1 + 1) & 1, &R[cb0][0][0], &R[cb1][1][0] - x0,
-                        P.tadj, VIS);
+      if (wid * 64 < X.tot) {
+        const int nb = (wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
+        Work<2> W;
+        round_issue<2, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS);
+        Counts<2> K;
+        round_count<2>(K, W);
         TINY_PH(3)
-        if (W.qt0 | W.qt1) {  // uniform
-          // record slots from one DPP scan of the degrees (both sides as 16-bit
-          // halves), both counters in ONE ds_add_rtn_u64 (TinyCtl field layout)
-          const uint32_t ei = wave_scan(W.ep);
-          const uint32_t et = lane63(ei);
+        if (K.qt[0] | K.qt[1]) {  // uniform
+          // ONE ds_add_rtn_u64 on the packed round counter (TinyCtl layout)
           unsigned long long base = 0;
           if (lane == 0)
-            base = atomicAdd(&C.cnt[slot], (unsigned long long)(et & 0xffffu) | (unsigned long long)(et >> 16) << 20 |
-                                               (unsigned long long)W.qt0 << 40 | (unsigned long long)W.qt1 << 52);
+            base = atomicAdd(&C.cnt[slot], (unsigned long long)(K.et & 0xffffu) |
+                                               (unsigned long long)(K.et >> 16) << 20 |
+                                               (unsigned long long)K.qt[0] << 40 | (unsigned long long)K.qt[1] << 52);
           const uint32_t blo = lane0((uint32_t)base), bhi = lane0((uint32_t)(base >> 32));
           TINY_PH(4)
-          const uint32_t ex = ei - W.ep;  // exclusive, per 16-bit half
-          const bool ovf = place<B>(W, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20), (blo & 0xFFFFFu) + (ex & 0xffffu),
-                                    ((blo >> 20) | (bhi << 12)) + (ex >> 16), cb0, cb1, d0, d1, x0, x1, QU, R, &C.meet);
-          if (ovf) atomicMin(&C.meet, 0ull);  // key 0 = overflow (a meet has length >= 1)
+          const uint32_t ovf = round_place<2, kSpecAll>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20),
+                                              blo & 0xFFFFFu, ((blo >> 20) | (bhi << 12)) & 0xFFFFFu, lane, P.tadj,
+                                              QU, JQ, JR, &C.meet);
+          if (ovf & kOvfQueue) atomicMin(&C.meet, 0ull);  // key 0 = overflow (a meet has length >= 1)
+          if (ovf & kOvfRec) C.rovf = 1u;
         }
       }
       TINY_PH(5)
       lds_barrier();
       TINY_PH(6)
-      einsp += tot;
+      einsp += X.tot;
       levels += (x0 != 0) + (x1 != 0);
       const unsigned long long cnt = uni64(C.cnt[slot]);
       meet = uni64(C.meet);
@@ -432,6 +519,10 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       if (x1) ql1 += (uint32_t)(cnt >> 52);
       if (meet != ~0ull) {
         status = meet == 0 ? kTinyOverflow : kTinyFound;
+        break;
+      }
+      if (uni(C.rovf)) {  // no meet, and the next round's records do not fit
+        status = kTinyOverflow;
         break;
       }
       if (x0) {

@@ -60,6 +60,7 @@ class HipBiBfs {
   double last_search_ms() const;         // device time of the last query()
   uint64_t last_edges_inspected() const;
   bool tiny_engine() const;              // the loaded graph has the tiny server's packed adjacency
+  uint64_t tiny_overflows() const;       // queries the tiny server handed back to the general engine (cumulative)
 
   // Throughput serving: answer K queries with one launch, one workgroup (one
   // CU) per query, up to 256 in flight.  Same results as K search() calls.

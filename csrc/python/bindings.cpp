@@ -266,6 +266,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("last_search_ms", &HipBiBfs::last_search_ms)
       .def_property_readonly("last_edges_inspected", &HipBiBfs::last_edges_inspected)
       .def_property_readonly("tiny_engine", &HipBiBfs::tiny_engine)
+      .def_property_readonly("tiny_overflows", &HipBiBfs::tiny_overflows)
       .def("release", &HipBiBfs::release, py::call_guard<py::gil_scoped_release>())
       .def("search_batch", &HipBiBfs::search_batch, py::arg("src"), py::arg("dst"),
            py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>())

@@ -320,6 +320,7 @@ def test_tiny_server_query_vs_oracle(gpu_engine):
     assert gpu_engine.tiny_engine
     pairs = pairs_for(g.n, 300, 41) + [(7, 7)]
     gpu_engine.set_resident(True)
+    ovf0 = gpu_engine.tiny_overflows
     try:
         for i, (s, d) in enumerate(pairs):
             h, path = gpu_engine.query(s, d)
@@ -334,6 +335,11 @@ def test_tiny_server_query_vs_oracle(gpu_engine):
                 check_result(g.csr, s, d, r.hops, r.path, truth)
         assert_engine(gpu_engine, g, pairs[:40])
         assert gpu_engine.query(0, 99999)[0] == 17
+        # reference-shape queries fit the tiny server: few may fall back (a
+        # fallback still answers correctly, so only this count catches a
+        # server that hands everything back)
+        ovf = gpu_engine.tiny_overflows - ovf0
+        assert ovf <= len(pairs) // 20, ovf
     finally:
         gpu_engine.set_resident(False)
 
@@ -346,10 +352,12 @@ def test_tiny_server_overflow_falls_back(gpu_engine):
     gpu_engine.load(g)
     assert gpu_engine.tiny_engine
     gpu_engine.set_resident(True)
+    ovf0 = gpu_engine.tiny_overflows
     try:
         for s, d in pairs_for(g.n, 40, 5):
             h, path = gpu_engine.query(s, d)
             check_result(g.csr, s, d, h, path, native.bfs_oracle(g.csr, s, d).hops)
+        assert gpu_engine.tiny_overflows > ovf0  # this graph's frontiers do outgrow the tiny server
     finally:
         gpu_engine.set_resident(False)
 
