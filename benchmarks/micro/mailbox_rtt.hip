@@ -52,6 +52,57 @@ __global__ void k_echo(const uint32_t* req, uint32_t* resp, uint32_t n, int pipe
   }
 }
 
+// Ring of 4 poll loads kept in flight (a new one issued as each returns),
+// spaced by s_sleep: a request is seen one PCIe read after it lands plus a
+// fraction of the spacing, instead of up to two reads later.
+__global__ void k_echo_ring(const uint32_t* req, uint32_t* resp, uint32_t n) {
+  uint32_t last = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t s, a, b, c, d, k = 0;
+    asm volatile(
+        "global_load_dword %[a], %[p], off sc0 sc1\n\t"
+        "s_sleep 2\n\t"
+        "global_load_dword %[b], %[p], off sc0 sc1\n\t"
+        "s_sleep 2\n\t"
+        "global_load_dword %[c], %[p], off sc0 sc1\n\t"
+        "s_sleep 2\n\t"
+        "global_load_dword %[d], %[p], off sc0 sc1\n"
+        "1:\n\t"
+        "s_waitcnt vmcnt(3)\n\t"
+        "v_readfirstlane_b32 %[s], %[a]\n\t"
+        "s_cmp_lg_u32 %[s], %[last]\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "global_load_dword %[a], %[p], off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(3)\n\t"
+        "v_readfirstlane_b32 %[s], %[b]\n\t"
+        "s_cmp_lg_u32 %[s], %[last]\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "global_load_dword %[b], %[p], off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(3)\n\t"
+        "v_readfirstlane_b32 %[s], %[c]\n\t"
+        "s_cmp_lg_u32 %[s], %[last]\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "global_load_dword %[c], %[p], off sc0 sc1\n\t"
+        "s_waitcnt vmcnt(3)\n\t"
+        "v_readfirstlane_b32 %[s], %[d]\n\t"
+        "s_cmp_lg_u32 %[s], %[last]\n\t"
+        "s_cbranch_scc1 2f\n\t"
+        "global_load_dword %[d], %[p], off sc0 sc1\n\t"
+        "s_add_u32 %[k], %[k], 1\n\t"
+        "s_cmp_lt_u32 %[k], 0x800000\n\t"  // bounded: ~4 polls per pass, a few seconds
+        "s_cbranch_scc1 1b\n\t"
+        "s_mov_b32 %[s], %[last]\n"
+        "2:\n\t"
+        "s_waitcnt vmcnt(0)"
+        : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [s] "=&s"(s), [k] "+s"(k)
+        : [p] "v"(req), [last] "s"(last)
+        : "scc", "memory");
+    if (s == last) return;  // timed out
+    last = s;
+    __hip_atomic_store(resp, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ void k_flag(uint32_t* resp, uint32_t v) {
   __hip_atomic_store(resp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -67,7 +118,10 @@ static double run_echo(uint32_t* req_host_view, const uint32_t* req_dev_view, ui
   *(volatile uint32_t*)resp = 0;
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  k_echo<<<1, 64, 0, st>>>(req_dev_view, resp, n, pipelined);
+  if (pipelined == 2)
+    k_echo_ring<<<1, 64, 0, st>>>(req_dev_view, resp, n);
+  else
+    k_echo<<<1, 64, 0, st>>>(req_dev_view, resp, n, pipelined);
   CK(hipGetLastError());
   std::vector<double> rt;
   for (uint32_t i = 1; i <= n; ++i) {
@@ -95,6 +149,9 @@ int main() {
   CK(hipHostMalloc(reinterpret_cast<void**>(&resp), 4096, hipHostMallocMapped | hipHostMallocCoherent));
   std::printf("host-pinned mailbox, serial polls    : %.2f us\n", run_echo(hreq, hreq, resp, 0));
   std::printf("host-pinned mailbox, pipelined polls : %.2f us\n", run_echo(hreq, hreq, resp, 1));
+  std::printf("host-pinned mailbox, ring of 4 polls : %.2f us\n", run_echo(hreq, hreq, resp, 2));
+  std::printf("host-pinned mailbox, serial polls    : %.2f us (again)\n", run_echo(hreq, hreq, resp, 0));
+  std::printf("host-pinned mailbox, ring of 4 polls : %.2f us (again)\n", run_echo(hreq, hreq, resp, 2));
 
   uint32_t* dfine = nullptr;
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&dfine), 4096, hipDeviceMallocFinegrained) == hipSuccess) {

@@ -720,7 +720,7 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_pkts), kTinyPktCap * sizeof(TinyPkt),
                           hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(p_->h_pkts, 0, kTinyPktCap * sizeof(TinyPkt));
-  HIP_CHECK(hipMalloc(&p_->d_stamps, 16 * sizeof(unsigned long long)));
+  HIP_CHECK(hipMalloc(&p_->d_stamps, 32 * sizeof(unsigned long long)));
   HIP_CHECK(hipEventCreate(&p_->ev0));
   HIP_CHECK(hipEventCreate(&p_->ev1));
 }

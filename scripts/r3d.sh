@@ -5,3 +5,5 @@ BIBFS_TINY_STAMP=1 timeout -k 10 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999
 head -4 $O/r3d_stamp.txt
 timeout -k 10 600 bash scripts/ab_tiny.sh > $O/r3d_ab.log 2>&1 || { echo AB_FAILED; tail $O/r3d_ab.log; exit 1; }
 cat $O/ab_tiny.jsonl
+timeout -k 10 60 ./build/bin/mailbox_rtt > $O/r3d_mailbox.txt 2>&1 || { echo MAILBOX_FAILED; tail $O/r3d_mailbox.txt; exit 1; }
+cat $O/r3d_mailbox.txt
