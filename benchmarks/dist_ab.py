@@ -7,6 +7,8 @@ first design); K > 0 enqueues K device-planned rounds per host wait.  Pairs and
 their hop counts come from the single-GPU engine; every answer is checked.
 
     python benchmarks/dist_ab.py --specs gnp:1000000::2,kron:22 --modes 0,2,4,8 --queries 24
+
+A mode "K:E" also sets the one-rank solo workgroup's edge cap (E = 0: solo off).
 """
 import argparse
 import json
@@ -41,8 +43,14 @@ def main():
         t0 = time.perf_counter()
         bench.generate(eng, spec)
         build_ms = (time.perf_counter() - t0) * 1e3
-        for k in [int(x) for x in a.modes.split(",")]:
-            eng.set_tuning(make_tuning(spec_rounds=k))
+        for mode in a.modes.split(","):
+            k, _, e = mode.partition(":")
+            k = int(k)
+            solo_e = int(e) if e else None
+            if solo_e is None:
+                eng.set_tuning(make_tuning(spec_rounds=k))
+            else:
+                eng.set_tuning(make_tuning(spec_rounds=k, solo=solo_e > 0, solo_edges=max(solo_e, 1)))
             for s, d, _ in pairs[:3]:
                 eng.search(s, d)  # warm
             qms, dms, st = [], [], []
@@ -55,13 +63,15 @@ def main():
                     dms.append(r.search_ms)
                     st.append(eng.last_stats)
             rec = {
-                "spec": spec, "n": n, "spec_rounds": k, "queries": len(qms), "build_ms": round(build_ms, 2),
+                "spec": spec, "n": n, "spec_rounds": k, "solo_edges": solo_e, "queries": len(qms),
+                "build_ms": round(build_ms, 2),
                 "median_query_ms": round(statistics.median(qms), 4), "mean_query_ms": round(statistics.mean(qms), 4),
                 "median_device_ms": round(statistics.median(dms), 4),
                 "mean_rounds": round(statistics.mean(x["rounds"] for x in st), 3),
                 "mean_host_syncs": round(statistics.mean(x["host_syncs"] for x in st), 3),
                 "mean_host_rounds": round(statistics.mean(x["host_rounds"] for x in st), 3),
                 "mean_spec_rounds": round(statistics.mean(x["spec_rounds"] for x in st), 3),
+                "mean_solo_rounds": round(statistics.mean(x["solo_rounds"] for x in st), 3),
                 "mean_collectives": round(statistics.mean(x["collectives"] for x in st), 3),
                 "mean_dense_levels": round(statistics.mean(x["dense_levels"] for x in st), 3),
                 "mean_exchanged_kb": round(statistics.mean(x["exchanged_bytes"] for x in st) / 1024, 1),

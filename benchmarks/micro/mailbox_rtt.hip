@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <x86intrin.h>
 
+#include <setjmp.h>
+#include <signal.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -107,6 +110,24 @@ __global__ void k_flag(uint32_t* resp, uint32_t v) {
   __hip_atomic_store(resp, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+static sigjmp_buf g_jb;
+static void on_segv(int) { siglongjmp(g_jb, 1); }
+// Can the CPU store to this device pointer directly (large-BAR mapping)?
+static bool cpu_writable(uint32_t* p) {
+  struct sigaction sa{}, old{};
+  sa.sa_handler = on_segv;
+  sigaction(SIGSEGV, &sa, &old);
+  sigaction(SIGBUS, &sa, nullptr);
+  bool ok = false;
+  if (sigsetjmp(g_jb, 1) == 0) {
+    *(volatile uint32_t*)p = 0;
+    ok = true;
+  }
+  sigaction(SIGSEGV, &old, nullptr);
+  signal(SIGBUS, SIG_DFL);
+  return ok;
+}
+
 static double median(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v[v.size() / 2];
@@ -161,10 +182,25 @@ int main() {
     if (at.hostPointer) {
       std::printf("device-fine mailbox, serial polls    : %.2f us\n",
                   run_echo(static_cast<uint32_t*>(at.hostPointer), dfine, resp, 0));
+    } else if (cpu_writable(dfine)) {
+      std::printf("device-fine mailbox (CPU stores through the device pointer), serial polls : %.2f us\n",
+                  run_echo(dfine, dfine, resp, 0));
+      std::printf("device-fine mailbox (CPU stores through the device pointer), ring of 4    : %.2f us\n",
+                  run_echo(dfine, dfine, resp, 2));
     } else {
-      std::printf("device-fine mailbox: not host-mapped\n");
+      std::printf("device-fine mailbox: not CPU-writable\n");
     }
   }
+  uint32_t* dunc = nullptr;
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&dunc), 4096, hipDeviceMallocUncached) == hipSuccess) {
+    if (cpu_writable(dunc))
+      std::printf("device-uncached mailbox, serial polls : %.2f us\n", run_echo(dunc, dunc, resp, 0));
+    else
+      std::printf("device-uncached mailbox: not CPU-writable\n");
+  }
+  uint32_t* dplain = nullptr;
+  CK(hipMalloc(reinterpret_cast<void**>(&dplain), 4096));
+  std::printf("plain hipMalloc: CPU-writable %d\n", (int)cpu_writable(dplain));
   // launch round trip
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));

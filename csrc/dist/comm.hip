@@ -74,12 +74,19 @@ class RcclComm final : public Comm {
     RCCL_CHECK(ncclGroupStart());
   }
   void group_end() override { RCCL_CHECK(ncclGroupEnd()); }
+  // A one-rank collective is the identity: no RCCL launch (and none of its
+  // internal stream hand-offs) on the world-1 path.
   void allreduce(void* buf, size_t count, DType t, ROp op, hipStream_t s) override {
     live();
+    if (size_ == 1) return;
     RCCL_CHECK(ncclAllReduce(buf, buf, count, nccl_type(t), nccl_op(op), comm_, s));
   }
   void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
     live();
+    if (size_ == 1) {
+      if (send != recv && bytes) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+      return;
+    }
     if (bytes % 4 == 0)
       RCCL_CHECK(ncclAllGather(send, recv, bytes / 4, ncclUint32, comm_, s));
     else

@@ -71,6 +71,9 @@ constexpr uint32_t kSpecCapMin = 1024;          // smallest speculative candidat
 // that holds it: it is deferred to a hub list whose edges the whole grid then
 // walks edge-parallel (a degree-10^6 hub would otherwise serialise on one CU).
 constexpr uint64_t kHubDeg = 512;
+// Levels with more frontier edges than this read the visited word before the
+// claim's atomicOr (ClaimMeet::precheck).
+constexpr uint64_t kPrecheckEdges = 1u << 16;
 constexpr uint64_t kNoHubs = ~0ull;
 constexpr int kHubTile = 1024;                  // hubs staged in LDS per pass
 constexpr uint32_t kSpecHubCap = 4096;          // speculative blocks up to this size skip the hub pass
@@ -95,6 +98,7 @@ struct Ctl {
   unsigned long long vis[2];   // vertices side s claimed (incl. the root)
   unsigned long long key;      // (length << 32) | meet vertex, once found
   unsigned long long einsp;    // edges inspected by the expanded levels
+  unsigned long long ticks;    // device time of the search (s_memrealtime, 100 MHz): seed -> this plan
   uint32_t depth[2];           // depth of the current frontier
   uint32_t dir[2];             // 1 top-down, 2 bottom-up (Beamer state)
   uint32_t turn;               // alternate policy
@@ -104,7 +108,7 @@ struct Ctl {
   uint32_t want, want_modes;   // the planned round (kept when it stalls)
   uint32_t stall;              // kStall* reason
   uint32_t rounds, lockstep_rounds, levels, sparse_levels;
-  uint32_t pad;
+  uint32_t next_it;            // k_spec_solo's exit: the round the host continues with
 };
 
 struct Policy {
@@ -112,6 +116,9 @@ struct Policy {
   unsigned long long nnz_total;
   uint32_t n;
   int lockstep, side, direction;
+  uint32_t epoch;     // search number: tags the plan words (a late no-op round of the previous search never matches)
+  uint32_t walk_cap;  // words of the pinned path buffer (one rank: the round that ends the search walks the path)
+  int want_path;
 };
 
 // Reduced across ranks (device words), double-buffered like Ctl.
@@ -141,6 +148,7 @@ struct DState {
   uint32_t pad;
   unsigned long long new_edges[2];      // degree sum of the vertices side s claimed this level
   uint32_t meet_found;                  // a single-side level claimed a vertex the other side holds
+  unsigned long long t0;                // s_memrealtime at the seed
   uint32_t pad2;
 };
 
@@ -163,6 +171,8 @@ struct DView {
   DState* st;
   Ctl* ctl;                   // [2]
   uint64_t* plan_ring;        // pinned [kPlanRing]: slot it % kPlanRing = fed_max << 32 | (it + 1) << 8 | state << 2 | sides
+  Ctl* host_ctl;              // pinned: the accounted Ctl, written by the round whose plan ends the search
+  uint32_t* host_walk;        // pinned: {status, dS, dT, epoch, path[]} (one rank, the same round)
   struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
   uint32_t trace_cap;
   Reduced* red;               // [2]
@@ -175,12 +185,35 @@ __device__ __forceinline__ T* pick(T* const (&a)[2], int s) {
 
 __host__ __device__ inline uint64_t block_words(uint32_t cap) { return 2 + 2 * (uint64_t)cap; }
 
+// Copy a small struct into LDS, one 32-bit word per thread (the block's
+// threads issue the loads together).
+__device__ __forceinline__ void stage_words(void* dst, const void* src, size_t bytes) {
+  for (uint32_t k = threadIdx.x; k < bytes / 4; k += blockDim.x)
+    static_cast<uint32_t*>(dst)[k] = static_cast<const uint32_t*>(src)[k];
+}
+
 // ---------------------------------------------------------------------------
 // Round policy (device).  Accounts the previous round, then plans this one.
 // Every input is a reduced value, so every rank computes the same plan.
 // ---------------------------------------------------------------------------
-__device__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, uint64_t spec_cap, int flags,
-                           Ctl& c) {
+__device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd, const Policy& pol,
+                                                uint64_t spec_cap, int flags, Ctl& c);
+
+// The planner runs on one thread with every operand in registers: its inputs
+// are copied in once (one round of independent loads, LDS or global) and the
+// plan copied out once -- on references into LDS or global memory its ~50
+// dependent field accesses cost ~8k cycles per round (measured, k_spec_solo).
+__device__ __forceinline__ void plan_round(const Ctl& p, const Reduced& rd, const Policy& pol, uint64_t spec_cap,
+                                           int flags, Ctl& out) {
+  const Ctl pl = p;
+  const Reduced rl = rd;
+  Ctl cl;
+  plan_round_regs(pl, rl, pol, spec_cap, flags, cl);
+  out = cl;
+}
+
+__device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd, const Policy& pol,
+                                                uint64_t spec_cap, int flags, Ctl& c) {
   c = p;
   c.sides = 0;
   c.modes = 0;
@@ -309,6 +342,11 @@ struct ClaimMeet {
   unsigned long long* meetkey = nullptr;
   uint32_t dother = 0;  // the other side's frontier depth this round
   bool single = false;
+  // read the visited word before the atomicOr (skips the atomic for a vertex
+  // already held): pays on big levels, where most edges lead to visited
+  // vertices and the atomics' throughput counts; a small level's latency
+  // chain is one round trip shorter without it
+  bool precheck = true;
 };
 
 // Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
@@ -320,9 +358,15 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
   uint32_t* vis = pick(V.vis, s);
   bool mine = false;
   unsigned long long best = kNoKey;
+  unsigned long long rb = 0, re = 0;
   if (want) {
     const uint32_t bit = 1u << (li & 31);
-    if (!(vis[li >> 5] & bit)) mine = !(atomicOr(&vis[li >> 5], bit) & bit);
+    if (!cm.precheck || !(vis[li >> 5] & bit)) {
+      const uint32_t old = atomicOr(&vis[li >> 5], bit);
+      rb = V.row_off[li];  // the degree, fetched beside the claim (independent of its result)
+      re = V.row_off[li + 1];
+      mine = !(old & bit);
+    }
     if ((cm.meetkey || cm.single) && mine &&
         (__hip_atomic_load(&pick(V.vis, s ^ 1)[li >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) {
       if (cm.meetkey) {
@@ -349,7 +393,7 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
   if (mine) {
     pick(V.parent, s)[li] = u;
     pick(V.depth, s)[li] = dnew;
-    deg = V.row_off[li + 1] - V.row_off[li];
+    deg = re - rb;
   }
   uint32_t pos = 0;
   if (lane == (uint32_t)leader) pos = atomicAdd(&V.st->qtail[s], (uint32_t)__popcll(mask));
@@ -392,16 +436,16 @@ __device__ __forceinline__ bool meet_seen(const DView& V) {
 
 // exit_on_meet: a single-side level, which stops once a meet is claimed.
 __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pairs, uint32_t cap, uint32_t b0,
-                               uint32_t nb, uint64_t hub_deg, bool exit_on_meet, const ClaimMeet& cm) {
+                               uint32_t nb, uint64_t hub_deg, bool exit_on_meet, const ClaimMeet& cm, uint32_t fb,
+                               uint32_t F) {
   __shared__ uint32_t su[kThreads];
   __shared__ unsigned long long sb[kThreads], se[kThreads];
   __shared__ unsigned long long wsum[kThreads / kWave];
   __shared__ uint32_t sstop;
-  const uint32_t fb = V.st->fbeg[s], F = V.st->fend[s] - fb;
   const uint32_t* q = pick(V.queue, s);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   for (uint64_t c0 = (uint64_t)b0 * kThreads; c0 < F; c0 += (uint64_t)nb * kThreads) {
-    if (exit_on_meet) {  // block-uniform: the flag goes through LDS between barriers
+    if (exit_on_meet && c0 != (uint64_t)b0 * kThreads) {  // block-uniform: the flag goes through LDS between barriers
       if (tid == 0) sstop = meet_seen(V) ? 1u : 0u;
       __syncthreads();
       if (sstop) break;
@@ -512,6 +556,50 @@ __device__ __forceinline__ bool last_block(uint32_t* counter, uint32_t nblocks) 
   return last != 0;
 }
 
+// Plan-word tag: the search's epoch (8 bits) and the round number + 1 (16 bits;
+// the host waits for a round at most kPlanRing - 1 behind the newest).
+__host__ __device__ inline uint32_t plan_tag(uint32_t epoch, uint32_t it) {
+  return (epoch & 0xffu) << 16 | ((it + 1u) & 0xffffu);
+}
+
+// One rank, the round whose plan ends the search: the two parent chains from
+// the meet vertex into the pinned path buffer {status, dS, dT, epoch, path}
+// (status 0 = walked, 1 = inconsistent, 2 = longer than the buffer: the host
+// launches k_walk_local).  Called by a whole wave: lanes 0 and 1 walk one
+// side each (one dependent load per hop).
+__device__ void terminal_walk(const DView& V, unsigned long long key, const Policy& pol) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t* out = V.host_walk;
+  const uint32_t meet = (uint32_t)key, hops = (uint32_t)(key >> 32);
+  const bool fits = 4 + (uint64_t)hops + 1 <= pol.walk_cap && meet >= V.lo && meet < V.hi;
+  uint32_t d0 = 0, d1 = 0;
+  if (fits) {
+    d0 = V.depth[0][meet - V.lo];
+    d1 = V.depth[1][meet - V.lo];
+  }
+  bool ok = fits && d0 != kEmpty && d1 != kEmpty && d0 + d1 == hops;
+  if (lane < 2 && ok) {
+    const int sd = (int)lane;
+    const uint32_t len = sd ? d1 : d0;
+    uint32_t v = meet;
+    for (uint32_t k = 0; k <= len && ok; ++k) {
+      __hip_atomic_store(out + 4 + (sd ? d0 + k : d0 - k), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (k < len) {
+        v = V.parent[sd][v - V.lo];
+        ok = v >= V.lo && v < V.hi;
+      }
+    }
+  }
+  const bool both = __shfl(ok ? 1 : 0, 0) && __shfl(ok ? 1 : 0, 1);
+  if (lane == 0) {
+    __hip_atomic_store(out + 1, d0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out + 2, d1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out + 3, pol.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(out, !fits ? 2u : both ? 0u : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __threadfence_system();
+}
+
 // ---- speculative round kernels ---------------------------------------------
 
 // Plan (every block computes the same plan; block 0 publishes it) + top-down
@@ -521,27 +609,59 @@ __device__ __forceinline__ bool last_block(uint32_t* counter, uint32_t nblocks) 
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
                                                           int flags, uint64_t hub_deg, int header, int finish) {
   const int p = it & 1;
-  __shared__ Ctl c;
-  if (threadIdx.x == 0) plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, cap, flags, c);
+  __shared__ Ctl c, prev;
+  __shared__ Reduced rd;
+  __shared__ uint32_t fr[4];  // frontier bounds: fbeg[2], fend[2]
+  // the previous plan and reduction (and the frontier bounds) staged into LDS
+  // with one round of parallel loads (thread 0 alone would chain them
+  // through plan_round's branches)
+  stage_words(&prev, &V.ctl[p ^ 1], sizeof(Ctl));
+  stage_words(&rd, &V.red[p ^ 1], sizeof(Reduced));
+  if (threadIdx.x >= kThreads - 4) {
+    const uint32_t k = threadIdx.x - (kThreads - 4);
+    fr[k] = k < 2 ? V.st->fbeg[k] : V.st->fend[k - 2];
+  }
   __syncthreads();
+  if (threadIdx.x == 0) plan_round(prev, rd, pol, cap, flags, c);
+  __syncthreads();
+  const bool terminal = c.state == kDone || c.state == kDead;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < kWave) {
+    if (threadIdx.x == 0) publish(V, p, prev, rd, c);
+    // the round that ends the search hands the host its accounted Ctl directly
+    // (no k_final launch + wait after the batch); later no-op rounds repeat it
+    const bool first_end = terminal && prev.state == kRun;
+    // one rank holds every parent: walk the path now, into pinned memory
+    if (first_end && V.P == 1 && c.state == kDone && pol.want_path) terminal_walk(V, c.key, pol);
+    if (first_end && threadIdx.x == 0) {
+      c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
+      const uint64_t* src = reinterpret_cast<const uint64_t*>(&c);
+      uint64_t* dst = reinterpret_cast<uint64_t*>(V.host_ctl);
+      for (uint32_t k = 0; k < sizeof(Ctl) / 8; ++k)
+        __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
+  }
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
     // one 8-byte write-through store per round: the host paces its enqueueing
     // on the plan and sizes the rounds it enqueues from the frontier (larger
     // side's edge count, clamped to 32 bits)
     const unsigned long long fm = min(max(c.fmax[0], c.fmax[1]), 0xffffffffull);
     __hip_atomic_store(&V.plan_ring[it % kPlanRing],
-                       (uint64_t)fm << 32 | ((it + 1u) << 8) | (c.state << 2) | (c.sides & 3u), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+                       (uint64_t)fm << 32 | ((uint64_t)plan_tag(pol.epoch, it) << 8) | (c.state << 2) | (c.sides & 3u),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // a round enqueued past the end of the search: nothing to expand, no round
+  // end (every block sees the same plan, so no block counts itself in)
+  if (terminal) return;
   const int s = blockIdx.y;
   if ((c.sides >> s) & 1) {
     ClaimMeet cm;
     cm.meetkey = &V.red[p].meetkey;
     cm.dother = c.depth[s ^ 1];
     cm.single = c.sides != 3u;
+    cm.precheck = c.fed[s] > kPrecheckEdges;
     td_expand_side(V, s, c.depth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
-                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u, cm);
+                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u, cm, fr[s], fr[2 + s] - fr[s]);
   }
   if (!header) return;  // k_td_hubs runs next and writes the headers
   if (finish) drain_atomics();
@@ -554,6 +674,318 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     }
     if (finish && threadIdx.x == kWave) spec_round_end(V, it, c.sides);  // another wave: the header atomics are independent
   }
+}
+
+// ---- one-rank solo rounds -----------------------------------------------------
+// With one rank there is no exchange, so the sparse rounds need no kernel
+// boundary at all: ONE workgroup runs round after round with the frontiers,
+// their row offsets and degree prefixes in LDS, the round's counters in LDS
+// and the visited bitmaps claimed with L2 atomics (one CU: no device-scope
+// round trip, no last-block detection, no plan word per round).  It stops at
+// the first round it cannot hold -- a side above kSoloV vertices or kSoloE
+// edges, or a bottom-up plan -- and leaves the state exactly as a stalled
+// speculative round does (ctl/red/st), so the multi-workgroup rounds or a
+// host-planned round take over; a plan that ends the search walks the path
+// (terminal_walk) and publishes like k_spec_expand.
+constexpr int kSoloT = 512;  // 2 waves per SIMD: 256 VGPRs (the unrolled claims need them)
+constexpr uint32_t kSoloV = 2048;  // frontier vertices per side held in LDS
+constexpr uint32_t kSoloE = 8192;  // frontier edges per side one solo round expands
+constexpr uint32_t kSoloRounds = 1u << 16;
+constexpr int kSoloU = 4;          // edges per thread in flight per pass
+
+// Exclusive prefix of ND[0, cnt) into FP[0, cnt], FP[cnt] = total; half the
+// workgroup per side (t = thread index within the half).
+__device__ void solo_scan(const uint32_t* ND, uint32_t* FP, uint32_t cnt, uint32_t t, uint32_t* wtot) {
+  constexpr uint32_t kHalf = kSoloT / 2, kPer = kSoloV / kHalf, kWaves = kHalf / 64;
+  uint32_t v[kPer], run = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = t * kPer + k;
+    v[k] = i < cnt ? ND[i] : 0u;
+    run += v[k];
+  }
+  uint32_t x = run;  // inclusive wave scan of the per-thread sums
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if ((t & 63) >= (uint32_t)o) x += y;
+  }
+  if ((t & 63) == 63) wtot[t >> 6] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < kWaves; ++w) {
+    base += w < (t >> 6) ? wtot[w] : 0u;
+    tot += wtot[w];
+  }
+  uint32_t e = base + x - run;
+#pragma unroll
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = t * kPer + k;
+    if (i < cnt) FP[i] = e;
+    e += v[k];
+  }
+  if (t == 0) FP[cnt < kSoloV ? cnt : kSoloV] = tot;
+}
+
+// kStamp (BIBFS_DIST_STAMP=1): thread 0's cycles per phase summed over the
+// rounds into stamps[0..7] = {plan, edges, end, scan, rounds, edges expanded, setup, exit}.
+__device__ __forceinline__ unsigned long long solo_clock() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+template <bool kStamp>
+__global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, Policy pol, uint32_t emax,
+                                                         uint32_t* fin, uint32_t tag, unsigned long long* stamps) {
+  unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tp = kStamp ? solo_clock() : 0;
+#define SOLO_PH(k)                                \
+  if (kStamp && threadIdx.x == 0) {               \
+    const unsigned long long t_ = solo_clock();   \
+    ph[k] += t_ - tp;                             \
+    tp = t_;                                      \
+  }
+  __shared__ Ctl c, pc;  // this round's plan / the executed previous plan
+  __shared__ Reduced rd;  // the previous round's reduction (one rank: local)
+  __shared__ uint32_t FV[2][2][kSoloV];             // [buffer][side] frontier vertices
+  __shared__ unsigned long long FB[2][2][kSoloV];   // their row begins
+  __shared__ uint32_t FP[2][kSoloV + 1];             // [side] exclusive degree prefix of the current frontier
+  __shared__ uint32_t ND[2][kSoloV];                 // [side] degrees of the vertices claimed this round
+  __shared__ uint32_t wtot[2][kSoloT / 128];
+  __shared__ uint32_t nf[2], qt[2], fbg[2], fnd[2], cb[2], go;
+  __shared__ unsigned long long ne[2], best;
+  const uint32_t tid = threadIdx.x;
+  // the arrays in registers: selected per lane by side (an indexed DView
+  // member would be a vector load from the kernel arguments per use)
+  const uint32_t* const col = V.col;
+  const uint64_t* const row_off = V.row_off;
+  uint32_t* const vis0 = V.vis[0];
+  uint32_t* const vis1 = V.vis[1];
+  uint32_t* const par0 = V.parent[0];
+  uint32_t* const par1 = V.parent[1];
+  uint32_t* const dep0 = V.depth[0];
+  uint32_t* const dep1 = V.depth[1];
+  uint32_t* const que0 = V.queue[0];
+  uint32_t* const que1 = V.queue[1];
+  const uint32_t lo = V.lo;
+  const uint32_t half = tid / (kSoloT / 2);  // the side a thread scans for
+  const int pp = (it0 + 1) & 1;  // buffers of round it0 - 1
+  stage_words(&pc, &V.ctl[pp], sizeof(Ctl));
+  stage_words(&rd, &V.red[pp], sizeof(Reduced));
+  if (tid < 2) {
+    fbg[tid] = V.st->fbeg[tid];
+    fnd[tid] = V.st->fend[tid];
+    qt[tid] = V.st->qtail[tid];
+    cb[tid] = 0;
+  }
+  __syncthreads();
+  // the current frontiers (at most kSoloV each, or the first plan stops)
+  for (uint32_t i = tid; i < 2 * kSoloV; i += kSoloT) {
+    const uint32_t sd = i / kSoloV, k = i % kSoloV;
+    if (fbg[sd] + k < fnd[sd]) {
+      const uint32_t v = V.queue[sd][fbg[sd] + k];
+      const unsigned long long b = V.row_off[v - V.lo];
+      FV[0][sd][k] = v;
+      FB[0][sd][k] = b;
+      ND[sd][k] = (uint32_t)min(V.row_off[v - V.lo + 1] - b, (unsigned long long)kSoloE + 1);
+    }
+  }
+  __syncthreads();
+  solo_scan(ND[half], FP[half], min(fnd[half] - fbg[half], kSoloV), tid % (kSoloT / 2), wtot[half]);
+  __syncthreads();
+
+  uint32_t it = it0;
+  SOLO_PH(6)
+  for (uint32_t r = 0; r < kSoloRounds; ++r, ++it) {
+    if (tid == 0) {
+      const unsigned long long ta = kStamp ? solo_clock() : 0;
+      plan_round(pc, rd, pol, emax, 0, c);  // a side above emax frontier edges: kStallCap
+      if (kStamp) ph[8] += solo_clock() - ta;
+      bool fits = true;
+      for (int sd = 0; sd < 2; ++sd)
+        if (((c.want >> sd) & 1) && (c.cnt[sd] > kSoloV || fnd[sd] - fbg[sd] > kSoloV)) fits = false;
+      if (c.state == kRun && !fits) {  // the multi-workgroup rounds take it from here
+        c.state = kStall;
+        c.stall = kStallCap;
+        c.sides = c.modes = 0;
+        c.einsp = pc.einsp;
+        c.sparse_levels = pc.sparse_levels;
+      }
+      go = c.state == kRun;
+      if (go) {
+        const unsigned long long tb = kStamp ? solo_clock() : 0;
+        publish(V, it & 1, pc, rd, c);
+        if (kStamp) ph[9] += solo_clock() - tb;
+        nf[0] = nf[1] = 0;
+        ne[0] = ne[1] = 0;
+        best = kNoKey;
+      }
+    }
+    __syncthreads();
+    SOLO_PH(0)
+    if (!go) break;
+    const uint32_t sides = c.sides;
+    const uint32_t F0 = (sides & 1) ? fnd[0] - fbg[0] : 0u, F1 = (sides & 2) ? fnd[1] - fbg[1] : 0u;
+    const uint32_t E0 = (sides & 1) ? FP[0][F0] : 0u, E1 = (sides & 2) ? FP[1][F1] : 0u;
+    const bool pre = c.fed[0] + c.fed[1] > kPrecheckEdges;
+    const uint32_t dn0 = c.depth[0] + 1, dn1 = c.depth[1] + 1;  // depth of this round's claims per side
+    // kSoloU edges per thread per pass, every load of a pass in flight together;
+    // the pass loop is wave-uniform (appends are aggregated per wave)
+    const uint32_t E = E0 + E1, lane = tid & 63;
+    for (uint32_t base = 0; base + (tid & ~63u) < E; base += kSoloT * kSoloU) {
+      uint32_t uu[kSoloU], vv[kSoloU], old[kSoloU], oth[kSoloU];
+      unsigned long long ad[kSoloU], rb[kSoloU], re[kSoloU];
+      int ss[kSoloU];
+      bool ok[kSoloU], mine[kSoloU];
+#pragma unroll
+      for (int j = 0; j < kSoloU; ++j) {
+        const uint32_t e = base + (uint32_t)j * kSoloT + tid;
+        ok[j] = e < E;
+        const int sd = e >= E0;
+        ss[j] = sd;
+        const uint32_t k = ok[j] ? (sd ? e - E0 : e) : 0u, b = cb[sd];
+        uint32_t a = 0, z = ok[j] ? (sd ? F1 : F0) : 1u;  // last slot whose edge range starts at or before k
+        while (z - a > 1) {
+          const uint32_t mid = (a + z) >> 1;
+          if (FP[sd][mid] <= k) a = mid;
+          else z = mid;
+        }
+        uu[j] = FV[b][sd][a];
+        ad[j] = FB[b][sd][a] + (k - FP[sd][a]);
+      }
+#pragma unroll
+      for (int j = 0; j < kSoloU; ++j) vv[j] = col[ok[j] ? ad[j] : 0ull];  // an idle slot reads a valid word
+#pragma unroll
+      for (int j = 0; j < kSoloU; ++j) vv[j] = ok[j] ? vv[j] : lo;
+      // claims: one CU, so the atomics are performed in its L2 (workgroup
+      // scope); the degree is fetched beside the claim
+#pragma unroll
+      for (int j = 0; j < kSoloU; ++j) {
+        const uint32_t li = vv[j] - lo, bit = 1u << (li & 31);
+        uint32_t* w = (ss[j] ? vis1 : vis0) + (li >> 5);
+        const bool claim = ok[j] && (!pre || !(*w & bit));  // a stale L1 word only misses bits: safe
+        old[j] = claim ? __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : bit;
+        rb[j] = claim ? row_off[li] : 0ull;
+        re[j] = claim ? row_off[li + 1] : 0ull;
+      }
+      // the other side's word, read in L2 after this claim completed: of two
+      // same-round claims of a vertex the later one sees the earlier
+#pragma unroll
+      for (int j = 0; j < kSoloU; ++j) {
+        const uint32_t li = vv[j] - lo, bit = 1u << (li & 31);
+        mine[j] = !(old[j] & bit);
+        oth[j] = mine[j] ? __hip_atomic_fetch_or((ss[j] ? vis0 : vis1) + (li >> 5), 0u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP)
+                         : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < kSoloU; ++j) {
+        const uint32_t li = vv[j] - lo, bit = 1u << (li & 31);
+        const int sd = ss[j];
+        const uint32_t dnew = sd ? dn1 : dn0;
+        if (mine[j] && (oth[j] & bit)) {  // rare: a meet
+          uint32_t dd = __hip_atomic_fetch_add((sd ? dep0 : dep1) + li, 0u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (dd == kEmpty) dd = (sd ? dn0 : dn1);  // claimed this round, its store not performed yet
+          atomicMin(&best, ((unsigned long long)(dnew + dd) << 32) | vv[j]);
+        }
+        if (mine[j]) {
+          (sd ? par1 : par0)[li] = uu[j];
+          __hip_atomic_store((sd ? dep1 : dep0) + li, dnew, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {  // appends: one LDS atomic per wave and side
+          const bool here = mine[j] && sd == side;
+          const unsigned long long m = __ballot(here);
+          if (!m) continue;  // wave-uniform
+          uint32_t pos = 0;
+          if (lane == 0) pos = atomicAdd(&nf[side], (uint32_t)__popcll(m));
+          pos = __shfl(pos, 0) + mbcnt64(m);
+          const unsigned long long dg = here ? re[j] - rb[j] : 0ull;
+          const unsigned long long dsum = wave_sum(dg);
+          if (lane == 0) atomicAdd(&ne[side], dsum);
+          if (here) {
+            (side ? que1 : que0)[qt[side] + pos] = vv[j];
+            if (pos < kSoloV) {
+              FV[cb[side] ^ 1][side][pos] = vv[j];
+              FB[cb[side] ^ 1][side][pos] = rb[j];
+              ND[side][pos] = (uint32_t)min(dg, (unsigned long long)kSoloE + 1);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    SOLO_PH(1)
+    if (kStamp && tid == 0) {
+      ph[4] += 1;
+      ph[5] += E;
+    }
+    // round end: the local reduction, the frontiers advanced
+    if (tid == 0) {
+      for (int sd = 0; sd < 2; ++sd) {
+        const bool on = (sides >> sd) & 1;
+        rd.sums[2 * sd] = on ? (unsigned long long)nf[sd] : 0ull;
+        rd.sums[2 * sd + 1] = on ? ne[sd] : 0ull;
+        rd.nfmax[sd] = on ? ~ne[sd] : ~0ull;
+        if (on) {
+          fbg[sd] = fnd[sd];
+          fnd[sd] = qt[sd] + nf[sd];
+          qt[sd] = fnd[sd];
+          cb[sd] ^= 1u;
+        }
+      }
+      rd.meetkey = best;
+      pc = c;
+    }
+    __syncthreads();
+    SOLO_PH(2)
+    // every thread (the scan has a barrier): an idle side's prefix is rebuilt unchanged
+    solo_scan(ND[half], FP[half], min(fnd[half] - fbg[half], kSoloV), tid % (kSoloT / 2), wtot[half]);
+    __syncthreads();
+    SOLO_PH(3)
+  }
+  // ---- exit: the state a stalled speculative round leaves, or the end of the search
+  if (tid >= kWave) return;
+  if (V.P == 1 && c.state == kDone && pol.want_path) terminal_walk(V, c.key, pol);  // wave 0
+  if (tid != 0) return;
+  const int p = it & 1;
+  DState* st = V.st;
+  for (int sd = 0; sd < 2; ++sd) {
+    st->fbeg[sd] = fbg[sd];
+    st->fend[sd] = fnd[sd];
+    st->qtail[sd] = qt[sd];
+    st->send_count[sd] = 0;
+    st->hub_count[sd] = 0;
+    st->new_edges[sd] = 0;
+  }
+  st->done_blocks[0] = st->done_blocks[1] = st->done_blocks[2] = 0;
+  st->meet_found = 0;
+  V.ctl[p ^ 1] = pc;  // round it - 1, executed, and its reduction
+  V.red[p ^ 1] = rd;
+  publish(V, p, pc, rd, c);  // this round's plan (and the trace record of round it - 1)
+  Ctl h = c;
+  if (c.state == kDone || c.state == kDead) {
+    h.ticks = __builtin_amdgcn_s_memrealtime() - st->t0;
+    h.next_it = it + 1;
+  } else {
+    // as k_spec_expand(it) publishing the stall, then k_final(it + 1)
+    h.sides = h.modes = 0;
+    V.ctl[p ^ 1] = h;
+    V.red[p].meetkey = kNoKey;  // the buffer of round it + 2
+    h.next_it = it + 2;
+  }
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(&h);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(V.host_ctl);
+  for (uint32_t k = 0; k < sizeof(Ctl) / 8; ++k)
+    __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  SOLO_PH(7)
+  if (kStamp)
+    for (int k = 0; k < 10; ++k) stamps[k] = ph[k];
+#undef SOLO_PH
+  __threadfence_system();
+  __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Edge-parallel expansion of the deferred hubs.  side >= 0: that side (a
@@ -571,6 +1003,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   uint32_t sides = 1u << s, dnew = dnew_fixed;
   if (side < 0) {
     const Ctl& c = V.ctl[it & 1];
+    if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
     sides = c.sides;
     dnew = c.depth[s] + 1;
   }
@@ -673,6 +1106,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
 // workgroup closes the round)
 __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap) {
   const Ctl& c = V.ctl[it & 1];
+  if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
   const int s = blockIdx.y;
   const uint32_t dnew = c.depth[s] + 1;
   ClaimMeet cm;
@@ -759,6 +1193,7 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags, 
   const int p = it & 1;
   Ctl c;
   plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, flags, c);
+  c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
   publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
   V.red[p ^ 1].meetkey = kNoKey;  // read; it is the buffer of the next round (it + 1)
   *host = c;
@@ -790,8 +1225,9 @@ __global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t
                                                         int single) {
   ClaimMeet cm;  // host rounds: keys from k_meet_end; the flag only stops a single-side level early
   cm.single = single != 0;
+  const uint32_t fb = V.st->fbeg[s];
   td_expand_side(V, s, dnew, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(V.cap)) + 1, V.cap, blockIdx.x,
-                 gridDim.x, hub_deg, single != 0, cm);
+                 gridDim.x, hub_deg, single != 0, cm, fb, V.st->fend[s] - fb);
 }
 
 __global__ void k_send_header(DView V, int s, uint32_t it) {
@@ -923,6 +1359,7 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
       r.sums[2 * s + 1] = V.row_off[li + 1] - V.row_off[li];
     }
   }
+  st->t0 = __builtin_amdgcn_s_memrealtime();
   r.meetkey = kNoKey;
   V.red[0].meetkey = kNoKey;  // round 0 detects its meets into red[0]
   Ctl c = {};
@@ -1038,6 +1475,46 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
   }
 }
 
+// One rank owns every vertex: the two parent chains are walked straight from
+// the local parent arrays (two lanes, one dependent load per hop) and the
+// result goes to pinned host memory, then `tag` -- no pack, gather or copy.
+// out = {status, dS, dT, pad, path[hops + 1]} as k_walk.
+__global__ void k_walk_local(DView V, uint32_t meet, uint32_t hops, uint32_t* out, uint32_t* fin, uint32_t tag) {
+  const uint32_t s = threadIdx.x;
+  if (s < 2) {
+    const uint32_t li = meet - V.lo;
+    const uint32_t d0 = V.depth[0][li], d1 = V.depth[1][li];
+    bool ok = d0 != kEmpty && d1 != kEmpty && d0 + d1 == hops;
+    if (ok) {  // a parent outside the owned range (never, on a consistent state) stops the walk
+      uint32_t v = meet;
+      if (s == 0) {
+        for (int i = (int)d0; i >= 0 && ok; --i) {
+          out[4 + i] = v;
+          if (i) v = V.parent[0][v - V.lo];
+          ok = !i || (v >= V.lo && v < V.hi);
+        }
+      } else {
+        for (uint32_t i = d0; i <= hops && ok; ++i) {
+          out[4 + i] = v;
+          if (i < hops) v = V.parent[1][v - V.lo];
+          ok = i == hops || (v >= V.lo && v < V.hi);
+        }
+      }
+    }
+    const bool okx = __shfl_xor(ok ? 1 : 0, 1) != 0;
+    if (s == 0) {
+      out[0] = ok && okx ? 0u : 1u;
+      out[1] = d0;
+      out[2] = d1;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Fallback for very large visited sets: the owner of the meet vertex
 // contributes its two depths (others ~0, min-reduced) ...
 __global__ void k_meet_depth(DView V, uint32_t meet, uint32_t it) {
@@ -1129,7 +1606,10 @@ struct DistBiBfs::Impl {
   uint64_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
   uint32_t* h_walk = nullptr;  // pinned
   size_t h_walk_cap = 0;
+  uint32_t epoch = 0;          // searches run (Policy::epoch)
   double* d_scalar = nullptr;
+  unsigned long long* d_stamps = nullptr;  // k_spec_solo<true> phase cycles
+  bool solo_stamp = false;
   DistLevelStats stats;
   DistTuning tune;
   int fault_at = 0, fault_mode = 0;
@@ -1158,9 +1638,13 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 8, hipHostMallocDefault));
     std::memset(h_plan, 0, kPlanRing * 8);
     V.plan_ring = h_plan;
+    V.host_ctl = h_ctl;
+    ensure_walk_buf(1u << 14);
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
+    if (const char* t = std::getenv("BIBFS_DIST_STAMP")) solo_stamp = std::atoi(t) != 0;
+    HIP_CHECK(hipMalloc(&d_stamps, 16 * sizeof(unsigned long long)));
   }
 
   void set_partition(uint32_t nn) {
@@ -1259,6 +1743,21 @@ struct DistBiBfs::Impl {
 
   // bytes of the owned CSR shard (row offsets + columns) and the generator's
   // peak allocation while building it (streamed generation: shard + cursor)
+  // Largest degree of the whole graph (max over the shards).  No vertex above
+  // kHubDeg: no hub is ever deferred, so no speculative round launches the hub pass.
+  uint64_t max_deg = 0;
+  void finish_build() {
+    alloc_state();
+    double y = (double)launch::max_degree(d_row_off, hi - lo, stream);
+    if (size > 1) {
+      HIP_CHECK(hipMemcpyAsync(d_scalar, &y, 8, hipMemcpyHostToDevice, cstream));
+      comm->allreduce(d_scalar, 1, DType::kF64, ROp::kMax, cstream);
+      HIP_CHECK(hipMemcpyAsync(&y, d_scalar, 8, hipMemcpyDeviceToHost, cstream));
+      wait(cstream);
+    }
+    max_deg = (uint64_t)y;
+  }
+
   size_t gen_peak_bytes = 0;
   size_t shard_bytes() const { return ((size_t)(hi - lo) + 1) * 8 + (size_t)nnz * 4; }
 
@@ -1291,9 +1790,24 @@ struct DistBiBfs::Impl {
   // profiles/r2_dist_fintag_ab.txt).  An RCCL error reported by the
   // communicator, or no progress within timeout_s (a dead or hung peer leaves
   // our collective waiting forever), aborts the communicator and throws.
-  void wait(hipStream_t s) {
+  uint32_t next_tag() {
     fin_seq = fin_seq + 1 == 0 ? 1 : fin_seq + 1;
-    const uint32_t tag = fin_seq;
+    return fin_seq;
+  }
+
+  void ensure_walk_buf(size_t words) {
+    if (h_walk_cap >= words) return;
+    if (h_walk) {  // a round still in flight may write the old buffer
+      HIP_CHECK(hipStreamSynchronize(cstream));
+      HIP_CHECK(hipHostFree(h_walk));
+    }
+    h_walk_cap = std::max<size_t>(words, 1u << 14);
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_walk), h_walk_cap * 4, hipHostMallocDefault));
+    V.host_walk = h_walk;
+  }
+
+  void wait(hipStream_t s) {
+    const uint32_t tag = next_tag();
     k_host_tag<<<1, 64, 0, s>>>(h_fin, tag);
     HIP_CHECK(hipGetLastError());
     stats.host_syncs++;
@@ -1327,8 +1841,7 @@ struct DistBiBfs::Impl {
   // hipStreamQuery poll.  k_final is the last work in the stream here, so
   // this is a full host sync.  Same watchdog as wait().
   void final_and_wait(uint32_t it, const Policy& pol, int flags, hipStream_t s) {
-    fin_seq = fin_seq + 1 == 0 ? 1 : fin_seq + 1;
-    const uint32_t tag = fin_seq;
+    const uint32_t tag = next_tag();
     k_final<<<1, 64, 0, s>>>(V, it, pol, h_ctl, flags, h_fin, tag);
     HIP_CHECK(hipGetLastError());
     stats.host_syncs++;
@@ -1342,7 +1855,7 @@ struct DistBiBfs::Impl {
     const auto t0 = std::chrono::steady_clock::now();
     const auto deadline = t0 + std::chrono::duration<double>(tune.timeout_s);
     const uint64_t* slot = &h_plan[need % kPlanRing];
-    const uint64_t tag = (need + 1u) & 0xffffffu;
+    const uint64_t tag = plan_tag(epoch, need);
     for (uint64_t spin = 0;; ++spin) {
       const uint64_t w = __atomic_load_n(slot, __ATOMIC_ACQUIRE);
       if (((w >> 8) & 0xffffffu) == tag) return w;
@@ -1374,6 +1887,9 @@ struct DistBiBfs::Impl {
     p.lockstep = opt.lockstep ? 1 : 0;
     p.side = (int)opt.side;
     p.direction = (int)opt.direction;
+    p.epoch = epoch;
+    p.walk_cap = (uint32_t)std::min<size_t>(h_walk_cap, 0xffffffffu);
+    p.want_path = opt.want_path ? 1 : 0;
     return p;
   }
 
@@ -1510,16 +2026,22 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   }
   const int P = size;
   hipStream_t cs = cstream;
+  ++epoch;
   const Policy pol = policy(opt);
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
 
-  std::memset(h_plan, 0, kPlanRing * 8);  // round numbers restart per search
+  // Plan words of older searches must not match this one's tags.  Only the
+  // previous search's trailing no-op rounds can still be running (its
+  // terminal round ran after its own seed, behind everything before it);
+  // they carry the previous epoch.
+  std::memset(h_plan, 0, kPlanRing * 8);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  HIP_CHECK(hipEventRecord(ev_t0, cs));
   k_seed<<<1, 64, 0, cs>>>(V, src, dst);
-  comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
-  stats.collectives++;
+  if (P > 1) {
+    comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
+    stats.collectives++;
+  }
   uint32_t it = 0;
   uint32_t spec_cap = kSpecCapMin;
   int flags = 0;
@@ -1530,6 +2052,29 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   if (host_only) {
     final_and_wait(it++, pol, kPlanStall, cs);
     have_ctl = true;
+  } else if (P == 1 && tune.solo) {
+    // one launch for every round the solo workgroup can hold; it leaves the
+    // state of a stalled round (or the finished search) and its Ctl in h_ctl
+    const uint32_t tag = next_tag();
+    const uint32_t emax = std::min<uint32_t>(std::max<uint32_t>(tune.solo_edges, 1), kSoloE);
+    if (solo_stamp) k_spec_solo<true><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, h_fin, tag, d_stamps);
+    else k_spec_solo<false><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, h_fin, tag, nullptr);
+    HIP_CHECK(hipGetLastError());
+    stats.host_syncs++;
+    spin_tag(tag, cs);
+    if (solo_stamp) {
+      unsigned long long st8[10];
+      HIP_CHECK(hipMemcpy(st8, d_stamps, sizeof st8, hipMemcpyDeviceToHost));
+      std::fprintf(stderr,
+                   "[solo] rounds %llu edges %llu | cycles: setup %llu plan %llu (planner %llu publish %llu) edges %llu "
+                   "end %llu scan %llu exit %llu\n",
+                   st8[4], st8[5], st8[6], st8[0], st8[8], st8[9], st8[1], st8[2], st8[3], st8[7]);
+    }
+    have_ctl = true;
+    stats.solo_rounds = (int)(h_ctl->rounds);
+    it = h_ctl->next_it;
+    const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
+    spec_cap = std::min(spec_max, std::max<uint32_t>(kSpecCapMin, next_pow2(4 * fm)));
   }
   for (uint64_t guard = 0;; ++guard) {
     BIBFS_REQUIRE(guard <= 4ull * n + 16, "dist: search did not terminate");
@@ -1565,12 +2110,14 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     const uint32_t first = it;
     uint32_t cap_it = spec_cap;
     uint64_t f_prev = 0;
+    uint32_t seen_state = kRun;  // state of the last plan word read
     for (int k = 0;; ++k) {
       if (k >= K) {
         const uint32_t need = it - (uint32_t)K;
         const uint64_t w = wait_plan(need, cs);
         stats.plan_polls++;
-        if (((w >> 2) & 3u) != kRun) break;
+        seen_state = (uint32_t)(w >> 2) & 3u;
+        if (seen_state != kRun) break;
         const uint64_t f = w >> 32;
         uint64_t g = 2;  // growth per round; x2 until two plans are seen
         if (f_prev) g = std::min<uint64_t>(8, std::max<uint64_t>(1, (f + f_prev - 1) / f_prev));
@@ -1585,7 +2132,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       const uint64_t gather_bytes = 2 * block_words(cap_it) * 4;
       // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
       // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
-      const bool hubs = cap_it > kSpecHubCap;
+      const bool hubs = cap_it > kSpecHubCap && max_deg > kHubDeg;
       const unsigned hx = std::min<unsigned>((unsigned)cus, cap_it / kThreads + 1);
       maybe_fault((int)it);
       // The round's last claiming kernel closes it (meets were detected at
@@ -1614,8 +2161,15 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     }
     spec_cap = cap_it;
     flags = 0;
-    final_and_wait(it++, pol, kPlanAccountOnly, cs);
     have_ctl = true;
+    if (seen_state == kDone || seen_state == kDead) {
+      // the round that ended the search wrote its accounted Ctl to h_ctl
+      // before its plan word: no k_final + wait (the no-op rounds behind it
+      // drain before the search's last tag)
+      ++it;
+      break;
+    }
+    final_and_wait(it++, pol, kPlanAccountOnly, cs);
     if (h_ctl->state == kRun) {  // size the next batch for the frontier we have now
       const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
       spec_cap = std::min(spec_max, std::max<uint32_t>(spec_cap, next_pow2(4 * fm)));
@@ -1630,18 +2184,49 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   r.stats.edges_inspected = h.einsp;
   r.stats.visited = h.vis[0] + h.vis[1];
   stats.comm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  bool path_pending = false;  // the gathered-table walk is enqueued, not yet read
+  // The search's result is complete on the host when the walk (if any) is:
+  // with one rank the round that ended the search walked the path into
+  // pinned memory before its plan word (terminal_walk); otherwise a gathered
+  // walk, or k_walk_local when the path outgrew the pinned buffer.  The host
+  // waits on a tag only for those, and never for the reset of the search
+  // state: k_cleanup trails in cstream, where everything the next search
+  // enqueues is ordered behind it (the compute stream waits on an event of
+  // cstream before it is used).
+  bool path_pending = false;  // a walk result lands in h_walk behind `tag`
+  uint32_t tag = 0;
   if (h.state == kDone) {
     const uint64_t key = h.key;
     r.found = true;
     r.meet = (uint32_t)(key & 0xffffffffull);
     r.hops = (int64_t)(key >> 32);
-    if (opt.want_path && !(path_pending = walk_path(key, r))) walk_path_per_hop(key, it, r);
+    if (opt.want_path && P == 1) {
+      const bool walked = h_walk[3] == pol.epoch && h_walk[0] != 2u;
+      if (!walked) {
+        ensure_walk_buf(4 + (size_t)r.hops + 1);
+        tag = next_tag();
+        k_walk_local<<<1, 64, 0, cs>>>(V, r.meet, (uint32_t)r.hops, h_walk, h_fin, tag);
+        HIP_CHECK(hipGetLastError());
+      }
+      path_pending = true;
+    } else if (opt.want_path) {
+      if (!(path_pending = walk_path(key, r))) walk_path_per_hop(key, it, r);
+      if (path_pending) {
+        tag = next_tag();
+        k_host_tag<<<1, 64, 0, cs>>>(h_fin, tag);
+        HIP_CHECK(hipGetLastError());
+      }
+    }
   }
-  if (path_pending) cleanup_enqueue(h);  // behind the walk: one host wait for both
-  if (!path_pending) cleanup_enqueue(h);
-  HIP_CHECK(hipEventRecord(ev_t1, cs));
-  wait(cs);
+  if (opt.trace && !tag) {  // the trace records are plain device stores: drain the rounds first
+    tag = next_tag();
+    k_host_tag<<<1, 64, 0, cs>>>(h_fin, tag);
+    HIP_CHECK(hipGetLastError());
+  }
+  cleanup_enqueue(h);
+  if (tag) {
+    stats.host_syncs++;
+    spin_tag(tag, cs);
+  }
   if (path_pending) finish_walk(r);
   if (opt.trace && h.rounds) {
     std::vector<RoundRec> tr(std::min<uint32_t>(h.rounds, kTraceCap));
@@ -1659,10 +2244,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         r.stats.trace.push_back(lt);
       }
   }
-  float dms = 0.f;
-  // the host saw the stream's tag; the runtime may mark the event complete a moment later
-  HIP_CHECK(hipEventSynchronize(ev_t1));
-  HIP_CHECK(hipEventElapsedTime(&dms, ev_t0, ev_t1));
+  const double dms = (double)h.ticks / 1e5;  // s_memrealtime: 100 MHz
   stats.device_ms = dms;
   r.stats.grid_levels = r.stats.levels;
   r.search_ms = dms;
@@ -1693,11 +2275,7 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, d_walk);
   HIP_CHECK(hipGetLastError());
   const size_t words = 4 + (size_t)hops + 1;
-  if (h_walk_cap < words) {
-    if (h_walk) HIP_CHECK(hipHostFree(h_walk));
-    h_walk_cap = std::max<size_t>(words, 1024);
-    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_walk), h_walk_cap * 4, hipHostMallocDefault));
-  }
+  ensure_walk_buf(words);
   HIP_CHECK(hipMemcpyAsync(h_walk, d_walk, words * 4, hipMemcpyDeviceToHost, cs));
   return true;  // read by finish_walk after the search's last wait
 }
@@ -1773,6 +2351,7 @@ DistBiBfs::~DistBiBfs() {
   } catch (...) {
   }
   p_->comm.reset();
+  (void)hipFree(p_->d_stamps);
   (void)hipHostFree(p_->h_red);
   (void)hipHostFree(p_->h_ctl);
   (void)hipHostFree(p_->h_fin);
@@ -1800,7 +2379,7 @@ void DistBiBfs::load_edges(const EdgeList& el) {
   part.lo = I.lo;
   part.hi = I.hi;
   I.upload_rows(build_csr_rows(el, part));
-  I.alloc_state();
+  I.finish_build();
 }
 
 void DistBiBfs::load_bin(const std::string& path) {
@@ -1819,7 +2398,7 @@ void DistBiBfs::load_bin(const std::string& path) {
   part.lo = I.lo;
   part.hi = I.hi;
   I.upload_rows(build_csr_rows(shard, part));
-  I.alloc_state();
+  I.finish_build();
 }
 
 void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
@@ -1834,7 +2413,7 @@ void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
   I.nnz = launch::gen_rows_gnp(n, p, seed, I.lo, I.hi, I.d_row_off, &I.d_col, &m, I.stream);
   I.m_input = m;
   I.gen_peak_bytes = I.shard_bytes() + ((size_t)(I.hi - I.lo) + 1) * 8;  // + the scatter cursor
-  I.alloc_state();
+  I.finish_build();
 }
 
 void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, double b, double c) {
@@ -1848,7 +2427,7 @@ void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, d
   I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, I.lo, I.hi, I.d_row_off, &I.d_col, I.stream);
   I.m_input = m;
   I.gen_peak_bytes = I.shard_bytes() + ((size_t)(I.hi - I.lo) + 1) * 8;  // + the scatter cursor
-  I.alloc_state();
+  I.finish_build();
 }
 
 SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {

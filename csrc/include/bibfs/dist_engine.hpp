@@ -65,6 +65,7 @@ struct DistLevelStats {
   double comm_ms = 0.0;            // host wall time of the round loop (this rank)
   double device_ms = 0.0;          // device time from the first to the last op of the search (events)
   int path_collectives = 0;        // collectives spent reconstructing the path
+  int solo_rounds = 0;             // rounds run by the one-workgroup solo kernel (one rank)
 };
 
 // Knobs of the partitioned engine (defaults are the production settings; the
@@ -76,6 +77,8 @@ struct DistTuning {
   uint64_t nosync_bytes = 1u << 20;  // host-planned round: size the exchange from host bounds up to this
   double timeout_s = 120.0;        // a host wait longer than this aborts the communicator and throws
   uint32_t walk_max = 15000;       // path from one gathered parent table when both sides claimed <= this
+  bool solo = true;                // one rank: small rounds in one persistent workgroup (k_spec_solo)
+  uint32_t solo_edges = 2048;      // ... while every expanding side has at most this many frontier edges (<= 8192)
 };
 
 class DistBiBfs {

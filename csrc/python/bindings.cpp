@@ -82,6 +82,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["host_rounds"] = s.host_rounds;
   d["collectives"] = s.collectives;
   d["path_collectives"] = s.path_collectives;
+  d["solo_rounds"] = s.solo_rounds;
   d["exchanged_bytes"] = s.exchanged_bytes;
   d["comm_ms"] = s.comm_ms;
   d["device_ms"] = s.device_ms;
@@ -338,7 +339,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("cap", &DistTuning::cap)
       .def_readwrite("nosync_bytes", &DistTuning::nosync_bytes)
       .def_readwrite("timeout_s", &DistTuning::timeout_s)
-      .def_readwrite("walk_max", &DistTuning::walk_max);
+      .def_readwrite("walk_max", &DistTuning::walk_max)
+      .def_readwrite("solo", &DistTuning::solo)
+      .def_readwrite("solo_edges", &DistTuning::solo_edges);
   py::class_<DistLocalFault>(m, "DistLocalFault")
       .def(py::init<>())
       .def_readwrite("rank", &DistLocalFault::rank)

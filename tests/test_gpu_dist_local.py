@@ -226,3 +226,60 @@ def test_generated_shards_hold_only_their_rows(spec):
         assert peak <= shard + (rows + 1) * 8
         assert peak < edge_list_bytes  # the old path held the whole edge list on every rank
     assert sum(t["local_nnz"]) == g.csr.nnz
+
+
+# ---- one rank: the solo workgroup (k_spec_solo), its hand-off and the terminal walk ----
+
+@pytest.mark.parametrize("spec", ["gnp:20000::6", "kron:14:16:3", "rmat:16384:262144:3"])
+def test_world1_solo_matches_oracle_and_hands_off(spec):
+    """One rank: the solo workgroup runs the small rounds, hands big frontiers
+    (Kronecker hubs) and bottom-up plans to the multi-workgroup / host rounds,
+    and the round that ends the search walks the path into pinned memory.
+    Every option combination against the oracle, solo on and off."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    g = bb.from_spec(spec)
+    qs = _pairs(g.n, 12, 21)
+    expect = [native.bfs_oracle(g.csr, s, d).hops for s, d in qs]
+    for solo in (True, False):
+        for kw in ({}, {"lockstep": False}, {"direction": "bottomup"}, {"side": "alternate"},
+                   {"want_path": False}):
+            rs, st = dist_local_run(1, g, qs, tuning=make_tuning(solo=solo), return_stats=True, **kw)
+            for (s, d), r, e in zip(qs, rs, expect):
+                if kw.get("want_path") is False:
+                    assert r.hops == e, (s, d, r.hops, e)
+                else:
+                    check_result(g.csr, s, d, r.hops, r.path, e)
+            if solo and not kw:
+                assert any(x["solo_rounds"] > 0 for x in st), st[:3]
+            if not solo:
+                assert all(x["solo_rounds"] == 0 for x in st)
+
+
+def test_world1_solo_long_path_and_disconnected():
+    """A 5000-hop path (one vertex per frontier: every round in the one
+    launch) and unreachable pairs (a side exhausted inside the solo loop)."""
+    import torch  # noqa: F401
+
+    n = 5000
+    line = np.stack([np.arange(n - 1), np.arange(1, n)], 1).astype(np.uint32)
+    g = Graph.from_edges(n + 3, np.concatenate([line, np.array([[n, n + 1]], np.uint32)]))
+    rs, st = dist_local_run(1, g, [(0, n - 1), (17, 2900), (0, n + 1), (n + 2, 3)], return_stats=True)
+    assert rs[0].hops == n - 1 and list(rs[0].path) == list(range(n))
+    assert rs[1].hops == 2900 - 17 and list(rs[1].path) == list(range(17, 2901))
+    assert not rs[2].found and not rs[3].found
+    assert st[0]["solo_rounds"] >= (n - 1) // 2 and st[0]["host_rounds"] == 0
+
+
+def test_world1_back_to_back_queries_keep_state_clean():
+    """No host wait for the state reset between searches (k_cleanup trails in
+    the stream): many back-to-back queries, alternating roots, stay exact."""
+    import torch  # noqa: F401
+
+    g = bb.from_spec("gnp:30000::4")
+    rnd = random.Random(5)
+    qs = [(rnd.randrange(g.n), rnd.randrange(g.n)) for _ in range(60)]
+    rs = dist_local_run(1, g, qs)
+    for (s, d), r in zip(qs, rs):
+        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
