@@ -203,6 +203,18 @@ class HipEngine:
     def download_edges(self):
         return self._e.download_edges()
 
+    def neighbors(self, u: int):
+        """Row ``u`` of the device CSR (one row copied to the host)."""
+        return self._e.neighbors(int(u))
+
+    def check_path(self, src: int, dst: int, hops: int, path) -> bool:
+        """``path`` is a src -> dst walk of ``hops`` edges of the loaded graph
+        (each edge checked against its row on the device)."""
+        p = [int(x) for x in path]
+        if len(p) != hops + 1 or p[0] != src or p[-1] != dst:
+            return False
+        return all(b in set(self._e.neighbors(a)) for a, b in zip(p, p[1:]))
+
     def synchronize(self) -> None:
         self._e.synchronize()
 

@@ -156,7 +156,11 @@ struct DView {
   uint32_t n, lo, hi, chunk;  // owned = [lo, hi); owner(v) = v / chunk
   const uint64_t* row_off;    // owned rows
   const uint32_t* col;        // global column ids
-  uint32_t* vis[2];           // owned slices, chunk/32 words
+  // Visited bits of both sides interleaved: owned word w of side s is
+  // vis[s][2 * w] (vis[1] = vis[0] + 1), so the 64-bit word w of vis[0]
+  // holds side 0 in its low and side 1 in its high half -- a claim's one
+  // 64-bit atomicOr returns the other side's bit with its own.
+  uint32_t* vis[2];
   uint32_t* parent[2];        // chunk entries, valid where visited
   uint32_t* depth[2];         // chunk entries, valid where visited
   uint32_t* queue[2];         // owned vertices (global ids) in claim order
@@ -279,9 +283,10 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
       } else if (pol.direction == (int)Direction::kBottomUp) {
         mode = 2;
       } else {
+        // Beamer: m_f > m_u / alpha and n_f < n / beta, multiplied out (no f64 division)
         const double m_u = (double)pol.nnz_total - (double)c.ved[s];
-        if (c.dir[s] == 1 && (double)c.fed[s] > m_u / pol.alpha) c.dir[s] = 2;
-        else if (c.dir[s] == 2 && (double)c.cnt[s] < (double)pol.n / pol.beta) c.dir[s] = 1;
+        if (c.dir[s] == 1 && (double)c.fed[s] * pol.alpha > m_u) c.dir[s] = 2;
+        else if (c.dir[s] == 2 && (double)c.cnt[s] * pol.beta < (double)pol.n) c.dir[s] = 1;
         mode = c.dir[s];
       }
       if (mode == 2) wm |= 1u << s;
@@ -355,20 +360,22 @@ struct ClaimMeet {
 __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uint32_t v, uint32_t u,
                                            uint32_t dnew, const ClaimMeet& cm = ClaimMeet{}) {
   const uint32_t li = v - V.lo;
-  uint32_t* vis = pick(V.vis, s);
-  bool mine = false;
+  bool mine = false, other = false;
   unsigned long long best = kNoKey;
   unsigned long long rb = 0, re = 0;
   if (want) {
-    const uint32_t bit = 1u << (li & 31);
-    if (!cm.precheck || !(vis[li >> 5] & bit)) {
-      const uint32_t old = atomicOr(&vis[li >> 5], bit);
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(V.vis[0]) + (li >> 5);
+    const unsigned long long m = 1ull << ((li & 31) + 32 * s);
+    if (!cm.precheck || !(*w & m)) {
+      // both sides' bits in one word: the claim returns the other side's too;
+      // of two same-round claims of v the later atomic sees the earlier
+      const unsigned long long old = atomicOr(w, m);
       rb = V.row_off[li];  // the degree, fetched beside the claim (independent of its result)
       re = V.row_off[li + 1];
-      mine = !(old & bit);
+      mine = !(old & m);
+      other = (old >> ((li & 31) + 32 * (s ^ 1))) & 1ull;
     }
-    if ((cm.meetkey || cm.single) && mine &&
-        (__hip_atomic_load(&pick(V.vis, s ^ 1)[li >> 5], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit)) {
+    if ((cm.meetkey || cm.single) && mine && other) {
       if (cm.meetkey) {
         uint32_t dd = __hip_atomic_load(&pick(V.depth, s ^ 1)[li], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (dd == kEmpty) dd = cm.dother + 1;
@@ -693,6 +700,9 @@ constexpr uint32_t kSoloE = 8192;  // frontier edges per side one solo round exp
 constexpr uint32_t kSoloRounds = 1u << 16;
 constexpr int kSoloU = 4;          // edges per thread in flight per pass
 
+// Workgroup barrier that waits for LDS traffic only (no vmcnt drain).
+__device__ __forceinline__ void solo_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Exclusive prefix of ND[0, cnt) into FP[0, cnt], FP[cnt] = total; half the
 // workgroup per side (t = thread index within the half).
 __device__ void solo_scan(const uint32_t* ND, uint32_t* FP, uint32_t cnt, uint32_t t, uint32_t* wtot) {
@@ -711,7 +721,7 @@ __device__ void solo_scan(const uint32_t* ND, uint32_t* FP, uint32_t cnt, uint32
     if ((t & 63) >= (uint32_t)o) x += y;
   }
   if ((t & 63) == 63) wtot[t >> 6] = x;
-  __syncthreads();
+  solo_lds_barrier();
   uint32_t base = 0, tot = 0;
 #pragma unroll
   for (uint32_t w = 0; w < kWaves; ++w) {
@@ -738,6 +748,7 @@ __device__ __forceinline__ unsigned long long solo_clock() {
 
 template <bool kStamp>
 __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, Policy pol, uint32_t emax,
+                                                         int seed, uint32_t seed_src, uint32_t seed_dst,
                                                          uint32_t* fin, uint32_t tag, unsigned long long* stamps) {
   unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, tp = kStamp ? solo_clock() : 0;
 #define SOLO_PH(k)                                \
@@ -760,8 +771,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
   // member would be a vector load from the kernel arguments per use)
   const uint32_t* const col = V.col;
   const uint64_t* const row_off = V.row_off;
-  uint32_t* const vis0 = V.vis[0];
-  uint32_t* const vis1 = V.vis[1];
+  unsigned long long* const visw = reinterpret_cast<unsigned long long*>(V.vis[0]);  // both sides per word
   uint32_t* const par0 = V.parent[0];
   uint32_t* const par1 = V.parent[1];
   uint32_t* const dep0 = V.depth[0];
@@ -770,28 +780,61 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
   uint32_t* const que1 = V.queue[1];
   const uint32_t lo = V.lo;
   const uint32_t half = tid / (kSoloT / 2);  // the side a thread scans for
-  const int pp = (it0 + 1) & 1;  // buffers of round it0 - 1
-  stage_words(&pc, &V.ctl[pp], sizeof(Ctl));
-  stage_words(&rd, &V.red[pp], sizeof(Reduced));
-  if (tid < 2) {
-    fbg[tid] = V.st->fbeg[tid];
-    fnd[tid] = V.st->fend[tid];
-    qt[tid] = V.st->qtail[tid];
-    cb[tid] = 0;
-  }
-  __syncthreads();
-  // the current frontiers (at most kSoloV each, or the first plan stops)
-  for (uint32_t i = tid; i < 2 * kSoloV; i += kSoloT) {
-    const uint32_t sd = i / kSoloV, k = i % kSoloV;
-    if (fbg[sd] + k < fnd[sd]) {
-      const uint32_t v = V.queue[sd][fbg[sd] + k];
-      const unsigned long long b = V.row_off[v - V.lo];
-      FV[0][sd][k] = v;
-      FB[0][sd][k] = b;
-      ND[sd][k] = (uint32_t)min(V.row_off[v - V.lo + 1] - b, (unsigned long long)kSoloE + 1);
+  if (seed) {
+    // the seeding pseudo-round (k_seed) done here: one launch fewer, and the
+    // state goes straight into LDS (round it0 = 0 accounts it)
+    if (tid < 2) {
+      const uint32_t v = tid ? seed_dst : seed_src, li = v - lo;
+      const unsigned long long b = row_off[li], d = row_off[li + 1] - b;
+      __hip_atomic_fetch_or(visw + (li >> 5), 1ull << ((li & 31) + 32 * tid), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP);
+      (tid ? par1 : par0)[li] = kEmpty;
+      __hip_atomic_store((tid ? dep1 : dep0) + li, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      (tid ? que1 : que0)[0] = v;
+      fbg[tid] = 0;
+      fnd[tid] = qt[tid] = 1;
+      cb[tid] = 0;
+      FV[0][tid][0] = v;
+      FB[0][tid][0] = b;
+      ND[tid][0] = (uint32_t)min(d, (unsigned long long)kSoloE + 1);
+      rd.sums[2 * tid] = 1;
+      rd.sums[2 * tid + 1] = d;
     }
+    if (tid == 0) {
+      V.st->t0 = __builtin_amdgcn_s_memrealtime();
+      rd.meetkey = kNoKey;
+      Ctl z = {};
+      z.dir[0] = z.dir[1] = 1;
+      z.state = kRun;
+      z.sides = kSeedBit;
+      z.key = kNoKey;
+      pc = z;
+    }
+    __syncthreads();
+  } else {
+    const int pp = (it0 + 1) & 1;  // buffers of round it0 - 1
+    stage_words(&pc, &V.ctl[pp], sizeof(Ctl));
+    stage_words(&rd, &V.red[pp], sizeof(Reduced));
+    if (tid < 2) {
+      fbg[tid] = V.st->fbeg[tid];
+      fnd[tid] = V.st->fend[tid];
+      qt[tid] = V.st->qtail[tid];
+      cb[tid] = 0;
+    }
+    __syncthreads();
+    // the current frontiers (at most kSoloV each, or the first plan stops)
+    for (uint32_t i = tid; i < 2 * kSoloV; i += kSoloT) {
+      const uint32_t sd = i / kSoloV, k = i % kSoloV;
+      if (fbg[sd] + k < fnd[sd]) {
+        const uint32_t v = V.queue[sd][fbg[sd] + k];
+        const unsigned long long b = V.row_off[v - V.lo];
+        FV[0][sd][k] = v;
+        FB[0][sd][k] = b;
+        ND[sd][k] = (uint32_t)min(V.row_off[v - V.lo + 1] - b, (unsigned long long)kSoloE + 1);
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   solo_scan(ND[half], FP[half], min(fnd[half] - fbg[half], kSoloV), tid % (kSoloT / 2), wtot[half]);
   __syncthreads();
 
@@ -822,7 +865,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
         best = kNoKey;
       }
     }
-    __syncthreads();
+    solo_lds_barrier();  // LDS only: the plan's global stores (publish) need no wait
     SOLO_PH(0)
     if (!go) break;
     const uint32_t sides = c.sides;
@@ -834,7 +877,8 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
     // the pass loop is wave-uniform (appends are aggregated per wave)
     const uint32_t E = E0 + E1, lane = tid & 63;
     for (uint32_t base = 0; base + (tid & ~63u) < E; base += kSoloT * kSoloU) {
-      uint32_t uu[kSoloU], vv[kSoloU], old[kSoloU], oth[kSoloU];
+      uint32_t uu[kSoloU], vv[kSoloU], oth[kSoloU];
+      unsigned long long old[kSoloU];
       unsigned long long ad[kSoloU], rb[kSoloU], re[kSoloU];
       int ss[kSoloU];
       bool ok[kSoloU], mine[kSoloU];
@@ -859,25 +903,24 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
 #pragma unroll
       for (int j = 0; j < kSoloU; ++j) vv[j] = ok[j] ? vv[j] : lo;
       // claims: one CU, so the atomics are performed in its L2 (workgroup
-      // scope); the degree is fetched beside the claim
+      // scope); one 64-bit atomicOr returns both sides' bits (of two
+      // same-round claims of a vertex the later sees the earlier); the
+      // degree is fetched beside the claim
 #pragma unroll
       for (int j = 0; j < kSoloU; ++j) {
-        const uint32_t li = vv[j] - lo, bit = 1u << (li & 31);
-        uint32_t* w = (ss[j] ? vis1 : vis0) + (li >> 5);
-        const bool claim = ok[j] && (!pre || !(*w & bit));  // a stale L1 word only misses bits: safe
-        old[j] = claim ? __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : bit;
+        const uint32_t li = vv[j] - lo;
+        const unsigned long long m = 1ull << ((li & 31) + 32 * ss[j]);
+        unsigned long long* w = visw + (li >> 5);
+        const bool claim = ok[j] && (!pre || !(*w & m));  // a stale L1 word only misses bits: safe
+        old[j] = claim ? __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : m;
         rb[j] = claim ? row_off[li] : 0ull;
         re[j] = claim ? row_off[li + 1] : 0ull;
       }
-      // the other side's word, read in L2 after this claim completed: of two
-      // same-round claims of a vertex the later one sees the earlier
 #pragma unroll
       for (int j = 0; j < kSoloU; ++j) {
-        const uint32_t li = vv[j] - lo, bit = 1u << (li & 31);
-        mine[j] = !(old[j] & bit);
-        oth[j] = mine[j] ? __hip_atomic_fetch_or((ss[j] ? vis0 : vis1) + (li >> 5), 0u, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_WORKGROUP)
-                         : 0u;
+        const uint32_t li = vv[j] - lo;
+        mine[j] = !((old[j] >> ((li & 31) + 32 * ss[j])) & 1ull);
+        oth[j] = (uint32_t)(old[j] >> (32 * (ss[j] ^ 1)));  // the other side's half
       }
 #pragma unroll
       for (int j = 0; j < kSoloU; ++j) {
@@ -916,13 +959,18 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
         }
       }
     }
-    __syncthreads();
+    __syncthreads();  // (with vmcnt(0)): this round's depth stores are in L2 before a later round reads them
     SOLO_PH(1)
     if (kStamp && tid == 0) {
       ph[4] += 1;
       ph[5] += E;
     }
-    // round end: the local reduction, the frontiers advanced
+    // the next frontiers' degree prefix (an idle side's is rebuilt unchanged),
+    // then -- thread 0, behind the scan's barrier -- the round's bookkeeping;
+    // thread 0 plans the next round right after it (the post-plan barrier
+    // orders all of it for everyone)
+    const uint32_t cnt_next = ((sides >> half) & 1) ? nf[half] : fnd[half] - fbg[half];
+    solo_scan(ND[half], FP[half], min(cnt_next, kSoloV), tid % (kSoloT / 2), wtot[half]);
     if (tid == 0) {
       for (int sd = 0; sd < 2; ++sd) {
         const bool on = (sides >> sd) & 1;
@@ -939,11 +987,6 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       rd.meetkey = best;
       pc = c;
     }
-    __syncthreads();
-    SOLO_PH(2)
-    // every thread (the scan has a barrier): an idle side's prefix is rebuilt unchanged
-    solo_scan(ND[half], FP[half], min(fnd[half] - fbg[half], kSoloV), tid % (kSoloT / 2), wtot[half]);
-    __syncthreads();
     SOLO_PH(3)
   }
   // ---- exit: the state a stalled speculative round leaves, or the end of the search
@@ -1154,7 +1197,7 @@ __global__ __launch_bounds__(kThreads) void k_meet_end(DView V, uint32_t it) {
     const int s = i < n0 ? 0 : 1;
     const uint32_t v = pick(V.queue, s)[s ? f1 + (uint32_t)(i - n0) : f0 + (uint32_t)i];
     const uint32_t li = v - V.lo;
-    if ((pick(V.vis, s ^ 1)[li >> 5] >> (li & 31)) & 1u) {
+    if ((pick(V.vis, s ^ 1)[2 * (li >> 5)] >> (li & 31)) & 1u) {
       const unsigned long long key =
           ((unsigned long long)(V.ctl[p].depth[s] + 1 + pick(V.depth, s ^ 1)[li]) << 32) | v;
       best = key < best ? key : best;
@@ -1288,7 +1331,7 @@ __global__ __launch_bounds__(kThreads) void k_bu(DView V, int s, uint32_t dnew) 
   const uint64_t ws = (uint64_t)gridDim.x * blockDim.x / kWave;
   for (uint64_t gw = w0; gw < nw; gw += ws) {
     const uint32_t li = (uint32_t)(gw * 64 + lane);
-    const uint32_t word = vis[gw * 2 + (lane >> 5)];
+    const uint32_t word = vis[2 * (gw * 2 + (lane >> 5))];
     const uint32_t bit = 1u << (lane & 31);
     bool found = false;
     uint32_t pu = 0;
@@ -1316,8 +1359,8 @@ __global__ __launch_bounds__(kThreads) void k_bu(DView V, int s, uint32_t dnew) 
     }
     const unsigned long long mask = __ballot(found);
     if (!mask) continue;  // wave-uniform
-    if (lane == 0) vis[gw * 2] = word | (uint32_t)mask;
-    if (lane == 32) vis[gw * 2 + 1] = word | (uint32_t)(mask >> 32);
+    if (lane == 0) vis[2 * (gw * 2)] = word | (uint32_t)mask;  // this side's half only
+    if (lane == 32) vis[2 * (gw * 2 + 1)] = word | (uint32_t)(mask >> 32);
     const int leader = __ffsll((long long)mask) - 1;
     if (found) {
       pick(V.parent, s)[li] = pu;
@@ -1350,7 +1393,7 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
       const uint32_t li = v - V.lo;
-      pick(V.vis, s)[li >> 5] |= 1u << (li & 31);
+      pick(V.vis, s)[2 * (li >> 5)] |= 1u << (li & 31);
       pick(V.parent, s)[li] = kEmpty;
       pick(V.depth, s)[li] = 0;
       pick(V.queue, s)[0] = v;
@@ -1553,7 +1596,7 @@ __global__ void k_cleanup(DView V, uint64_t sent_words) {
     uint32_t* dep = pick(V.depth, s);
     for (uint64_t i = tid; i < qn; i += nth) {
       const uint32_t li = q[i] - V.lo;
-      vis[li >> 5] = 0u;
+      vis[2 * (li >> 5)] = 0u;
       dep[li] = kEmpty;  // claim-time meet detection reads kEmpty as "not visible yet"
     }
   }
@@ -1686,7 +1729,7 @@ struct DistBiBfs::Impl {
     size_t o_vis[2], o_par[2], o_dep[2], o_q[2], o_ob[2], o_gb[2], o_hub[2];
     for (int s = 0; s < 2; ++s) {
       o_hub[s] = take((size_t)chunk * 4);
-      o_vis[s] = take(words * 4);
+      o_vis[s] = s ? o_vis[0] : take(words * 8);  // interleaved: one allocation for both sides
       o_par[s] = take((size_t)chunk * 4);
       o_dep[s] = take((size_t)chunk * 4);
       o_q[s] = take((size_t)chunk * 4);
@@ -1709,7 +1752,7 @@ struct DistBiBfs::Impl {
     V.col = d_col;
     sent_base = reinterpret_cast<uint32_t*>(b + o_sent);
     for (int s = 0; s < 2; ++s) {
-      V.vis[s] = reinterpret_cast<uint32_t*>(b + o_vis[s]);
+      V.vis[s] = reinterpret_cast<uint32_t*>(b + o_vis[0]) + s;
       V.parent[s] = reinterpret_cast<uint32_t*>(b + o_par[s]);
       V.depth[s] = reinterpret_cast<uint32_t*>(b + o_dep[s]);
       V.queue[s] = reinterpret_cast<uint32_t*>(b + o_q[s]);
@@ -1717,7 +1760,7 @@ struct DistBiBfs::Impl {
       V.obits[s] = reinterpret_cast<uint32_t*>(b + o_ob[s]);
       V.gbits[s] = reinterpret_cast<uint32_t*>(b + o_gb[s]);
       V.sent[s] = sent_base + (size_t)s * gwords;
-      HIP_CHECK(hipMemsetAsync(V.vis[s], 0, words * 4, stream));
+      if (!s) HIP_CHECK(hipMemsetAsync(V.vis[0], 0, words * 8, stream));
       HIP_CHECK(hipMemsetAsync(V.depth[s], 0xff, (size_t)chunk * 4, stream));  // kEmpty
     }
     V.sendbuf = reinterpret_cast<uint32_t*>(b + o_send);
@@ -2037,7 +2080,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   // they carry the previous epoch.
   std::memset(h_plan, 0, kPlanRing * 8);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  k_seed<<<1, 64, 0, cs>>>(V, src, dst);
+  const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
+  if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
   if (P > 1) {
     comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
     stats.collectives++;
@@ -2052,13 +2096,13 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   if (host_only) {
     final_and_wait(it++, pol, kPlanStall, cs);
     have_ctl = true;
-  } else if (P == 1 && tune.solo) {
+  } else if (solo) {
     // one launch for every round the solo workgroup can hold; it leaves the
     // state of a stalled round (or the finished search) and its Ctl in h_ctl
     const uint32_t tag = next_tag();
     const uint32_t emax = std::min<uint32_t>(std::max<uint32_t>(tune.solo_edges, 1), kSoloE);
-    if (solo_stamp) k_spec_solo<true><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, h_fin, tag, d_stamps);
-    else k_spec_solo<false><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, h_fin, tag, nullptr);
+    if (solo_stamp) k_spec_solo<true><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, 1, src, dst, h_fin, tag, d_stamps);
+    else k_spec_solo<false><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, 1, src, dst, h_fin, tag, nullptr);
     HIP_CHECK(hipGetLastError());
     stats.host_syncs++;
     spin_tag(tag, cs);

@@ -1263,6 +1263,21 @@ Csr HipBiBfs::download_csr() const {
   return g;
 }
 
+// Row u of the device CSR (for checking paths on graphs too large to copy to
+// the host: one row per call).
+std::vector<vid_t> HipBiBfs::neighbors(vid_t u) const {
+  const auto& I = *p_;
+  BIBFS_REQUIRE(u < I.n, "neighbors: vertex out of range");
+  uint64_t r[2];
+  HIP_CHECK(hipMemcpyAsync(r, I.d_row_off + u, 16, hipMemcpyDeviceToHost, I.stream));
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  std::vector<vid_t> out(r[1] - r[0]);
+  if (!out.empty())
+    HIP_CHECK(hipMemcpyAsync(out.data(), I.d_col + r[0], out.size() * 4, hipMemcpyDeviceToHost, I.stream));
+  HIP_CHECK(hipStreamSynchronize(I.stream));
+  return out;
+}
+
 EdgeList HipBiBfs::download_edges() const {
   const auto& I = *p_;
   EdgeList el;

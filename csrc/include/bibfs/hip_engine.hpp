@@ -97,6 +97,7 @@ class HipBiBfs {
 
   // --- introspection for tests --------------------------------------------
   Csr download_csr() const;
+  std::vector<vid_t> neighbors(vid_t u) const;  // one CSR row, copied from the device
   EdgeList download_edges() const;      // edges of the last generate_* call
   int device() const;
   DeviceInfo info() const;

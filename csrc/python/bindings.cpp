@@ -323,6 +323,7 @@ PYBIND11_MODULE(_native, m) {
       .def("check_meet", &HipBiBfs::check_meet, py::call_guard<py::gil_scoped_release>())
       .def("finish", &HipBiBfs::finish, py::call_guard<py::gil_scoped_release>())
       .def("download_csr", &HipBiBfs::download_csr)
+      .def("neighbors", &HipBiBfs::neighbors)
       .def("download_edges", &HipBiBfs::download_edges)
       .def("info", &HipBiBfs::info)
       .def("synchronize", &HipBiBfs::synchronize, py::call_guard<py::gil_scoped_release>());
