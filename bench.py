@@ -4,7 +4,7 @@ shape, reported as GTEPS(M/t) (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--graph gnp:100000::6]
                     [--mode replicated|partitioned] [--extra-graph gnp:10000000::1,kron:22:16:1]
-                    [--dist-graphs gnp:1000000::2,kron:22:16:1,kron:27:16:1]
+                    [--dist-graphs gnp:1000000::2,kron:22:16:1,kron:auto]
 
 One step = one bidirectional-BFS query per GPU: host call -> search on the
 MI355X -> hop count AND the full path back in host memory ("end-to-end ms to
@@ -64,8 +64,10 @@ def parse_args(argv=None):
     ap.add_argument("--mode", choices=["replicated", "partitioned"], default="replicated")
     ap.add_argument("--extra-graph", default="gnp:10000000::1,kron:22:16:1",
                     help="comma-separated secondary configs reported under 'extra' (empty to skip)")
-    ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1,kron:27:16:1",
-                    help="configs run through the partitioned RCCL engine at every N (empty to skip)")
+    ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1,kron:auto",
+                    help="configs run through the partitioned RCCL engine at every N (empty to skip); "
+                         "kron:auto = the world-scaled Kronecker graph kron:min(30, 27 + log2 N):16 "
+                         "(~17 GB CSR shard per GPU at every N; 137 GB of columns at N = 8)")
     ap.add_argument("--dist-steps", type=int, default=20)
     ap.add_argument("--secondary-timeout", type=float, default=420.0,
                     help="seconds allowed for the extra + partitioned configs together; past it the "
@@ -134,6 +136,15 @@ def parse_spec(spec: str):
         scale, ef = int(f[1]), (int(f[2]) if len(f) > 2 else 16)
         return "rmat", 1 << scale, ef << scale, (int(f[3]) if len(f) > 3 else 1)
     raise ValueError(f"bench graph spec must be gnp:/rmat:/kron:, got {spec!r}")
+
+
+def world_scaled(spec: str, world: int) -> str:
+    """kron:auto -> the Kronecker scale that keeps the CSR shard per GPU at
+    ~17 GB (scale 27 on one GPU, +1 per doubling of N, capped at 30)."""
+    if spec != "kron:auto":
+        return spec
+    scale = min(30, 27 + max(0, int(world).bit_length() - 1))
+    return f"kron:{scale}:16:1"
 
 
 def generate(eng, spec: str):
@@ -520,6 +531,7 @@ def main(argv=None) -> int:
             failed = True
     if a.mode == "replicated" and (world == 1 or (a.dist_backend == "nccl" and not shared_gpu)):
         for spec in filter(None, a.dist_graphs.split(",")):
+            spec = world_scaled(spec, world)
             partitioned[spec] = None
             try:
                 partitioned[spec], state["rccl_ranks"] = run_partitioned(spec, a.dist_steps, 3)

@@ -71,3 +71,12 @@ def test_launcher_command_and_world_check(monkeypatch):
     monkeypatch.setattr(bench, "spawn_ranks", fake_spawn)
     assert bench.main(["--gpus", "8", "--steps", "2"]) == 0
     assert called == {"n": 8, "argv": ["--gpus", "8", "--steps", "2"]}
+
+
+def test_world_scaled_partitioned_config():
+    """kron:auto keeps ~17 GB of CSR per GPU: scale 27 on one GPU, +1 per doubling, capped at 30."""
+    import bench
+
+    assert [bench.world_scaled("kron:auto", w) for w in (1, 2, 4, 8, 16)] == [
+        "kron:27:16:1", "kron:28:16:1", "kron:29:16:1", "kron:30:16:1", "kron:30:16:1"]
+    assert bench.world_scaled("gnp:1000000::2", 8) == "gnp:1000000::2"
