@@ -92,6 +92,26 @@ class RcclComm final : public Comm {
     else
       RCCL_CHECK(ncclAllGather(send, recv, bytes, ncclUint8, comm_, s));
   }
+  // One grouped send/recv per peer (RCCL fuses the group into one launch);
+  // a message to itself is a device copy.
+  void alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    live();
+    const char* sp = static_cast<const char*>(send);
+    char* rp = static_cast<char*>(recv);
+    if (bytes) HIP_CHECK(hipMemcpyAsync(rp + (size_t)rank_ * bytes, sp + (size_t)rank_ * bytes, bytes,
+                                        hipMemcpyDeviceToDevice, s));
+    if (size_ == 1) return;
+    const bool words = bytes % 4 == 0;
+    const size_t count = words ? bytes / 4 : bytes;
+    const ncclDataType_t ty = words ? ncclUint32 : ncclUint8;
+    RCCL_CHECK(ncclGroupStart());
+    for (int r = 0; r < size_; ++r) {
+      if (r == rank_) continue;
+      RCCL_CHECK(ncclSend(sp + (size_t)r * bytes, count, ty, r, comm_, s));
+      RCCL_CHECK(ncclRecv(rp + (size_t)r * bytes, count, ty, r, comm_, s));
+    }
+    RCCL_CHECK(ncclGroupEnd());
+  }
   void check() override {
     live();
     ncclResult_t e = ncclSuccess;
@@ -224,6 +244,14 @@ class LocalComm final : public Comm {
     exchange(send, recv, bytes, s);
   }
 
+  void alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    if (g_->P == 1) {
+      if (bytes && send != recv) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, s));
+      return;
+    }
+    exchange(send, recv, bytes, s, true);
+  }
+
   void abort() override {
     aborted_ = true;
     abort_local_group(*g_);
@@ -231,10 +259,10 @@ class LocalComm final : public Comm {
   bool aborted() const override { return aborted_; }
 
  private:
-  // recv[r] = rank r's src, for every r; ordered on `s` after every rank's
-  // producer work, and every rank's later writes to its src ordered after
-  // every copy out of it.
-  void exchange(const void* src, void* recv, size_t bytes, hipStream_t s) {
+  // recv[r] = rank r's src, for every r (addressed: rank r's src block
+  // `rank_`); ordered on `s` after every rank's producer work, and every
+  // rank's later writes to its src ordered after every copy out of it.
+  void exchange(const void* src, void* recv, size_t bytes, hipStream_t s, bool addressed = false) {
     if (aborted_) throw Error("local group communicator was aborted after an earlier failure");
     LocalGroup& G = *g_;
     HIP_CHECK(hipEventRecord(ready_, s));
@@ -252,7 +280,8 @@ class LocalComm final : public Comm {
       const LocalGroup::Slot& x = peers[(size_t)r];
       if (r != rank_) HIP_CHECK(hipStreamWaitEvent(s, x.ready, 0));
       if (bytes)
-        HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)r * bytes, x.src, bytes,
+        HIP_CHECK(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)r * bytes,
+                                 static_cast<const char*>(x.src) + (addressed ? (size_t)rank_ * bytes : 0), bytes,
                                  hipMemcpyDeviceToDevice, s));
     }
     HIP_CHECK(hipEventRecord(done_, s));

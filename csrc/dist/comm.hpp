@@ -45,6 +45,9 @@ class Comm {
   virtual void allreduce(void* buf, size_t count, DType t, ROp op, hipStream_t s) = 0;
   // recv = P consecutive blocks of `bytes` (block r from rank r); device memory.
   virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // Owner-addressed exchange: send = P blocks of `bytes` (block r goes to rank
+  // r), recv = P blocks (block r came from rank r); device memory.
+  virtual void alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
   // Throw if the communicator reported an asynchronous error (peer failure).
   virtual void check() {}
   // Abort every outstanding and future collective of this communicator

@@ -79,6 +79,8 @@ constexpr int kHubTile = 1024;                  // hubs staged in LDS per pass
 constexpr uint32_t kSpecHubCap = 4096;          // speculative blocks up to this size skip the hub pass
 constexpr uint32_t kTraceCap = 4096;            // rounds recorded with SearchOptions::trace
 constexpr uint32_t kPlanRing = 64;              // pinned per-round plan words (lookahead < this)
+constexpr int kStageRanks = 16;
+constexpr uint32_t kOwnerCapMin = 256;          // smallest owner-addressed candidate block (pairs)                 // gathered reductions staged in LDS up to this many ranks
 
 // Search control state: identical on every rank (computed from reduced
 // values only).  Double-buffered by round parity: round `it` reads
@@ -99,6 +101,7 @@ struct Ctl {
   unsigned long long key;      // (length << 32) | meet vertex, once found
   unsigned long long einsp;    // edges inspected by the expanded levels
   unsigned long long ticks;    // device time of the search (s_memrealtime, 100 MHz): seed -> this plan
+  unsigned long long pkey;     // meet key found while a continuation round is still due (min so far)
   uint32_t depth[2];           // depth of the current frontier
   uint32_t dir[2];             // 1 top-down, 2 bottom-up (Beamer state)
   uint32_t turn;               // alternate policy
@@ -109,6 +112,10 @@ struct Ctl {
   uint32_t stall;              // kStall* reason
   uint32_t rounds, lockstep_rounds, levels, sparse_levels;
   uint32_t next_it;            // k_spec_solo's exit: the round the host continues with
+  uint32_t cont;               // sides THIS round continues: re-offer their spilled candidates (no expansion)
+  uint32_t cont_due;           // sides whose level is incomplete (spilled candidates wait to be offered)
+  uint32_t cont_rounds;        // continuation rounds run
+  uint32_t pad3;
 };
 
 struct Policy {
@@ -129,6 +136,8 @@ struct Reduced {
   uint32_t maxsend[2];         // candidates of side s on this rank (max; host-planned rounds)
   uint32_t md[2];              // depth of the meet vertex from each root (owner contributes; min)
   uint32_t pad[2];
+  unsigned long long spill[2]; // candidates of side s that did not fit their owner's block (sum)
+  unsigned long long nocmax;   // ~(largest candidate count this rank addressed to one owner): min = ~max
 };
 
 // One accounted round (SearchOptions::trace): the frontiers it expanded and
@@ -149,6 +158,9 @@ struct DState {
   unsigned long long new_edges[2];      // degree sum of the vertices side s claimed this level
   uint32_t meet_found;                  // a single-side level claimed a vertex the other side holds
   unsigned long long t0;                // s_memrealtime at the seed
+  uint32_t spill_n[2][2];               // [side][list] spilled candidates held (owner-addressed rounds)
+  uint32_t spill_cur[2];                // [side] the list holding the candidates still to be offered
+  uint32_t ocmax;                       // largest per-owner candidate count of this round (the header writer)
   uint32_t pad2;
 };
 
@@ -168,18 +180,27 @@ struct DView {
   uint32_t* sent[2];          // bitmaps over ALL vertices: remote vertices already offered this search
   uint32_t* obits[2];         // owned frontier slice (chunk/32 words)
   uint32_t* gbits[2];         // allgathered frontier bitmap (P * chunk/32 words: global index)
-  uint32_t* sendbuf;          // candidate blocks {count, pad, (v, u) pairs}: 2 sides
+  uint32_t* sendbuf;          // candidate blocks {count, pad, (v, u) pairs}: 2 sides (x P owners in
+                              // owner-addressed rounds: block (o, s) at (2 o + s) * block_words)
+  uint32_t* ocount;           // [2][P] candidates addressed to each owner this round
+  uint2* spill[2][2];         // [side][list] candidates that did not fit their owner's block
+  uint32_t spill_cap;
   uint32_t* recvbuf;          // P ranks x 2 sides of blocks
   uint32_t cap;               // host-planned round: candidate pairs per rank per level
   int P;
   DState* st;
   Ctl* ctl;                   // [2]
   uint64_t* plan_ring;        // pinned [kPlanRing]: slot it % kPlanRing = fed_max << 32 | (it + 1) << 8 | state << 2 | sides
+  uint64_t* plan_aux;         // pinned [kPlanRing]: largest per-owner candidate count of the round before it
   Ctl* host_ctl;              // pinned: the accounted Ctl, written by the round whose plan ends the search
   uint32_t* host_walk;        // pinned: {status, dS, dT, epoch, path[]} (one rank, the same round)
   struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
   uint32_t trace_cap;
-  Reduced* red;               // [2]
+  Reduced* red;               // [2] this rank's values of a round (claims min the meet key here)
+  // [2] x P: every rank's `red` of a round, allgathered (ONE collective per
+  // round's reduction); readers reduce them (reduce_gathered).  One rank:
+  // redg[p] = &red[p], nothing is gathered.
+  Reduced* redg[2];
 };
 
 template <typename T>
@@ -194,6 +215,26 @@ __host__ __device__ inline uint64_t block_words(uint32_t cap) { return 2 + 2 * (
 __device__ __forceinline__ void stage_words(void* dst, const void* src, size_t bytes) {
   for (uint32_t k = threadIdx.x; k < bytes / 4; k += blockDim.x)
     static_cast<uint32_t*>(dst)[k] = static_cast<const uint32_t*>(src)[k];
+}
+
+// The reduction of a round from every rank's gathered values: counts and
+// degree sums add, the meet key / frontier-max complements / meet depths
+// take the min, send counts the max.
+__device__ void reduce_gathered(const Reduced* g, int P, Reduced& out) {
+  Reduced r = g[0];
+  for (int k = 1; k < P; ++k) {
+    const Reduced& x = g[k];
+    for (int i = 0; i < 4; ++i) r.sums[i] += x.sums[i];
+    r.meetkey = min(r.meetkey, x.meetkey);
+    r.nocmax = min(r.nocmax, x.nocmax);
+    for (int s = 0; s < 2; ++s) {
+      r.spill[s] += x.spill[s];
+      r.nfmax[s] = min(r.nfmax[s], x.nfmax[s]);
+      r.maxsend[s] = max(r.maxsend[s], x.maxsend[s]);
+      r.md[s] = min(r.md[s], x.md[s]);
+    }
+  }
+  out = r;
 }
 
 // ---------------------------------------------------------------------------
@@ -221,6 +262,7 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
   c = p;
   c.sides = 0;
   c.modes = 0;
+  c.cont = 0;
   uint32_t want = 0, wm = 0;
   if (p.state == kStall) {
     if (!(flags & (kPlanResume | kPlanForce))) return;  // stays stalled until the host acts
@@ -235,30 +277,58 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
         c.ved[s] = c.fed[s];
         c.vis[s] = c.cnt[s];
       }
-    } else if (p.sides) {
+    } else if (p.sides | p.cont) {
       int ns = 0;
       for (int s = 0; s < 2; ++s) {
-        if (!((p.sides >> s) & 1)) continue;
-        ++ns;
-        c.depth[s] += 1;
-        c.levels += 1;
-        c.cnt[s] = rd.sums[2 * s];
-        c.fed[s] = rd.sums[2 * s + 1];
-        c.fmax[s] = ~rd.nfmax[s];
-        c.ved[s] += c.fed[s];
-        c.vis[s] += c.cnt[s];
+        if ((p.sides >> s) & 1) {
+          ++ns;
+          c.depth[s] += 1;
+          c.levels += 1;
+          c.cnt[s] = rd.sums[2 * s];
+          c.fed[s] = rd.sums[2 * s + 1];
+          c.fmax[s] = ~rd.nfmax[s];
+          c.ved[s] += c.fed[s];
+          c.vis[s] += c.cnt[s];
+        } else if ((p.cont >> s) & 1) {  // more of the same level (depth unchanged)
+          c.cnt[s] += rd.sums[2 * s];
+          c.fed[s] += rd.sums[2 * s + 1];
+          c.fmax[s] += ~rd.nfmax[s];  // per-rank maxima added: an upper bound
+          c.ved[s] += rd.sums[2 * s + 1];
+          c.vis[s] += rd.sums[2 * s];
+        }
       }
-      c.rounds += 1;
-      if (ns == 2) c.lockstep_rounds += 1;
-      if (rd.meetkey != kNoKey) {
-        c.state = kDone;
-        c.key = rd.meetkey;
-        return;
+      if (p.sides) {  // a continuation completes its round's levels: not a round of its own
+        c.rounds += 1;
+        if (ns == 2) c.lockstep_rounds += 1;
       }
-      for (int s = 0; s < 2; ++s)
-        if (((p.sides >> s) & 1) && c.cnt[s] == 0) c.state = kDead;  // that side's component is exhausted
+      // Candidates that did not fit their owner's block (owner-addressed
+      // exchange) leave their side's level incomplete: a continuation round
+      // offers them before anything else is decided -- the level's meets
+      // are only complete (and its minimum exact) once they are claimed.
+      c.pkey = min(p.pkey, rd.meetkey);
+      c.cont_due = (rd.spill[0] ? 1u : 0u) | (rd.spill[1] ? 2u : 0u);
+      if (!c.cont_due) {
+        if (c.pkey != kNoKey) {
+          c.state = kDone;
+          c.key = c.pkey;
+          return;
+        }
+        // an empty frontier: that side's component is exhausted (checked for
+        // both sides: a side that emptied while the other one's level was
+        // still being completed by continuation rounds is caught here too)
+        for (int s = 0; s < 2; ++s)
+          if (c.cnt[s] == 0) c.state = kDead;
+      }
     }
     if (c.state != kRun || (flags & kPlanAccountOnly)) return;
+    if (c.cont_due) {  // the continuation round: no expansion, the spilled candidates offered again
+      c.cont = c.cont_due;
+      c.cont_due = 0;
+      c.cont_rounds += 1;
+      c.state = kRun;
+      c.stall = kStallNone;
+      return;
+    }
     if ((uint64_t)c.rounds > 2ull * pol.n + 2) {  // safety net (v3 parity: iteration cap N)
       c.state = kDead;
       return;
@@ -329,6 +399,10 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
     }
     for (int k = 0; k < 4; ++k) t.sums[k] = rd.sums[k];
     t.meetkey = rd.meetkey;
+  } else if (V.trace && prev.cont && c.rounds >= 1 && c.rounds <= V.trace_cap) {
+    RoundRec& t = V.trace[c.rounds - 1];  // a continuation adds to its round's record
+    for (int k = 0; k < 4; ++k) t.sums[k] += rd.sums[k];
+    t.meetkey = min(t.meetkey, rd.meetkey);
   }
 }
 
@@ -345,7 +419,7 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
 // also raises DState::meet_found and the expansion loops stop early.
 struct ClaimMeet {
   unsigned long long* meetkey = nullptr;
-  uint32_t dother = 0;  // the other side's frontier depth this round
+  uint32_t dclaim = 0;  // the depth the other side's claims of this round get (its kEmpty depth reads)
   bool single = false;
   // read the visited word before the atomicOr (skips the atomic for a vertex
   // already held): pays on big levels, where most edges lead to visited
@@ -378,7 +452,7 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
     if ((cm.meetkey || cm.single) && mine && other) {
       if (cm.meetkey) {
         uint32_t dd = __hip_atomic_load(&pick(V.depth, s ^ 1)[li], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (dd == kEmpty) dd = cm.dother + 1;
+        if (dd == kEmpty) dd = cm.dclaim;
         best = ((unsigned long long)(dnew + dd) << 32) | v;
       }
       if (cm.single) __hip_atomic_store(&V.st->meet_found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -414,13 +488,51 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
 // Offer remote vertex v (parent u) to its owner -- at most once per search and
 // side: after the level that offered it, v is visited by its owner (claimed
 // from the exchange, or by the bottom-up fallback of an overflowing level).
+// Owner-addressed emission (speculative rounds with more than one rank): one
+// block of `cap` pairs per owner rank; a candidate that does not fit goes to
+// the round's spill list and is offered by a continuation round.
+struct OwnerEmit {
+  uint32_t cap = 0;           // pairs per owner block; 0 = one block per side (host-planned rounds)
+  uint32_t bw = 0;            // words per block
+  uint2* spill = nullptr;     // this round's overflow list of the side
+  uint32_t* spill_n = nullptr;
+};
+
+__device__ __forceinline__ void emit_owned_pair(const DView& V, int s, uint32_t v, uint32_t u, const OwnerEmit& oe) {
+  const uint32_t o = v / V.chunk;
+  const uint32_t pos = atomicAdd(&V.ocount[s * V.P + o], 1u);
+  if (pos < oe.cap) {
+    reinterpret_cast<uint2*>(V.sendbuf + (size_t)(2 * o + s) * oe.bw)[1 + pos] = make_uint2(v, u);
+  } else {
+    const uint32_t q = atomicAdd(oe.spill_n, 1u);
+    if (q < V.spill_cap) oe.spill[q] = make_uint2(v, u);  // (a rank's candidates of a level never exceed it)
+  }
+}
+
+// The last workgroup of a round's emitting kernel: every owner block's count
+// into its header, the counters reset, the largest per-owner count kept for
+// the host's sizing of the next blocks.
+__device__ void write_owner_headers(const DView& V, uint32_t cap) {
+  const uint64_t bw = block_words(cap);
+  for (uint32_t t = threadIdx.x; t < 2u * V.P; t += blockDim.x) {
+    const uint32_t ss = t / V.P, o = t % V.P;
+    const uint32_t cnt = atomicExch(&V.ocount[t], 0u);
+    V.sendbuf[(2 * o + ss) * bw] = min(cnt, cap);
+    if (cnt) atomicMax(&V.st->ocmax, cnt);
+  }
+}
+
 __device__ __forceinline__ void wave_emit(const DView& V, int s, bool want, uint32_t v, uint32_t u, uint2* pairs,
-                                          uint32_t cap) {
+                                          uint32_t cap, const OwnerEmit& oe) {
   uint32_t* sb = pick(V.sent, s);
   bool emit = false;
   if (want) {
     const uint32_t bit = 1u << (v & 31);
     if (!(sb[v >> 5] & bit)) emit = !(atomicOr(&sb[v >> 5], bit) & bit);
+  }
+  if (oe.cap) {
+    if (emit) emit_owned_pair(V, s, v, u, oe);
+    return;
   }
   const unsigned long long mask = __ballot(emit);
   if (!mask) return;  // wave-uniform
@@ -444,7 +556,7 @@ __device__ __forceinline__ bool meet_seen(const DView& V) {
 // exit_on_meet: a single-side level, which stops once a meet is claimed.
 __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pairs, uint32_t cap, uint32_t b0,
                                uint32_t nb, uint64_t hub_deg, bool exit_on_meet, const ClaimMeet& cm, uint32_t fb,
-                               uint32_t F) {
+                               uint32_t F, const OwnerEmit& oe) {
   __shared__ uint32_t su[kThreads];
   __shared__ unsigned long long sb[kThreads], se[kThreads];
   __shared__ unsigned long long wsum[kThreads / kWave];
@@ -513,7 +625,7 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
       }
       const bool own = valid && v >= V.lo && v < V.hi;
       wave_claim(V, s, own, v, uu, dnew, cm);
-      wave_emit(V, s, valid && !own, v, uu, pairs, cap);
+      wave_emit(V, s, valid && !own, v, uu, pairs, cap, oe);
     }
     __syncthreads();
   }
@@ -525,22 +637,32 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
 // -- every workgroup of its first kernel -- has read that buffer).  `sides`
 // comes from the caller's own copy of the plan: inside the planning kernel
 // ctl[p] is block 0's plain store, not yet visible to the other workgroups.
-__device__ void spec_round_end(const DView& V, uint32_t it, uint32_t sides) {
+// A continuation side (`cont`) extends its current frontier with what it
+// claimed (same level) instead of advancing it, and its spill lists swap:
+// the candidates still unsent are the ones this round could not place.
+__device__ void spec_round_end(const DView& V, uint32_t it, uint32_t sides, uint32_t cont) {
   const int p = it & 1;
   DState* st = V.st;
   for (int s = 0; s < 2; ++s) {
-    const bool on = (sides >> s) & 1;
+    const bool on = (sides >> s) & 1, co = (cont >> s) & 1;
     const uint32_t qt = atomicAdd(&st->qtail[s], 0u);
     const unsigned long long ne = atomicExch(&st->new_edges[s], 0ull);
-    V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - st->fend[s]) : 0ull;
-    V.red[p].sums[2 * s + 1] = on ? ne : 0ull;
-    V.red[p].nfmax[s] = on ? ~ne : ~0ull;
-    if (on) {
-      st->fbeg[s] = st->fend[s];
-      st->fend[s] = qt;
+    V.red[p].sums[2 * s] = (on || co) ? (unsigned long long)(qt - st->fend[s]) : 0ull;
+    V.red[p].sums[2 * s + 1] = (on || co) ? ne : 0ull;
+    V.red[p].nfmax[s] = (on || co) ? ~ne : ~0ull;
+    if (on) st->fbeg[s] = st->fend[s];
+    if (on || co) st->fend[s] = qt;
+    const uint32_t cur = st->spill_cur[s];
+    if (co) {
+      V.red[p].spill[s] = st->spill_n[s][cur ^ 1];
+      st->spill_n[s][cur] = 0;
+      st->spill_cur[s] = cur ^ 1;
+    } else {
+      V.red[p].spill[s] = on ? st->spill_n[s][cur] : 0ull;
     }
     st->hub_count[s] = 0;
   }
+  V.red[p].nocmax = ~(unsigned long long)atomicExch(&st->ocmax, 0u);
   V.red[p ^ 1].meetkey = kNoKey;
 }
 
@@ -614,7 +736,8 @@ __device__ void terminal_walk(const DView& V, unsigned long long key, const Poli
 // header = 0: k_td_hubs runs next (it writes the headers); finish: this
 // kernel ends the round's claims on this rank (one rank, no hub pass).
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
-                                                          int flags, uint64_t hub_deg, int header, int finish) {
+                                                          int flags, uint64_t hub_deg, int header, int finish,
+                                                          uint32_t ocap) {
   const int p = it & 1;
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
@@ -623,13 +746,17 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // with one round of parallel loads (thread 0 alone would chain them
   // through plan_round's branches)
   stage_words(&prev, &V.ctl[p ^ 1], sizeof(Ctl));
-  stage_words(&rd, &V.red[p ^ 1], sizeof(Reduced));
+  __shared__ Reduced gst[kStageRanks];
+  if (V.P <= kStageRanks) stage_words(gst, V.redg[p ^ 1], (size_t)V.P * sizeof(Reduced));
   if (threadIdx.x >= kThreads - 4) {
     const uint32_t k = threadIdx.x - (kThreads - 4);
     fr[k] = k < 2 ? V.st->fbeg[k] : V.st->fend[k - 2];
   }
   __syncthreads();
-  if (threadIdx.x == 0) plan_round(prev, rd, pol, cap, flags, c);
+  if (threadIdx.x == 0) {
+    reduce_gathered(V.P <= kStageRanks ? gst : V.redg[p ^ 1], V.P, rd);
+    plan_round(prev, rd, pol, cap, flags, c);
+  }
   __syncthreads();
   const bool terminal = c.state == kDone || c.state == kDead;
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < kWave) {
@@ -649,6 +776,10 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     }
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    // the largest per-owner candidate count of the round before (sizes the
+    // host's owner blocks), then the plan word behind it
+    __hip_atomic_store(&V.plan_aux[it % kPlanRing], ~rd.nocmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
     // one 8-byte write-through store per round: the host paces its enqueueing
     // on the plan and sizes the rounds it enqueues from the frontier (larger
     // side's edge count, clamped to 32 bits)
@@ -661,25 +792,46 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // end (every block sees the same plan, so no block counts itself in)
   if (terminal) return;
   const int s = blockIdx.y;
+  OwnerEmit oe;
+  if (ocap) {
+    const uint32_t cur = V.st->spill_cur[s], tgt = ((c.cont >> s) & 1) ? cur ^ 1 : cur;
+    oe.cap = ocap;
+    oe.bw = (uint32_t)block_words(ocap);
+    oe.spill = V.spill[s][tgt];
+    oe.spill_n = &V.st->spill_n[s][tgt];
+  }
   if ((c.sides >> s) & 1) {
     ClaimMeet cm;
     cm.meetkey = &V.red[p].meetkey;
-    cm.dother = c.depth[s ^ 1];
+    cm.dclaim = c.depth[s ^ 1] + 1;  // (only a claim of the other side this round reads kEmpty)
     cm.single = c.sides != 3u;
     cm.precheck = c.fed[s] > kPrecheckEdges;
     td_expand_side(V, s, c.depth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
-                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u, cm, fr[s], fr[2 + s] - fr[s]);
+                   blockIdx.x, gridDim.x, hub_deg, c.sides != 3u, cm, fr[s], fr[2 + s] - fr[s], oe);
+  } else if (ocap && ((c.cont >> s) & 1)) {
+    // a continuation: the candidates of this side's level that did not fit
+    // their owner's block last time, offered again (their `sent` bits stay set)
+    const uint32_t cur = V.st->spill_cur[s];
+    const uint32_t nsp = min(V.st->spill_n[s][cur], V.spill_cap);
+    const uint2* sp = V.spill[s][cur];
+    for (uint64_t i = blockIdx.x * (uint64_t)kThreads + threadIdx.x; i < nsp; i += (uint64_t)gridDim.x * kThreads) {
+      const uint2 x = sp[i];
+      emit_owned_pair(V, s, x.x, x.y, oe);
+    }
   }
   if (!header) return;  // k_td_hubs runs next and writes the headers
   if (finish) drain_atomics();
   if (last_block(&V.st->done_blocks[0], gridDim.x * gridDim.y)) {
-    if (threadIdx.x < 2) {
+    if (ocap) {
+      write_owner_headers(V, ocap);
+      if (threadIdx.x == 0) atomicExch(&V.st->done_blocks[0], 0u);
+    } else if (threadIdx.x < 2) {
       const int ss = threadIdx.x;
       const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
       V.sendbuf[ss * block_words(cap)] = ((c.sides >> ss) & 1) ? min(cnt, cap) : 0u;
       if (ss == 0) atomicExch(&V.st->done_blocks[0], 0u);
     }
-    if (finish && threadIdx.x == kWave) spec_round_end(V, it, c.sides);  // another wave: the header atomics are independent
+    if (finish && threadIdx.x == kWave) spec_round_end(V, it, c.sides, c.cont);  // another wave: the header atomics are independent
   }
 }
 
@@ -807,8 +959,10 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       z.dir[0] = z.dir[1] = 1;
       z.state = kRun;
       z.sides = kSeedBit;
-      z.key = kNoKey;
+      z.key = z.pkey = kNoKey;
       pc = z;
+      rd.spill[0] = rd.spill[1] = 0;
+      rd.nocmax = ~0ull;
     }
     __syncthreads();
   } else {
@@ -985,6 +1139,8 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
         }
       }
       rd.meetkey = best;
+      rd.spill[0] = rd.spill[1] = 0;
+      rd.nocmax = ~0ull;
       pc = c;
     }
     SOLO_PH(3)
@@ -1038,7 +1194,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
 // of hubs with their degree prefix in LDS and walks the tile's flattened edge
 // range with a grid stride, so each hub's edges spread over all CUs.
 __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int side, uint32_t dnew_fixed,
-                                                      uint32_t cap, int single, int finish) {
+                                                      uint32_t cap, int single, int finish, uint32_t ocap) {
   __shared__ uint32_t hu[kHubTile];
   __shared__ unsigned long long hb[kHubTile], hp[kHubTile + 1];
   __shared__ unsigned long long wsum[kThreads / kWave];
@@ -1056,9 +1212,17 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   const bool exit_on_meet = side < 0 ? sides != 3u : single != 0;
   ClaimMeet cm;  // speculative rounds detect meets at claim time; host rounds in k_meet_end
   cm.single = exit_on_meet;
+  OwnerEmit oe;
   if (side < 0) {
     cm.meetkey = &V.red[it & 1].meetkey;
-    cm.dother = V.ctl[it & 1].depth[s ^ 1];
+    cm.dclaim = V.ctl[it & 1].depth[s ^ 1] + 1;
+    if (ocap) {  // (a continuation round has no hubs: the expanding side's list)
+      const uint32_t cur = V.st->spill_cur[s];
+      oe.cap = ocap;
+      oe.bw = (uint32_t)block_words(ocap);
+      oe.spill = V.spill[s][cur];
+      oe.spill_n = &V.st->spill_n[s][cur];
+    }
   }
   __shared__ uint32_t sstop;
   if ((sides >> s) & 1) {
@@ -1125,7 +1289,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
         }
         const bool own = valid && v >= V.lo && v < V.hi;
         wave_claim(V, s, own, v, uu, dnew, cm);
-        wave_emit(V, s, valid && !own, v, uu, pairs, cap);
+        wave_emit(V, s, valid && !own, v, uu, pairs, cap, oe);
       }
       __syncthreads();
     }
@@ -1133,13 +1297,16 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   if (side >= 0) return;
   if (finish) drain_atomics();
   if (last_block(&V.st->done_blocks[2], gridDim.x * gridDim.y)) {
-    if (threadIdx.x < 2) {
+    if (ocap) {
+      write_owner_headers(V, ocap);
+      if (threadIdx.x == 0) atomicExch(&V.st->done_blocks[2], 0u);
+    } else if (threadIdx.x < 2) {
       const int ss = threadIdx.x;
       const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
       V.sendbuf[ss * block_words(cap)] = ((sides >> ss) & 1) ? min(cnt, cap) : 0u;
       if (ss == 0) atomicExch(&V.st->done_blocks[2], 0u);
     }
-    if (finish && threadIdx.x == kWave) spec_round_end(V, it, sides);
+    if (finish && threadIdx.x == kWave) spec_round_end(V, it, sides, V.ctl[it & 1].cont);
   }
 }
 
@@ -1151,12 +1318,13 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   const Ctl& c = V.ctl[it & 1];
   if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
   const int s = blockIdx.y;
-  const uint32_t dnew = c.depth[s] + 1;
+  // a continuation side claims at the depth its level already has
+  const uint32_t dnew = ((c.sides >> s) & 1) ? c.depth[s] + 1 : c.depth[s];
   ClaimMeet cm;
   cm.meetkey = &V.red[it & 1].meetkey;
-  cm.dother = c.depth[s ^ 1];
+  cm.dclaim = ((c.sides >> (s ^ 1)) & 1) ? c.depth[s ^ 1] + 1 : c.depth[s ^ 1];
   cm.single = c.sides != 3u;
-  for (int r = 0; ((c.sides >> s) & 1) && r < V.P; ++r) {  // block-uniform
+  for (int r = 0; (((c.sides | c.cont) >> s) & 1) && r < V.P; ++r) {  // block-uniform
     const uint32_t* b = V.recvbuf + (2 * (uint64_t)r + s) * block_words(cap);
     const uint32_t cnt = min(b[0], cap);
     const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
@@ -1175,7 +1343,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   }
   drain_atomics();
   if (last_block(&V.st->done_blocks[1], gridDim.x * gridDim.y) && threadIdx.x == 0) {
-    spec_round_end(V, it, c.sides);
+    spec_round_end(V, it, c.sides, c.cont);
     atomicExch(&V.st->done_blocks[1], 0u);
   }
 }
@@ -1222,7 +1390,9 @@ __global__ __launch_bounds__(kThreads) void k_meet_end(DView V, uint32_t it) {
         st->fend[s] = qt;
       }
       st->hub_count[s] = 0;
+      V.red[p].spill[s] = 0;  // host-planned exchanges are sized exactly: nothing spills
     }
+    V.red[p].nocmax = ~0ull;
     atomicExch(&st->done_blocks[1], 0u);
   }
 }
@@ -1235,9 +1405,11 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags, 
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int p = it & 1;
   Ctl c;
-  plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, flags, c);
+  Reduced rd;
+  reduce_gathered(V.redg[p ^ 1], V.P, rd);
+  plan_round(V.ctl[p ^ 1], rd, pol, 0, flags, c);
   c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
-  publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
+  publish(V, p, V.ctl[p ^ 1], rd, c);
   V.red[p ^ 1].meetkey = kNoKey;  // read; it is the buffer of the next round (it + 1)
   *host = c;
   __threadfence_system();
@@ -1259,8 +1431,10 @@ __global__ void k_plan_force(DView V, uint32_t it, Policy pol) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   const int p = it & 1;
   Ctl c;
-  plan_round(V.ctl[p ^ 1], V.red[p ^ 1], pol, 0, kPlanForce, c);
-  publish(V, p, V.ctl[p ^ 1], V.red[p ^ 1], c);
+  Reduced rd;
+  reduce_gathered(V.redg[p ^ 1], V.P, rd);
+  plan_round(V.ctl[p ^ 1], rd, pol, 0, kPlanForce, c);
+  publish(V, p, V.ctl[p ^ 1], rd, c);
   V.red[p].meetkey = kNoKey;
 }
 
@@ -1270,7 +1444,7 @@ __global__ __launch_bounds__(kThreads) void k_td_expand(DView V, int s, uint32_t
   cm.single = single != 0;
   const uint32_t fb = V.st->fbeg[s];
   td_expand_side(V, s, dnew, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(V.cap)) + 1, V.cap, blockIdx.x,
-                 gridDim.x, hub_deg, single != 0, cm, fb, V.st->fend[s] - fb);
+                 gridDim.x, hub_deg, single != 0, cm, fb, V.st->fend[s] - fb, OwnerEmit{});
 }
 
 __global__ void k_send_header(DView V, int s, uint32_t it) {
@@ -1389,6 +1563,9 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     st->hub_count[s] = 0;
     st->new_edges[s] = 0;
     st->meet_found = 0;
+    st->spill_n[s][0] = st->spill_n[s][1] = 0;
+    st->spill_cur[s] = 0;
+    r.spill[s] = 0;
     r.sums[2 * s] = r.sums[2 * s + 1] = 0;
     const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
@@ -1403,13 +1580,15 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     }
   }
   st->t0 = __builtin_amdgcn_s_memrealtime();
+  st->ocmax = 0;
+  r.nocmax = ~0ull;
   r.meetkey = kNoKey;
   V.red[0].meetkey = kNoKey;  // round 0 detects its meets into red[0]
   Ctl c = {};
   c.dir[0] = c.dir[1] = 1;
   c.state = kRun;
   c.sides = kSeedBit;
-  c.key = kNoKey;
+  c.key = c.pkey = kNoKey;
   V.ctl[1] = c;
 }
 
@@ -1647,6 +1826,7 @@ struct DistBiBfs::Impl {
   uint32_t* h_fin = nullptr;   // pinned, k_final's tag (written after h_ctl)
   uint32_t fin_seq = 0;
   uint64_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
+  uint64_t* h_aux = nullptr;   // pinned: per-round largest per-owner candidate count
   uint32_t* h_walk = nullptr;  // pinned
   size_t h_walk_cap = 0;
   uint32_t epoch = 0;          // searches run (Policy::epoch)
@@ -1681,6 +1861,9 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 8, hipHostMallocDefault));
     std::memset(h_plan, 0, kPlanRing * 8);
     V.plan_ring = h_plan;
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_aux), kPlanRing * 8, hipHostMallocDefault));
+    std::memset(h_aux, 0, kPlanRing * 8);
+    V.plan_aux = h_aux;
     V.host_ctl = h_ctl;
     ensure_walk_buf(1u << 14);
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
@@ -1736,9 +1919,15 @@ struct DistBiBfs::Impl {
       o_ob[s] = take(words * 4);
       o_gb[s] = take(words * 4 * size);
     }
-    const size_t o_send = take(2 * block * 4), o_recv = take(2 * block * 4 * size);
+    // send: one block per side, or (owner-addressed rounds) one per side and owner
+    const size_t o_send = take(2 * block * 4 * size), o_recv = take(2 * block * 4 * size);
+    const size_t o_ocount = take(2 * (size_t)size * 4);
+    size_t o_spill[2][2];
+    for (int s = 0; s < 2; ++s)
+      for (int l = 0; l < 2; ++l) o_spill[s][l] = take(size > 1 ? (size_t)block_cap * 8 : 8);
     const size_t o_sent = take((size_t)gwords * 4 * 2);
     const size_t o_st = take(sizeof(DState)), o_ctl = take(2 * sizeof(Ctl)), o_red = take(2 * sizeof(Reduced)),
+                 o_redg = take(2 * (size_t)size * sizeof(Reduced)),
                  o_cur = take(64), o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4),
                  o_walk = take(((size_t)n + 8) * 4), o_sc = take(64),
                  o_tr = take((size_t)kTraceCap * sizeof(RoundRec));
@@ -1764,6 +1953,11 @@ struct DistBiBfs::Impl {
       HIP_CHECK(hipMemsetAsync(V.depth[s], 0xff, (size_t)chunk * 4, stream));  // kEmpty
     }
     V.sendbuf = reinterpret_cast<uint32_t*>(b + o_send);
+    V.ocount = reinterpret_cast<uint32_t*>(b + o_ocount);
+    HIP_CHECK(hipMemsetAsync(V.ocount, 0, 2 * (size_t)size * 4, stream));
+    for (int s = 0; s < 2; ++s)
+      for (int l = 0; l < 2; ++l) V.spill[s][l] = reinterpret_cast<uint2*>(b + o_spill[s][l]);
+    V.spill_cap = size > 1 ? block_cap : 1;
     V.recvbuf = reinterpret_cast<uint32_t*>(b + o_recv);
     HIP_CHECK(hipMemsetAsync(sent_base, 0, (size_t)gwords * 4 * 2, stream));
     V.cap = cap();
@@ -1771,6 +1965,8 @@ struct DistBiBfs::Impl {
     V.st = reinterpret_cast<DState*>(b + o_st);
     V.ctl = reinterpret_cast<Ctl*>(b + o_ctl);
     V.red = reinterpret_cast<Reduced*>(b + o_red);
+    for (int q = 0; q < 2; ++q)
+      V.redg[q] = size == 1 ? V.red + q : reinterpret_cast<Reduced*>(b + o_redg) + (size_t)q * size;
     d_cur = reinterpret_cast<uint32_t*>(b + o_cur);
     d_pathS = reinterpret_cast<uint32_t*>(b + o_ps);
     d_pathT = reinterpret_cast<uint32_t*>(b + o_pt);
@@ -1981,7 +2177,7 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
       k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, hubs ? kHubDeg : kNoHubs, ns == 1);
       if (hubs)
         k_td_hubs<<<blocks_for(std::min<uint64_t>(h.fed[s], (uint64_t)cus * 8 * kThreads), cus), kThreads, 0, ps>>>(
-            V, it, s, dnew, capr, ns == 1, 0);
+            V, it, s, dnew, capr, ns == 1, 0, 0);
       k_send_header<<<1, 64, 0, ps>>>(V, s, it);
     } else {
       HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
@@ -2042,11 +2238,10 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
   const uint64_t claimed_bound = std::min<uint64_t>((uint64_t)nloc, h.fed[0] + h.fed[1] + 1);
   k_meet_end<<<blocks_for(claimed_bound, cus), kThreads, 0, cs>>>(V, it);
   HIP_CHECK(hipGetLastError());
-  comm->group_begin();
-  comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
-  comm->allreduce(&V.red[it & 1].meetkey, 3, DType::kU64, ROp::kMin, cs);  // meet key, ~per-rank frontier max
-  comm->group_end();
-  stats.collectives += 2;
+  if (P > 1) {
+    comm->allgather(&V.red[it & 1], V.redg[it & 1], sizeof(Reduced), cs);
+    stats.collectives++;
+  }
 }
 
 SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& opt) {
@@ -2083,11 +2278,12 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
   if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
   if (P > 1) {
-    comm->allreduce(V.red[1].sums, 4, DType::kU64, ROp::kSum, cs);
+    comm->allgather(&V.red[1], V.redg[1], sizeof(Reduced), cs);
     stats.collectives++;
   }
   uint32_t it = 0;
   uint32_t spec_cap = kSpecCapMin;
+  uint32_t ocap_last = 0;  // owner block capacity of the last speculative round
   int flags = 0;
   bool have_ctl = false;  // h_ctl describes the current device state
   const int K = std::min<int>(std::max(0, tune.spec_rounds), (int)kPlanRing - 1);
@@ -2153,6 +2349,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     // every rank: every rank enqueues the same rounds with the same sizes.
     const uint32_t first = it;
     uint32_t cap_it = spec_cap;
+    uint32_t ocap = ocap_last;
     uint64_t f_prev = 0;
     uint32_t seen_state = kRun;  // state of the last plan word read
     for (int k = 0;; ++k) {
@@ -2169,11 +2366,23 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         for (int j = 0; j < K && pred < spec_max; ++j) pred *= g;
         cap_it = std::max<uint32_t>(cap_it, std::min<uint32_t>(spec_max, next_pow2(std::min<uint64_t>(pred + pred / 2, spec_max))));
         f_prev = f;
+        // owner blocks: the largest per-owner count of round need - 1, grown
+        // over the K + 1 rounds since, with half again as slack; too small
+        // costs a continuation round, too big only bytes
+        const uint64_t om = __atomic_load_n(&h_aux[need % kPlanRing], __ATOMIC_ACQUIRE);
+        uint64_t op = om;
+        for (int j = 0; j <= K && op < cap_it; ++j) op *= g;
+        ocap = std::min<uint32_t>(cap_it, std::max<uint32_t>(kOwnerCapMin, next_pow2(op + op / 2 + 16)));
       }
+      if (P == 1) ocap = 0;  // nothing is ever offered
+      else if (tune.owner_cap) ocap = tune.owner_cap;
+      else if (!ocap) ocap = kOwnerCapMin;
+      ocap = std::min(ocap, cap_it);
       if ((uint64_t)(it - first) > 4ull * n + 16) break;  // safety net
       const unsigned bx = std::min<unsigned>((unsigned)cus * 2, cap_it / kThreads + 1);  // ~ this rank's edges
-      const unsigned cx = std::min<unsigned>((unsigned)cus * 2, std::max<unsigned>(1, cap_it / kThreads / 4 + 1));
-      const uint64_t gather_bytes = 2 * block_words(cap_it) * 4;
+      const unsigned cx = std::min<unsigned>((unsigned)cus * 2,
+                                             std::max<unsigned>(1, (uint32_t)P * ocap / kThreads / 4 + 1));
+      const uint64_t peer_bytes = 2 * block_words(ocap) * 4;  // both sides' blocks for one owner
       // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
       // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
       const bool hubs = cap_it > kSpecHubCap && max_deg > kHubDeg;
@@ -2184,26 +2393,25 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       // pass or the expansion itself -- no separate meet / round-end kernel.
       const int end_in_expand = (P == 1 && !hubs) ? 1 : 0;
       k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
-                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand);
-      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0);
+                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap);
       HIP_CHECK(hipGetLastError());
-      if (P > 1) {  // one rank owns every vertex: expand claimed them all, the blocks are empty
-        comm->allgather(V.sendbuf, V.recvbuf, gather_bytes, cs);
-        k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, cap_it);
+      if (P > 1) {  // one rank owns every vertex: expand claimed them all, nothing to exchange
+        // owner-addressed: each rank receives only the blocks addressed to it
+        comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
+        k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, ocap);
       }
       HIP_CHECK(hipGetLastError());
-      if (P > 1) {  // a one-rank reduction is the identity
-        comm->group_begin();
-        comm->allreduce(V.red[it & 1].sums, 4, DType::kU64, ROp::kSum, cs);
-        comm->allreduce(&V.red[it & 1].meetkey, 3, DType::kU64, ROp::kMin, cs);  // + ~per-rank frontier max
-        comm->group_end();
-        stats.collectives += 3;
-        stats.exchanged_bytes += gather_bytes * P;
+      if (P > 1) {  // the round's reduction: every rank's values gathered, reduced by the reader
+        comm->allgather(&V.red[it & 1], V.redg[it & 1], sizeof(Reduced), cs);
+        stats.collectives += 2;  // the candidate exchange + this one
+        stats.exchanged_bytes += peer_bytes * (P - 1) + sizeof(Reduced) * (P - 1);
       }
       stats.spec_rounds++;
       ++it;
     }
     spec_cap = cap_it;
+    ocap_last = ocap;
     flags = 0;
     have_ctl = true;
     if (seen_state == kDone || seen_state == kDead) {
@@ -2224,6 +2432,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   stats.lockstep_rounds = (int)h.lockstep_rounds;
   stats.levels = (int)h.levels;
   stats.sparse_levels = (int)h.sparse_levels;
+  stats.cont_rounds = (int)h.cont_rounds;
   r.stats.levels = (int)h.levels;
   r.stats.edges_inspected = h.einsp;
   r.stats.visited = h.vis[0] + h.vis[1];
@@ -2400,6 +2609,7 @@ DistBiBfs::~DistBiBfs() {
   (void)hipHostFree(p_->h_ctl);
   (void)hipHostFree(p_->h_fin);
   (void)hipHostFree(p_->h_plan);
+  (void)hipHostFree(p_->h_aux);
   if (p_->h_walk) (void)hipHostFree(p_->h_walk);
   for (auto e : p_->ev_pre) (void)hipEventDestroy(e);
   (void)hipEventDestroy(p_->ev_round);

@@ -66,6 +66,7 @@ struct DistLevelStats {
   double device_ms = 0.0;          // device time from the first to the last op of the search (events)
   int path_collectives = 0;        // collectives spent reconstructing the path
   int solo_rounds = 0;             // rounds run by the one-workgroup solo kernel (one rank)
+  int cont_rounds = 0;             // continuation rounds: candidates that overflowed an owner block re-offered
 };
 
 // Knobs of the partitioned engine (defaults are the production settings; the
@@ -79,6 +80,7 @@ struct DistTuning {
   uint32_t walk_max = 15000;       // path from one gathered parent table when both sides claimed <= this
   bool solo = true;                // one rank: small rounds in one persistent workgroup (k_spec_solo)
   uint32_t solo_edges = 2048;      // ... while every expanding side has at most this many frontier edges (<= 8192)
+  uint32_t owner_cap = 0;          // > 1 rank: pairs per owner-addressed block (0 = predicted per round)
 };
 
 class DistBiBfs {

@@ -83,6 +83,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["collectives"] = s.collectives;
   d["path_collectives"] = s.path_collectives;
   d["solo_rounds"] = s.solo_rounds;
+  d["cont_rounds"] = s.cont_rounds;
   d["exchanged_bytes"] = s.exchanged_bytes;
   d["comm_ms"] = s.comm_ms;
   d["device_ms"] = s.device_ms;
@@ -342,7 +343,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("timeout_s", &DistTuning::timeout_s)
       .def_readwrite("walk_max", &DistTuning::walk_max)
       .def_readwrite("solo", &DistTuning::solo)
-      .def_readwrite("solo_edges", &DistTuning::solo_edges);
+      .def_readwrite("solo_edges", &DistTuning::solo_edges)
+      .def_readwrite("owner_cap", &DistTuning::owner_cap);
   py::class_<DistLocalFault>(m, "DistLocalFault")
       .def(py::init<>())
       .def_readwrite("rank", &DistLocalFault::rank)

@@ -176,7 +176,8 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
         for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False},
                    {"direction": "bottomup"}):
             for tune in (make_tuning(spec_rounds=spec_rounds), make_tuning(spec_rounds=spec_rounds, cap=4,
-                                                                          nosync_bytes=0)):
+                                                                          nosync_bytes=0),
+                         make_tuning(spec_rounds=spec_rounds, owner_cap=2)):
                 rs = dist_local_run(ranks, g, qs, tuning=tune, trace=True, **kw)
                 for (s, d), r in zip(qs, rs):
                     want, hops = round_trace(g.csr, s, d, side=kw.get("side", "edges"),
@@ -283,3 +284,40 @@ def test_world1_back_to_back_queries_keep_state_clean():
     rs = dist_local_run(1, g, qs)
     for (s, d), r in zip(qs, rs):
         check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+
+
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+def test_owner_blocks_overflow_into_continuation_rounds(ranks):
+    """Owner-addressed exchange with 2-pair blocks: candidates that do not fit
+    their owner's block are re-offered by continuation rounds (same level, no
+    expansion) until every one is claimed; answers stay exact and meets found
+    before the level completes wait for it (the level's minimum)."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    cont = 0
+    for spec in ("gnp:20000::6", "kron:14:16:3"):
+        g = bb.from_spec(spec)
+        qs = _pairs(g.n, 10, 17)
+        for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"direction": "topdown"}):
+            rs, st = dist_local_run(ranks, g, qs, tuning=make_tuning(owner_cap=2), return_stats=True, **kw)
+            _check_all(g, qs, rs)
+            cont += sum(x["cont_rounds"] for x in st)
+    assert cont > 0
+
+
+def test_owner_addressed_exchange_moves_only_addressed_bytes():
+    """Default sizing: the bytes a rank receives per query are the blocks
+    addressed to it (plus the per-round status), far below P full candidate
+    blocks per round."""
+    import torch  # noqa: F401
+
+    g = bb.from_spec("gnp:100000::6")
+    qs = _pairs(g.n, 8, 3)
+    for ranks in (2, 4):
+        rs, st = dist_local_run(ranks, g, qs, return_stats=True)
+        _check_all(g, qs, rs)
+        for x, r in zip(st, rs):
+            if r.found and r.hops > 2:
+                # a 256-pair block per owner and side at most once per round, in the worst case
+                assert x["exchanged_bytes"] <= x["rounds"] * (ranks - 1) * 2 * (2 + 2 * 4096) * 4 + 65536, x
