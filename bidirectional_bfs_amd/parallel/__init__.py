@@ -34,7 +34,8 @@ MPIEXEC = os.environ.get("BIBFS_MPIEXEC", "/opt/conda/bin/mpiexec")
 def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] = None, cap: Optional[int] = None,
                 nosync_bytes: Optional[int] = None, timeout_s: Optional[float] = None,
                 walk_max: Optional[int] = None, solo: Optional[bool] = None,
-                solo_edges: Optional[int] = None, owner_cap: Optional[int] = None) -> "native.DistTuning":
+                solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
+                overlap: Optional[bool] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
 
     solo (one rank only): run the small rounds in one persistent workgroup
@@ -44,11 +45,15 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
 
     owner_cap (more than one rank): pairs per owner-addressed candidate block
     of a speculative round (0 = predicted per round from the last per-owner
-    counts); candidates that do not fit are re-offered by a continuation round."""
+    counts); candidates that do not fit are re-offered by a continuation round.
+
+    overlap (more than one rank): the two sides of a speculative round expand
+    as separate launches (side 1 on the compute stream) so side 0's exchange
+    overlaps side 1's expansion."""
     t = native.DistTuning()
     for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
-                 ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap)):
+                 ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap)):
         if v is not None:
             setattr(t, k, v)
     return t

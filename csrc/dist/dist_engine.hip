@@ -161,6 +161,7 @@ struct DState {
   uint32_t spill_n[2][2];               // [side][list] spilled candidates held (owner-addressed rounds)
   uint32_t spill_cur[2];                // [side] the list holding the candidates still to be offered
   uint32_t ocmax;                       // largest per-owner candidate count of this round (the header writer)
+  uint32_t done_side[2];                // last-block detection of a one-side expansion launch (overlap)
   uint32_t pad2;
 };
 
@@ -502,7 +503,7 @@ __device__ __forceinline__ void emit_owned_pair(const DView& V, int s, uint32_t 
   const uint32_t o = v / V.chunk;
   const uint32_t pos = atomicAdd(&V.ocount[s * V.P + o], 1u);
   if (pos < oe.cap) {
-    reinterpret_cast<uint2*>(V.sendbuf + (size_t)(2 * o + s) * oe.bw)[1 + pos] = make_uint2(v, u);
+    reinterpret_cast<uint2*>(V.sendbuf + ((size_t)s * V.P + o) * oe.bw)[1 + pos] = make_uint2(v, u);
   } else {
     const uint32_t q = atomicAdd(oe.spill_n, 1u);
     if (q < V.spill_cap) oe.spill[q] = make_uint2(v, u);  // (a rank's candidates of a level never exceed it)
@@ -512,12 +513,12 @@ __device__ __forceinline__ void emit_owned_pair(const DView& V, int s, uint32_t 
 // The last workgroup of a round's emitting kernel: every owner block's count
 // into its header, the counters reset, the largest per-owner count kept for
 // the host's sizing of the next blocks.
-__device__ void write_owner_headers(const DView& V, uint32_t cap) {
+__device__ void write_owner_headers(const DView& V, uint32_t cap, int side0 = 0, int nsides = 2) {
   const uint64_t bw = block_words(cap);
-  for (uint32_t t = threadIdx.x; t < 2u * V.P; t += blockDim.x) {
-    const uint32_t ss = t / V.P, o = t % V.P;
-    const uint32_t cnt = atomicExch(&V.ocount[t], 0u);
-    V.sendbuf[(2 * o + ss) * bw] = min(cnt, cap);
+  for (uint32_t t = threadIdx.x; t < (uint32_t)nsides * V.P; t += blockDim.x) {
+    const uint32_t ss = side0 + t / V.P, o = t % V.P, k = ss * V.P + o;
+    const uint32_t cnt = atomicExch(&V.ocount[k], 0u);
+    V.sendbuf[k * bw] = min(cnt, cap);
     if (cnt) atomicMax(&V.st->ocmax, cnt);
   }
 }
@@ -737,7 +738,7 @@ __device__ void terminal_walk(const DView& V, unsigned long long key, const Poli
 // kernel ends the round's claims on this rank (one rank, no hub pass).
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
                                                           int flags, uint64_t hub_deg, int header, int finish,
-                                                          uint32_t ocap) {
+                                                          uint32_t ocap, int side0, int nsides) {
   const int p = it & 1;
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
@@ -759,7 +760,8 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   }
   __syncthreads();
   const bool terminal = c.state == kDone || c.state == kDead;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < kWave) {
+  const bool planner = blockIdx.x == 0 && blockIdx.y == 0 && side0 == 0;  // one block publishes
+  if (planner && threadIdx.x < kWave) {
     if (threadIdx.x == 0) publish(V, p, prev, rd, c);
     // the round that ends the search hands the host its accounted Ctl directly
     // (no k_final launch + wait after the batch); later no-op rounds repeat it
@@ -775,7 +777,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
       __threadfence_system();
     }
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+  if (planner && threadIdx.x == 0) {
     // the largest per-owner candidate count of the round before (sizes the
     // host's owner blocks), then the plan word behind it
     __hip_atomic_store(&V.plan_aux[it % kPlanRing], ~rd.nocmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -791,7 +793,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // a round enqueued past the end of the search: nothing to expand, no round
   // end (every block sees the same plan, so no block counts itself in)
   if (terminal) return;
-  const int s = blockIdx.y;
+  const int s = side0 + (int)blockIdx.y;
   OwnerEmit oe;
   if (ocap) {
     const uint32_t cur = V.st->spill_cur[s], tgt = ((c.cont >> s) & 1) ? cur ^ 1 : cur;
@@ -821,10 +823,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   }
   if (!header) return;  // k_td_hubs runs next and writes the headers
   if (finish) drain_atomics();
-  if (last_block(&V.st->done_blocks[0], gridDim.x * gridDim.y)) {
+  uint32_t* done = nsides == 2 ? &V.st->done_blocks[0] : &V.st->done_side[side0];
+  if (last_block(done, gridDim.x * gridDim.y)) {
     if (ocap) {
-      write_owner_headers(V, ocap);
-      if (threadIdx.x == 0) atomicExch(&V.st->done_blocks[0], 0u);
+      write_owner_headers(V, ocap, side0, nsides);
+      if (threadIdx.x == 0) atomicExch(done, 0u);
     } else if (threadIdx.x < 2) {
       const int ss = threadIdx.x;
       const uint32_t cnt = atomicExch(&V.st->send_count[ss], 0u);
@@ -1160,6 +1163,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
     st->new_edges[sd] = 0;
   }
   st->done_blocks[0] = st->done_blocks[1] = st->done_blocks[2] = 0;
+  st->done_side[0] = st->done_side[1] = 0;
   st->meet_found = 0;
   V.ctl[p ^ 1] = pc;  // round it - 1, executed, and its reduction
   V.red[p ^ 1] = rd;
@@ -1325,7 +1329,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   cm.dclaim = ((c.sides >> (s ^ 1)) & 1) ? c.depth[s ^ 1] + 1 : c.depth[s ^ 1];
   cm.single = c.sides != 3u;
   for (int r = 0; (((c.sides | c.cont) >> s) & 1) && r < V.P; ++r) {  // block-uniform
-    const uint32_t* b = V.recvbuf + (2 * (uint64_t)r + s) * block_words(cap);
+    const uint32_t* b = V.recvbuf + ((uint64_t)s * V.P + r) * block_words(cap);
     const uint32_t cnt = min(b[0], cap);
     const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
     for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < cnt; base += (uint64_t)gridDim.x * kThreads) {
@@ -2382,7 +2386,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       const unsigned bx = std::min<unsigned>((unsigned)cus * 2, cap_it / kThreads + 1);  // ~ this rank's edges
       const unsigned cx = std::min<unsigned>((unsigned)cus * 2,
                                              std::max<unsigned>(1, (uint32_t)P * ocap / kThreads / 4 + 1));
-      const uint64_t peer_bytes = 2 * block_words(ocap) * 4;  // both sides' blocks for one owner
+      const uint64_t peer_bytes = block_words(ocap) * 4;  // one side's block for one owner
       // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
       // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
       const bool hubs = cap_it > kSpecHubCap && max_deg > kHubDeg;
@@ -2392,20 +2396,45 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       // claim time): the claim kernel with more than one rank, else the hub
       // pass or the expansion itself -- no separate meet / round-end kernel.
       const int end_in_expand = (P == 1 && !hubs) ? 1 : 0;
-      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
-                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap);
-      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap);
+      // Owner-addressed exchange, one alltoall per side (block (s, o) at
+      // sendbuf + (s P + o) * block_words): each rank receives only the
+      // blocks addressed to it.  With DistTuning::overlap the two sides
+      // expand as separate launches -- side 1 on the compute stream -- so
+      // side 0's exchange runs while side 1 is still expanding.
+      const uint64_t side_words = (uint64_t)P * block_words(ocap);
+      const bool split = P > 1 && tune.overlap && !hubs;
+      if (split) {
+        HIP_CHECK(hipEventRecord(ev_round, cs));  // the previous round is complete on cs
+        HIP_CHECK(hipStreamWaitEvent(stream, ev_round, 0));
+        k_spec_expand<<<dim3(bx, 1), kThreads, 0, stream>>>(V, it, pol, cap_it, k == 0 ? flags : 0, kNoHubs, 1, 0,
+                                                            ocap, 1, 1);
+        HIP_CHECK(hipEventRecord(ev_pre[1], stream));
+        k_spec_expand<<<dim3(bx, 1), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0, kNoHubs, 1, 0,
+                                                        ocap, 0, 1);
+        comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
+        HIP_CHECK(hipStreamWaitEvent(cs, ev_pre[1], 0));
+        comm->alltoall(V.sendbuf + side_words, V.recvbuf + side_words, peer_bytes, cs);
+      } else {
+        k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
+                                                        hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap,
+                                                        0, 2);
+        if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap);
+        if (P > 1) {
+          comm->group_begin();
+          comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
+          comm->alltoall(V.sendbuf + side_words, V.recvbuf + side_words, peer_bytes, cs);
+          comm->group_end();
+        }
+      }
       HIP_CHECK(hipGetLastError());
       if (P > 1) {  // one rank owns every vertex: expand claimed them all, nothing to exchange
-        // owner-addressed: each rank receives only the blocks addressed to it
-        comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
         k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, ocap);
       }
       HIP_CHECK(hipGetLastError());
       if (P > 1) {  // the round's reduction: every rank's values gathered, reduced by the reader
         comm->allgather(&V.red[it & 1], V.redg[it & 1], sizeof(Reduced), cs);
         stats.collectives += 2;  // the candidate exchange + this one
-        stats.exchanged_bytes += peer_bytes * (P - 1) + sizeof(Reduced) * (P - 1);
+        stats.exchanged_bytes += 2 * peer_bytes * (P - 1) + sizeof(Reduced) * (P - 1);
       }
       stats.spec_rounds++;
       ++it;

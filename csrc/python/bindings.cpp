@@ -344,7 +344,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("walk_max", &DistTuning::walk_max)
       .def_readwrite("solo", &DistTuning::solo)
       .def_readwrite("solo_edges", &DistTuning::solo_edges)
-      .def_readwrite("owner_cap", &DistTuning::owner_cap);
+      .def_readwrite("owner_cap", &DistTuning::owner_cap)
+      .def_readwrite("overlap", &DistTuning::overlap);
   py::class_<DistLocalFault>(m, "DistLocalFault")
       .def(py::init<>())
       .def_readwrite("rank", &DistLocalFault::rank)

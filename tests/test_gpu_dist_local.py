@@ -177,7 +177,8 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
                    {"direction": "bottomup"}):
             for tune in (make_tuning(spec_rounds=spec_rounds), make_tuning(spec_rounds=spec_rounds, cap=4,
                                                                           nosync_bytes=0),
-                         make_tuning(spec_rounds=spec_rounds, owner_cap=2)):
+                         make_tuning(spec_rounds=spec_rounds, owner_cap=2),
+                         make_tuning(spec_rounds=spec_rounds, overlap=True, owner_cap=64)):
                 rs = dist_local_run(ranks, g, qs, tuning=tune, trace=True, **kw)
                 for (s, d), r in zip(qs, rs):
                     want, hops = round_trace(g.csr, s, d, side=kw.get("side", "edges"),
@@ -321,3 +322,19 @@ def test_owner_addressed_exchange_moves_only_addressed_bytes():
             if r.found and r.hops > 2:
                 # a 256-pair block per owner and side at most once per round, in the worst case
                 assert x["exchanged_bytes"] <= x["rounds"] * (ranks - 1) * 2 * (2 + 2 * 4096) * 4 + 65536, x
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 3, 4])
+def test_overlap_knob_matches_oracle(ranks):
+    """DistTuning.overlap: each speculative round's sides expand as separate
+    launches on two streams, side 0's exchange beside side 1's expansion;
+    every answer still matches the oracle (and ranks agree)."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    for spec in ("gnp:20000::6", "rmat:16384:262144:3"):
+        g = bb.from_spec(spec)
+        qs = _pairs(g.n, 10, 29)
+        for kw in ({}, {"lockstep": False}, {"direction": "bottomup"}):
+            rs = dist_local_run(ranks, g, qs, tuning=make_tuning(overlap=True), **kw)
+            _check_all(g, qs, rs)
