@@ -449,9 +449,12 @@ def main(argv=None) -> int:
         eng.barrier()
         barrier()
         done = []
+        qt = []
         t0 = time.perf_counter()
         for i in range(steps):
+            q0 = time.perf_counter()
             done.append((query(warmup + i), eng.last_stats))
+            qt.append(time.perf_counter() - q0)
         eng.barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
         ok = all_ranks_ok(not wrong)
@@ -467,6 +470,8 @@ def main(argv=None) -> int:
             "gen_peak_bytes_max": int(max_over_ranks(float(eng.gen_peak_bytes))),
             "hbm_used_bytes_max": int(max_over_ranks(float(hbm_used))),
             "queries": steps, "ms_per_query": round(dt * 1e3 / steps, 5),
+            "median_query_ms_rank0": round(sorted(qt)[len(qt) // 2] * 1e3, 5),
+            "max_query_ms_rank0": round(max(qt) * 1e3, 5),
             "single_gpu_ms": round(single_ms, 5),
             "speedup_vs_single_gpu": round(single_ms / (dt * 1e3 / steps), 4),
             "gteps": m * steps / dt / 1e9,

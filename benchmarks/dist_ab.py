@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--queries", type=int, default=24)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out")
+    ap.add_argument("--slow-ms", type=float, default=0.0, help="also print every query slower than this (stats)")
     a = ap.parse_args()
     out = open(a.out, "a") if a.out else None
     eng = DistEngine(0, 1, 0, DistEngine.unique_id())
@@ -62,6 +63,11 @@ def main():
                     assert r.found and r.hops == h and len(r.path) == h + 1, (spec, s, d, r.hops, h)
                     dms.append(r.search_ms)
                     st.append(eng.last_stats)
+                    if a.slow_ms and qms[-1] > a.slow_ms:
+                        x = dict(st[-1])
+                        x.pop("trace", None)
+                        print(json.dumps({"slow_query": [s, d, h], "ms": round(qms[-1], 4),
+                                          "device_ms": round(r.search_ms, 4), "stats": x}), flush=True)
             rec = {
                 "spec": spec, "n": n, "spec_rounds": k, "solo_edges": solo_e, "queries": len(qms),
                 "build_ms": round(build_ms, 2),

@@ -35,7 +35,7 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                 nosync_bytes: Optional[int] = None, timeout_s: Optional[float] = None,
                 walk_max: Optional[int] = None, solo: Optional[bool] = None,
                 solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
-                overlap: Optional[bool] = None) -> "native.DistTuning":
+                overlap: Optional[bool] = None, spec_stall_edges: Optional[int] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
 
     solo (one rank only): run the small rounds in one persistent workgroup
@@ -53,7 +53,8 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
     t = native.DistTuning()
     for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
-                 ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap)):
+                 ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap),
+                 ("spec_stall_edges", spec_stall_edges)):
         if v is not None:
             setattr(t, k, v)
     return t

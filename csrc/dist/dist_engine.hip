@@ -738,7 +738,7 @@ __device__ void terminal_walk(const DView& V, unsigned long long key, const Poli
 // kernel ends the round's claims on this rank (one rank, no hub pass).
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
                                                           int flags, uint64_t hub_deg, int header, int finish,
-                                                          uint32_t ocap, int side0, int nsides) {
+                                                          uint32_t ocap, int side0, int nsides, uint32_t plan_cap) {
   const int p = it & 1;
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
@@ -756,7 +756,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   __syncthreads();
   if (threadIdx.x == 0) {
     reduce_gathered(V.P <= kStageRanks ? gst : V.redg[p ^ 1], V.P, rd);
-    plan_round(prev, rd, pol, cap, flags, c);
+    plan_round(prev, rd, pol, plan_cap, flags, c);
   }
   __syncthreads();
   const bool terminal = c.state == kDone || c.state == kDead;
@@ -2033,6 +2033,16 @@ struct DistBiBfs::Impl {
   // profiles/r2_dist_fintag_ab.txt).  An RCCL error reported by the
   // communicator, or no progress within timeout_s (a dead or hung peer leaves
   // our collective waiting forever), aborts the communicator and throws.
+  // Largest per-rank frontier (edges) a speculative round may expand before
+  // the plan stalls it for the host: one rank exchanges nothing, so nothing
+  // bounds it; more ranks' candidates (at most their frontier edges) must fit
+  // the spill lists.  DistTuning::spec_stall_edges lowers it (tests force
+  // host-planned rounds with it).
+  uint32_t round_edge_cap() const {
+    const uint32_t hard = size == 1 ? 0xFFFFFFFFu : V.spill_cap;
+    return tune.spec_stall_edges ? std::min<uint32_t>(tune.spec_stall_edges, hard) : hard;
+  }
+
   uint32_t next_tag() {
     fin_seq = fin_seq + 1 == 0 ? 1 : fin_seq + 1;
     return fin_seq;
@@ -2328,8 +2338,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       uint64_t need = 0;
       for (int s = 0; s < 2; ++s)
         if ((h.want >> s) & 1) need = std::max<uint64_t>(need, h.fmax[s]);
-      if (!host_only && h.stall == kStallCap && need <= spec_max) {
-        spec_cap = std::max<uint32_t>(spec_cap, next_pow2(need));
+      if (!host_only && h.stall == kStallCap && need <= round_edge_cap()) {
+        spec_cap = std::min<uint32_t>(spec_max, std::max<uint32_t>(spec_cap, next_pow2(need)));
         flags = kPlanResume;  // re-run the stalled plan speculatively with a bigger block
       } else {
         maybe_fault((int)it);
@@ -2381,7 +2391,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       if (P == 1) ocap = 0;  // nothing is ever offered
       else if (tune.owner_cap) ocap = tune.owner_cap;
       else if (!ocap) ocap = kOwnerCapMin;
-      ocap = std::min(ocap, cap_it);
+      ocap = std::min(std::min(ocap, cap_it), spec_max);  // (the buffers hold blocks of spec_max pairs)
       if ((uint64_t)(it - first) > 4ull * n + 16) break;  // safety net
       const unsigned bx = std::min<unsigned>((unsigned)cus * 2, cap_it / kThreads + 1);  // ~ this rank's edges
       const unsigned cx = std::min<unsigned>((unsigned)cus * 2,
@@ -2402,22 +2412,27 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       // expand as separate launches -- side 1 on the compute stream -- so
       // side 0's exchange runs while side 1 is still expanding.
       const uint64_t side_words = (uint64_t)P * block_words(ocap);
+      // The plan stalls a round whose per-rank frontier edges exceed this:
+      // with one rank nothing is exchanged, so nothing bounds a round; with
+      // more, a rank's candidates (at most its frontier edges) must fit the
+      // spill lists (owner blocks overflow into them).
+      const uint32_t plan_cap = round_edge_cap();
       const bool split = P > 1 && tune.overlap && !hubs;
       if (split) {
         HIP_CHECK(hipEventRecord(ev_round, cs));  // the previous round is complete on cs
         HIP_CHECK(hipStreamWaitEvent(stream, ev_round, 0));
         k_spec_expand<<<dim3(bx, 1), kThreads, 0, stream>>>(V, it, pol, cap_it, k == 0 ? flags : 0, kNoHubs, 1, 0,
-                                                            ocap, 1, 1);
+                                                            ocap, 1, 1, plan_cap);
         HIP_CHECK(hipEventRecord(ev_pre[1], stream));
         k_spec_expand<<<dim3(bx, 1), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0, kNoHubs, 1, 0,
-                                                        ocap, 0, 1);
+                                                        ocap, 0, 1, plan_cap);
         comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
         HIP_CHECK(hipStreamWaitEvent(cs, ev_pre[1], 0));
         comm->alltoall(V.sendbuf + side_words, V.recvbuf + side_words, peer_bytes, cs);
       } else {
         k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
                                                         hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap,
-                                                        0, 2);
+                                                        0, 2, plan_cap);
         if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap);
         if (P > 1) {
           comm->group_begin();

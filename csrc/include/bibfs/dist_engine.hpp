@@ -81,6 +81,8 @@ struct DistTuning {
   bool solo = true;                // one rank: small rounds in one persistent workgroup (k_spec_solo)
   uint32_t solo_edges = 2048;      // ... while every expanding side has at most this many frontier edges (<= 8192)
   uint32_t owner_cap = 0;          // > 1 rank: pairs per owner-addressed block (0 = predicted per round)
+  uint32_t spec_stall_edges = 0;   // a speculative round above this many per-rank frontier edges stalls for a
+                                   // host-planned round (0 = only when the spill lists could overflow)
   bool overlap = false;            // > 1 rank: lockstep rounds expand side 1 on the compute stream while side 0's
                                    // candidates are exchanged (off until measured on a multi-GPU node)
 };

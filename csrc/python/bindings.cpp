@@ -345,7 +345,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("solo", &DistTuning::solo)
       .def_readwrite("solo_edges", &DistTuning::solo_edges)
       .def_readwrite("owner_cap", &DistTuning::owner_cap)
-      .def_readwrite("overlap", &DistTuning::overlap);
+      .def_readwrite("overlap", &DistTuning::overlap)
+      .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges);
   py::class_<DistLocalFault>(m, "DistLocalFault")
       .def(py::init<>())
       .def_readwrite("rank", &DistLocalFault::rank)

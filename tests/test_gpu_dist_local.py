@@ -114,7 +114,7 @@ def test_tiny_capacities_force_count_sync_and_overflow(ranks):
     import torch  # noqa: F401
     from bidirectional_bfs_amd.parallel import make_tuning
 
-    tune = make_tuning(cap=4, nosync_bytes=0, spec_cap_max=1024)
+    tune = make_tuning(cap=4, nosync_bytes=0, spec_cap_max=1024, spec_stall_edges=1024)
     seen = {"host_rounds": 0, "count_syncs": 0, "overflow_levels": 0}
     for spec in ("kron:14:16:3", "gnp:20000::6"):
         g = bb.from_spec(spec)
@@ -176,7 +176,7 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
         for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False},
                    {"direction": "bottomup"}):
             for tune in (make_tuning(spec_rounds=spec_rounds), make_tuning(spec_rounds=spec_rounds, cap=4,
-                                                                          nosync_bytes=0),
+                                                                          nosync_bytes=0, spec_stall_edges=64),
                          make_tuning(spec_rounds=spec_rounds, owner_cap=2),
                          make_tuning(spec_rounds=spec_rounds, overlap=True, owner_cap=64)):
                 rs = dist_local_run(ranks, g, qs, tuning=tune, trace=True, **kw)
