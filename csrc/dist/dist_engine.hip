@@ -901,6 +901,31 @@ __device__ __forceinline__ unsigned long long solo_clock() {
   return t;
 }
 
+// The same prefix by ONE wave (32 entries per lane, one wave scan): no barrier.
+__device__ void solo_wave_scan(const uint32_t* ND, uint32_t* FP, uint32_t cnt, uint32_t lane) {
+  constexpr uint32_t kPer = kSoloV / kWave;
+  uint32_t run = 0;
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = lane * kPer + k;
+    run += i < cnt ? ND[i] : 0u;
+  }
+  uint32_t x = run;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  uint32_t e = x - run;
+  for (uint32_t k = 0; k < kPer; ++k) {
+    const uint32_t i = lane * kPer + k;
+    if (i < cnt) {
+      FP[i] = e;
+      e += ND[i];
+    }
+  }
+  if (lane == kWave - 1) FP[cnt < kSoloV ? cnt : kSoloV] = x;
+}
+
 template <bool kStamp>
 __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, Policy pol, uint32_t emax,
                                                          int seed, uint32_t seed_src, uint32_t seed_dst,
@@ -997,32 +1022,32 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
 
   uint32_t it = it0;
   SOLO_PH(6)
-  for (uint32_t r = 0; r < kSoloRounds; ++r, ++it) {
-    if (tid == 0) {
-      const unsigned long long ta = kStamp ? solo_clock() : 0;
-      plan_round(pc, rd, pol, emax, 0, c);  // a side above emax frontier edges: kStallCap
-      if (kStamp) ph[8] += solo_clock() - ta;
-      bool fits = true;
-      for (int sd = 0; sd < 2; ++sd)
-        if (((c.want >> sd) & 1) && (c.cnt[sd] > kSoloV || fnd[sd] - fbg[sd] > kSoloV)) fits = false;
-      if (c.state == kRun && !fits) {  // the multi-workgroup rounds take it from here
-        c.state = kStall;
-        c.stall = kStallCap;
-        c.sides = c.modes = 0;
-        c.einsp = pc.einsp;
-        c.sparse_levels = pc.sparse_levels;
-      }
-      go = c.state == kRun;
-      if (go) {
-        const unsigned long long tb = kStamp ? solo_clock() : 0;
-        publish(V, it & 1, pc, rd, c);
-        if (kStamp) ph[9] += solo_clock() - tb;
-        nf[0] = nf[1] = 0;
-        ne[0] = ne[1] = 0;
-        best = kNoKey;
-      }
+  // One lane plans round `it` (from pc / rd); stalls a round the solo
+  // workgroup cannot hold, and resets the round's LDS counters.
+  auto plan_next = [&](uint32_t it_) {
+    plan_round(pc, rd, pol, emax, 0, c);  // a side above emax frontier edges: kStallCap
+    bool fits = true;
+    for (int sd = 0; sd < 2; ++sd)
+      if (((c.want >> sd) & 1) && (c.cnt[sd] > kSoloV || fnd[sd] - fbg[sd] > kSoloV)) fits = false;
+    if (c.state == kRun && !fits) {  // the multi-workgroup rounds take it from here
+      c.state = kStall;
+      c.stall = kStallCap;
+      c.sides = c.modes = 0;
+      c.einsp = pc.einsp;
+      c.sparse_levels = pc.sparse_levels;
     }
-    solo_lds_barrier();  // LDS only: the plan's global stores (publish) need no wait
+    go = c.state == kRun;
+    if (go) {
+      publish(V, it_ & 1, pc, rd, c);
+      nf[0] = nf[1] = 0;
+      ne[0] = ne[1] = 0;
+      best = kNoKey;
+    }
+  };
+  constexpr uint32_t kPlanner = 2 * kWave;  // lane 0 of wave 2: plans while waves 0-1 scan
+  if (tid == kPlanner) plan_next(it);
+  solo_lds_barrier();
+  for (uint32_t r = 0; r < kSoloRounds; ++r, ++it) {
     SOLO_PH(0)
     if (!go) break;
     const uint32_t sides = c.sides;
@@ -1122,13 +1147,15 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       ph[4] += 1;
       ph[5] += E;
     }
-    // the next frontiers' degree prefix (an idle side's is rebuilt unchanged),
-    // then -- thread 0, behind the scan's barrier -- the round's bookkeeping;
-    // thread 0 plans the next round right after it (the post-plan barrier
-    // orders all of it for everyone)
-    const uint32_t cnt_next = ((sides >> half) & 1) ? nf[half] : fnd[half] - fbg[half];
-    solo_scan(ND[half], FP[half], min(cnt_next, kSoloV), tid % (kSoloT / 2), wtot[half]);
-    if (tid == 0) {
+    // The next frontiers' degree prefix -- wave 0 side 0, wave 1 side 1, no
+    // barrier inside (an idle side's prefix is rebuilt unchanged) -- while
+    // lane 0 of wave 2 does the round's bookkeeping and plans the next
+    // round; ONE LDS barrier orders all of it for everyone.
+    const uint32_t wid = tid / kWave;
+    if (wid < 2) {
+      const uint32_t cnt_next = ((sides >> wid) & 1) ? nf[wid] : fnd[wid] - fbg[wid];
+      solo_wave_scan(ND[wid], FP[wid], min(cnt_next, kSoloV), lane);
+    } else if (tid == kPlanner) {
       for (int sd = 0; sd < 2; ++sd) {
         const bool on = (sides >> sd) & 1;
         rd.sums[2 * sd] = on ? (unsigned long long)nf[sd] : 0ull;
@@ -1145,13 +1172,16 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       rd.spill[0] = rd.spill[1] = 0;
       rd.nocmax = ~0ull;
       pc = c;
+      plan_next(it + 1);
     }
+    solo_lds_barrier();
     SOLO_PH(3)
   }
   // ---- exit: the state a stalled speculative round leaves, or the end of the search
-  if (tid >= kWave) return;
+  const bool ended = c.state == kDone || c.state == kDead;
+  if (tid < kWave) {
   if (V.P == 1 && c.state == kDone && pol.want_path) terminal_walk(V, c.key, pol);  // wave 0
-  if (tid != 0) return;
+  if (tid == 0) {
   const int p = it & 1;
   DState* st = V.st;
   for (int sd = 0; sd < 2; ++sd) {
@@ -1189,6 +1219,23 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
 #undef SOLO_PH
   __threadfence_system();
   __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }  // tid == 0
+  }  // wave 0
+  // A search that ended here resets its own state after the host has its
+  // answer (no k_cleanup launch; the next search's launch queues behind this
+  // one): every vertex it claimed is in the queues.
+  // (not when the path outgrew the pinned buffer: k_walk_local still reads the depths)
+  if (!ended || (c.state == kDone && pol.want_path && 4 + (c.key >> 32) + 1 > pol.walk_cap)) return;
+  for (int sd = 0; sd < 2; ++sd) {
+    uint32_t* vis = pick(V.vis, sd);
+    uint32_t* dep = sd ? dep1 : dep0;
+    const uint32_t* q = sd ? que1 : que0;
+    for (uint32_t i = tid; i < qt[sd]; i += kSoloT) {
+      const uint32_t li = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - lo;
+      vis[2 * (li >> 5)] = 0u;
+      dep[li] = kEmpty;
+    }
+  }
 }
 
 // Edge-parallel expansion of the deferred hubs.  side >= 0: that side (a
@@ -2298,6 +2345,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   uint32_t it = 0;
   uint32_t spec_cap = kSpecCapMin;
   uint32_t ocap_last = 0;  // owner block capacity of the last speculative round
+  bool solo_cleaned = false;
   int flags = 0;
   bool have_ctl = false;  // h_ctl describes the current device state
   const int K = std::min<int>(std::max(0, tune.spec_rounds), (int)kPlanRing - 1);
@@ -2326,6 +2374,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     }
     have_ctl = true;
     stats.solo_rounds = (int)(h_ctl->rounds);
+    solo_cleaned = h_ctl->state == kDead ||
+                   (h_ctl->state == kDone && !(pol.want_path && 4 + (h_ctl->key >> 32) + 1 > pol.walk_cap));
     it = h_ctl->next_it;
     const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
     spec_cap = std::min(spec_max, std::max<uint32_t>(kSpecCapMin, next_pow2(4 * fm)));
@@ -2519,7 +2569,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     k_host_tag<<<1, 64, 0, cs>>>(h_fin, tag);
     HIP_CHECK(hipGetLastError());
   }
-  cleanup_enqueue(h);
+  if (!solo_cleaned) cleanup_enqueue(h);
   if (tag) {
     stats.host_syncs++;
     spin_tag(tag, cs);
