@@ -202,6 +202,21 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
   }
 }
 
+// The claimed vertices' first edges (the next round's records), fetched as
+// soon as the claims are known -- their latency overlaps the counts and the
+// round counter's atomic instead of stalling the place step.
+template <int NB>
+__device__ __forceinline__ void round_fetch(Work<NB>& W, int nb, const unsigned long long* __restrict__ tadj) {
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b >= nb) continue;
+    const uint32_t base = tw_base(W.rec[b]);
+#pragma unroll
+    for (uint32_t j = 0; j < kTinyUnroll; ++j)
+      if (j < W.deg[b]) W.nbw[b][j] = tadj[base + j];
+  }
+}
+
 // Per-lane and per-wave counts of the new vertices: queue slots from ballots,
 // record slots from ONE DPP scan of the degrees (side 0 [15:0], side 1 [31:16]).
 template <int NB>
@@ -242,16 +257,8 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
                                                 uint32_t* JQ, unsigned long long* JR, unsigned long long* meet) {
   uint32_t ovf = 0;
   uint32_t e0 = e0b + (K.ex & 0xffffu), e1 = e1b + (K.ex >> 16);
-  if (!kSpec) {  // the claimed vertices' first edges, fetched now
-#pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      if (b >= nb) continue;
-      const uint32_t base = tw_base(W.rec[b]);
-#pragma unroll
-      for (uint32_t j = 0; j < kTinyUnroll; ++j)
-        if (j < W.deg[b]) W.nbw[b][j] = tadj[base + j];
-    }
-  }
+  // (!kSpec: the claimed vertices' first edges were fetched by round_fetch,
+  // right after the claims, so their latency overlaps the counting)
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b >= nb) continue;
@@ -490,6 +497,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         const int nb = (wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
         Work<2> W;
         round_issue<2, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS);
+        if (!kSpecAll) round_fetch<2>(W, nb, P.tadj);
         Counts<2> K;
         round_count<2>(K, W);
         TINY_PH(3)
