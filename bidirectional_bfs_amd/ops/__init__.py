@@ -159,6 +159,16 @@ class HipEngine:
     def resident(self) -> bool:
         return self._e.resident
 
+    @property
+    def auto_handoff(self) -> bool:
+        """Resident searches enqueue their first grid level before they start,
+        gated on the device (no host round trip when a search leaves LDS)."""
+        return self._e.auto_handoff
+
+    @auto_handoff.setter
+    def auto_handoff(self, on: bool) -> None:
+        self._e.auto_handoff = bool(on)
+
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:
         self._e.begin(int(src), int(dst))

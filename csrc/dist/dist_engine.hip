@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -169,6 +170,10 @@ struct DView {
   uint32_t n, lo, hi, chunk;  // owned = [lo, hi); owner(v) = v / chunk
   const uint64_t* row_off;    // owned rows
   const uint32_t* col;        // global column ids
+  // One rank: packed adjacency {v, deg(v), row_off[v] lo, hi} per edge (16 B;
+  // when it fits DistTuning's budget), so a solo round's claims need no
+  // dependent row-offset load; nullptr = col + row_off.
+  const uint4* padj;
   // Visited bits of both sides interleaved: owned word w of side s is
   // vis[s][2 * w] (vis[1] = vis[0] + 1), so the 64-bit word w of vis[0]
   // holds side 0 in its low and side 1 in its high half -- a claim's one
@@ -432,8 +437,10 @@ struct ClaimMeet {
 // Claim owned vertex v for side s (parent u, depth dnew).  Wave-cooperative:
 // every lane of the wave calls it, `want` masks lanes.  One queue append and
 // one degree-sum atomic per wave.
+// have_row: the caller read v's row [prb, pre_) with v itself (packed adjacency).
 __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uint32_t v, uint32_t u,
-                                           uint32_t dnew, const ClaimMeet& cm = ClaimMeet{}) {
+                                           uint32_t dnew, const ClaimMeet& cm = ClaimMeet{}, bool have_row = false,
+                                           unsigned long long prb = 0, unsigned long long pre_ = 0) {
   const uint32_t li = v - V.lo;
   bool mine = false, other = false;
   unsigned long long best = kNoKey;
@@ -445,8 +452,8 @@ __device__ __forceinline__ void wave_claim(const DView& V, int s, bool want, uin
       // both sides' bits in one word: the claim returns the other side's too;
       // of two same-round claims of v the later atomic sees the earlier
       const unsigned long long old = atomicOr(w, m);
-      rb = V.row_off[li];  // the degree, fetched beside the claim (independent of its result)
-      re = V.row_off[li + 1];
+      rb = have_row ? prb : V.row_off[li];  // the degree, fetched beside the claim (independent of its result)
+      re = have_row ? pre_ : V.row_off[li + 1];
       mine = !(old & m);
       other = (old >> ((li & 31) + 32 * (s ^ 1))) & 1ull;
     }
@@ -614,6 +621,7 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
       const unsigned long long e = base + tid;
       const bool valid = e < tot;
       uint32_t uu = 0, v = 0;
+      unsigned long long prb = 0, pre_ = 0;
       if (valid) {
         uint32_t a = 0, z = kThreads;  // last slot whose edge range starts at or before e
         while (z - a > 1) {
@@ -622,10 +630,18 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
           else z = mid;
         }
         uu = su[a];
-        v = V.col[sb[a] + (e - se[a])];
+        const unsigned long long k = sb[a] + (e - se[a]);
+        if (V.padj) {  // one rank: the neighbour's row comes with its id
+          const uint4 q = V.padj[k];
+          v = q.x;
+          prb = (unsigned long long)q.z | (unsigned long long)q.w << 32;
+          pre_ = prb + q.y;
+        } else {
+          v = V.col[k];
+        }
       }
       const bool own = valid && v >= V.lo && v < V.hi;
-      wave_claim(V, s, own, v, uu, dnew, cm);
+      wave_claim(V, s, own, v, uu, dnew, cm, V.padj != nullptr, prb, pre_);
       wave_emit(V, s, valid && !own, v, uu, pairs, cap, oe);
     }
     __syncthreads();
@@ -951,6 +967,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
   // member would be a vector load from the kernel arguments per use)
   const uint32_t* const col = V.col;
   const uint64_t* const row_off = V.row_off;
+  const uint4* const padj = V.padj;
   unsigned long long* const visw = reinterpret_cast<unsigned long long*>(V.vis[0]);  // both sides per word
   uint32_t* const par0 = V.parent[0];
   uint32_t* const par1 = V.parent[1];
@@ -1080,8 +1097,20 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
         uu[j] = FV[b][sd][a];
         ad[j] = FB[b][sd][a] + (k - FP[sd][a]);
       }
+      unsigned long long pb[kSoloU];
+      uint32_t pd[kSoloU];
+      if (padj) {  // kernel argument: uniform
 #pragma unroll
-      for (int j = 0; j < kSoloU; ++j) vv[j] = col[ok[j] ? ad[j] : 0ull];  // an idle slot reads a valid word
+        for (int j = 0; j < kSoloU; ++j) {
+          const uint4 q = padj[ok[j] ? ad[j] : 0ull];  // an idle slot reads a valid entry
+          vv[j] = q.x;
+          pd[j] = q.y;
+          pb[j] = (unsigned long long)q.z | (unsigned long long)q.w << 32;
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < kSoloU; ++j) vv[j] = col[ok[j] ? ad[j] : 0ull];  // an idle slot reads a valid word
+      }
 #pragma unroll
       for (int j = 0; j < kSoloU; ++j) vv[j] = ok[j] ? vv[j] : lo;
       // claims: one CU, so the atomics are performed in its L2 (workgroup
@@ -1095,8 +1124,13 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
         unsigned long long* w = visw + (li >> 5);
         const bool claim = ok[j] && (!pre || !(*w & m));  // a stale L1 word only misses bits: safe
         old[j] = claim ? __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : m;
-        rb[j] = claim ? row_off[li] : 0ull;
-        re[j] = claim ? row_off[li + 1] : 0ull;
+        if (padj) {  // the row came with the neighbour id
+          rb[j] = claim ? pb[j] : 0ull;
+          re[j] = claim ? pb[j] + pd[j] : 0ull;
+        } else {
+          rb[j] = claim ? row_off[li] : 0ull;
+          re[j] = claim ? row_off[li + 1] : 0ull;
+        }
       }
 #pragma unroll
       for (int j = 0; j < kSoloU; ++j) {
@@ -1864,6 +1898,7 @@ struct DistBiBfs::Impl {
   uint64_t m_input = 0, nnz = 0;
   uint64_t* d_row_off = nullptr;
   uint32_t* d_col = nullptr;
+  uint4* d_padj = nullptr;  // one rank: packed adjacency (DView::padj)
   void* state = nullptr;
   uint32_t* sent_base = nullptr;  // both sides' sent bitmaps, contiguous (one memset)
   DView V{};
@@ -1935,9 +1970,11 @@ struct DistBiBfs::Impl {
   void free_all() {
     if (d_row_off) HIP_CHECK(hipFree(d_row_off));
     if (d_col) HIP_CHECK(hipFree(d_col));
+    if (d_padj) HIP_CHECK(hipFree(d_padj));
     if (state) HIP_CHECK(hipFree(state));
     d_row_off = nullptr;
     d_col = nullptr;
+    d_padj = nullptr;
     state = nullptr;
     n = 0;
   }
@@ -2038,6 +2075,19 @@ struct DistBiBfs::Impl {
   uint64_t max_deg = 0;
   void finish_build() {
     alloc_state();
+    // One rank owns every row: the packed adjacency of the single-GPU engine
+    // (16 B per edge) within BIBFS_PADJ_MAX_MB (default 4096 MiB, 0 = off).
+    V.padj = nullptr;
+    if (size == 1 && lo == 0 && nnz) {
+      const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
+      const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
+      if (nnz * 16 <= budget) {
+        HIP_CHECK(hipMalloc(&d_padj, nnz * 16));
+        launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
+        HIP_CHECK(hipStreamSynchronize(stream));
+        V.padj = d_padj;
+      }
+    }
     double y = (double)launch::max_degree(d_row_off, hi - lo, stream);
     if (size > 1) {
       HIP_CHECK(hipMemcpyAsync(d_scalar, &y, 8, hipMemcpyHostToDevice, cstream));

@@ -181,6 +181,12 @@ struct SearchBuffers {
   dev::LevelTraceDev* trace;
   uint32_t trace_cap;
   uint32_t words;       // n/32 + 1
+  // Device hand-off words (resident searches, grid_auto): [0..1] gate = 64-bit
+  // {handed off (0/1), seq} the LDS engine stores (agent scope, after its
+  // release) when a search leaves it; [2..6] the auto level's plan (k_handoff)
+  // for the kernels behind it.
+  uint32_t* aux;
+  uint32_t* hdump;      // raw LDS hash tables of a hash-set search's hand-off (handoff_dump_bytes())
 };
 
 struct HostSide {
@@ -260,6 +266,10 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
                   uint64_t frontier_edges, dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
                   uint32_t hub_deg, hipStream_t s);
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s);
+// Behind a hash-set LDS search's hand-off (n > 2^17): scatter the dumped hash
+// tables into the global visited bitmaps, grid-wide (grid_auto does it itself).
+void handoff_scatter(const GraphView& g, const SearchBuffers& b, hipStream_t s);
+size_t handoff_dump_bytes();
 void build_frontier_bits(const GraphView& g, const SearchBuffers& b, int side, hipStream_t s);
 void finish_level(const SearchBuffers& b, int side, int mode, int trace, dev::DevState* mirror, uint32_t seq,
                   const HostSide& h, uint32_t res_seq, uint32_t n, hipStream_t s);
@@ -267,8 +277,20 @@ uint32_t grid_hub_degree();
 void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
                uint32_t n, hipStream_t s);
+// if_done: 0 = always; 1 = only once a grid level ended the search; 2 = and
+// only behind an auto level that ran (aux[2] active)
 void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
-             bool if_done, hipStream_t s);
+             int if_done, hipStream_t s);
+// Device hand-off: one top-down level enqueued BEFORE the resident LDS search
+// it continues.  Its workgroups wait on the gate (aux) for search `gate_seq`
+// to leave LDS, plan the level on the device (side, hub degree, chunk size:
+// the host rules of grid_level), run it and finish it like grid_topdown
+// (mirror `seq`, result `res_seq`); a search that ended in LDS, or a first
+// level the Beamer rule sends bottom-up, makes it a no-op (the latter
+// publishes the mirror unchanged, so the host loop takes that level).
+void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
+               dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
+               hipStream_t s);
 
 }  // namespace launch
 }  // namespace bibfs

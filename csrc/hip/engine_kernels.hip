@@ -306,6 +306,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   __shared__ LevelPlan plan;
   __shared__ uint32_t won;
   __shared__ Rec junk[kWave];            // record writes of finished lanes land here (no divergence)
+  __shared__ __attribute__((aligned(16))) uint32_t pub_img[64];  // hand-off DevState [0, 32) / HostResult [32, 64) images
 
   const int tid = threadIdx.x;
   const int wid = kWidUniform ? (int)__builtin_amdgcn_readfirstlane((uint32_t)tid >> 6) : tid >> 6;
@@ -318,6 +319,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   // (~1.6k cycles) is only resolved after the block-private initialisation
   // below; a losing candidate's few global writes there are idempotent.
   unsigned long long e0 = 0, e1 = 0, e3 = 0, e4 = 0;  // kStamp: entry / elected / loop end / walked
+  unsigned long long e5 = 0, e6 = 0, e7 = 0, e8 = 0;  // kStamp: publish split
   if (kStamp && tid == 0) e0 = __builtin_amdgcn_s_memtime();
   const bool cand = elected || (P.pin_xcc < 0 ? blockIdx.x == 0 : xcc_id() == (uint32_t)P.pin_xcc);
   if (!cand) return;  // block-uniform
@@ -1157,65 +1159,63 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         __hip_atomic_store(&P.h.path[i], pbuf[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     if (kStamp && tid == 0) e4 = __builtin_amdgcn_s_memtime();
-    if (status == kHandoff && tid == 0 && !P.batch) {
-      DevState* st = P.b.st;
-      st->status = kRunning;
-      st->meet = kEmpty;
-      st->meet_side = 0;
-      st->levels = levels;
-      st->hub_count = 0;
-      st->chunk = 0;
-      st->hub_edge_cursor = 0;
-      st->nedges = 0;
-      st->einsp = einsp;
-      for (int q = 0; q < 2; ++q) {
-        const SideState x = sel(q, s0, s1);
-        st->depth[q] = x.depth;
-        st->fbeg[q] = x.fbeg;
-        st->fend[q] = x.qend;
-        st->qtail[q] = x.qend;
-        st->fedges[q] = x.fed;
-        st->vedges[q] = x.ved;
-      }
-      if (DevState* m = P.h.state) {  // the host continues from this mirror: no copy + sync
-        auto put = [](auto* p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-        put(&m->status, (uint32_t)kRunning);
-        put(&m->meet, kEmpty);
-        put(&m->meet_side, 0u);
-        put(&m->levels, levels);
-        put(&m->hub_count, 0u);
-        put(&m->chunk, 0u);
-        put(&m->nedges, 0ull);
-        put(&m->einsp, einsp);
-        put(&m->pad[1], 0u);
+    // Hand-off state and result record: lane 0 builds both images in LDS, then
+    // every lane stores one word -- one store instruction per record instead of
+    // ~30 serial single-lane stores (~4k cycles of a 10M hand-off).
+    const bool hand = status == kHandoff && !P.batch;
+    constexpr uint32_t kStW = (uint32_t)(sizeof(DevState) / 4), kMirW = (uint32_t)(offsetof(DevState, pad) / 4);
+    constexpr uint32_t kResW = (uint32_t)(offsetof(HostResult, rt_pickup) / 4);
+    static_assert(kStW <= 32 && kResW <= 32, "one lane per word");
+    if (lane == 0) {
+      DevState& sv = *reinterpret_cast<DevState*>(&pub_img[0]);
+      if (hand) {
+        sv = DevState{};
+        sv.status = kRunning;
+        sv.meet = kEmpty;
+        sv.levels = levels;
+        sv.einsp = einsp;
         for (int q = 0; q < 2; ++q) {
           const SideState x = sel(q, s0, s1);
-          put(&m->depth[q], (int32_t)x.depth);
-          put(&m->fbeg[q], x.fbeg);
-          put(&m->fend[q], x.qend);
-          put(&m->qtail[q], x.qend);
-          put(&m->fedges[q], x.fed);
-          put(&m->vedges[q], x.ved);
+          sv.depth[q] = x.depth;
+          sv.fbeg[q] = x.fbeg;
+          sv.fend[q] = x.qend;
+          sv.qtail[q] = x.qend;
+          sv.fedges[q] = x.fed;
+          sv.vedges[q] = x.ved;
         }
       }
+      HostResult& rv = *reinterpret_cast<HostResult*>(&pub_img[32]);
+      rv.status = status;
+      rv.hops = status == kFound ? (int32_t)hops : -1;
+      rv.meet = meet;
+      rv.levels = levels;
+      rv.lds_levels = levels;
+      rv.visited = s0.hcnt + s1.hcnt;
+      rv.einsp = einsp;
+      rv.depth[0] = status == kFound ? (int32_t)md0 : s0.depth;
+      rv.depth[1] = status == kFound ? (int32_t)md1 : s1.depth;
+      rv.path_len = path_len;
+      rv.path_on_device = path_dev ? 1u : path_skip ? 2u : 0u;
+      rv.rt_begin = rt0;
+      rv.rt_end = __builtin_amdgcn_s_memrealtime();
     }
-    if (tid == 0) {  // write-through (system-scope) stores: no L2 writeback needed for the host
-      auto put = [](auto* p, auto v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); };
-      put(&Rr->status, status);
-      put(&Rr->hops, status == kFound ? (int32_t)hops : -1);
-      put(&Rr->meet, meet);
-      put(&Rr->levels, levels);
-      put(&Rr->lds_levels, levels);
-      put(&Rr->visited, s0.hcnt + s1.hcnt);
-      put(&Rr->einsp, einsp);
-      put(&Rr->depth[0], status == kFound ? (int32_t)md0 : s0.depth);
-      put(&Rr->depth[1], status == kFound ? (int32_t)md1 : s1.depth);
-      put(&Rr->path_len, path_len);
-      put(&Rr->path_on_device, path_dev ? 1u : path_skip ? 2u : 0u);
-      put(&Rr->rt_begin, rt0);
-      put(&Rr->rt_end, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same wave: lane 0's LDS writes precede the reads
+    if (hand && lane < kStW) {
+      const uint32_t w = pub_img[lane];
+      reinterpret_cast<uint32_t*>(P.b.st)[lane] = w;  // pad included: zero (done counter, gate words elsewhere)
+      // the host continues from this mirror (no copy + sync); pad[0] is the
+      // mirror's seq and stays, pad[1] (the level done counter) is cleared
+      if (DevState* m = P.h.state; m && (lane < kMirW || lane == kMirW + 1))
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(m) + lane, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (kStamp && tid == 0) e5 = __builtin_amdgcn_s_memtime();
+    // write-through (system-scope) stores: no L2 writeback needed for the host;
+    // seq (word 0) is written last, below
+    if (lane >= 1 && lane < kResW && lane != offsetof(HostResult, pad) / 4)
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(Rr) + lane, pub_img[32 + lane], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  if (kStamp && tid == 0) e6 = __builtin_amdgcn_s_memtime();
   if (fstatus == kHandoff && !P.batch) {
     // Materialise the LDS visited sets as global bitmaps for the grid engine.
     if constexpr (kBm) {
@@ -1227,17 +1227,19 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         (q ? P.b.vis[1] : P.b.vis[0])[wi] = (uint32_t)w | (uint32_t)(w >> 32);
       }
     } else {
-      for (uint32_t i = tid; i < 2 * kHashSize; i += kLdsThreads) {
-        const uint32_t k = Hflat[i];
-        if (k != kEmpty) {
-          const uint32_t v = k & kIdMask;
-          atomicOr(&((i >> kHashBits) ? P.b.vis[1] : P.b.vis[0])[v >> 5], 1u << (v & 31));
-        }
-      }
+      // The raw hash tables, coalesced; the whole grid scatters them into the
+      // bitmaps (k_handoff_scatter).  Scattering them here -- ~10^4 atomics on
+      // distinct lines from ONE CU at ~1 line per cycle -- cost ~7 us of a 10M
+      // hand-off.
+      const uint4* h4 = reinterpret_cast<const uint4*>(Hflat);
+      uint4* d4 = reinterpret_cast<uint4*>(P.b.hdump);
+      for (uint32_t i = tid; i < 2 * kHashSize / 4; i += kLdsThreads) d4[i] = h4[i];
     }
   }
+  if (kStamp && tid == 0) e7 = __builtin_amdgcn_s_memtime();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();  // every wave's path / state / bitmap stores drained before publishing
+  if (kStamp && tid == 0) e8 = __builtin_amdgcn_s_memtime();
   if (tid == 0) {
     // Device-memory results (hand-off state and bitmaps, an over-long path)
     // are read next by kernels / copies that may run on other XCDs: write
@@ -1252,8 +1254,24 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       t.depth = (uint32_t)(clk0 - e1);
       t.frontier = (uint32_t)(e4 - e3);
       t.mode = (uint32_t)(__builtin_amdgcn_s_memtime() - e4);
+      if (P.b.trace_cap > 3) {  // publish split: state / result puts / bitmaps issued / drained / fence
+        LevelTraceDev& u = P.b.trace[P.b.trace_cap - 3];
+        u.side = (uint32_t)(e5 - e4);
+        u.depth = (uint32_t)(e6 - e5);
+        u.frontier = (uint32_t)(e7 - e6);
+        u.mode = (uint32_t)(e8 - e7);
+        u.edges = __builtin_amdgcn_s_memtime() - e8;
+      }
     }
     __hip_atomic_store(&Rr->seq, P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (!P.batch) {
+      // the gate of an auto level enqueued behind this search (grid_auto):
+      // {handed off, seq}, behind the hand-off state's release above
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.b.aux),
+                         ((unsigned long long)P.seq << 32) | (fstatus == kHandoff ? 1ull : 0ull), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if constexpr (kLq && kBm) {
     if (P.resident) {
@@ -1453,6 +1471,15 @@ struct GridParams {
   uint32_t res_seq;
   uint32_t hub_deg;    // frontier vertices above this degree go to k_grid_hubs (~0u: never)
   uint32_t chunk_v;    // k_grid_topdown: frontier vertices per chunk ticket (<= kGridThreads)
+  // auto level (grid_auto): the gate's search seq, the CU count and the graph
+  // facts the device-side plan needs
+  uint32_t gate_seq;
+  uint32_t cus;
+  unsigned long long max_deg;
+  unsigned long long nnz;
+  float alpha;
+  uint32_t nparts;     // workgroups taking part in the level (0 = gridDim.x); the rest exit at once
+  uint32_t fbase, fcount;  // auto level: the frontier, from the plan (0/0 = read DevState)
 };
 
 template <typename OffT>
@@ -1491,8 +1518,127 @@ __device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid
   if (lane == leader) atomicAdd(&st->nedges, dsum);
 }
 
+// Hand-off kernel: the first kernel behind an LDS search that left LDS.
+//  * gated (grid_auto: enqueued before the search started): wave 0 of every
+//    workgroup waits for the gate -- search `gate_seq` has left LDS -- with
+//    relaxed agent-scope polls and s_sleep, then one agent acquire (the
+//    hand-off state was released by the LDS engine before the gate); block 0
+//    plans the auto level from DevState with the host's rules (grid_level /
+//    choose_side / choose_mode: the side with fewer frontier edges, declined
+//    when the Beamer rule wants bottom-up, hub degree, chunk size) into aux
+//    for the kernels behind it; a declined level publishes the host mirror
+//    unchanged, so the host loop takes it over.
+//  * hash-set searches (n > kBmMaxN): the LDS engine dumped its raw hash
+//    tables (coalesced); every thread scatters one slot into the global
+//    visited bitmaps (a single CU issuing them cost ~7 us on 10M G(n, p)).
+constexpr unsigned long long kGateTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+constexpr int kHandoffBlocks = 64;  // x kGridThreads = 2 * kHashSize: one slot per thread
+static_assert(kHandoffBlocks * kGridThreads == 2 * kHashSize, "one hash slot per thread");
 template <typename OffT>
+__global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, int gated, int scatter) {
+  __shared__ uint32_t shand;
+  DevState* st = P.b.st;
+  if (gated) {
+    if (threadIdx.x < kWave) {  // wave 0, uniformly
+      const uint32_t lane = threadIdx.x;
+      const unsigned long long* gate = reinterpret_cast<const unsigned long long*>(P.b.aux);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned long long g = 0;
+      bool seen = false;
+      for (;;) {
+        g = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
+            __builtin_amdgcn_readfirstlane((uint32_t)g);
+        if ((uint32_t)(g >> 32) == P.gate_seq) {
+          seen = true;
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) break;
+        __builtin_amdgcn_s_sleep(8);  // ~0.2 us: the pollers must not crowd the LDS search's memory
+      }
+      const bool hand = seen && (uint32_t)g == 1u;
+      if (hand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (blockIdx.x == 0) {
+        uint32_t active = hand, side = 0, hub = ~0u, cv = kGridThreads, fb = 0, F = 0;
+        bool declined = false;
+        if (hand) {
+          // the whole DevState in one round trip: lane i loads word i
+          constexpr uint32_t kW = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
+          const uint32_t w = lane < kW ? load_agent(reinterpret_cast<const uint32_t*>(st) + lane) : 0u;
+          auto word = [&](const void* field) {
+            return (uint32_t)__builtin_amdgcn_readlane(
+                (int)w, (int)((reinterpret_cast<const char*>(field) - reinterpret_cast<const char*>(st)) / 4));
+          };
+          auto dword = [&](const unsigned long long* field) {
+            return (unsigned long long)word(field) |
+                   (unsigned long long)word(reinterpret_cast<const uint32_t*>(field) + 1) << 32;
+          };
+          const unsigned long long fe0 = dword(&st->fedges[0]), fe1 = dword(&st->fedges[1]);
+          side = fe0 <= fe1 ? 0u : 1u;
+          const unsigned long long fe = side ? fe1 : fe0;
+          const double m_u = (double)P.nnz - (double)(side ? dword(&st->vedges[1]) : dword(&st->vedges[0]));
+          fb = side ? word(&st->fbeg[1]) : word(&st->fbeg[0]);
+          F = (side ? word(&st->fend[1]) : word(&st->fend[0])) - fb;
+          if ((double)fe > m_u / (double)P.alpha) {
+            active = 0;
+            declined = true;
+          } else {
+            if (P.max_deg > kHubDegree && fe > kHubDegree) hub = kHubDegree;
+            if (F <= 4096 && fe > 16384 && P.max_deg > 64) hub = 64;
+            if ((F + kGridThreads - 1) / kGridThreads < P.cus * 4u && fe > 0)
+              cv = (uint32_t)min<uint64_t>(kGridThreads, max<uint64_t>(kGridChunkMin, kGridThreads * (uint64_t)F / fe));
+          }
+        }
+        if (lane == 0) {
+          // the plan for the kernels behind: [2] bit 0 active, bit 1 side;
+          // [3] frontier size; [4] hub degree; [5] chunk size; [6] frontier base
+          P.b.aux[2] = active | side << 1;
+          P.b.aux[3] = F;
+          P.b.aux[4] = hub;
+          P.b.aux[5] = cv;
+          P.b.aux[6] = fb;
+          if (declined && P.mirror)
+            __hip_atomic_store(&P.mirror->pad[0], P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      if (lane == 0) shand = hand;
+    }
+    __syncthreads();
+    if (!__builtin_amdgcn_readfirstlane(shand)) return;
+  }
+  if (scatter) {
+    const uint32_t i = blockIdx.x * kGridThreads + threadIdx.x;
+    const uint32_t k = P.b.hdump[i];
+    if (k != kEmpty) {
+      const uint32_t v = k & kIdMask;
+      atomicOr(&(i >= kHashSize ? P.b.vis[1] : P.b.vis[0])[v >> 5], 1u << (v & 31));
+    }
+  }
+}
+
+// Auto level (grid_auto): the plan k_handoff left in aux (written by the
+// kernel before: plain loads).  false = no level to run, or this workgroup is
+// beyond the level's chunk count (the host's launch size) -- it leaves before
+// any ticket or done-counter atomic.
+template <typename OffT>
+__device__ bool auto_plan(GridParams<OffT>& P) {
+  const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
+  if (!(xp & 1u)) return false;
+  P.side = (int)((xp >> 1) & 1u);
+  P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
+  P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
+  P.chunk_v = __builtin_amdgcn_readfirstlane(P.b.aux[5]);
+  P.fbase = __builtin_amdgcn_readfirstlane(P.b.aux[6]);
+  const uint32_t chunks = (P.fcount + P.chunk_v - 1) / P.chunk_v;
+  P.nparts = max(1u, min(gridDim.x, chunks));
+  return blockIdx.x < P.nparts;
+}
+
+template <typename OffT, bool kAuto = false>
 __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> P) {
+  if constexpr (kAuto) {
+    if (!auto_plan(P)) return;
+  }
   __shared__ uint32_t sv[kGridThreads];
   __shared__ OffT sb[kGridThreads];
   __shared__ uint32_t sEb[kGridThreads];
@@ -1501,8 +1647,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
   const int s = P.side;
   DevState* st = P.b.st;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint32_t fbase = st->fbeg[s];
-  const uint32_t F = st->fend[s] - fbase;
+  const uint32_t fbase = kAuto ? P.fbase : st->fbeg[s];
+  const uint32_t F = kAuto ? P.fcount : st->fend[s] - fbase;
   for (;;) {
     if (tid == 0) schunk = (load_agent(&st->meet) != kEmpty) ? kEmpty : atomicAdd(&st->chunk, 1u);
     __syncthreads();
@@ -1579,13 +1725,22 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
 // a no-op when that level deferred nothing (its finisher reset hub_count),
 // otherwise its last workgroup finishes the level.
 constexpr int kHubTile = 1024;
-template <typename OffT>
+template <typename OffT, bool kAuto = false>
 __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) {
   __shared__ uint32_t hu[kHubTile];
   __shared__ OffT hb[kHubTile];
   __shared__ unsigned long long hp[kHubTile + 1];
   __shared__ unsigned long long wsum[kGridThreads / kWave];
   DevState* st = P.b.st;
+  if constexpr (kAuto) {  // behind an auto level: its plan (written by the kernel before)
+    const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
+    if (!(xp & 1u)) return;
+    P.side = (int)((xp >> 1) & 1u);
+    P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
+    // the host's hub launch size: 4 workgroups per frontier vertex
+    P.nparts = max(1u, min(gridDim.x, 4u * __builtin_amdgcn_readfirstlane(P.b.aux[3])));
+    if (blockIdx.x >= P.nparts) return;
+  }
   const uint32_t H = st->hub_count;
   if (H == 0) return;  // grid-uniform: the top-down finisher completed the level
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -1629,7 +1784,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
     __syncthreads();
     uint32_t it = 0;
     for (unsigned long long base = (unsigned long long)blockIdx.x * kGridThreads; base < tot;
-         base += (unsigned long long)gridDim.x * kGridThreads, ++it) {
+         base += (unsigned long long)(P.nparts ? P.nparts : gridDim.x) * kGridThreads, ++it) {
       if (it > 0 && (it & kMeetCheckMask) == kMeetCheckMask &&
           __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty)
         break;
@@ -1862,7 +2017,8 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   const uint32_t tid = threadIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's atomics and sc1 stores have completed
   __syncthreads();
-  if (tid == 0) slast = atomicAdd(&b.st->pad[1], 1u) == gridDim.x - 1;
+  const uint32_t parts = P.nparts ? P.nparts : gridDim.x;
+  if (tid == 0) slast = atomicAdd(&b.st->pad[1], 1u) == parts - 1;
   __syncthreads();
   if (!__builtin_amdgcn_readfirstlane(slast)) return;
   uint32_t* w = reinterpret_cast<uint32_t*>(b.st);
@@ -1955,6 +2111,7 @@ __global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t 
 __global__ void k_cleanup(launch::SearchBuffers b, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
                           int if_done) {
   const DevState* st = b.st;
+  if (if_done == 2 && !(load_agent(&b.aux[2]) & 1u)) return;   // no auto level ran (grid-uniform)
   if (if_done && load_agent(&st->status) == kRunning) return;  // grid-uniform
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (((uint64_t)st->qtail[0] + st->qtail[1]) * 32 > b.words) {
@@ -1972,8 +2129,15 @@ __global__ void k_cleanup(launch::SearchBuffers b, uint32_t* done_ctr, uint32_t*
       for (uint64_t i = t0; i < q; i += stride) b.vis[s][b.queue[s][i] >> 5] = 0u;
     }
   }
-  __threadfence();  // this thread's clears are device-visible before the block counts itself done
+  // every wave's clears drained, then ONE agent release per workgroup (a
+  // __threadfence() in every thread was a write-back + invalidate per lane:
+  // ~20 us of a 10M cleanup) before the block counts itself done
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
   if (threadIdx.x == 0 && atomicAdd(done_ctr, 1u) == gridDim.x - 1) {
     *done_ctr = 0;
     __threadfence_system();
@@ -2005,6 +2169,13 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.res_seq = 0;
   P.hub_deg = kHubDegree;
   P.chunk_v = kGridThreads;
+  P.gate_seq = 0;
+  P.cus = 0;
+  P.max_deg = 0;
+  P.nnz = g.nnz;
+  P.alpha = 14.0f;
+  P.nparts = 0;
+  P.fbase = P.fcount = 0;
   return P;
 }
 
@@ -2119,6 +2290,42 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   HIP_CHECK(hipGetLastError());
 }
 
+void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
+               dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
+               hipStream_t s) {
+  // The grid size is fixed before the frontier exists: cus / 4 workgroups
+  // (a 10M G(n, p) hand-off level is ~17 chunks; every workgroup takes chunk
+  // tickets, and fewer blocks keep the ticket and done counters cheap).  The
+  // hub pass behind is enqueued only when the graph has a vertex above 64.
+  const unsigned blocks = (unsigned)std::max(8, cus / 4);
+  const unsigned hblocks = (unsigned)std::max(8, cus);
+  const int scatter = g.n > kBmMaxN ? 1 : 0;
+  auto launch_one = [&](auto P) {
+    using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
+    P.mirror = mirror, P.seq = seq, P.trace = 0, P.h = h, P.res_seq = res_seq;
+    P.gate_seq = gate_seq;
+    P.cus = (uint32_t)cus;
+    P.max_deg = max_deg;
+    P.nnz = g.nnz;
+    P.alpha = (float)alpha;
+    k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
+    k_grid_topdown<OffT, true><<<blocks, kGridThreads, 0, s>>>(P);
+    if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
+  };
+  if (g.row_off32) launch_one(gp<uint32_t>(g, b, 0));
+  else launch_one(gp<uint64_t>(g, b, 0));
+  HIP_CHECK(hipGetLastError());
+}
+
+void handoff_scatter(const GraphView& g, const SearchBuffers& b, hipStream_t s) {
+  if (g.n <= kBmMaxN) return;  // bitmap-mode searches copied their bitmaps themselves
+  if (g.row_off32) k_handoff<uint32_t><<<kHandoffBlocks, kGridThreads, 0, s>>>(gp<uint32_t>(g, b, 0), 0, 1);
+  else k_handoff<uint64_t><<<kHandoffBlocks, kGridThreads, 0, s>>>(gp<uint64_t>(g, b, 0), 0, 1);
+  HIP_CHECK(hipGetLastError());
+}
+
+size_t handoff_dump_bytes() { return 2 * kHashSize * sizeof(uint32_t); }
+
 void grid_bottomup(const GraphView& g, const SearchBuffers& b, int side, int cus, hipStream_t s) {
   const uint64_t waves = ((uint64_t)g.n + 63) / 64;
   uint64_t blocks = (waves + 3) / 4;
@@ -2163,9 +2370,9 @@ void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t
 }
 
 void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
-             bool if_done, hipStream_t s) {
+             int if_done, hipStream_t s) {
   (void)n;
-  k_cleanup<<<64, 1024, 0, s>>>(b, done_ctr, host_tag, tag, if_done ? 1 : 0);  // few blocks: one done-counter atomic each
+  k_cleanup<<<64, 1024, 0, s>>>(b, done_ctr, host_tag, tag, if_done);  // few blocks: one done-counter atomic each
   HIP_CHECK(hipGetLastError());
 }
 

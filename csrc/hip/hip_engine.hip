@@ -62,12 +62,47 @@ struct HipBiBfs::Impl {
   uint32_t clean_tag[2] = {0, 0};  // last cleanup enqueued on each set
   bool grid_cleaned = false;  // the search's last grid level enqueued the cleanup that ran
 
+  // Device hand-off (grid_auto): on by default for resident searches of
+  // graphs the general server takes, with the default level policy;
+  // BIBFS_AUTO_HANDOFF=0 turns it off (A/B).
+  bool auto_on = [] {
+    const char* e = std::getenv("BIBFS_AUTO_HANDOFF");
+    return !(e && e[0] == '0');
+  }();
+  bool auto_usable(const SearchOptions& opt) const {
+    return auto_on && nnz > 0 && !opt.trace && !opt.force_grid && opt.direction == Direction::kAuto &&
+           opt.side == SidePolicy::kSmallerEdges;
+  }
+  // After an auto level's search handed off: wait for the auto level's result
+  // (true) or its mirror publish (false: the search continues on the host).
+  bool wait_auto(uint32_t pub, uint32_t ls) {
+    for (uint64_t it = 1;; ++it) {
+      if (__atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub) return true;
+      if (__atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) == ls) {
+        return __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub;
+      }
+      if ((it & 8191) == 0) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess && __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) != pub &&
+            __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != ls)
+          throw Error("bibfs: auto grid level finished without publishing");
+        if (e != hipSuccess && e != hipErrorNotReady)
+          throw Error(std::string("bibfs: auto grid level failed: ") + hipGetErrorString(e));
+      } else {
+        _mm_pause();
+      }
+    }
+  }
+  uint32_t next_clean_tag() {
+    clean_seq = clean_seq + 1 == 0 ? 1 : clean_seq + 1;
+    return clean_seq;
+  }
+
   // async cleanup of the global visited words; its tag lets the host order
   // the resident server's next hand-off (another stream) after it
   // tags increase and cleanups finish in stream order, so "done" is h_clean >= tag
   void cleanup_async(bool if_done = false) {
-    clean_seq = clean_seq + 1 == 0 ? 1 : clean_seq + 1;
-    clean_tag[cur] = clean_seq;
+    clean_tag[cur] = next_clean_tag();
     launch::cleanup(buf, n, d_flag + 8, h_clean, clean_seq, if_done, stream);
   }
   void wait_tag(uint32_t tag) {
@@ -96,6 +131,11 @@ struct HipBiBfs::Impl {
 
   // pinned host memory
   HostResult* h_res = nullptr;
+  // The grid levels of a search publish into `gres`: h_res, or for a search
+  // with an auto level behind it h_gres -- a record of its own, so the auto
+  // level never writes over the LDS answer the host is reading.
+  HostResult* h_gres = nullptr;
+  HostResult* gres = nullptr;
   uint32_t* h_path = nullptr;
   uint32_t h_path_cap = 1u << 20;
   DevState* h_state = nullptr;
@@ -346,11 +386,14 @@ struct HipBiBfs::Impl {
     srv_running = false;
   }
 
-  // Post one query to the server and wait for its answer.
-  void server_query(uint32_t src, uint32_t dst, const SearchOptions& opt, uint32_t qseq) {
+  // Post one query to the server; server_wait then waits for its answer (the
+  // LDS engine answers every search, a hand-off included).
+  void server_post(uint32_t src, uint32_t dst, const SearchOptions& opt, uint32_t qseq) {
     ensure_server(kSrvLds);
     post(qseq, src, dst, (opt.lockstep ? kReqLockstep : 0u) | ((uint32_t)opt.side & 3u) << 2 | (cur ? kReqAltBuf : 0u));
     if (dbg()) std::fprintf(stderr, "[server] post %u (stage %u alive %u)\n", qseq, h_box->stage, h_box->alive);
+  }
+  void server_wait(uint32_t qseq) {
     const auto t0 = std::chrono::steady_clock::now();
     wait_server(kSrvLds, qseq, [&] { return __atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq; });
     if (dbg()) {
@@ -443,6 +486,8 @@ struct HipBiBfs::Impl {
     size_t o_st = take(sizeof(DevState));
     size_t o_tr = take(trace_cap * sizeof(LevelTraceDev));
     size_t o_flag = take(64);
+    size_t o_aux = take(64);
+    size_t o_hdump = take(launch::handoff_dump_bytes());
     state_bytes = off;
     HIP_CHECK(hipMalloc(&state_block, state_bytes));
     char* base = static_cast<char*>(state_block);
@@ -460,10 +505,13 @@ struct HipBiBfs::Impl {
     buf.trace_cap = (uint32_t)trace_cap;
     buf.words = (uint32_t)words;
     d_flag = reinterpret_cast<uint32_t*>(base + o_flag);
+    buf.aux = reinterpret_cast<uint32_t*>(base + o_aux);
+    buf.hdump = reinterpret_cast<uint32_t*>(base + o_hdump);
     // visited bitmaps must start (and stay) all-zero
     for (int s = 0; s < 2; ++s) HIP_CHECK(hipMemsetAsync(buf.vis[s], 0, words * 4, stream));
     HIP_CHECK(hipMemsetAsync(buf.st, 0, sizeof(DevState), stream));
     HIP_CHECK(hipMemsetAsync(d_flag, 0, 64, stream));  // bitmap-meet flag + LDS-engine election ticket
+    HIP_CHECK(hipMemsetAsync(buf.aux, 0, 64, stream));  // gate / auto plan
     HIP_CHECK(hipStreamSynchronize(stream));
   }
 
@@ -504,13 +552,14 @@ struct HipBiBfs::Impl {
     HIP_CHECK(hipFree(cursor));
   }
 
-  void wait_seq(uint32_t want) {
+  void wait_seq(uint32_t want, const HostResult* rec = nullptr) {
+    const HostResult* R = rec ? rec : h_res;
     for (uint64_t it = 1;; ++it) {
-      if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want) return;
+      if (__atomic_load_n(&R->seq, __ATOMIC_ACQUIRE) == want) return;
       if ((it & 4095) == 0) {
         hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess) {
-          if (__atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == want) return;
+          if (__atomic_load_n(&R->seq, __ATOMIC_ACQUIRE) == want) return;
           throw Error("bibfs: search kernel finished without publishing a result");
         }
         if (e != hipErrorNotReady)
@@ -565,7 +614,7 @@ struct HipBiBfs::Impl {
   uint32_t res_seq = 0;
   void grid_level(int s, int mode, int trace) {
     const auto g = view();
-    const launch::HostSide hs{h_res, h_path, h_path_cap, h_state};
+    const launch::HostSide hs{gres, h_path, h_path_cap, h_state};
     const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
     if (mode == 2) {
       if (!fbits_valid[s]) launch::build_frontier_bits(g, buf, s, stream);
@@ -638,17 +687,15 @@ struct HipBiBfs::Impl {
     }
   }
 
-  SearchResult collect(uint32_t want_seq, const SearchOptions& opt, SearchStats stats) {
+  SearchResult collect(const HostResult& R, const SearchOptions& opt, SearchStats stats) {
     SearchResult r;
     r.stats = std::move(stats);
-    const HostResult& R = *h_res;
     r.found = R.status == kFound;
     r.hops = r.found ? R.hops : -1;
     r.meet = r.found ? R.meet : kNoVertex;
     r.stats.levels = (int)R.levels;
     r.stats.edges_inspected = R.einsp;
     r.stats.visited = R.visited;
-    (void)want_seq;
     if (r.found && opt.want_path) {
       r.path.resize(R.path_len);
       if (R.path_on_device) {
@@ -674,6 +721,11 @@ struct HipBiBfs::Impl {
     HIP_CHECK(hipStreamSynchronize(stream));
     std::fprintf(stderr, "[stamp] cycles: election %u init %u search-loop %llu path-walk %u publish %u\n", u.side,
                  u.depth, (unsigned long long)t.edges, u.frontier, u.mode);
+    LevelTraceDev w{};
+    HIP_CHECK(hipMemcpyAsync(&w, buf.trace + buf.trace_cap - 3, sizeof w, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    std::fprintf(stderr, "[stamp] publish: hand-off state %u result puts %u bitmaps issued %u drained %u fence %llu\n",
+                 w.side, w.depth, w.frontier, w.mode, (unsigned long long)w.edges);
   }
 
   void fetch_trace(SearchResult& r) {
@@ -715,6 +767,10 @@ HipBiBfs::HipBiBfs(int device) : p_(new Impl) {
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_state), sizeof(DevState),
                           hipHostMallocMapped | hipHostMallocCoherent));  // k_finish_level writes it
   std::memset(p_->h_res, 0, sizeof(HostResult));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_gres), sizeof(HostResult),
+                          hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(p_->h_gres, 0, sizeof(HostResult));
+  p_->gres = p_->h_res;
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_clean), 64, hipHostMallocMapped | hipHostMallocCoherent));
   std::memset(p_->h_clean, 0, 64);
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p_->h_pkts), kTinyPktCap * sizeof(TinyPkt),
@@ -736,6 +792,7 @@ HipBiBfs::~HipBiBfs() {
   (void)hipStreamDestroy(p_->sstream);
   (void)hipHostFree(p_->h_box);
   (void)hipHostFree(p_->h_res);
+  (void)hipHostFree(p_->h_gres);
   (void)hipHostFree(p_->h_clean);
   (void)hipHostFree(p_->h_pkts);
   (void)hipFree(p_->d_stamps);
@@ -1053,6 +1110,8 @@ int64_t HipBiBfs::query(vid_t src, vid_t dst, std::vector<vid_t>* path) {
 double HipBiBfs::last_search_ms() const { return p_->last_ms; }
 uint64_t HipBiBfs::last_edges_inspected() const { return p_->last_einsp; }
 bool HipBiBfs::tiny_engine() const { return p_->tiny_ok; }
+void HipBiBfs::set_auto_handoff(bool on) { p_->auto_on = on; }
+bool HipBiBfs::auto_handoff() const { return p_->auto_on; }
 uint64_t HipBiBfs::tiny_overflows() const { return p_->tiny_overflows; }
 
 SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
@@ -1097,9 +1156,18 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   const uint32_t seq = ++I.seq == 0 ? ++I.seq : I.seq;
   const auto g = I.view();
   launch::HostSide hs{I.h_res, I.h_path, I.h_path_cap, I.h_state};
+  // the grid levels' record (h_gres behind an auto level, else h_res)
+  I.gres = I.h_res;
+  struct GresReset {
+    Impl& I;
+    ~GresReset() { I.gres = I.h_res; }
+  } gres_reset{I};
+  auto hsg = [&I] { return launch::HostSide{I.gres, I.h_path, I.h_path_cap, I.h_state}; };
   SearchStats stats;
   bool grid = opt.force_grid;
   double lds_ms = 0.0;
+  bool use_auto = false, auto_final = false;  // device hand-off (grid_auto) behind a resident search
+  uint32_t pub_auto = 0, auto_ls = 0, auto_tag = 0;
   grid = grid || I.n > 0x7fffffffu;
   // device time: the LDS kernel stamps itself (s_memrealtime); events only
   // around grid levels, where their ~µs cost is noise
@@ -1113,7 +1181,22 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
     // (non-default options, overflow) run one-shot beside it
     if (I.resident && !I.tiny_ok && (!opt.trace || stamp_srv) && I.server_usable()) {
       I.flip_state_set();  // the server (own stream) must not share state with a running cleanup
-      I.server_query(src, dst, opt, seq);
+      use_auto = I.auto_usable(opt);
+      I.gres = use_auto ? I.h_gres : I.h_res;
+      if (use_auto) {
+        // device hand-off: the first grid level is enqueued before the search
+        // starts and waits on the device for it to leave LDS (grid_auto)
+        pub_auto = ++I.seq == 0 ? ++I.seq : I.seq;
+        auto_ls = ++I.level_seq == 0 ? ++I.level_seq : I.level_seq;
+      }
+      I.server_post(src, dst, opt, seq);
+      if (use_auto) {
+        launch::grid_auto(g, I.buf, I.cus, I.max_deg, opt.alpha, I.h_state, auto_ls, hsg(), pub_auto, seq,
+                          I.stream);
+        auto_tag = I.next_clean_tag();
+        launch::cleanup(I.buf, I.n, I.d_flag + 8, I.h_clean, auto_tag, 2, I.stream);
+      }
+      I.server_wait(seq);
       if (I.dbg())
         std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",
                      I.h_res->seq, I.h_res->status, I.h_res->hops, I.h_res->levels, I.h_box->stage,
@@ -1122,25 +1205,50 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
       launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, I.pin_xcc, I.d_flag + 4, lock,
                          I.stream);
     }
-    if (I.h_res->seq != seq && !I.wait_seq_or_done(seq)) {
-      // no block reached the pinned XCD: relaunch unpinned, and stop pinning
-      I.pin_xcc = -1;
-      launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, -1, I.d_flag + 4, lock, I.stream);
-      I.wait_seq(seq);
-    }
-    lds_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;  // 100 MHz
-    if (I.h_res->status == kHandoff) {
-      grid = true;
-      stats.handoff = true;
-      I.mirror_valid = true;  // the LDS kernel published the hand-off state
+    if (use_auto) {
+      // every resident search answers through h_res (a hand-off too); the
+      // auto level behind it publishes into its own record, h_gres
+      lds_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;
+      if (I.h_res->status == kHandoff) {
+        grid = true;
+        stats.handoff = true;
+        const uint32_t lv1 = I.h_res->levels;
+        auto_final = I.wait_auto(pub_auto, auto_ls);
+        if (auto_final) {
+          stats.grid_levels = 1;
+          I.clean_tag[I.cur] = auto_tag;  // the cleanup behind the auto level ran (its tag)
+        } else {
+          // the auto level finished without ending the search, or declined
+          // (bottom-up): the host loop continues from its mirror
+          if (I.h_state->levels > lv1) stats.grid_levels = (int)(I.h_state->levels - lv1);
+          I.mirror_valid = true;
+        }
+      }
+    } else {
+      if (I.h_res->seq != seq && !I.wait_seq_or_done(seq)) {
+        // no block reached the pinned XCD: relaunch unpinned, and stop pinning
+        I.pin_xcc = -1;
+        launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, -1, I.d_flag + 4, lock, I.stream);
+        I.wait_seq(seq);
+      }
+      lds_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;  // 100 MHz
+      if (I.h_res->status == kHandoff) {
+        grid = true;
+        stats.handoff = true;
+        I.mirror_valid = true;  // the LDS kernel published the hand-off state
+        launch::handoff_scatter(g, I.buf, I.stream);
+      }
     }
   } else {
     launch::seed_state(g, I.buf, src, dst, I.stream);
   }
   uint32_t pub_seq = seq;
-  if (grid) {
+  if (auto_final) {
+    pub_seq = pub_auto;
+    I.grid_cleaned = true;
+  } else if (grid) {
     TraceRange grange("bibfs:grid_levels");
-    pub_seq = ++I.seq == 0 ? ++I.seq : I.seq;
+    pub_seq = use_auto ? pub_auto : (++I.seq == 0 ? ++I.seq : I.seq);
     I.res_seq = pub_seq;  // the level that ends the search publishes the path + result
     try {
       I.grid_loop(opt, stats);
@@ -1158,9 +1266,9 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
     I.res_seq = 0;
     I.mirror_valid = false;
     I.grid_cleaned = stats.grid_levels > 0;
-    if (I.h_res->seq != pub_seq) {  // ended before any grid level ran (meet at hand-off / seed)
-      launch::walk_path(I.buf, hs, src, dst, pub_seq, I.n, I.stream);
-      I.wait_seq(pub_seq);
+    if (I.gres->seq != pub_seq) {  // ended before any grid level ran (meet at hand-off / seed)
+      launch::walk_path(I.buf, hsg(), src, dst, pub_seq, I.n, I.stream);
+      I.wait_seq(pub_seq, I.gres);
       I.grid_cleaned = false;
     }
   }
@@ -1169,11 +1277,11 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   // on the query path); a search that never ran in LDS is timed with events
   const bool timed_by_events = grid && !stats.handoff;
   if (timed_by_events) HIP_CHECK(hipEventRecord(I.ev1, I.stream));
-  SearchResult r = I.collect(pub_seq, opt, std::move(stats));
+  SearchResult r = I.collect(grid ? *I.gres : *I.h_res, opt, std::move(stats));
   r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   r.search_ms = lds_ms;
-  if (grid && !timed_by_events && I.h_res->seq == pub_seq)
-    r.search_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;
+  if (grid && !timed_by_events && I.gres->seq == pub_seq)
+    r.search_ms = (double)(I.gres->rt_end - I.h_res->rt_begin) * 1e-5;
   // the last grid level's predicated cleanup did the work (its tag is the
   // pending one); a search that ended before any grid level cleans up here
   if (grid && !I.grid_cleaned) I.cleanup_async();
@@ -1239,7 +1347,7 @@ SearchResult HipBiBfs::finish() {
     launch::walk_path(I.buf, hs, I.step_src, I.step_dst, seq, I.n, I.stream);
     I.wait_seq(seq);
     SearchOptions opt;
-    r = I.collect(seq, opt, SearchStats{});
+    r = I.collect(*I.h_res, opt, SearchStats{});
   }
   I.cleanup_async();
   HIP_CHECK(hipStreamSynchronize(I.stream));

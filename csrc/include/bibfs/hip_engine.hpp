@@ -85,6 +85,12 @@ class HipBiBfs {
   // and is stopped before any graph change or destruction.
   void set_resident(bool on, double idle_ms = 200.0);
   bool resident() const;
+  // Device hand-off (default on; env BIBFS_AUTO_HANDOFF=0 sets the default
+  // off): a resident search enqueues its first grid level before the search
+  // starts, gated on the device, so a search that outgrows LDS continues
+  // without a host round trip (docs/DESIGN.md §3).
+  void set_auto_handoff(bool on);
+  bool auto_handoff() const;
 
   // --- step-wise API (parity with the reference's per-level C API,
   //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)

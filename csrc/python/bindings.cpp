@@ -305,6 +305,7 @@ PYBIND11_MODULE(_native, m) {
       .def("set_resident", &HipBiBfs::set_resident, py::arg("on"), py::arg("idle_ms") = 200.0,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("resident", &HipBiBfs::resident)
+      .def_property("auto_handoff", &HipBiBfs::auto_handoff, &HipBiBfs::set_auto_handoff)
       .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
       .def_property_readonly("last_batch_fallbacks", &HipBiBfs::last_batch_fallbacks)
       .def("set_batch_tuning", &HipBiBfs::set_batch_tuning, py::arg("lds_first") = -1, py::arg("threads") = 0)

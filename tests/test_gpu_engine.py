@@ -310,6 +310,40 @@ def test_resident_back_to_back_handoffs(gpu_engine):
         gpu_engine.set_resident(False)
 
 
+@pytest.mark.parametrize("spec", ["kron:20:16:2", "gnp:3000000::4"])
+def test_resident_auto_handoff_vs_oracle(gpu_engine, spec):
+    """Device hand-off (grid_auto): resident searches that leave LDS continue in
+    a grid level enqueued before they started, gated on the device.  Back to
+    back on both state sets with the knob on, off and on again (the auto
+    chain's no-op launches and cleanups must not disturb the host loop), plus
+    first levels the Beamer rule sends bottom-up (the auto level declines and
+    the host loop takes them); every answer against the oracle."""
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 40, 5)
+    truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
+    gpu_engine.set_resident(True)
+    try:
+        for on in (True, False, True):
+            gpu_engine.auto_handoff = on
+            assert gpu_engine.auto_handoff == on
+            handed = 0
+            for (s, d), h in zip(pairs, truth):
+                r = gpu_engine.search(s, d)
+                check_result(g.csr, s, d, r.hops, r.path, h)
+                handed += bool(r.handoff)
+            assert handed > 0, "expected searches that leave LDS"
+        for (s, d), h in zip(pairs[:10], truth[:10]):
+            r = gpu_engine.search(s, d, make_options(alpha=1e-9))
+            check_result(g.csr, s, d, r.hops, r.path, h)
+        for (s, d), h in zip(pairs[:10], truth[:10]):  # query() serving path
+            hops, path = gpu_engine.query(s, d)
+            check_result(g.csr, s, d, hops, path, h)
+    finally:
+        gpu_engine.auto_handoff = True
+        gpu_engine.set_resident(False)
+
+
 # ---------------------------------------------------------------- tiny server
 def test_tiny_server_query_vs_oracle(gpu_engine):
     """Resident small-graph server (tiny_engine.hip): hops + path of query()
