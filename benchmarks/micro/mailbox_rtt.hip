@@ -6,9 +6,13 @@
 //   host     : request word in pinned host memory (GPU polls over PCIe)
 //   devfine  : request word in fine-grained device memory written by the CPU
 //              through the BAR (GPU polls its own HBM, bypassing L2)
+//   hsa      : the same, allocated from the GPU's fine-grained HSA pool with
+//              access granted to the CPU agent (hsa_amd_agents_allow_access)
 // plus the kernel-launch round trip (empty kernel + host spin on a flag) for
 // reference.  Build: make micro.
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <x86intrin.h>
 
 #include <setjmp.h>
@@ -128,6 +132,50 @@ static bool cpu_writable(uint32_t* p) {
   return ok;
 }
 
+// Fine-grained VRAM from the HSA pool, CPU access granted: nullptr if the
+// runtime refuses (no large BAR, no such pool).
+struct HsaFind {
+  hsa_agent_t cpu{}, gpu{};
+  bool have_cpu = false, have_gpu = false;
+  hsa_amd_memory_pool_t pool{};
+  bool have_pool = false;
+};
+static hsa_status_t find_agent(hsa_agent_t a, void* d) {
+  auto* f = static_cast<HsaFind*>(d);
+  hsa_device_type_t t;
+  hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t);
+  if (t == HSA_DEVICE_TYPE_CPU && !f->have_cpu) f->cpu = a, f->have_cpu = true;
+  if (t == HSA_DEVICE_TYPE_GPU && !f->have_gpu) f->gpu = a, f->have_gpu = true;
+  return HSA_STATUS_SUCCESS;
+}
+static hsa_status_t find_pool(hsa_amd_memory_pool_t p, void* d) {
+  auto* f = static_cast<HsaFind*>(d);
+  hsa_amd_segment_t seg;
+  uint32_t flags = 0;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
+  if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && !f->have_pool)
+    f->pool = p, f->have_pool = true;
+  return HSA_STATUS_SUCCESS;
+}
+static uint32_t* hsa_fine_vram(size_t bytes) {
+  if (hsa_init() != HSA_STATUS_SUCCESS) return nullptr;
+  HsaFind f;
+  hsa_iterate_agents(find_agent, &f);
+  if (!f.have_cpu || !f.have_gpu) return nullptr;
+  hsa_amd_agent_iterate_memory_pools(f.gpu, find_pool, &f);
+  if (!f.have_pool) {
+    std::printf("hsa: no fine-grained global pool on the GPU agent\n");
+    return nullptr;
+  }
+  void* p = nullptr;
+  if (hsa_amd_memory_pool_allocate(f.pool, bytes, 0, &p) != HSA_STATUS_SUCCESS) return nullptr;
+  const hsa_status_t s = hsa_amd_agents_allow_access(1, &f.cpu, nullptr, p);
+  std::printf("hsa: fine-grained VRAM %p, allow_access(cpu) status %d\n", p, (int)s);
+  if (s != HSA_STATUS_SUCCESS) return nullptr;
+  return static_cast<uint32_t*>(p);
+}
+
 static double median(std::vector<double> v) {
   std::sort(v.begin(), v.end());
   return v[v.size() / 2];
@@ -197,6 +245,15 @@ int main() {
       std::printf("device-uncached mailbox, serial polls : %.2f us\n", run_echo(dunc, dunc, resp, 0));
     else
       std::printf("device-uncached mailbox: not CPU-writable\n");
+  }
+  if (uint32_t* hf = hsa_fine_vram(4096)) {
+    if (cpu_writable(hf)) {
+      std::printf("hsa fine VRAM mailbox, serial polls   : %.2f us\n", run_echo(hf, hf, resp, 0));
+      std::printf("hsa fine VRAM mailbox, ring of 4      : %.2f us\n", run_echo(hf, hf, resp, 2));
+      std::printf("hsa fine VRAM mailbox, serial (again) : %.2f us\n", run_echo(hf, hf, resp, 0));
+    } else {
+      std::printf("hsa fine VRAM mailbox: not CPU-writable\n");
+    }
   }
   uint32_t* dplain = nullptr;
   CK(hipMalloc(reinterpret_cast<void**>(&dplain), 4096));

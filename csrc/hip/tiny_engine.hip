@@ -362,15 +362,16 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     // wave -- no barrier, the round state in SGPRs, the counters from the
     // wave's own ballots and scan.  The other waves sleep in the barrier below.
     if (wid == 0) {
-      // wait for a request: one 16-byte system-scope load of the pinned
-      // mailbox per poll (relaxed: the XCD's L2 -- the graph -- is never
+      // wait for a request: one 16-byte system-scope load of the mailbox per
+      // poll -- pinned host memory, or with BIBFS_VRAM_MAILBOX=1 a CPU-written
+      // fine-grained VRAM slot (relaxed: the XCD's L2 -- the graph -- is never
       // invalidated)
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t stop = 0;
       u32x4 rq;
       for (;;) {
         u32x4 r4;
-        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r4) : "v"(P.box) : "memory");
+        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r4) : "v"(P.req) : "memory");
         rq.x = uni(r4.x), rq.y = uni(r4.y), rq.z = uni(r4.z), rq.w = uni(r4.w);
         rt0 = __builtin_amdgcn_s_memrealtime();
         const bool whole = (rq.w >> 8) == (rq.x & 0xffffffu);  // not torn
