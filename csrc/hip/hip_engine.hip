@@ -604,7 +604,7 @@ struct HipBiBfs::Impl {
     max_deg = launch::max_degree(d_row_off, n, stream);
     // small graphs: the packed 8-byte adjacency of the tiny server (8 (nnz + n) B)
     if (!tiny_disabled() && launch::tiny_supported(n, nnz, max_deg)) {
-      HIP_CHECK(hipMalloc(&d_tadj, std::max<uint64_t>(nnz, 1) * 8));
+      HIP_CHECK(hipMalloc(&d_tadj, (std::max<uint64_t>(nnz, 1) + 4) * 8));  // +4: 16-byte first-edge loads
       HIP_CHECK(hipMalloc(&d_tinfo, (size_t)n * 8));
       launch::build_tiny_adj(d_row_off, d_col, n, nnz, d_tadj, d_tinfo, stream);
       tiny_ok = true;

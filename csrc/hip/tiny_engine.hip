@@ -61,6 +61,20 @@ constexpr uint32_t kLockMax = BIBFS_TINY_LOCK_MAX;
 #define BIBFS_TINY_SPEC_ALL 0
 #endif
 constexpr bool kSpecAll = BIBFS_TINY_SPEC_ALL;
+// 1 = a neighbour's first kTinyUnroll edge words come in with two 16-byte
+// loads under one exec mask (tadj is padded by kTinyUnroll words), 0 = one
+// 8-byte load per word, each under its own degree mask.
+#ifndef BIBFS_TINY_X4
+#define BIBFS_TINY_X4 0
+#endif
+constexpr bool kX4 = BIBFS_TINY_X4;
+typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
+static_assert(kTinyUnroll == 4, "two 16-byte loads per neighbour");
+__device__ __forceinline__ void load_first4(unsigned long long (&w)[kTinyUnroll],
+                                            const unsigned long long* __restrict__ p) {
+  const u64x2a8 a = *reinterpret_cast<const u64x2a8*>(p), b = *reinterpret_cast<const u64x2a8*>(p + 2);
+  w[0] = a.x, w[1] = a.y, w[2] = b.x, w[3] = b.y;
+}
 static_assert(kTinyQ == 1u << kQBits, "queue index width");
 
 // Per-round counter (three slots, rotated): new records of side 0 [19:0] and
@@ -175,6 +189,10 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
     for (int b = 0; b < NB; ++b) {
       if (b >= nb) continue;
       const uint32_t base = tw_base(W.rec[b]), deg = W.act[b] ? tw_deg(W.rec[b]) : 0u;
+      if (kX4) {
+        if (deg) load_first4(W.nbw[b], tadj + base);
+        continue;
+      }
 #pragma unroll
       for (uint32_t j = 0; j < kTinyUnroll; ++j)
         if (j < deg) W.nbw[b][j] = tadj[base + j];  // exec-masked: no address for a missing edge
@@ -211,6 +229,10 @@ __device__ __forceinline__ void round_fetch(Work<NB>& W, int nb, const unsigned 
   for (int b = 0; b < NB; ++b) {
     if (b >= nb) continue;
     const uint32_t base = tw_base(W.rec[b]);
+    if (kX4) {
+      if (W.deg[b]) load_first4(W.nbw[b], tadj + base);
+      continue;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < kTinyUnroll; ++j)
       if (j < W.deg[b]) W.nbw[b][j] = tadj[base + j];

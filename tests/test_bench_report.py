@@ -80,3 +80,14 @@ def test_world_scaled_partitioned_config():
     assert [bench.world_scaled("kron:auto", w) for w in (1, 2, 4, 8, 16)] == [
         "kron:27:16:1", "kron:28:16:1", "kron:29:16:1", "kron:30:16:1", "kron:30:16:1"]
     assert bench.world_scaled("gnp:1000000::2", 8) == "gnp:1000000::2"
+
+
+def test_secondary_errors_listed_without_touching_the_headline():
+    """A failed, unverified or unfinished secondary config is named in
+    detail.secondary_errors; the headline fields are unchanged."""
+    extra = {"gnp:10000000::1": {"ms_per_step": 0.09}, "kron:22:16:1": {"error": "RuntimeError('x')"}}
+    part = {"gnp:1000000::2": {"verified": False}, "kron:30:16:1": None, "kron:22:16:1": {"verified": True}}
+    out = bench.report(_args(), 8, _head(gteps=36.0), extra, part)
+    assert out["detail"]["secondary_errors"] == ["gnp:1000000::2", "kron:22:16:1", "kron:30:16:1"]
+    assert out["value"] == 36.0
+    assert bench.report(_args(), 1, _head(), {}, {})["detail"]["secondary_errors"] == []
