@@ -977,7 +977,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
   uint32_t* const que1 = V.queue[1];
   const uint32_t lo = V.lo;
   const uint32_t half = tid / (kSoloT / 2);  // the side a thread scans for
-  if (seed) {
+  if (seed & 1) {
     // the seeding pseudo-round (k_seed) done here: one launch fewer, and the
     // state goes straight into LDS (round it0 = 0 accounts it)
     if (tid < 2) {
@@ -1259,7 +1259,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
   // answer (no k_cleanup launch; the next search's launch queues behind this
   // one): every vertex it claimed is in the queues.
   // (not when the path outgrew the pinned buffer: k_walk_local still reads the depths)
-  if (!ended || (c.state == kDone && pol.want_path && 4 + (c.key >> 32) + 1 > pol.walk_cap)) return;
+  if (!ended || (seed & 2) || (c.state == kDone && pol.want_path && 4 + (c.key >> 32) + 1 > pol.walk_cap)) return;
   for (int sd = 0; sd < 2; ++sd) {
     uint32_t* vis = pick(V.vis, sd);
     uint32_t* dep = sd ? dep1 : dep0;
@@ -1869,6 +1869,15 @@ __global__ void k_cleanup(DView V, uint64_t sent_words) {
   for (uint64_t i = sent_words / 4 * 4 + tid; i < sent_words; i += nth) V.sent[0][i] = 0u;
 }
 
+// A/B: BIBFS_SOLO_SELFCLEAN=0 leaves a solo-ended search's reset to k_cleanup.
+bool solo_selfclean() {
+  static const bool on = [] {
+    const char* e = std::getenv("BIBFS_SOLO_SELFCLEAN");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 unsigned blocks_for(uint64_t work, int cus) {
   uint64_t b = (work + kThreads - 1) / kThreads;
   b = std::min<uint64_t>(b, (uint64_t)cus * 8);
@@ -2388,7 +2397,11 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   // they carry the previous epoch.
   std::memset(h_plan, 0, kPlanRing * 8);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
+  static const bool no_solo = [] {  // A/B: BIBFS_DIST_SOLO=0 turns the solo workgroup off
+    const char* e = std::getenv("BIBFS_DIST_SOLO");
+    return e && e[0] == '0';
+  }();
+  const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0 && !no_solo;
   if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
   if (P > 1) {
     comm->allgather(&V.red[1], V.redg[1], sizeof(Reduced), cs);
@@ -2411,8 +2424,10 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     // state of a stalled round (or the finished search) and its Ctl in h_ctl
     const uint32_t tag = next_tag();
     const uint32_t emax = std::min<uint32_t>(std::max<uint32_t>(tune.solo_edges, 1), kSoloE);
-    if (solo_stamp) k_spec_solo<true><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, 1, src, dst, h_fin, tag, d_stamps);
-    else k_spec_solo<false><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, 1, src, dst, h_fin, tag, nullptr);
+    // bit 0: the workgroup seeds the search; bit 1: no self-cleanup (k_cleanup after the search instead)
+    const int sflags = 1 | (solo_selfclean() ? 0 : 2);
+    if (solo_stamp) k_spec_solo<true><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, sflags, src, dst, h_fin, tag, d_stamps);
+    else k_spec_solo<false><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, sflags, src, dst, h_fin, tag, nullptr);
     HIP_CHECK(hipGetLastError());
     stats.host_syncs++;
     spin_tag(tag, cs);
@@ -2426,8 +2441,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     }
     have_ctl = true;
     stats.solo_rounds = (int)(h_ctl->rounds);
-    solo_cleaned = h_ctl->state == kDead ||
-                   (h_ctl->state == kDone && !(pol.want_path && 4 + (h_ctl->key >> 32) + 1 > pol.walk_cap));
+    solo_cleaned = solo_selfclean() && (h_ctl->state == kDead ||
+                   (h_ctl->state == kDone && !(pol.want_path && 4 + (h_ctl->key >> 32) + 1 > pol.walk_cap)));
     it = h_ctl->next_it;
     const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
     spec_cap = std::min(spec_max, std::max<uint32_t>(kSpecCapMin, next_pow2(4 * fm)));

@@ -8,7 +8,16 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 T="timeout -k 10"
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
-$T 600 $PT -m gpu tests > gpurun_out/ra_pytest.log 2>&1 || exit $?
+# world-1 partitioned diagnosis: the two tests that failed (wrong parent chain at
+# world 1), with the solo workgroup's self-cleanup on (default) / off, solo off
+K="tiny_capacities_force_count_sync_and_overflow or native_rounds_follow_protocol_spec or world1"
+for cfg in default selfclean0 solo0; do
+  case $cfg in selfclean0) E="BIBFS_SOLO_SELFCLEAN=0";; solo0) E="BIBFS_DIST_SOLO=0";; *) E="BIBFS_NONE=1";; esac
+  env $E $T 400 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_dist_local.py -k "$K" > gpurun_out/ra_diag_$cfg.log 2>&1
+  rc=$?; echo "diag $cfg rc=$rc"; [ $rc -le 1 ] || exit $rc
+done
+$T 600 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests > gpurun_out/ra_pytest.log 2>&1
+rc=$?; echo "suite rc=$rc"; [ $rc -le 1 ] || exit $rc
 $T 120 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/ra_smoke.log 2>&1 || exit $?
 $T 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/ra_bench.json 2> gpurun_out/ra_bench.err || exit $?
 for a in 1 0; do
