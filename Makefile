@@ -35,7 +35,7 @@ HIPFLAGS  := -O3 -fPIC $(CXXSTD) $(INC) --offload-arch=$(ARCH) -mcode-object-ver
 MPI_INC   := -I$(MPI_HOME)/include
 # system libstdc++ first: conda ships an older one
 MPI_LD    := $(MPI_HOME)/lib/libmpi.so -Wl,-rpath,/usr/lib/x86_64-linux-gnu:$(MPI_HOME)/lib
-HIP_LD    := -L$(ROCM)/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
+HIP_LD    := -L$(ROCM)/lib -lamdhip64 -lrocprofiler-sdk-roctx -Wl,-rpath,$(ROCM)/lib
 RCCL_LD   := -L$(ROCM)/lib -lrccl
 
 PY_INC    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()['include'])")

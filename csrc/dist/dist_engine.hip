@@ -1255,6 +1255,11 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
   __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }  // tid == 0
   }  // wave 0
+  // The reset below must not start before wave 0's terminal walk has read the
+  // meet vertex's depths and parent chains: without this barrier waves 1..15
+  // cleared them under it (an intermittent "parent chains do not add up" at
+  // world 1, GPU suite, round 3).
+  __syncthreads();
   // A search that ended here resets its own state after the host has its
   // answer (no k_cleanup launch; the next search's launch queues behind this
   // one): every vertex it claimed is in the queues.

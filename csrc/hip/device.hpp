@@ -228,7 +228,7 @@ struct TinyArgs {
   const unsigned long long* tinfo;  // n packed words (the vertex's own)
   uint32_t n;
   dev::ServerBox* box;               // pinned: alive word (and the request, unless `req` is elsewhere)
-  const void* req;                  // the 16-byte request the server polls: box, or a VRAM slot
+  const void* req;                  // the 16-byte request the server polls (the pinned box)
   dev::TinyPkt* pkts;               // pinned, kTinyPktCap packets
   uint32_t launch_seq, last_seq;
   int pin_xcc;

@@ -7,8 +7,6 @@
 // Differences by design: device state is allocated once per graph and kept
 // clean between queries, the per-level loop runs on the device, and the host
 // learns the result by polling a pinned word instead of a memcpy + sync chain.
-#include <hsa/hsa.h>
-#include <hsa/hsa_ext_amd.h>
 #include <immintrin.h>
 
 #include <algorithm>
@@ -25,58 +23,6 @@
 namespace bibfs {
 
 using namespace dev;
-
-namespace {
-// A 64-byte request slot in fine-grained VRAM of `device` that the CPU may
-// store to directly (HSA pool allocation + allow_access for the CPU agent):
-// the tiny server then polls its own HBM instead of reading pinned host
-// memory across PCIe per poll.  nullptr when the runtime refuses (no large
-// BAR, no fine-grained pool) or the agent does not map to `device`.
-struct HsaPick {
-  hsa_agent_t cpu{}, gpu{};
-  int want = 0, seen = 0;
-  bool have_cpu = false, have_gpu = false, have_pool = false;
-  hsa_amd_memory_pool_t pool{};
-};
-hsa_status_t pick_agent(hsa_agent_t a, void* d) {
-  auto* f = static_cast<HsaPick*>(d);
-  hsa_device_type_t t;
-  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
-  if (t == HSA_DEVICE_TYPE_CPU && !f->have_cpu) f->cpu = a, f->have_cpu = true;
-  if (t == HSA_DEVICE_TYPE_GPU && f->seen++ == f->want) f->gpu = a, f->have_gpu = true;
-  return HSA_STATUS_SUCCESS;
-}
-hsa_status_t pick_pool(hsa_amd_memory_pool_t p, void* d) {
-  auto* f = static_cast<HsaPick*>(d);
-  hsa_amd_segment_t seg;
-  uint32_t flags = 0;
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg);
-  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &flags);
-  if (seg == HSA_AMD_SEGMENT_GLOBAL && (flags & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_FINE_GRAINED) && !f->have_pool)
-    f->pool = p, f->have_pool = true;
-  return HSA_STATUS_SUCCESS;
-}
-void* vram_request_slot(int device, bool verbose) {
-  if (hsa_init() != HSA_STATUS_SUCCESS) return nullptr;  // refcounted: HIP initialised it already
-  HsaPick f;
-  f.want = device;
-  hsa_iterate_agents(pick_agent, &f);
-  void* p = nullptr;
-  if (f.have_cpu && f.have_gpu) hsa_amd_agent_iterate_memory_pools(f.gpu, pick_pool, &f);
-  if (f.have_pool && hsa_amd_memory_pool_allocate(f.pool, 64, 0, &p) == HSA_STATUS_SUCCESS) {
-    hipPointerAttribute_t at{};
-    const bool mine = hipPointerGetAttributes(&at, p) == hipSuccess && at.device == device;
-    if (!mine || hsa_amd_agents_allow_access(1, &f.cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
-      hsa_amd_memory_pool_free(p);
-      p = nullptr;
-    }
-  }
-  if (p) std::memset(p, 0, 64);  // the CPU store path itself (a BAR-less system faults here, not later)
-  if (verbose) std::fprintf(stderr, "[server] VRAM request slot: %p\n", p);
-  hsa_shut_down();
-  return p;
-}
-}  // namespace
 
 struct HipBiBfs::Impl {
   int device = 0;
@@ -259,17 +205,6 @@ struct HipBiBfs::Impl {
   int srv_kind = 0;              // kSrvLds / kSrvTiny: which server kernel is running
   uint32_t srv_launch_seq = 0;
   unsigned long long srv_idle_ticks = 20000000ull;  // 200 ms of s_memrealtime
-  // BIBFS_VRAM_MAILBOX=1: the tiny server polls a CPU-writable VRAM slot
-  // (vram_request_slot) instead of the pinned box; post() writes both
-  void* d_req = nullptr;
-  bool req_tried = false;
-  static bool vram_mailbox() {
-    static const bool on = [] {
-      const char* e = std::getenv("BIBFS_VRAM_MAILBOX");
-      return e && e[0] == '1';
-    }();
-    return on;
-  }
   static constexpr int kSrvLds = 1, kSrvTiny = 2;
 
   // small-graph server (tiny_engine.hip): packed adjacency + self-tagged result packets
@@ -315,8 +250,7 @@ struct HipBiBfs::Impl {
   void post(uint32_t s, uint32_t src, uint32_t dst, uint32_t flags) {
     const __m128i v = _mm_set_epi32((int)req_tag(s, flags), (int)dst, (int)src, (int)s);
     _mm_store_si128(reinterpret_cast<__m128i*>(h_box), v);
-    if (d_req) _mm_store_si128(reinterpret_cast<__m128i*>(d_req), v);  // write-combined BAR store
-    std::atomic_thread_fence(std::memory_order_seq_cst);  // (mfence also drains the WC buffer)
+    std::atomic_thread_fence(std::memory_order_seq_cst);
   }
 
   // Launch a server kernel of `kind`; it serves requests whose seq != last.
@@ -326,12 +260,7 @@ struct HipBiBfs::Impl {
     HIP_CHECK(hipSetDevice(device));
     __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
     if (kind == kSrvTiny) {
-      if (vram_mailbox() && !req_tried) {
-        req_tried = true;
-        d_req = vram_request_slot(device, dbg());
-        if (d_req) std::memcpy(d_req, h_box, 16);  // the last request: not served again
-      }
-      launch::TinyArgs a{d_tadj, d_tinfo, n, h_box, d_req ? d_req : static_cast<const void*>(h_box), h_pkts,
+      launch::TinyArgs a{d_tadj, d_tinfo, n, h_box, h_box, h_pkts,
                          srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, d_stamps};
       launch::tiny_server(a, tiny_stamp(), sstream);
     } else {
@@ -862,11 +791,6 @@ HipBiBfs::~HipBiBfs() {
   }
   (void)hipStreamDestroy(p_->sstream);
   (void)hipHostFree(p_->h_box);
-  if (p_->d_req) {
-    hsa_init();
-    hsa_amd_memory_pool_free(p_->d_req);
-    hsa_shut_down();
-  }
   (void)hipHostFree(p_->h_res);
   (void)hipHostFree(p_->h_gres);
   (void)hipHostFree(p_->h_clean);

@@ -64,8 +64,10 @@ constexpr bool kSpecAll = BIBFS_TINY_SPEC_ALL;
 // 1 = a neighbour's first kTinyUnroll edge words come in with two 16-byte
 // loads under one exec mask (tadj is padded by kTinyUnroll words), 0 = one
 // 8-byte load per word, each under its own degree mask.
+// 1 measured 14.5 vs 14.8 us mean query, device 11.45 vs 11.77 us
+// (profiles/r3_tiny_x4_ab.jsonl).
 #ifndef BIBFS_TINY_X4
-#define BIBFS_TINY_X4 0
+#define BIBFS_TINY_X4 1
 #endif
 constexpr bool kX4 = BIBFS_TINY_X4;
 typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
@@ -384,10 +386,10 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     // wave -- no barrier, the round state in SGPRs, the counters from the
     // wave's own ballots and scan.  The other waves sleep in the barrier below.
     if (wid == 0) {
-      // wait for a request: one 16-byte system-scope load of the mailbox per
-      // poll -- pinned host memory, or with BIBFS_VRAM_MAILBOX=1 a CPU-written
-      // fine-grained VRAM slot (relaxed: the XCD's L2 -- the graph -- is never
-      // invalidated)
+      // wait for a request: one 16-byte system-scope load of the pinned
+      // mailbox per poll (relaxed: the XCD's L2 -- the graph -- is never
+      // invalidated).  A CPU-written VRAM slot was measured instead and not
+      // kept (no faster; benchmarks/micro/mailbox_rtt.hip)
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       uint32_t stop = 0;
       u32x4 rq;
