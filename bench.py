@@ -360,6 +360,16 @@ def main(argv=None) -> int:
             hops += query(warmup + i)
             dev_ms += eng.last_search_ms
             insp += eng.last_edges_inspected
+        # direction-optimizing evidence (BASELINE config 4), untimed: how many
+        # levels ran on the grid / bottom-up, and how many searches left LDS
+        nd = min(steps, 64)
+        gl = bu = ho = 0
+        for i in range(nd):
+            s_, d_, _ = pairs[((warmup + i) * world + rank) % len(pairs)]
+            st = eng.search(s_, d_).stats
+            gl += st["grid_levels"]
+            bu += st["bottomup_levels"]
+            ho += 1 if st["handoff"] else 0
         park()
         barrier()  # device-wide synchronize with the server down
         queries = steps * world
@@ -400,6 +410,8 @@ def main(argv=None) -> int:
             "tiny_overflows": eng.tiny_overflows,  # queries re-run on the general engine (cumulative)
             "end_to_end_first_query_ms": build_s * 1e3 + launch_ms,
             "queries": queries, "batched": batched,
+            "grid_levels_per_query": gl / nd, "bottomup_levels_per_query": bu / nd,
+            "handoff_fraction": ho / nd,
         }
         eng.release()  # free HBM before the next config
         if cpu_ref and not a.no_cpu_ref:
