@@ -918,28 +918,34 @@ __device__ __forceinline__ unsigned long long solo_clock() {
 }
 
 // The same prefix by ONE wave (32 entries per lane, one wave scan): no barrier.
+// Inclusive wave64 prefix sum on the VALU via DPP (row shifts, then the
+// row-15 / row-31 broadcasts): no LDS permutes.
+__device__ __forceinline__ uint32_t dpp_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+// Exclusive degree prefix FP[0..cnt] of ND[0..cnt) by one wave (cnt uniform,
+// <= kSoloV): 64 consecutive entries per step -- conflict-free LDS accesses,
+// one DPP scan, the running total carried in an SGPR -- so a round pays
+// ceil(cnt / 64) steps.  (It was 32 fixed steps of lane-blocked entries, each
+// LDS access a 32-word-stride bank conflict: ~5.4k cycles per G(1M) round,
+// profiles/r3_dist_solo_stamps.txt.)
 __device__ void solo_wave_scan(const uint32_t* ND, uint32_t* FP, uint32_t cnt, uint32_t lane) {
-  constexpr uint32_t kPer = kSoloV / kWave;
-  uint32_t run = 0;
-  for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t i = lane * kPer + k;
-    run += i < cnt ? ND[i] : 0u;
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < cnt; c0 += kWave) {
+    const uint32_t i = c0 + lane;
+    const uint32_t v = i < cnt ? ND[i] : 0u;
+    const uint32_t x = dpp_scan(v);
+    if (i < cnt) FP[i] = carry + x - v;
+    carry += (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
   }
-  uint32_t x = run;
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const uint32_t y = __shfl_up(x, o);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  uint32_t e = x - run;
-  for (uint32_t k = 0; k < kPer; ++k) {
-    const uint32_t i = lane * kPer + k;
-    if (i < cnt) {
-      FP[i] = e;
-      e += ND[i];
-    }
-  }
-  if (lane == kWave - 1) FP[cnt < kSoloV ? cnt : kSoloV] = x;
+  if (lane == 0) FP[cnt] = carry;
 }
 
 template <bool kStamp>

@@ -1,13 +1,19 @@
 #!/bin/bash
-# Round 3g: partitioned engine after the terminal-Ctl / local-walk / deferred-cleanup change.
+# Round 3g: world-1 packed adjacency of the partitioned engine (16 B per edge:
+# the neighbour's row comes with its id) on / off, now that the world-1
+# failure is traced to the solo self-cleanup race: correctness on the world-1
+# tests with it on, then an interleaved A/B on G(1M) and Kronecker 22.
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_dist_local.py \
-  > gpurun_out/r3g_dist_tests.log 2>&1 || exit $?
-timeout -k 10 300 python3 benchmarks/dist_ab.py --specs gnp:1000000::2,kron:22 --modes 1,2,4 --queries 24 --reps 2 \
-  > gpurun_out/r3g_dist_ab.jsonl 2> gpurun_out/r3g_dist_ab.err || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3g_prof_dist -o run -- \
-  python3 benchmarks/dist_ab.py --specs gnp:1000000::2,kron:22 --modes 2 --queries 16 --reps 1 \
-  > gpurun_out/r3g_dist_prof.jsonl 2> gpurun_out/r3g_dist_prof.err || exit $?
+T="timeout -k 10"
+K="tiny_capacities_force_count_sync_and_overflow or native_rounds_follow_protocol_spec or world1 or local_group"
+BIBFS_PADJ_MAX_MB=4096 $T 400 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_dist_local.py -k "$K" > gpurun_out/rg_padj_tests.log 2>&1
+rc=$?; echo "padj tests rc=$rc"; [ $rc -le 1 ] || exit $rc
+for rep in 1 2; do
+  for mb in 4096 0; do
+    BIBFS_PADJ_MAX_MB=$mb $T 300 python3 benchmarks/dist_ab.py --specs gnp:1000000::2,kron:22 --modes 1 --queries 48 \
+      --reps 1 > gpurun_out/rg_dist_padj${mb}_$rep.jsonl 2> gpurun_out/rg_dist_padj${mb}_$rep.err || exit $?
+  done
+done
 echo done
