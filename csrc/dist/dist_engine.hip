@@ -2096,13 +2096,12 @@ struct DistBiBfs::Impl {
   void finish_build() {
     alloc_state();
     // One rank owns every row: the packed adjacency of the single-GPU engine
-    // (16 B per edge) within BIBFS_PADJ_MAX_MB (default 0 = off: with tiny
-    // exchange capacities -- host-planned rounds -- it produced a wrong parent
-    // chain at world 1 on the GPU suite, test_tiny_capacities_force_count_sync_and_overflow[1]).
+    // (16 B per edge) within BIBFS_PADJ_MAX_MB (default 4096 MiB, 0 = off).
+    // G(1M) world-1 query 0.108 -> 0.103 ms (profiles/r3_dist_padj_ab.jsonl).
     V.padj = nullptr;
     if (size == 1 && lo == 0 && nnz) {
       const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
-      const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 0ull) << 20;
+      const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
       if (nnz * 16 <= budget) {
         HIP_CHECK(hipMalloc(&d_padj, nnz * 16));
         launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
