@@ -74,3 +74,4 @@ def test_bench_py_contract(repo_root):
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in d
     assert d["n_gpus"] == 1 and d["steps"] == 20 and d["value"] > 0
+    assert d["detail"]["secondary_errors"] == [], d["detail"]["secondary_errors"]  # partitioned configs verified
