@@ -55,10 +55,13 @@ constexpr uint32_t kTinyUnroll = 4;  // record stores per new vertex without a l
 constexpr uint32_t kLockMax = BIBFS_TINY_LOCK_MAX;
 // All-wave rounds: 1 = fetch each neighbour's first edges speculatively at the
 // round's start (beside the claim), 0 = only for the vertices claimed, after
-// the claim (16 waves of speculative scattered loads queue on the address
-// unit; one wave's do not).
+// the claim.  With one 8-byte load per edge word 16 waves of speculative
+// scattered loads queued on the address unit (17.6 vs 17.2 us,
+// profiles/r3_tiny_ab.jsonl); with the two 16-byte loads of BIBFS_TINY_X4 the
+// speculation wins: 14.15-14.19 vs 14.42-14.52 us mean query
+// (profiles/r3_tiny_specall_ab.jsonl).
 #ifndef BIBFS_TINY_SPEC_ALL
-#define BIBFS_TINY_SPEC_ALL 0
+#define BIBFS_TINY_SPEC_ALL 1
 #endif
 constexpr bool kSpecAll = BIBFS_TINY_SPEC_ALL;
 // 1 = a neighbour's first kTinyUnroll edge words come in with two 16-byte
