@@ -63,15 +63,19 @@ struct HipBiBfs::Impl {
   bool grid_cleaned = false;  // the search's last grid level enqueued the cleanup that ran
 
   // Device hand-off (grid_auto): on by default for resident searches of
-  // graphs the general server takes, with the default level policy;
-  // BIBFS_AUTO_HANDOFF=0 turns it off (A/B).
+  // graphs the general server takes, with the default level policy, when no
+  // vertex has more than kAutoMaxDeg edges; BIBFS_AUTO_HANDOFF=0 turns it off
+  // (A/B).  Hub graphs keep the host-planned first level: on Kronecker 22 the
+  // auto level lost in three A/Bs (0.058-0.060 vs 0.054-0.057 ms) while
+  // 10M G(n, p) gains ~1% (profiles/r3_auto_handoff_ab2.jsonl).
+  static constexpr uint64_t kAutoMaxDeg = 64;
   bool auto_on = [] {
     const char* e = std::getenv("BIBFS_AUTO_HANDOFF");
     return !(e && e[0] == '0');
   }();
   bool auto_usable(const SearchOptions& opt) const {
-    return auto_on && nnz > 0 && !opt.trace && !opt.force_grid && opt.direction == Direction::kAuto &&
-           opt.side == SidePolicy::kSmallerEdges;
+    return auto_on && nnz > 0 && max_deg <= kAutoMaxDeg && !opt.trace && !opt.force_grid &&
+           opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
   }
   // After an auto level's search handed off: wait for the auto level's result
   // (true) or its mirror publish (false: the search continues on the host).
