@@ -74,8 +74,8 @@ def parse_args(argv=None):
                          "headline line is printed with the unfinished configs marked")
     ap.add_argument("--strict", action="store_true",
                     help="exit non-zero when a secondary (extra / partitioned) config fails or times out; "
-                         "by default the failure is reported in detail.secondary_errors and the exit status "
-                         "reflects the headline measurement only")
+                         "by default such a failure is reported in detail.secondary_errors only.  A partitioned "
+                         "config that returns WRONG answers (verified false) always exits 5")
     ap.add_argument("--extra-steps", type=int, default=50)
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--no-resident", action="store_true",
@@ -207,6 +207,7 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks
             "graph_build_ms": round(head["build_ms"], 3),
             "server_launch_ms": head.get("server_launch_ms"),
             "tiny_server": head.get("tiny_server"),
+            "tiny_overflows": head.get("tiny_overflows"),
             "resident_server": (not part) and not a.no_resident,
             "batched_serving": head["batched"],
             "rccl_ranks": rccl_ranks,
@@ -220,6 +221,19 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks
                 if v is None or "error" in v or v.get("verified") is False),
         },
     }
+
+
+def exit_status(partitioned: dict, failed: bool, strict: bool) -> int:
+    """Wrong answers are never a soft failure: a partitioned config that ran
+    and returned a wrong hop count or path fails the run (5).  Timeouts and
+    setup errors of secondary configs fail it only with --strict (4)."""
+    wrong = sorted(k for k, v in partitioned.items() if isinstance(v, dict) and v.get("verified") is False)
+    if wrong:
+        print(f"bench.py: partitioned config(s) {wrong} returned wrong answers", file=sys.stderr)
+        return 5
+    if failed:
+        print("bench.py: a secondary config failed (detail.secondary_errors)", file=sys.stderr)
+    return 4 if (failed and strict) else 0
 
 
 def cpu_serial_ms(spec: str, pairs, reps: int = 20):
@@ -347,11 +361,14 @@ def main(argv=None) -> int:
             eng.synchronize()
 
         stream_barrier()
+        ov0 = eng.tiny_overflows
         t0 = time.perf_counter()
         for i in range(steps):
             query(warmup + i)  # answer checked in query()
         stream_barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
+        # queries of the timed loop the tiny server handed to the general engine
+        timed_overflows = int(max_over_ranks(float(eng.tiny_overflows - ov0)))
         # statistics, untimed: the same queries again, reading the per-query
         # device time and edges inspected the timed loop did not touch
         hops = insp = 0
@@ -407,7 +424,7 @@ def main(argv=None) -> int:
             "mean_hops": hops / steps, "device_ms_per_query": dev_ms / steps,
             "build_ms": build_s * 1e3, "server_launch_ms": round(launch_ms, 4),
             "tiny_server": bool(eng.tiny_engine and resident),
-            "tiny_overflows": eng.tiny_overflows,  # queries re-run on the general engine (cumulative)
+            "tiny_overflows": timed_overflows,  # timed-loop queries re-run on the general engine (max over ranks)
             "end_to_end_first_query_ms": build_s * 1e3 + launch_ms,
             "queries": queries, "batched": batched,
             "grid_levels_per_query": gl / nd, "bottomup_levels_per_query": bu / nd,
@@ -449,7 +466,10 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
-        eng = generate(dist_engine(), spec)
+        eng = dist_engine()  # RCCL communicator bootstrap (reported apart from the graph build)
+        comm_init_ms = max_over_ranks((time.perf_counter() - t0) * 1e3)
+        t0 = time.perf_counter()
+        generate(eng, spec)
         build_ms = max_over_ranks((time.perf_counter() - t0) * 1e3)
         free_b, total_b = torch.cuda.mem_get_info(dev)
         hbm_used = total_b - free_b
@@ -481,7 +501,7 @@ def main(argv=None) -> int:
         rounds = sum(s["rounds"] for s in st) / steps
         out = {
             "engine": f"DistBiBfs/{eng.backend}", "ranks": world, "rccl_ranks": eng.world,
-            "n": n, "m": m, "seed": seed, "build_ms": round(build_ms, 3),
+            "n": n, "m": m, "seed": seed, "comm_init_ms": round(comm_init_ms, 3), "build_ms": round(build_ms, 3),
             "local_nnz_max": int(max_over_ranks(float(eng.local_nnz))),
             # per-rank HBM: the CSR shard, and the generator's peak (shard + one
             # cursor array: the edge list is never materialised on any rank)
@@ -540,7 +560,8 @@ def main(argv=None) -> int:
         emit()
         sys.stdout.flush()
         sys.stderr.write("bench.py: secondary configs unfinished at the watchdog deadline\n")
-        os._exit(3 if a.strict else 0)
+        rc = exit_status(partitioned, True, a.strict)
+        os._exit(3 if rc == 4 else rc)
 
     dog = threading.Timer(a.secondary_timeout, watchdog)
     dog.daemon = True
@@ -570,9 +591,7 @@ def main(argv=None) -> int:
         dist.barrier()
         dist.destroy_process_group()
     dog.cancel()  # after the teardown: a hung final barrier is covered too
-    if failed:
-        print("bench.py: a secondary config failed (detail.secondary_errors)", file=sys.stderr)
-    return 4 if (failed and a.strict) else 0
+    return exit_status(partitioned, failed, a.strict)
 
 
 if __name__ == "__main__":

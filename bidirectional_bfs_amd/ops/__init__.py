@@ -169,6 +169,22 @@ class HipEngine:
     def auto_handoff(self, on: bool) -> None:
         self._e.auto_handoff = bool(on)
 
+    @property
+    def auto_gate_timeout_us(self) -> float:
+        """How long the gated first grid level waits on the device for its
+        search to leave LDS (default 6 s, above the host's 5 s server wait)."""
+        return self._e.auto_gate_timeout_us
+
+    @auto_gate_timeout_us.setter
+    def auto_gate_timeout_us(self, us: float) -> None:
+        self._e.auto_gate_timeout_us = float(us)
+
+    @property
+    def auto_gate_misses(self) -> int:
+        """Hand-offs the gated level missed (gave up first); each continued
+        on the host from the LDS engine's mirror."""
+        return self._e.auto_gate_misses
+
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:
         self._e.begin(int(src), int(dst))

@@ -31,6 +31,11 @@ from ..ops import _DEFAULT_OPTIONS, HipEngine, make_options
 MPIEXEC = os.environ.get("BIBFS_MPIEXEC", "/opt/conda/bin/mpiexec")
 
 
+def gpu_count() -> int:
+    """Visible HIP devices (0 without a GPU), from the native library."""
+    return int(native.gpu_count())
+
+
 def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] = None, cap: Optional[int] = None,
                 nosync_bytes: Optional[int] = None, timeout_s: Optional[float] = None,
                 walk_max: Optional[int] = None, solo: Optional[bool] = None,

@@ -80,8 +80,8 @@ constexpr int kHubTile = 1024;                  // hubs staged in LDS per pass
 constexpr uint32_t kSpecHubCap = 4096;          // speculative blocks up to this size skip the hub pass
 constexpr uint32_t kTraceCap = 4096;            // rounds recorded with SearchOptions::trace
 constexpr uint32_t kPlanRing = 64;              // pinned per-round plan words (lookahead < this)
-constexpr int kStageRanks = 16;
-constexpr uint32_t kOwnerCapMin = 256;          // smallest owner-addressed candidate block (pairs)                 // gathered reductions staged in LDS up to this many ranks
+constexpr int kStageRanks = 16;                 // gathered reductions staged in LDS up to this many ranks
+constexpr uint32_t kOwnerCapMin = 256;          // smallest owner-addressed candidate block (pairs)
 
 // Search control state: identical on every rank (computed from reduced
 // values only).  Double-buffered by round parity: round `it` reads
@@ -1904,6 +1904,11 @@ uint32_t next_pow2(uint64_t x) {
 }  // namespace
 
 std::vector<uint8_t> dist_unique_id() { return dist::rccl_unique_id(); }
+
+int gpu_count() {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
 
 struct DistBiBfs::Impl {
   int rank = 0, size = 1, device = 0, cus = 256;

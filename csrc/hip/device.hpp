@@ -291,6 +291,7 @@ void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* h
 // publishes the mirror unchanged, so the host loop takes that level).
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
+               unsigned long long gate_ticks,
                hipStream_t s);
 
 }  // namespace launch

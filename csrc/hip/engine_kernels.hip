@@ -1474,6 +1474,7 @@ struct GridParams {
   // auto level (grid_auto): the gate's search seq, the CU count and the graph
   // facts the device-side plan needs
   uint32_t gate_seq;
+  unsigned long long gate_ticks;  // k_handoff gives up on the gate after this many s_memrealtime ticks
   uint32_t cus;
   unsigned long long max_deg;
   unsigned long long nnz;
@@ -1531,7 +1532,11 @@ __device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid
 //  * hash-set searches (n > kBmMaxN): the LDS engine dumped its raw hash
 //    tables (coalesced); every thread scatters one slot into the global
 //    visited bitmaps (a single CU issuing them cost ~7 us on 10M G(n, p)).
-constexpr unsigned long long kGateTimeoutTicks = 200000000ull;  // 2 s of s_memrealtime (100 MHz)
+// The gate wait gives up after GridParams::gate_ticks (default 6 s of
+// s_memrealtime, 100 MHz -- longer than the host's 5 s server wait).  A wait
+// that gives up runs no level and publishes nothing (aux[2] = 0); the host
+// sees the auto chain drain unpublished and continues the search itself from
+// the hand-off mirror (HipBiBfs::Impl::wait_auto, fallback path).
 constexpr int kHandoffBlocks = 64;  // x kGridThreads = 2 * kHashSize: one slot per thread
 static_assert(kHandoffBlocks * kGridThreads == 2 * kHashSize, "one hash slot per thread");
 template <typename OffT>
@@ -1553,7 +1558,7 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
           seen = true;
           break;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > kGateTimeoutTicks) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > P.gate_ticks) break;
         __builtin_amdgcn_s_sleep(8);  // ~0.2 us: the pollers must not crowd the LDS search's memory
       }
       const bool hand = seen && (uint32_t)g == 1u;
@@ -2170,6 +2175,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.hub_deg = kHubDegree;
   P.chunk_v = kGridThreads;
   P.gate_seq = 0;
+  P.gate_ticks = 0;
   P.cus = 0;
   P.max_deg = 0;
   P.nnz = g.nnz;
@@ -2292,7 +2298,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
 
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
-               hipStream_t s) {
+               unsigned long long gate_ticks, hipStream_t s) {
   // The grid size is fixed before the frontier exists: cus / 4 workgroups
   // (a 10M G(n, p) hand-off level is ~17 chunks; every workgroup takes chunk
   // tickets, and fewer blocks keep the ticket and done counters cheap).  The
@@ -2304,6 +2310,7 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
     P.mirror = mirror, P.seq = seq, P.trace = 0, P.h = h, P.res_seq = res_seq;
     P.gate_seq = gate_seq;
+    P.gate_ticks = gate_ticks;
     P.cus = (uint32_t)cus;
     P.max_deg = max_deg;
     P.nnz = g.nnz;

@@ -77,19 +77,28 @@ struct HipBiBfs::Impl {
     return auto_on && nnz > 0 && max_deg <= kAutoMaxDeg && !opt.trace && !opt.force_grid &&
            opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
   }
+  // k_handoff's gate wait limit (microseconds; set_auto_gate_timeout_us).
+  // Longer than the host's 5 s server wait, so a late server does not strand
+  // the auto chain; a wait that gives up anyway is recovered on the host.
+  double auto_gate_us = 6e6;
+  uint64_t auto_gate_misses = 0;  // hand-offs the auto chain missed (host fallback ran)
   // After an auto level's search handed off: wait for the auto level's result
-  // (true) or its mirror publish (false: the search continues on the host).
-  bool wait_auto(uint32_t pub, uint32_t ls) {
+  // (kAutoFinal), its mirror publish (kAutoMirror: the search continues on the
+  // host), or the chain draining with neither (kAutoMissed: the gate wait gave
+  // up before the search handed off -- no level ran, no scatter, no publish;
+  // the caller continues from the LDS engine's own hand-off mirror).
+  enum AutoOutcome { kAutoFinal, kAutoMirror, kAutoMissed };
+  AutoOutcome wait_auto(uint32_t pub, uint32_t ls) {
     for (uint64_t it = 1;; ++it) {
-      if (__atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub) return true;
+      if (__atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub) return kAutoFinal;
       if (__atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) == ls) {
-        return __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub;
+        return __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub ? kAutoFinal : kAutoMirror;
       }
       if ((it & 8191) == 0) {
         const hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess && __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) != pub &&
             __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != ls)
-          throw Error("bibfs: auto grid level finished without publishing");
+          return kAutoMissed;
         if (e != hipSuccess && e != hipErrorNotReady)
           throw Error(std::string("bibfs: auto grid level failed: ") + hipGetErrorString(e));
       } else {
@@ -1115,6 +1124,9 @@ double HipBiBfs::last_search_ms() const { return p_->last_ms; }
 uint64_t HipBiBfs::last_edges_inspected() const { return p_->last_einsp; }
 bool HipBiBfs::tiny_engine() const { return p_->tiny_ok; }
 void HipBiBfs::set_auto_handoff(bool on) { p_->auto_on = on; }
+void HipBiBfs::set_auto_gate_timeout_us(double us) { p_->auto_gate_us = us; }
+double HipBiBfs::auto_gate_timeout_us() const { return p_->auto_gate_us; }
+uint64_t HipBiBfs::auto_gate_misses() const { return p_->auto_gate_misses; }
 bool HipBiBfs::auto_handoff() const { return p_->auto_on; }
 uint64_t HipBiBfs::tiny_overflows() const { return p_->tiny_overflows; }
 
@@ -1196,7 +1208,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
       I.server_post(src, dst, opt, seq);
       if (use_auto) {
         launch::grid_auto(g, I.buf, I.cus, I.max_deg, opt.alpha, I.h_state, auto_ls, hsg(), pub_auto, seq,
-                          I.stream);
+                          (unsigned long long)(std::max(0.0, I.auto_gate_us) * 100.0), I.stream);
         auto_tag = I.next_clean_tag();
         launch::cleanup(I.buf, I.n, I.d_flag + 8, I.h_clean, auto_tag, 2, I.stream);
       }
@@ -1217,10 +1229,21 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         grid = true;
         stats.handoff = true;
         const uint32_t lv1 = I.h_res->levels;
-        auto_final = I.wait_auto(pub_auto, auto_ls);
+        const auto outcome = I.wait_auto(pub_auto, auto_ls);
+        auto_final = outcome == Impl::kAutoFinal;
         if (auto_final) {
           stats.grid_levels = 1;
           I.clean_tag[I.cur] = auto_tag;  // the cleanup behind the auto level ran (its tag)
+        } else if (outcome == Impl::kAutoMissed) {
+          // the gate wait gave up before this search handed off: nothing ran
+          // behind it (no scatter, no level, no cleanup), so continue exactly
+          // like a non-auto hand-off -- scatter the dumped hash tables and run
+          // the host loop from the mirror the LDS engine published
+          ++I.auto_gate_misses;
+          I.mirror_valid = true;
+          I.gres = I.h_res;
+          pub_auto = 0;
+          launch::handoff_scatter(g, I.buf, I.stream);
         } else {
           // the auto level finished without ending the search, or declined
           // (bottom-up): the host loop continues from its mirror
@@ -1252,7 +1275,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
     I.grid_cleaned = true;
   } else if (grid) {
     TraceRange grange("bibfs:grid_levels");
-    pub_seq = use_auto ? pub_auto : (++I.seq == 0 ? ++I.seq : I.seq);
+    pub_seq = (use_auto && pub_auto) ? pub_auto : (++I.seq == 0 ? ++I.seq : I.seq);
     I.res_seq = pub_seq;  // the level that ends the search publishes the path + result
     try {
       I.grid_loop(opt, stats);

@@ -46,6 +46,7 @@
 namespace bibfs {
 
 std::vector<uint8_t> dist_unique_id();  // ncclGetUniqueId as bytes
+int gpu_count();                         // visible HIP devices (0 when none / no driver)
 
 namespace dist {
 class Comm;  // collective backend (RCCL, or the in-process test group): csrc/dist/comm.hpp

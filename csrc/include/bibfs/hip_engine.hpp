@@ -91,6 +91,11 @@ class HipBiBfs {
   // without a host round trip (docs/DESIGN.md §3).
   void set_auto_handoff(bool on);
   bool auto_handoff() const;
+  // How long the device-gated first grid level waits for its search to leave
+  // LDS (default 6 s); hand-offs it missed continue on the host (counted).
+  void set_auto_gate_timeout_us(double us);
+  double auto_gate_timeout_us() const;
+  uint64_t auto_gate_misses() const;
 
   // --- step-wise API (parity with the reference's per-level C API,
   //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)

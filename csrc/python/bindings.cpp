@@ -306,6 +306,8 @@ PYBIND11_MODULE(_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("resident", &HipBiBfs::resident)
       .def_property("auto_handoff", &HipBiBfs::auto_handoff, &HipBiBfs::set_auto_handoff)
+      .def_property("auto_gate_timeout_us", &HipBiBfs::auto_gate_timeout_us, &HipBiBfs::set_auto_gate_timeout_us)
+      .def_property_readonly("auto_gate_misses", &HipBiBfs::auto_gate_misses)
       .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
       .def_property_readonly("last_batch_fallbacks", &HipBiBfs::last_batch_fallbacks)
       .def("set_batch_tuning", &HipBiBfs::set_batch_tuning, py::arg("lds_first") = -1, py::arg("threads") = 0)
@@ -331,6 +333,7 @@ PYBIND11_MODULE(_native, m) {
       .def("synchronize", &HipBiBfs::synchronize, py::call_guard<py::gil_scoped_release>());
 
   // ---------------------------------------------------------------- multi-GPU engine
+  m.def("gpu_count", &gpu_count);
   m.def("rccl_unique_id", []() {
     auto id = dist_unique_id();
     return py::bytes(reinterpret_cast<const char*>(id.data()), id.size());

@@ -18,6 +18,7 @@
 #
 #   scripts/benchmark_test.sh [GRAPH_DIR]            (default graphs/)
 #   TIERS="v1 v3" REPEAT=20 NP=4 NGPU=1 scripts/benchmark_test.sh
+#   V3_FLAGS="" scripts/benchmark_test.sh   (v3 one launch per query instead of the resident server)
 set -uo pipefail
 
 ROOT="$(cd "$(dirname "${BASH_SOURCE[0]}")/.." && pwd)"
@@ -44,7 +45,7 @@ tool_cmd() {  # tier graph.bin src dst -> command line
   case $tier in
     v1) echo "$BIN/bibfs_serial $g $s $d --repeat $REPEAT" ;;
     v2) echo "$MPIEXEC -n $NP $BIN/second_try $g $s $d --repeat $REPEAT" ;;
-    v3) echo "$BIN/bibfs_hip $g $s $d --repeat $REPEAT --warmup $WARMUP" ;;
+    v3) echo "$BIN/bibfs_hip $g $s $d --repeat $REPEAT --warmup $WARMUP ${V3_FLAGS---resident}" ;;
     v4) echo "$MPIEXEC -n $NGPU $BIN/mpi_bibfs $g $s $d --repeat $REPEAT --warmup $WARMUP" ;;
     *) return 1 ;;
   esac

@@ -91,3 +91,19 @@ def test_secondary_errors_listed_without_touching_the_headline():
     assert out["detail"]["secondary_errors"] == ["gnp:1000000::2", "kron:22:16:1", "kron:30:16:1"]
     assert out["value"] == 36.0
     assert bench.report(_args(), 1, _head(), {}, {})["detail"]["secondary_errors"] == []
+
+
+def test_reporting_hygiene_fields_and_exit_status():
+    """Round-4 reporting fields: the headline carries the timed loop's tiny-
+    server fallbacks; a partitioned entry reports communicator bootstrap
+    apart from the graph build; wrong answers always fail the run."""
+    head = dict(_head(), tiny_overflows=3)
+    part = {"gnp:1000000::2": {"verified": True, "comm_init_ms": 3650.0, "build_ms": 70.0}}
+    out = bench.report(_args(), 1, head, {}, part)
+    assert out["detail"]["tiny_overflows"] == 3
+    p = out["detail"]["partitioned"]["gnp:1000000::2"]
+    assert "comm_init_ms" in p and "build_ms" in p
+    assert bench.exit_status(part, False, False) == 0
+    assert bench.exit_status({"x": {"verified": False}}, False, False) == 5
+    assert bench.exit_status({"x": {"error": "timeout"}}, True, False) == 0
+    assert bench.exit_status({"x": {"error": "timeout"}}, True, True) == 4

@@ -344,6 +344,36 @@ def test_resident_auto_handoff_vs_oracle(gpu_engine, spec):
         gpu_engine.set_resident(False)
 
 
+def test_auto_handoff_gate_timeout_falls_back_to_host(gpu_engine):
+    """The gated first grid level gives up when its search has not left LDS in
+    time (forced here: a zero wait).  Such a search still hands off later; the
+    host must then see the auto chain drain unpublished and continue like a
+    non-auto hand-off (scatter + host levels from the mirror) -- every answer
+    against the oracle, and the fallback counted."""
+    g = bb.from_spec("gnp:3000000::4")
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 24, 9)
+    truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
+    gpu_engine.set_resident(True)
+    m0 = gpu_engine.auto_gate_misses
+    try:
+        gpu_engine.auto_gate_timeout_us = 0.0
+        handed = 0
+        for (s, d), h in zip(pairs, truth):
+            r = gpu_engine.search(s, d)
+            check_result(g.csr, s, d, r.hops, r.path, h)
+            handed += bool(r.handoff)
+        assert handed > 0, "expected searches that leave LDS"
+        assert gpu_engine.auto_gate_misses > m0, "the host fallback never ran"
+        gpu_engine.auto_gate_timeout_us = 6e6  # back to the default: the next searches are fine too
+        for (s, d), h in zip(pairs[:8], truth[:8]):
+            hops, path = gpu_engine.query(s, d)
+            check_result(g.csr, s, d, hops, path, h)
+    finally:
+        gpu_engine.auto_gate_timeout_us = 6e6
+        gpu_engine.set_resident(False)
+
+
 # ---------------------------------------------------------------- tiny server
 def test_tiny_server_query_vs_oracle(gpu_engine):
     """Resident small-graph server (tiny_engine.hip): hops + path of query()

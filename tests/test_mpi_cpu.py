@@ -55,3 +55,16 @@ def test_mpi_rmat():
     for s, d in [(1, 2), (7, 4000), (100, 3000)]:
         out = run_json("second_try", "rmat:4096:30000:2", s, d, 3)
         assert out["hops"] == native.bfs_oracle(g.csr, s, d).hops
+
+
+def test_mpi_bibfs_more_ranks_than_gpus_fails_clearly():
+    """mpi_bibfs is one rank per GPU: a launch with more ranks on the node than
+    visible GPUs (every rank here: no GPU at all, or np 3 on a 1-GPU box) ends
+    with one clear message on the over-subscribed ranks and rc 1 -- no raw HIP
+    error, no rank left waiting in RCCL bootstrap."""
+    from bidirectional_bfs_amd.parallel import gpu_count
+
+    np_ = gpu_count() + 2
+    r = run_mpi("mpi_bibfs", ["gnp:1000::1", 0, 999], np=np_, timeout=60)
+    assert r.returncode != 0
+    assert "one rank per GPU" in r.stderr and "ranks on this node > GPUs" in r.stderr

@@ -36,6 +36,24 @@ int main(int argc, char** argv) {
   int rc = 0;
   try {
     const int device = a.has("device") ? (int)a.geti("device", 0) : local_rank_from_env(rank);
+    // One rank per GPU (the reference ran 4-6 ranks on 1-2 GPUs, v4/Makefile:64,
+    // README.md:16; here a rank owns a GPU's HBM and its RCCL endpoint).  Every
+    // rank checks its device and the verdict is agreed on before any rank
+    // touches RCCL, so a bad launch fails with one clear message, not a raw
+    // HIP error on some ranks and a hang on the others.
+    const int ndev = bibfs::gpu_count();
+    int bad = (device < 0 || device >= ndev) ? 1 : 0, any_bad = 0;
+    MPI_Allreduce(&bad, &any_bad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+    if (any_bad) {
+      if (bad)
+        std::fprintf(stderr,
+                     "[rank %d] mpi_bibfs runs one rank per GPU: this rank maps to device %d but only %d GPU(s) "
+                     "are visible (ranks on this node > GPUs); launch with at most %d ranks per node or pass "
+                     "--device\n",
+                     rank, device, ndev, ndev);
+      MPI_Finalize();
+      return 1;
+    }
     std::vector<uint8_t> uid(128);
     if (rank == 0) uid = bibfs::dist_unique_id();
     int len = (int)uid.size();
