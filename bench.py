@@ -66,8 +66,10 @@ def parse_args(argv=None):
                     help="comma-separated secondary configs reported under 'extra' (empty to skip)")
     ap.add_argument("--dist-graphs", default="gnp:1000000::2,kron:22:16:1,kron:auto",
                     help="configs run through the partitioned RCCL engine at every N (empty to skip); "
-                         "kron:auto = the world-scaled Kronecker graph kron:min(30, 27 + log2 N):16 "
-                         "(~17 GB CSR shard per GPU at every N; 137 GB of columns at N = 8)")
+                         "kron:auto = Kronecker 27 (2.15B edges, ~17 GB of CSR) on one GPU, and for N >= 2 "
+                         "Kronecker 30 with the edge factor that makes the CSR ~1.35x ONE GPU's HBM (a graph "
+                         "no single MI355X can hold: edge factor 44, ~390 GB, on 288 GB parts), verified "
+                         "without any single-GPU copy")
     ap.add_argument("--dist-steps", type=int, default=20)
     ap.add_argument("--secondary-timeout", type=float, default=420.0,
                     help="seconds allowed for the extra + partitioned configs together; past it the "
@@ -141,13 +143,30 @@ def parse_spec(spec: str):
     raise ValueError(f"bench graph spec must be gnp:/rmat:/kron:, got {spec!r}")
 
 
-def world_scaled(spec: str, world: int) -> str:
-    """kron:auto -> the Kronecker scale that keeps the CSR shard per GPU at
-    ~17 GB (scale 27 on one GPU, +1 per doubling of N, capped at 30)."""
+HBM_DEFAULT = 288 * 10**9  # MI355X HBM3E per GPU (used when the device does not say)
+
+
+def csr_bytes(spec: str) -> int:
+    """Device bytes of the whole graph's CSR (u64 row offsets, u32 columns, both directions)."""
+    kind, n, arg, _ = parse_spec(spec)
+    m = int(arg) if kind == "rmat" else int(arg * n * (n - 1) / 2)
+    return 8 * (n + 1) + 4 * 2 * m
+
+
+def world_scaled(spec: str, world: int, hbm_bytes: int = HBM_DEFAULT) -> str:
+    """kron:auto -> Kronecker 27 (2.15B edges, ~17 GB CSR) on one GPU, where the
+    single-GPU engine is the reference; for N >= 2 a graph NO single GPU can
+    hold: Kronecker 30 with the edge factor that makes the CSR ~1.35x one
+    GPU's HBM (edge factor 44, ~390 GB on 288 GB parts), capped so a rank's
+    shard stays within ~70% of its HBM."""
     if spec != "kron:auto":
         return spec
-    scale = min(30, 27 + max(0, int(world).bit_length() - 1))
-    return f"kron:{scale}:16:1"
+    if world <= 1:
+        return "kron:27:16:1"
+    unit = 8 * (1 << 30)  # CSR bytes per unit of edge factor at scale 30 (4 B x 2 directions x 2^30)
+    ef = int((1.35 * hbm_bytes - 8 * (1 << 30)) // unit)
+    ef = min(ef, int((0.7 * hbm_bytes * world - 8 * (1 << 30)) // unit))
+    return f"kron:30:{max(16, ef)}:1"
 
 
 def generate(eng, spec: str):
@@ -445,24 +464,37 @@ def main(argv=None) -> int:
 
     def run_partitioned(spec: str, steps: int, warmup: int):
         """Strong scaling: the graph sharded over all ranks, one collective search per query.
-        Pairs and their hop counts come from the single-GPU engine on the same graph."""
+        Where the graph fits one GPU, pairs, hop counts and the speedup come
+        from the single-GPU engine on the same graph; a graph that does not
+        (kron:auto at N >= 2) is verified without any single-GPU copy: pairs
+        picked by the partitioned engine, every checked path validated edge by
+        edge by the owners of its vertices, and hop counts cross-checked by a
+        unidirectional partitioned BFS."""
         _, n, _, seed = parse_spec(spec)
-        ref = generate(HipEngine(local), spec)
-        pairs = pick_pairs(ref, n, min(a.pairs, steps + warmup), 12345)
-        assert pairs, f"no connected pairs found in {spec}"
-        # the single-GPU engine on the same graph and pairs (resident serving),
-        # so every partitioned entry states its speedup over one GPU
-        ref.set_resident(True)
-        for i in range(warmup):
-            ref.query(*pairs[i % len(pairs)][:2])
-        ts = time.perf_counter()
-        for i in range(steps):
-            s_, d_, h_ = pairs[(warmup + i) % len(pairs)]
-            assert ref.query(s_, d_)[0] == h_
-        single_ms = max_over_ranks((time.perf_counter() - ts) * 1e3 / steps)
-        ref.set_resident(False)
-        ref.release()
-        del ref
+        hbm_total = torch.cuda.mem_get_info(dev)[1]
+        fits = csr_bytes(spec) <= 0.6 * hbm_total
+        single_ms, single_reason, pairs = None, None, None
+        npairs = min(a.pairs, steps + warmup)
+        if fits:
+            ref = generate(HipEngine(local), spec)
+            pairs = pick_pairs(ref, n, npairs, 12345)
+            assert pairs, f"no connected pairs found in {spec}"
+            # the single-GPU engine on the same graph and pairs (resident serving),
+            # so every partitioned entry states its speedup over one GPU
+            ref.set_resident(True)
+            for i in range(warmup):
+                ref.query(*pairs[i % len(pairs)][:2])
+            ts = time.perf_counter()
+            for i in range(steps):
+                s_, d_, h_ = pairs[(warmup + i) % len(pairs)]
+                assert ref.query(s_, d_)[0] == h_
+            single_ms = max_over_ranks((time.perf_counter() - ts) * 1e3 / steps)
+            ref.set_resident(False)
+            ref.release()
+            del ref
+        else:
+            single_reason = (f"the graph's CSR ({csr_bytes(spec) / 1e9:.0f} GB) does not fit one GPU's HBM "
+                             f"({hbm_total / 1e9:.0f} GB): there is no single-GPU run to compare with")
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
@@ -474,6 +506,9 @@ def main(argv=None) -> int:
         free_b, total_b = torch.cuda.mem_get_info(dev)
         hbm_used = total_b - free_b
         m = eng.m
+        if pairs is None:  # picked by the partitioned engine itself (collective searches)
+            pairs = pick_pairs(eng, n, npairs, 12345)
+            assert pairs, f"no connected pairs found in {spec}"
         wrong = []
 
         def query(i):
@@ -503,16 +538,22 @@ def main(argv=None) -> int:
             "engine": f"DistBiBfs/{eng.backend}", "ranks": world, "rccl_ranks": eng.world,
             "n": n, "m": m, "seed": seed, "comm_init_ms": round(comm_init_ms, 3), "build_ms": round(build_ms, 3),
             "local_nnz_max": int(max_over_ranks(float(eng.local_nnz))),
-            # per-rank HBM: the CSR shard, and the generator's peak (shard + one
-            # cursor array: the edge list is never materialised on any rank)
+            "csr_bytes_total": csr_bytes(spec), "hbm_bytes_per_gpu": int(hbm_total), "fits_one_gpu": fits,
+            # per-rank HBM, measured: the CSR shard; the most the rank held at
+            # once during the build (shard + generator temporaries + search
+            # state, counted per allocation) and the device's free-memory drop
+            # over it (hipMemGetInfo low-water mark); what it holds for search
             "shard_bytes_max": int(max_over_ranks(float(eng.shard_bytes))),
             "gen_peak_bytes_max": int(max_over_ranks(float(eng.gen_peak_bytes))),
+            "gen_hbm_peak_bytes_max": int(max_over_ranks(float(eng.gen_hbm_peak_bytes))),
+            "resident_bytes_max": int(max_over_ranks(float(eng.resident_bytes))),
             "hbm_used_bytes_max": int(max_over_ranks(float(hbm_used))),
             "queries": steps, "ms_per_query": round(dt * 1e3 / steps, 5),
             "median_query_ms_rank0": round(sorted(qt)[len(qt) // 2] * 1e3, 5),
             "max_query_ms_rank0": round(max(qt) * 1e3, 5),
-            "single_gpu_ms": round(single_ms, 5),
-            "speedup_vs_single_gpu": round(single_ms / (dt * 1e3 / steps), 4),
+            "single_gpu_ms": round(single_ms, 5) if single_ms is not None else None,
+            "speedup_vs_single_gpu": round(single_ms / (dt * 1e3 / steps), 4) if single_ms is not None else None,
+            "single_gpu_reason": single_reason,
             "gteps": m * steps / dt / 1e9,
             "device_ms_per_query": round(sum(r.search_ms for r, _ in done) / steps, 5),
             "mean_hops": sum(r.hops for r, _ in done) / steps,
@@ -526,10 +567,73 @@ def main(argv=None) -> int:
             "dense_levels_per_query": sum(s["dense_levels"] for s in st) / steps,
             "verified": ok, "checked_queries": steps + warmup,
         }
+        # distributed verification (untimed, no graph copy anywhere): each
+        # checked path edge looked up by the owner of its first vertex, and the
+        # hop counts re-derived by a unidirectional partitioned BFS
+        nchk = min(len(pairs), 8)
+        bad_paths, bad_hops = 0, 0
+        for i in range(nchk):
+            s_, d_, h_ = pairs[i]
+            r = eng.search(s_, d_)
+            if not eng.validate_path(s_, d_, r.hops, list(r.path)):
+                bad_paths += 1
+            if i < 3 and eng.search_unidirectional(s_, d_).hops != h_:
+                bad_hops += 1
+        dist_ok = all_ranks_ok(bad_paths == 0 and bad_hops == 0)
+        out["verification"] = {
+            "pairs_from": "single-GPU engine" if fits else "partitioned engine",
+            "hops_vs_single_gpu": fits,
+            "paths_checked_distributed": nchk, "bad_paths": bad_paths,
+            "unidirectional_bfs_checked": min(nchk, 3), "bad_hops": bad_hops}
+        out["verified"] = ok and dist_ok
+        # per-round split (untimed): device stamps at the entry and exit of
+        # every speculative round's kernels -> kernel time vs the gaps the
+        # candidate exchange and the status allgather leave
+        out.update(round_split(eng, query, warmup, min(steps, 8)))
+        if world > 1:
+            # the same timed loop with DistTuning.overlap on (side 0's exchange
+            # overlapping side 1's expansion), side by side with the default
+            eng.set_tuning(overlap=True)
+            for i in range(2):
+                query(i)
+            eng.barrier()
+            barrier()
+            t1 = time.perf_counter()
+            for i in range(steps):
+                query(warmup + i)
+            eng.barrier()
+            dto = max_over_ranks(time.perf_counter() - t1)
+            ov = {"ms_per_query": round(dto * 1e3 / steps, 5),
+                  "speedup_vs_overlap_off": round(dt / dto, 4)}
+            ov.update(round_split(eng, query, warmup, min(steps, 8), overlap=True))
+            out["overlap_on"] = ov
+            eng.set_tuning()
+            out["verified"] = all_ranks_ok(not wrong) and dist_ok
+        else:
+            out["overlap_on"] = None  # one rank: nothing is exchanged, nothing to overlap
         if wrong:
             out["mismatch"] = wrong[:4]
         eng.release()
         return out, eng.world
+
+    def round_split(eng, query, first: int, count: int, overlap: bool = False) -> dict:
+        eng.set_tuning(stamps=True, overlap=overlap)
+        acc = {"stamped_rounds": 0, "expand_us": 0.0, "claim_us": 0.0, "exchange_us": 0.0, "status_us": 0.0}
+        for i in range(count):
+            query(first + i)
+            st = eng.last_stats
+            for k in acc:
+                acc[k] += st[k]
+        eng.set_tuning(overlap=overlap)
+        nr = acc["stamped_rounds"]
+        if not nr:
+            return {"stamped_rounds_per_query": 0.0}
+        per = {k: round(max_over_ranks(acc[k] / nr), 3) for k in ("expand_us", "claim_us", "exchange_us", "status_us")}
+        return {"stamped_rounds_per_query": nr / count,
+                "kernel_us_per_round": round(per["expand_us"] + per["claim_us"], 3),
+                "exchange_us_per_round": per["exchange_us"],
+                "status_us_per_round": per["status_us"],
+                "expand_us_per_round": per["expand_us"], "claim_us_per_round": per["claim_us"]}
 
     if a.mode == "partitioned":
         ph, rccl_ranks = run_partitioned(a.graph, a.steps, a.warmup)
@@ -576,7 +680,7 @@ def main(argv=None) -> int:
             failed = True
     if a.mode == "replicated" and (world == 1 or (a.dist_backend == "nccl" and not shared_gpu)):
         for spec in filter(None, a.dist_graphs.split(",")):
-            spec = world_scaled(spec, world)
+            spec = world_scaled(spec, world, torch.cuda.mem_get_info(dev)[1])
             partitioned[spec] = None
             try:
                 partitioned[spec], state["rccl_ranks"] = run_partitioned(spec, a.dist_steps, 3)

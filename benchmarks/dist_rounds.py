@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Where a partitioned round's time goes: kernel vs exchange, per round.
+
+P ranks run as threads of this process on ONE GPU (the in-process local
+group, csrc/dist/comm.hip), each generating its own CSR shard, with
+DistTuning.stamps on: every speculative round records s_memrealtime at the
+entry and the last-workgroup exit of its expansion launch(es) and of its
+claim launch (csrc/dist/dist_engine.hip, RoundStamp).  Per round:
+
+  expand_us    k_spec_expand (+ k_td_hubs) on this rank
+  claim_us     k_spec_claim
+  exchange_us  expansion end -> claim start: the owner-addressed candidate
+               exchange (here device-to-device copies between the ranks'
+               streams; RCCL send/recv on a node) plus the launch gap
+  status_us    claim end -> next expansion start: the status allgather plus
+               the launch gap
+
+Rank 0's numbers, median over queries of the per-round means.  The ranks
+share the GPU's CUs, so kernel times are an upper bound for one rank per
+GPU; the exchange column is the local group's copies, not xGMI.
+
+    python benchmarks/dist_rounds.py --specs gnp:1000000::2,kron:22 --ranks 1,2,4 --overlap 0,1
+"""
+import argparse
+import json
+import random
+import statistics
+import sys
+
+import torch  # noqa: F401  (binds the HIP runtime first)
+
+sys.path.insert(0, __file__.rsplit("/benchmarks/", 1)[0])
+from bidirectional_bfs_amd.models import parse_spec  # noqa: E402
+from bidirectional_bfs_amd.parallel import dist_local_generate_run, make_tuning  # noqa: E402
+
+
+def per_round(stats, key):
+    vals = [st[key] / st["stamped_rounds"] for st in stats if st["stamped_rounds"]]
+    return round(statistics.median(vals), 3) if vals else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--specs", default="gnp:1000000::2,kron:22")
+    ap.add_argument("--ranks", default="1,2,4")
+    ap.add_argument("--overlap", default="0,1")
+    ap.add_argument("--queries", type=int, default=24)
+    ap.add_argument("--seed", type=int, default=7)
+    ap.add_argument("--solo", type=int, default=1, help="P = 1: 0 runs the multi-workgroup rounds (stampable)")
+    a = ap.parse_args()
+    for spec in a.specs.split(","):
+        _, n, _, _ = parse_spec(spec)
+        rnd = random.Random(a.seed)
+        qs = [(rnd.randrange(n), rnd.randrange(n)) for _ in range(a.queries)]
+        for ranks in [int(x) for x in a.ranks.split(",")]:
+            for ov in [int(x) for x in a.overlap.split(",")]:
+                if ov and ranks == 1:
+                    continue
+                tun = make_tuning(stamps=True, overlap=bool(ov), solo=bool(a.solo))
+                rs, t = dist_local_generate_run(ranks, spec, qs, tuning=tun)
+                keep = [(r, ms, st) for r, ms, st in zip(rs, t["query_ms"], t["stats"]) if r.found and r.hops > 0]
+                sts = [st for _, _, st in keep]
+                rec = {
+                    "spec": spec, "ranks": ranks, "overlap": bool(ov), "queries": len(keep),
+                    "median_query_ms": round(statistics.median(ms for _, ms, _ in keep), 4) if keep else None,
+                    "mean_rounds": round(statistics.mean(st["rounds"] for st in sts), 2) if sts else None,
+                    "mean_stamped_rounds": round(statistics.mean(st["stamped_rounds"] for st in sts), 2) if sts else None,
+                    "expand_us_per_round": per_round(sts, "expand_us"),
+                    "claim_us_per_round": per_round(sts, "claim_us"),
+                    "exchange_us_per_round": per_round(sts, "exchange_us"),
+                    "status_us_per_round": per_round(sts, "status_us"),
+                    "host_rounds": sum(st["host_rounds"] for st in sts),
+                    "solo_rounds": sum(st["solo_rounds"] for st in sts),
+                }
+                if rec["expand_us_per_round"] is not None:
+                    rec["kernel_us_per_round"] = round(rec["expand_us_per_round"] + (rec["claim_us_per_round"] or 0), 3)
+                print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -40,7 +40,8 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                 nosync_bytes: Optional[int] = None, timeout_s: Optional[float] = None,
                 walk_max: Optional[int] = None, solo: Optional[bool] = None,
                 solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
-                overlap: Optional[bool] = None, spec_stall_edges: Optional[int] = None) -> "native.DistTuning":
+                overlap: Optional[bool] = None, spec_stall_edges: Optional[int] = None,
+                stamps: Optional[bool] = None, hbm_cap_bytes: Optional[int] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
 
     solo (one rank only): run the small rounds in one persistent workgroup
@@ -54,12 +55,21 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
 
     overlap (more than one rank): the two sides of a speculative round expand
     as separate launches (side 1 on the compute stream) so side 0's exchange
-    overlaps side 1's expansion."""
+    overlaps side 1's expansion.
+
+    stamps: per-round device stamps; ``last_stats`` then splits the
+    speculative rounds into ``expand_us`` / ``claim_us`` (kernels) and
+    ``exchange_us`` / ``status_us`` (the gaps the two collectives and the
+    launches leave), summed over ``stamped_rounds``.  Diagnostics: one extra
+    host wait and a copy per search.
+
+    hbm_cap_bytes: a build that would make a rank hold more device memory
+    than this throws (rehearses "does not fit one GPU" at small scale)."""
     t = native.DistTuning()
     for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
                  ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap),
-                 ("spec_stall_edges", spec_stall_edges)):
+                 ("spec_stall_edges", spec_stall_edges), ("stamps", stamps), ("hbm_cap_bytes", hbm_cap_bytes)):
         if v is not None:
             setattr(t, k, v)
     return t
@@ -138,6 +148,28 @@ class DistEngine:
         shard plus one cursor array (the edge list is never materialised)."""
         return self._e.gen_peak_bytes
 
+    @property
+    def gen_hbm_peak_bytes(self) -> int:
+        """The device's free-memory drop over the last build (hipMemGetInfo
+        low-water mark); equals gen_peak_bytes up to allocator granularity
+        with one rank per GPU."""
+        return self._e.gen_hbm_peak_bytes
+
+    @property
+    def resident_bytes(self) -> int:
+        """Device bytes this rank holds now (shard + search state)."""
+        return self._e.resident_bytes
+
+    def validate_path(self, src: int, dst: int, hops: int, path) -> bool:
+        """Collective: each path edge looked up by the owner of its first
+        vertex, one sum-allreduce (no copy of the graph anywhere)."""
+        return bool(self._e.validate_path(int(src), int(dst), int(hops), [int(v) for v in path]))
+
+    def search_unidirectional(self, src: int, dst: int):
+        """Collective: a plain partitioned BFS from src (hop count only), an
+        independent check of the bidirectional engine's distance."""
+        return self._e.search_unidirectional(int(src), int(dst))
+
     def allreduce_max(self, x: float) -> float:
         return self._e.allreduce_max(float(x))
 
@@ -193,18 +225,21 @@ def dist_local_run(ranks: int, graph: Graph, queries: Sequence, device: int = 0,
 
 
 def dist_local_generate_run(ranks: int, spec: str, queries: Sequence, device: int = 0, options=None, tuning=None,
-                            **kw):
+                            verify: int = 0, **kw):
     """Like :func:`dist_local_run`, but every rank generates ``spec``
     (``gnp:``/``rmat:``/``kron:``) on the device and keeps only its own CSR
     shard, as the multi-GPU bench does.  Returns ``(results, timing)`` with
-    ``timing = {"build_ms", "query_ms": [rank 0 wall per query], "local_nnz": [per rank]}``.
+    ``timing = {"build_ms", "query_ms": [rank 0 wall per query], "local_nnz": [per rank], ...}``.
+    ``verify`` > 0: every found path is also checked collectively
+    (``timing["path_valid"]``) and the first ``verify`` queries are re-run as
+    a unidirectional partitioned BFS (``timing["uni_hops"]``).
     """
     if options is None:
         options = make_options(**kw) if kw else _DEFAULT_OPTIONS
     kind, n, arg, seed = parse_spec(spec)
     q = [(int(s), int(d)) for s, d in queries]
     return native.dist_local_generate_run(int(ranks), int(device), kind, n, float(arg), seed, q, options,
-                                          tuning if tuning is not None else native.DistTuning())
+                                          tuning if tuning is not None else native.DistTuning(), int(verify))
 
 
 class ReplicatedServer:

@@ -49,6 +49,7 @@
 #include "bibfs/trace.hpp"
 #include "comm.hpp"
 #include "device.hpp"
+#include "devmem.hpp"
 
 namespace bibfs {
 
@@ -82,6 +83,11 @@ constexpr uint32_t kTraceCap = 4096;            // rounds recorded with SearchOp
 constexpr uint32_t kPlanRing = 64;              // pinned per-round plan words (lookahead < this)
 constexpr int kStageRanks = 16;                 // gathered reductions staged in LDS up to this many ranks
 constexpr uint32_t kOwnerCapMin = 256;          // smallest owner-addressed candidate block (pairs)
+// Small rounds at P > 1 (one workgroup per rank, see small_expand):
+constexpr uint32_t kSmallE = 1024;              // frontier edges per side (any rank)
+constexpr uint32_t kSmallV = 512;               // frontier vertices per side (all ranks) staged in LDS
+constexpr uint32_t kSmallClaim = 2048;          // candidates (all senders, both sides) one block claims
+constexpr int kSmallU = 4;                      // items per thread in flight per pass
 
 // Search control state: identical on every rank (computed from reduced
 // values only).  Double-buffered by round parity: round `it` reads
@@ -116,7 +122,7 @@ struct Ctl {
   uint32_t cont;               // sides THIS round continues: re-offer their spilled candidates (no expansion)
   uint32_t cont_due;           // sides whose level is incomplete (spilled candidates wait to be offered)
   uint32_t cont_rounds;        // continuation rounds run
-  uint32_t pad3;
+  uint32_t lost;               // a rank's spill list overflowed (candidates dropped): the search failed
 };
 
 struct Policy {
@@ -126,6 +132,8 @@ struct Policy {
   int lockstep, side, direction;
   uint32_t epoch;     // search number: tags the plan words (a late no-op round of the previous search never matches)
   uint32_t walk_cap;  // words of the pinned path buffer (one rank: the round that ends the search walks the path)
+  uint32_t spill_cap; // candidates a rank's spill list holds per side (DView::spill_cap)
+  int source_only;    // unidirectional BFS from src (DistBiBfs::search_unidirectional): side 0 expands alone
   int want_path;
 };
 
@@ -136,7 +144,10 @@ struct Reduced {
   unsigned long long nfmax[2]; // ~(this rank's degree sum of side s's new frontier): min = ~max over ranks
   uint32_t maxsend[2];         // candidates of side s on this rank (max; host-planned rounds)
   uint32_t md[2];              // depth of the meet vertex from each root (owner contributes; min)
-  uint32_t pad[2];
+  // candidates of side s one rank tried to spill this round (max): above the
+  // spill list's capacity some were DROPPED and the level would be incomplete,
+  // so the plan ends the search as an error (Ctl::lost) instead of going on
+  uint32_t spillmax[2];
   unsigned long long spill[2]; // candidates of side s that did not fit their owner's block (sum)
   unsigned long long nocmax;   // ~(largest candidate count this rank addressed to one owner): min = ~max
 };
@@ -148,6 +159,16 @@ struct RoundRec {
   unsigned long long cnt[2], fed[2];  // expanded frontiers (vertices, degree sum)
   unsigned long long sums[4];         // discovered: [2s] vertices, [2s+1] their degree sum
   unsigned long long meetkey;
+};
+
+// Per-round device stamps (DistTuning::stamps): s_memrealtime (100 MHz) at
+// the entry of the round's expansion launch(es) and of its claim launch, and
+// when their last workgroup finishes -- so the host can split a round into
+// kernel time and the gaps the exchanges (and launch latencies) leave between
+// the kernels.  eb1/ee1: the side-1 launch of a split (overlap) round.
+struct RoundStamp {
+  unsigned long long eb, ee, cb, ce, eb1, ee1;
+  uint32_t tag, pad;
 };
 
 struct DState {
@@ -202,6 +223,7 @@ struct DView {
   uint32_t* host_walk;        // pinned: {status, dS, dT, epoch, path[]} (one rank, the same round)
   struct RoundRec* trace;     // per-round record (SearchOptions::trace), or nullptr
   uint32_t trace_cap;
+  RoundStamp* rstamp;         // [kTraceCap] per-round stamps (DistTuning::stamps), or nullptr
   Reduced* red;               // [2] this rank's values of a round (claims min the meet key here)
   // [2] x P: every rank's `red` of a round, allgathered (ONE collective per
   // round's reduction); readers reduce them (reduce_gathered).  One rank:
@@ -238,6 +260,7 @@ __device__ void reduce_gathered(const Reduced* g, int P, Reduced& out) {
       r.nfmax[s] = min(r.nfmax[s], x.nfmax[s]);
       r.maxsend[s] = max(r.maxsend[s], x.maxsend[s]);
       r.md[s] = min(r.md[s], x.md[s]);
+      r.spillmax[s] = max(r.spillmax[s], x.spillmax[s]);
     }
   }
   out = r;
@@ -312,6 +335,13 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
       // offers them before anything else is decided -- the level's meets
       // are only complete (and its minimum exact) once they are claimed.
       c.pkey = min(p.pkey, rd.meetkey);
+      if (rd.spillmax[0] > pol.spill_cap || rd.spillmax[1] > pol.spill_cap) {
+        // candidates were dropped (emit_owned_pair): the level is incomplete,
+        // so neither a meet nor "no path" from here on would be exact
+        c.lost = 1;
+        c.state = kDead;
+        return;
+      }
       c.cont_due = (rd.spill[0] ? 1u : 0u) | (rd.spill[1] ? 2u : 0u);
       if (!c.cont_due) {
         if (c.pkey != kNoKey) {
@@ -340,7 +370,9 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
       return;
     }
     const unsigned long long flo = min(c.fed[0], c.fed[1]), fhi = max(c.fed[0], c.fed[1]);
-    if (pol.lockstep && pol.side != (int)SidePolicy::kAlternate &&
+    if (pol.source_only) {
+      want = 1;  // a plain BFS from src: it ends when it claims dst (held by side 1 at depth 0)
+    } else if (pol.lockstep && pol.side != (int)SidePolicy::kAlternate &&
         (fhi <= kLockstepEdges || (fhi <= 2 * flo && fhi <= kLockstepMaxEdges))) {
       want = 3;
     } else if (pol.side == (int)SidePolicy::kAlternate) {
@@ -512,8 +544,11 @@ __device__ __forceinline__ void emit_owned_pair(const DView& V, int s, uint32_t 
   if (pos < oe.cap) {
     reinterpret_cast<uint2*>(V.sendbuf + ((size_t)s * V.P + o) * oe.bw)[1 + pos] = make_uint2(v, u);
   } else {
+    // (a rank's candidates of a level never exceed the list while its frontier
+    // edges stay within round_edge_cap(); if they ever do, the count still
+    // grows past the cap and the next plan fails the search: Ctl::lost)
     const uint32_t q = atomicAdd(oe.spill_n, 1u);
-    if (q < V.spill_cap) oe.spill[q] = make_uint2(v, u);  // (a rank's candidates of a level never exceed it)
+    if (q < V.spill_cap) oe.spill[q] = make_uint2(v, u);
   }
 }
 
@@ -677,6 +712,7 @@ __device__ void spec_round_end(const DView& V, uint32_t it, uint32_t sides, uint
     } else {
       V.red[p].spill[s] = on ? st->spill_n[s][cur] : 0ull;
     }
+    V.red[p].spillmax[s] = (uint32_t)min(V.red[p].spill[s], 0xffffffffull);
     st->hub_count[s] = 0;
   }
   V.red[p].nocmax = ~(unsigned long long)atomicExch(&st->ocmax, 0u);
@@ -748,6 +784,29 @@ __device__ void terminal_walk(const DView& V, unsigned long long key, const Poli
 
 // ---- speculative round kernels ---------------------------------------------
 
+// Small rounds (P > 1): the whole rank's expansion / claims by one workgroup
+// (defined with the solo kernel's helpers below).  The tests are grid-uniform:
+// every block computed the same plan.
+__device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr);
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap);
+__device__ __forceinline__ bool small_expand_ok(const Ctl& c, int P) {
+  if (c.cont || !c.sides || P > kStageRanks) return false;
+  for (int s = 0; s < 2; ++s)
+    if (((c.sides >> s) & 1) && (c.fmax[s] > kSmallE || c.cnt[s] > kSmallV)) return false;
+  return true;
+}
+__device__ __forceinline__ bool small_claim_ok(const Ctl& c, int P) {
+  if (c.cont || !c.sides || P > kStageRanks) return false;
+  unsigned long long most = 0;  // a sender's block of side s holds at most its frontier edges of s
+  for (int s = 0; s < 2; ++s)
+    if ((c.sides >> s) & 1) most += c.fmax[s];
+  return most * (unsigned long long)P <= kSmallClaim;
+}
+
+__device__ __forceinline__ RoundStamp* round_stamp(const DView& V, uint32_t it) {
+  return V.rstamp ? V.rstamp + (it % kTraceCap) : nullptr;
+}
+
 // Plan (every block computes the same plan; block 0 publishes it) + top-down
 // pre phase of both sides (blockIdx.y = side) into blocks of `cap` pairs.
 // header = 0: k_td_hubs runs next (it writes the headers); finish: this
@@ -755,6 +814,7 @@ __device__ void terminal_walk(const DView& V, unsigned long long key, const Poli
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
                                                           int flags, uint64_t hub_deg, int header, int finish,
                                                           uint32_t ocap, int side0, int nsides, uint32_t plan_cap) {
+  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   const int p = it & 1;
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
@@ -809,6 +869,25 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // a round enqueued past the end of the search: nothing to expand, no round
   // end (every block sees the same plan, so no block counts itself in)
   if (terminal) return;
+  if (RoundStamp* rs = round_stamp(V, it); rs && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (side0 == 0) {
+      rs->eb = t_in;
+      rs->tag = plan_tag(pol.epoch, it);
+      if (nsides == 2) rs->eb1 = rs->ee1 = 0;
+    } else {
+      rs->eb1 = t_in;
+    }
+  }
+  if (ocap && header && nsides == 2 && small_expand_ok(c, V.P)) {  // small round: one workgroup
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      small_expand(V, c, it, ocap, fr);
+      if (RoundStamp* rs = round_stamp(V, it)) {
+        __syncthreads();
+        if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+    return;
+  }
   const int s = side0 + (int)blockIdx.y;
   OwnerEmit oe;
   if (ocap) {
@@ -851,6 +930,14 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
       if (ss == 0) atomicExch(&V.st->done_blocks[0], 0u);
     }
     if (finish && threadIdx.x == kWave) spec_round_end(V, it, c.sides, c.cont);  // another wave: the header atomics are independent
+    if (RoundStamp* rs = round_stamp(V, it)) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+        if (side0 == 0) rs->ee = t;
+        else rs->ee1 = t;
+      }
+    }
   }
 }
 
@@ -1013,6 +1100,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       z.key = z.pkey = kNoKey;
       pc = z;
       rd.spill[0] = rd.spill[1] = 0;
+      rd.spillmax[0] = rd.spillmax[1] = 0;
       rd.nocmax = ~0ull;
     }
     __syncthreads();
@@ -1210,6 +1298,7 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       }
       rd.meetkey = best;
       rd.spill[0] = rd.spill[1] = 0;
+      rd.spillmax[0] = rd.spillmax[1] = 0;
       rd.nocmax = ~0ull;
       pc = c;
       plan_next(it + 1);
@@ -1280,6 +1369,336 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
       vis[2 * (li >> 5)] = 0u;
       dep[li] = kEmpty;
     }
+  }
+}
+
+// ---- small rounds with more than one rank: ONE workgroup per rank ---------------
+// A sparse round's per-rank work at P > 1 is often a few hundred edges, yet
+// the multi-workgroup kernels pay a chain of device-scope round trips for it
+// (stamped, benchmarks/dist_rounds.py: G(1M) at P = 2 13 us of expansion and
+// 6 us of claims per round): queue / degree / candidate counters as global
+// atomics, last-block detection, owner headers by atomicExch.  When the plan
+// says the round is small (every expanding side at most kSmallE frontier
+// edges on any rank and kSmallV frontier vertices), block (0, 0) does the
+// whole rank's round alone: counters in LDS, claims and the `sent` test as
+// workgroup-scope atomics (performed in the CU's L2 -- no other workgroup
+// touches these words during the launch, and the kernel boundary publishes
+// them), the owner headers and the round state written once at the end.
+// Every block computes the same plan, so the choice is grid-uniform; the
+// other blocks return before touching any counter.
+
+struct SmallCtr {
+  uint32_t q[2];                 // queue entries this launch appended per side
+  unsigned long long ne[2];      // their degree sums
+  uint32_t oc[2][kStageRanks];   // candidates per (side, owner)
+  uint32_t sp[2];                // candidates per side that went to the spill list
+  unsigned long long best;       // meet key (min)
+  uint32_t found;                // a meet was claimed
+};
+
+__device__ __forceinline__ unsigned long long wg_fetch_or(unsigned long long* w, unsigned long long m) {
+  return __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t wg_fetch_or32(uint32_t* w, uint32_t m) {
+  return __hip_atomic_fetch_or(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Exclusive prefix of X[0, cnt) in place, X[cnt] = total (cnt <= 4 * kThreads,
+// whole block, values < 2^32): 4 consecutive entries per thread, one DPP
+// wave scan, the wave totals through LDS.
+__device__ void small_scan(uint32_t* X, uint32_t cnt) {
+  __shared__ uint32_t wt[kThreads / kWave];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint32_t v[4], run = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = 4 * tid + k;
+    v[k] = i < cnt ? X[i] : 0u;
+    run += v[k];
+  }
+  const uint32_t inc = dpp_scan(run);
+  if (lane == 63) wt[wid] = inc;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / kWave; ++w) {
+    pre += w < (int)wid ? wt[w] : 0u;
+    tot += wt[w];
+  }
+  uint32_t e = pre + inc - run;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t i = 4 * tid + k;
+    if (i < cnt) X[i] = e;
+    e += v[k];
+  }
+  if (tid == 0) X[cnt] = tot;
+  __syncthreads();
+}
+
+// Claim owned vertex v for side s (parent u, depth dn[s]) inside a small
+// round: the visited word by a workgroup-scope atomicOr (both sides' bits in
+// it), the meet by the other side's bit, queue appends and degree sums into
+// LDS.  Wave-cooperative (every lane calls it); the side is per lane, so one
+// call serves both sides of a lockstep round.  dcl[s]: the depth a claim of
+// the other side made in THIS round has (its depth store may not be visible).
+__device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const uint32_t* qbase, bool want, int s,
+                                            uint32_t v, uint32_t u, const uint32_t* dn, const uint32_t* dcl,
+                                            bool single) {
+  const uint32_t li = v - V.lo;
+  unsigned long long* const visw = reinterpret_cast<unsigned long long*>(V.vis[0]);
+  bool mine = false;
+  unsigned long long rb = 0, re = 0, best = kNoKey;
+  if (want) {
+    const unsigned long long m = 1ull << ((li & 31) + 32 * s);
+    const unsigned long long old = wg_fetch_or(visw + (li >> 5), m);
+    mine = !(old & m);
+    const bool other = (old >> ((li & 31) + 32 * (s ^ 1))) & 1ull;
+    if (mine) {
+      rb = V.row_off[li];
+      re = V.row_off[li + 1];
+      if (other) {
+        uint32_t dd = __hip_atomic_load(&pick(V.depth, s ^ 1)[li], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (dd == kEmpty) dd = s ? dcl[1] : dcl[0];
+        best = ((unsigned long long)((s ? dn[1] : dn[0]) + dd) << 32) | v;
+      }
+    }
+  }
+  if (__ballot(best != kNoKey)) {  // rare: the meeting round
+#pragma unroll
+    for (int o = kWave / 2; o >= 1; o >>= 1) {
+      const unsigned long long y = __shfl_xor(best, o);
+      best = y < best ? y : best;
+    }
+    if (__lane_id() == 0) {
+      atomicMin(&K.best, best);
+      if (single) K.found = 1;
+    }
+  }
+  if (!__ballot(mine)) return;  // wave-uniform
+  if (mine) {
+    pick(V.parent, s)[li] = u;
+    __hip_atomic_store(&pick(V.depth, s)[li], s ? dn[1] : dn[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  const uint32_t lane = __lane_id();
+#pragma unroll
+  for (int sd = 0; sd < 2; ++sd) {
+    const bool m = mine && s == sd;
+    const unsigned long long mask = __ballot(m);
+    if (!mask) continue;  // wave-uniform
+    const int leader = __ffsll((long long)mask) - 1;
+    uint32_t pos = 0;
+    if (lane == (uint32_t)leader) pos = atomicAdd(&K.q[sd], (uint32_t)__popcll(mask));
+    pos = __shfl(pos, leader);
+    if (m) pick(V.queue, sd)[qbase[sd] + pos + mbcnt64(mask)] = v;
+    const unsigned long long deg = wave_sum(m ? re - rb : 0ull);
+    if (lane == (uint32_t)leader) atomicAdd(&K.ne[sd], deg);
+  }
+}
+
+// Offer remote vertex v (parent u) of side s to its owner: once per search
+// (the `sent` bit, workgroup scope), into the owner's block or the spill list.
+__device__ __forceinline__ void small_emit(const DView& V, SmallCtr& K, const uint32_t* spbase, const uint32_t* lst,
+                                           bool want, int s, uint32_t v, uint32_t u, uint32_t ocap) {
+  if (!want) return;
+  const uint32_t bit = 1u << (v & 31);
+  if (wg_fetch_or32(&pick(V.sent, s)[v >> 5], bit) & bit) return;
+  const uint32_t o = v / V.chunk;
+  const uint32_t pos = atomicAdd(&K.oc[s][o], 1u);
+  if (pos < ocap) {
+    reinterpret_cast<uint2*>(V.sendbuf + ((size_t)s * V.P + o) * block_words(ocap))[1 + pos] = make_uint2(v, u);
+  } else {
+    const uint32_t q = (s ? spbase[1] : spbase[0]) + atomicAdd(&K.sp[s], 1u);
+    if (q < V.spill_cap) V.spill[s][s ? lst[1] : lst[0]][q] = make_uint2(v, u);  // past it: Ctl::lost (plan_round)
+  }
+}
+
+// The expansion of a small round by block (0, 0): both sides' frontiers
+// staged in LDS (side 0's vertices, then side 1's), one degree prefix, and
+// passes of kSmallU edges per thread (all their loads in flight together).
+__device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr) {
+  __shared__ uint32_t su[2 * kSmallV];
+  __shared__ unsigned long long sb[2 * kSmallV];
+  __shared__ uint32_t se[2 * kSmallV + 1];
+  __shared__ SmallCtr K;
+  __shared__ uint32_t qbase[2], spbase[2], lst[2];
+  const uint32_t tid = threadIdx.x;
+  const int p = it & 1;
+  DState* st = V.st;
+  const uint32_t F0 = (c.sides & 1) ? fr[2] - fr[0] : 0u, F1 = (c.sides & 2) ? fr[3] - fr[1] : 0u;
+  const uint32_t nv = F0 + F1;  // <= 2 kSmallV (the plan's vertex bound)
+  if (tid < 2) {
+    const uint32_t cur = st->spill_cur[tid];
+    qbase[tid] = st->qtail[tid];
+    lst[tid] = cur;
+    spbase[tid] = st->spill_n[tid][cur];
+    K.q[tid] = 0;
+    K.ne[tid] = 0;
+    K.sp[tid] = 0;
+  }
+  if (tid < 2 * kStageRanks) K.oc[tid / kStageRanks][tid % kStageRanks] = 0;
+  if (tid == 0) {
+    K.best = kNoKey;
+    K.found = 0;
+  }
+  for (uint32_t i = tid; i < nv; i += kThreads) {
+    const int s = i >= F0;
+    const uint32_t u = pick(V.queue, s)[fr[s] + (s ? i - F0 : i)];
+    const uint32_t li = u - V.lo;
+    const unsigned long long b = V.row_off[li];
+    su[i] = u;
+    sb[i] = b;
+    se[i] = (uint32_t)(V.row_off[li + 1] - b);
+  }
+  __syncthreads();
+  small_scan(se, nv);
+  const uint32_t E = se[nv];
+  const uint32_t dn[2] = {c.depth[0] + 1, c.depth[1] + 1};
+  const uint32_t dcl[2] = {c.depth[1] + 1, c.depth[0] + 1};  // (only this round's claims of the other side read kEmpty)
+  const bool single = c.sides != 3u;
+  for (uint32_t base = 0; base < E; base += kThreads * kSmallU) {  // block-uniform trip count
+    uint32_t vv[kSmallU], uu[kSmallU];
+    int ss[kSmallU];
+    bool ok[kSmallU];
+#pragma unroll
+    for (int k = 0; k < kSmallU; ++k) {
+      const uint32_t e = base + k * kThreads + tid;
+      ok[k] = e < E;
+      vv[k] = uu[k] = 0;
+      ss[k] = 0;
+      if (ok[k]) {
+        uint32_t a = 0, z = nv;  // last vertex whose edge range starts at or before e
+        while (z - a > 1) {
+          const uint32_t mid = (a + z) >> 1;
+          if (se[mid] <= e) a = mid;
+          else z = mid;
+        }
+        ss[k] = a >= F0;
+        uu[k] = su[a];
+        vv[k] = V.col[sb[a] + (e - se[a])];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSmallU; ++k) {
+      const bool own = ok[k] && vv[k] >= V.lo && vv[k] < V.hi;
+      small_claim(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
+      small_emit(V, K, spbase, lst, ok[k] && !own, ss[k], vv[k], uu[k], ocap);
+    }
+  }
+  __syncthreads();
+  // owner headers of both sides (count capped to the block), the round's state
+  const uint64_t bw = block_words(ocap);
+  for (uint32_t t = tid; t < 2u * V.P; t += kThreads) {
+    const uint32_t s = t / V.P, o = t % V.P;
+    const uint32_t cnt = K.oc[s][o];
+    V.sendbuf[((uint64_t)s * V.P + o) * bw] = min(cnt, ocap);
+    if (cnt) atomicMax(&st->ocmax, cnt);
+  }
+  if (tid == 0) {
+    for (int s = 0; s < 2; ++s) {
+      st->qtail[s] = qbase[s] + K.q[s];
+      st->new_edges[s] += K.ne[s];
+      st->spill_n[s][lst[s]] = spbase[s] + K.sp[s];
+    }
+    if (K.found) st->meet_found = 1;
+    if (K.best != kNoKey) atomicMin(&V.red[p].meetkey, K.best);
+  }
+}
+
+// The claims of a small round by block (0, 0) of k_spec_claim: every sender's
+// block of both sides, then the round's end (spec_round_end's bookkeeping,
+// from the LDS counters -- one thread, plain accesses).
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap) {
+  __shared__ uint32_t cnt[2 * kStageRanks + 1];
+  __shared__ SmallCtr K;
+  __shared__ uint32_t qbase[2];
+  const uint32_t tid = threadIdx.x;
+  const int p = it & 1;
+  const int P = V.P;
+  DState* st = V.st;
+  const uint64_t bw = block_words(cap);
+  if (tid < 2) {
+    qbase[tid] = st->qtail[tid];
+    K.q[tid] = 0;
+    K.ne[tid] = 0;
+  }
+  if (tid == 0) {
+    K.best = kNoKey;
+    K.found = 0;
+  }
+  // item space: side 0's P blocks, then side 1's (a side that did not expand: 0)
+  if (tid < 2u * P) {
+    const uint32_t s = tid / P;
+    cnt[tid] = ((c.sides >> s) & 1) ? min(V.recvbuf[(uint64_t)tid * bw], cap) : 0u;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t run = 0;
+    for (int k = 0; k < 2 * P; ++k) {
+      const uint32_t x = cnt[k];
+      cnt[k] = run;
+      run += x;
+    }
+    cnt[2 * P] = run;
+  }
+  __syncthreads();
+  const uint32_t tot = cnt[2 * P];
+  const uint32_t dn[2] = {c.depth[0] + 1, c.depth[1] + 1};
+  const uint32_t dcl[2] = {((c.sides >> 1) & 1) ? c.depth[1] + 1 : c.depth[1],
+                           (c.sides & 1) ? c.depth[0] + 1 : c.depth[0]};
+  const bool single = c.sides != 3u;
+  for (uint32_t base = 0; base < tot; base += kThreads * kSmallU) {
+    uint2 x[kSmallU];
+    int ss[kSmallU];
+    bool ok[kSmallU];
+#pragma unroll
+    for (int k = 0; k < kSmallU; ++k) {
+      const uint32_t i = base + k * kThreads + tid;
+      ok[k] = i < tot;
+      ss[k] = 0;
+      x[k] = make_uint2(0, 0);
+      if (ok[k]) {
+        uint32_t a = 0, z = 2 * P;  // the block holding item i
+        while (z - a > 1) {
+          const uint32_t mid = (a + z) >> 1;
+          if (cnt[mid] <= i) a = mid;
+          else z = mid;
+        }
+        ss[k] = (int)(a / P);
+        x[k] = reinterpret_cast<const uint2*>(V.recvbuf + (uint64_t)a * bw)[1 + (i - cnt[a])];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kSmallU; ++k) {
+      const bool want = ok[k] && x[k].x >= V.lo && x[k].x < V.hi;
+      small_claim(V, K, qbase, want, ss[k], x[k].x, x[k].y, dn, dcl, single);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {  // spec_round_end from the LDS counters (no continuation in a small round)
+    for (int s = 0; s < 2; ++s) {
+      const bool on = (c.sides >> s) & 1;
+      const uint32_t qt = qbase[s] + K.q[s];
+      const unsigned long long ne = st->new_edges[s] + K.ne[s];
+      st->qtail[s] = qt;
+      st->new_edges[s] = 0;
+      V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - st->fend[s]) : 0ull;
+      V.red[p].sums[2 * s + 1] = on ? ne : 0ull;
+      V.red[p].nfmax[s] = on ? ~ne : ~0ull;
+      if (on) {
+        st->fbeg[s] = st->fend[s];
+        st->fend[s] = qt;
+      }
+      const unsigned long long sp = on ? st->spill_n[s][st->spill_cur[s]] : 0ull;
+      V.red[p].spill[s] = sp;
+      V.red[p].spillmax[s] = (uint32_t)min(sp, 0xffffffffull);
+      st->hub_count[s] = 0;
+    }
+    if (K.found) st->meet_found = 1;
+    V.red[p].nocmax = ~(unsigned long long)st->ocmax;
+    st->ocmax = 0;
+    V.red[p].meetkey = min(V.red[p].meetkey, K.best);
+    V.red[p ^ 1].meetkey = kNoKey;
   }
 }
 
@@ -1403,6 +1822,10 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
       if (ss == 0) atomicExch(&V.st->done_blocks[2], 0u);
     }
     if (finish && threadIdx.x == kWave) spec_round_end(V, it, sides, V.ctl[it & 1].cont);
+    if (RoundStamp* rs = round_stamp(V, it)) {  // the hub pass ends the round's expansion
+      __syncthreads();
+      if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
+    }
   }
 }
 
@@ -1411,8 +1834,21 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
 // (more than one rank: this kernel ends the round's claims; its last
 // workgroup closes the round)
 __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap) {
+  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   const Ctl& c = V.ctl[it & 1];
   if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
+  RoundStamp* rs = round_stamp(V, it);
+  if (rs && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) rs->cb = t_in;
+  if (small_claim_ok(c, V.P)) {  // small round: one workgroup claims and closes it
+    if (blockIdx.x == 0 && blockIdx.y == 0) {
+      small_claim_round(V, c, it, cap);
+      if (rs) {
+        __syncthreads();
+        if (threadIdx.x == 0) rs->ce = __builtin_amdgcn_s_memrealtime();
+      }
+    }
+    return;
+  }
   const int s = blockIdx.y;
   // a continuation side claims at the depth its level already has
   const uint32_t dnew = ((c.sides >> s) & 1) ? c.depth[s] + 1 : c.depth[s];
@@ -1441,6 +1877,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   if (last_block(&V.st->done_blocks[1], gridDim.x * gridDim.y) && threadIdx.x == 0) {
     spec_round_end(V, it, c.sides, c.cont);
     atomicExch(&V.st->done_blocks[1], 0u);
+    if (rs) rs->ce = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1487,6 +1924,7 @@ __global__ __launch_bounds__(kThreads) void k_meet_end(DView V, uint32_t it) {
       }
       st->hub_count[s] = 0;
       V.red[p].spill[s] = 0;  // host-planned exchanges are sized exactly: nothing spills
+      V.red[p].spillmax[s] = 0;
     }
     V.red[p].nocmax = ~0ull;
     atomicExch(&st->done_blocks[1], 0u);
@@ -1662,6 +2100,7 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     st->spill_n[s][0] = st->spill_n[s][1] = 0;
     st->spill_cur[s] = 0;
     r.spill[s] = 0;
+    r.spillmax[s] = 0;
     r.sums[2 * s] = r.sums[2 * s + 1] = 0;
     const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
@@ -1689,6 +2128,25 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
 }
 
 // ---- path reconstruction ----------------------------------------------------
+
+// Distributed path check: block b takes the b-th path edge (path[i], path[i+1])
+// whose first vertex this rank owns (idx[b] = i) and scans that vertex's row
+// for the second one; found[b] = 1 if it is there.
+__global__ __launch_bounds__(kThreads) void k_path_edges(DView V, const uint32_t* __restrict__ path,
+                                                         const uint32_t* __restrict__ idx, uint32_t* found) {
+  const uint32_t i = idx[blockIdx.x];
+  const uint32_t u = path[i], v = path[i + 1];
+  const uint32_t li = u - V.lo;
+  const unsigned long long b = V.row_off[li], e = V.row_off[li + 1];
+  int hit = 0;
+  for (unsigned long long base = b; base < e; base += kThreads) {  // block-uniform trip count
+    const unsigned long long k = base + threadIdx.x;
+    const int mine = k < e && V.col[k] == v;
+    hit = __syncthreads_or(mine);
+    if (hit) break;
+  }
+  if (threadIdx.x == 0) found[blockIdx.x] = hit ? 1u : 0u;
+}
 
 // Pack this rank's claimed (vertex, parent) pairs of both sides: one block of
 // {count_S, count_T, S pairs[capS], T pairs[capT]} (the queues hold exactly
@@ -1925,6 +2383,15 @@ struct DistBiBfs::Impl {
   uint32_t* d_col = nullptr;
   uint4* d_padj = nullptr;  // one rank: packed adjacency (DView::padj)
   void* state = nullptr;
+  size_t state_bytes = 0, padj_bytes = 0;
+  // Everything this rank holds on the device goes through `mem` (devmem.hpp):
+  // exact current / peak bytes of the build (temporaries included), the
+  // device's free-memory low-water mark beside it, and DistTuning::hbm_cap_bytes.
+  devmem::Tracker mem;
+  size_t gen_hbm_peak_bytes = 0;  // hipMemGetInfo: free before the build - least free during it
+  // path reconstruction buffers: O(path length), grown on demand (never O(n))
+  uint32_t* d_pathbuf = nullptr;
+  size_t path_cap = 0;            // entries per path array (pathS, pathT; walk holds 4 + path)
   uint32_t* sent_base = nullptr;  // both sides' sent bitmaps, contiguous (one memset)
   DView V{};
   uint32_t* d_cur = nullptr;
@@ -1932,6 +2399,7 @@ struct DistBiBfs::Impl {
   uint32_t* d_pathT = nullptr;
   uint32_t* d_walk = nullptr;  // k_walk output
   RoundRec* d_trace = nullptr;
+  RoundStamp* d_rstamp = nullptr;
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
   uint32_t* h_fin = nullptr;   // pinned, k_final's tag (written after h_ctl)
@@ -1946,6 +2414,7 @@ struct DistBiBfs::Impl {
   bool solo_stamp = false;
   DistLevelStats stats;
   DistTuning tune;
+  bool source_only = false;  // the search in progress is search_unidirectional's
   int fault_at = 0, fault_mode = 0;
 
   void setup(int dev) {
@@ -1992,16 +2461,42 @@ struct DistBiBfs::Impl {
     hi = (uint32_t)std::min<uint64_t>((uint64_t)(rank + 1) * chunk, nn);
   }
 
+  size_t row_off_bytes() const { return ((size_t)(hi - lo) + 1) * 8; }
+  size_t col_bytes() const { return std::max<uint64_t>(nnz, 1) * 4; }
+
   void free_all() {
-    if (d_row_off) HIP_CHECK(hipFree(d_row_off));
-    if (d_col) HIP_CHECK(hipFree(d_col));
-    if (d_padj) HIP_CHECK(hipFree(d_padj));
-    if (state) HIP_CHECK(hipFree(state));
+    devmem::Scope scope(&mem);
+    devmem::release(d_row_off, row_off_bytes());
+    devmem::release(d_col, col_bytes());
+    devmem::release(d_padj, padj_bytes);
+    devmem::release(state, state_bytes);
+    devmem::release(d_pathbuf, path_cap * 3 * 4 + 64);
     d_row_off = nullptr;
     d_col = nullptr;
     d_padj = nullptr;
     state = nullptr;
+    d_pathbuf = nullptr;
+    path_cap = 0;
+    state_bytes = padj_bytes = 0;
     n = 0;
+    nnz = 0;
+  }
+
+  // Path buffers for at least `entries` vertices per chain: pathS / pathT of
+  // the per-hop walk and k_walk's {status, dS, dT, epoch, path} output.
+  void ensure_path_dev(size_t entries) {
+    entries += 8;
+    if (entries <= path_cap) return;
+    devmem::Scope scope(&mem);
+    if (d_pathbuf) {
+      HIP_CHECK(hipStreamSynchronize(cstream));  // an earlier walk may still read it
+      devmem::release(d_pathbuf, path_cap * 3 * 4 + 64);
+    }
+    path_cap = std::max<size_t>(entries, 1u << 14);
+    devmem::alloc(&d_pathbuf, path_cap * 3 * 4 + 64);
+    d_pathS = d_pathbuf;
+    d_pathT = d_pathbuf + path_cap;
+    d_walk = d_pathbuf + 2 * path_cap;
   }
 
   // effective host-planned block capacity (tuning may shrink it for tests)
@@ -2041,10 +2536,14 @@ struct DistBiBfs::Impl {
     const size_t o_sent = take((size_t)gwords * 4 * 2);
     const size_t o_st = take(sizeof(DState)), o_ctl = take(2 * sizeof(Ctl)), o_red = take(2 * sizeof(Reduced)),
                  o_redg = take(2 * (size_t)size * sizeof(Reduced)),
-                 o_cur = take(64), o_ps = take(((size_t)n + 2) * 4), o_pt = take(((size_t)n + 2) * 4),
-                 o_walk = take(((size_t)n + 8) * 4), o_sc = take(64),
-                 o_tr = take((size_t)kTraceCap * sizeof(RoundRec));
-    HIP_CHECK(hipMalloc(&state, off));
+                 o_cur = take(64), o_sc = take(64),
+                 o_tr = take((size_t)kTraceCap * sizeof(RoundRec)),
+                 o_rs = take((size_t)kTraceCap * sizeof(RoundStamp));
+    {
+      devmem::Scope scope(&mem);
+      devmem::alloc(&state, off);
+      state_bytes = off;
+    }
     char* b = static_cast<char*>(state);
     V.n = n;
     V.lo = lo;
@@ -2081,11 +2580,12 @@ struct DistBiBfs::Impl {
     for (int q = 0; q < 2; ++q)
       V.redg[q] = size == 1 ? V.red + q : reinterpret_cast<Reduced*>(b + o_redg) + (size_t)q * size;
     d_cur = reinterpret_cast<uint32_t*>(b + o_cur);
-    d_pathS = reinterpret_cast<uint32_t*>(b + o_ps);
-    d_pathT = reinterpret_cast<uint32_t*>(b + o_pt);
-    d_walk = reinterpret_cast<uint32_t*>(b + o_walk);
+    ensure_path_dev(1u << 14);
     d_scalar = reinterpret_cast<double*>(b + o_sc);
     d_trace = reinterpret_cast<RoundRec*>(b + o_tr);
+    d_rstamp = reinterpret_cast<RoundStamp*>(b + o_rs);
+    HIP_CHECK(hipMemsetAsync(d_rstamp, 0, (size_t)kTraceCap * sizeof(RoundStamp), stream));
+    V.rstamp = nullptr;
     V.trace = nullptr;
     V.trace_cap = kTraceCap;
     HIP_CHECK(hipMemsetAsync(V.st, 0, sizeof(DState), stream));
@@ -2099,6 +2599,7 @@ struct DistBiBfs::Impl {
   // kHubDeg: no hub is ever deferred, so no speculative round launches the hub pass.
   uint64_t max_deg = 0;
   void finish_build() {
+    devmem::Scope scope(&mem);
     alloc_state();
     // One rank owns every row: the packed adjacency of the single-GPU engine
     // (16 B per edge) within BIBFS_PADJ_MAX_MB (default 4096 MiB, 0 = off).
@@ -2108,7 +2609,9 @@ struct DistBiBfs::Impl {
       const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
       const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
       if (nnz * 16 <= budget) {
-        HIP_CHECK(hipMalloc(&d_padj, nnz * 16));
+        devmem::Scope scope(&mem);
+        devmem::alloc(&d_padj, nnz * 16);
+        padj_bytes = nnz * 16;
         launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
         HIP_CHECK(hipStreamSynchronize(stream));
         V.padj = d_padj;
@@ -2122,25 +2625,20 @@ struct DistBiBfs::Impl {
       wait(cstream);
     }
     max_deg = (uint64_t)y;
+    // measured, not a formula: the most this rank held at once during the
+    // build (CSR temporaries included) and the device's free-memory drop
+    gen_peak_bytes = mem.peak;
+    gen_hbm_peak_bytes = mem.hbm_peak();
   }
 
   size_t gen_peak_bytes = 0;
   size_t shard_bytes() const { return ((size_t)(hi - lo) + 1) * 8 + (size_t)nnz * 4; }
 
-  void build_rows_from_device_edges(const uint32_t* d_uv, uint64_t m) {
-    HIP_CHECK(hipMalloc(&d_row_off, ((size_t)(hi - lo) + 1) * 8));
-    nnz = launch::count_csr_rows(d_uv, m, lo, hi, d_row_off, stream);
-    HIP_CHECK(hipMalloc(&d_col, std::max<uint64_t>(nnz, 1) * 4));
-    uint64_t* cursor = nullptr;
-    HIP_CHECK(hipMalloc(&cursor, ((size_t)(hi - lo) + 1) * 8));
-    launch::fill_csr_rows(d_uv, m, lo, hi, d_row_off, cursor, d_col, stream);
-    HIP_CHECK(hipStreamSynchronize(stream));
-    HIP_CHECK(hipFree(cursor));
-  }
-
   void upload_rows(const Csr& rows) {
-    HIP_CHECK(hipMalloc(&d_row_off, ((size_t)rows.n + 1) * 8));
-    HIP_CHECK(hipMalloc(&d_col, std::max<uint64_t>(rows.nnz(), 1) * 4));
+    devmem::Scope scope(&mem);
+    mem.reset_peak();
+    devmem::alloc(&d_row_off, ((size_t)rows.n + 1) * 8);
+    devmem::alloc(&d_col, std::max<uint64_t>(rows.nnz(), 1) * 4);
     HIP_CHECK(hipMemcpyAsync(d_row_off, rows.row_off.data(), ((size_t)rows.n + 1) * 8, hipMemcpyHostToDevice,
                              stream));
     if (rows.nnz())
@@ -2266,6 +2764,8 @@ struct DistBiBfs::Impl {
     p.epoch = epoch;
     p.walk_cap = (uint32_t)std::min<size_t>(h_walk_cap, 0xffffffffu);
     p.want_path = opt.want_path ? 1 : 0;
+    p.spill_cap = V.spill_cap;
+    p.source_only = source_only ? 1 : 0;
     return p;
   }
 
@@ -2279,6 +2779,32 @@ struct DistBiBfs::Impl {
 
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt);
   void host_round(uint32_t it, const Policy& pol, SearchResult& r);
+
+  // DistTuning::stamps: split the search's speculative rounds (those stamped
+  // with this search's tags among rounds [0, it_end)) into kernel time and
+  // the gaps between the kernels (exchange + launch latency), in microseconds.
+  void collect_stamps(uint32_t it_end) {
+    std::vector<RoundStamp> ring(kTraceCap);
+    HIP_CHECK(hipMemcpy(ring.data(), d_rstamp, ring.size() * sizeof(RoundStamp), hipMemcpyDeviceToHost));
+    const uint32_t lo_it = it_end > kTraceCap ? it_end - kTraceCap : 0;
+    const RoundStamp* prev = nullptr;
+    uint32_t prev_it = 0;
+    auto us = [](unsigned long long a, unsigned long long b) { return b > a ? (double)(b - a) * 1e-2 : 0.0; };
+    for (uint32_t i = lo_it; i < it_end; ++i) {
+      const RoundStamp& x = ring[i % kTraceCap];
+      if (x.tag != plan_tag(epoch, i) || !x.eb || !x.ee) continue;
+      stats.stamped_rounds++;
+      const unsigned long long ee = std::max(x.ee, x.ee1);
+      stats.expand_us += us(x.eb, x.ee) + (x.eb1 ? us(x.eb1, x.ee1) : 0.0);
+      if (x.cb && x.ce && x.cb >= x.eb) {
+        stats.claim_us += us(x.cb, x.ce);
+        stats.exchange_us += us(ee, x.cb);
+      }
+      if (prev && prev_it + 1 == i) stats.status_us += us(prev->ce ? prev->ce : std::max(prev->ee, prev->ee1), x.eb);
+      prev = &x;
+      prev_it = i;
+    }
+  }
   bool walk_path(uint64_t key, SearchResult& r);
   void finish_walk(SearchResult& r);
   void cleanup_enqueue(const Ctl& h);
@@ -2405,6 +2931,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   const Policy pol = policy(opt);
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
+  V.rstamp = tune.stamps ? d_rstamp : nullptr;
 
   // Plan words of older searches must not match this one's tags.  Only the
   // previous search's trailing no-op rounds can still be running (its
@@ -2604,6 +3131,11 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     }
   }
   const Ctl h = *h_ctl;
+  if (h.lost) {
+    cleanup_enqueue(h);
+    throw Error("dist: a rank's candidate spill list overflowed (" + std::to_string(V.spill_cap) +
+                " pairs): candidates were dropped, the search result would not be exact");
+  }
   stats.rounds = (int)h.rounds;
   stats.lockstep_rounds = (int)h.lockstep_rounds;
   stats.levels = (int)h.levels;
@@ -2646,7 +3178,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       }
     }
   }
-  if (opt.trace && !tag) {  // the trace records are plain device stores: drain the rounds first
+  if ((opt.trace || tune.stamps) && !tag) {  // trace records / stamps are plain device stores: drain the rounds first
     tag = next_tag();
     k_host_tag<<<1, 64, 0, cs>>>(h_fin, tag);
     HIP_CHECK(hipGetLastError());
@@ -2657,6 +3189,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     spin_tag(tag, cs);
   }
   if (path_pending) finish_walk(r);
+  if (tune.stamps) collect_stamps(it);
   if (opt.trace && h.rounds) {
     std::vector<RoundRec> tr(std::min<uint32_t>(h.rounds, kTraceCap));
     HIP_CHECK(hipMemcpy(tr.data(), d_trace, tr.size() * sizeof(RoundRec), hipMemcpyDeviceToHost));
@@ -2701,6 +3234,7 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   stats.collectives++;
   stats.path_collectives++;
   stats.exchanged_bytes += blk * 4 * size;
+  ensure_path_dev((size_t)hops + 5);
   k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, d_walk);
   HIP_CHECK(hipGetLastError());
   const size_t words = 4 + (size_t)hops + 1;
@@ -2738,6 +3272,7 @@ void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult&
   const int dS = (int)h_red->md[0], dT = (int)h_red->md[1];
   BIBFS_REQUIRE((int64_t)dS + dT == r.hops, "dist: meet depths disagree with the path length");
   const int K = std::max(dS, dT);
+  ensure_path_dev((size_t)K + 1);
   const uint32_t init[2] = {meet, meet};
   HIP_CHECK(hipMemcpyAsync(d_cur, init, 8, hipMemcpyHostToDevice, cs));
   for (int i = 0; i <= K; ++i) {
@@ -2838,11 +3373,14 @@ void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
   I.free_all();
   I.set_partition(n);
   // owned rows straight from the generator (no edge list on any rank)
-  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)(I.hi - I.lo) + 1) * 8));
-  uint64_t m = 0;
-  I.nnz = launch::gen_rows_gnp(n, p, seed, I.lo, I.hi, I.d_row_off, &I.d_col, &m, I.stream);
-  I.m_input = m;
-  I.gen_peak_bytes = I.shard_bytes() + ((size_t)(I.hi - I.lo) + 1) * 8;  // + the scatter cursor
+  {
+    devmem::Scope scope(&I.mem);
+    I.mem.reset_peak();
+    devmem::alloc(&I.d_row_off, I.row_off_bytes());
+    uint64_t m = 0;
+    I.nnz = launch::gen_rows_gnp(n, p, seed, I.lo, I.hi, I.d_row_off, &I.d_col, &m, I.stream);
+    I.m_input = m;
+  }
   I.finish_build();
 }
 
@@ -2853,10 +3391,13 @@ void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, d
   I.free_all();
   I.set_partition(n);
   // owned rows straight from the generator (no edge list on any rank)
-  HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)(I.hi - I.lo) + 1) * 8));
-  I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, I.lo, I.hi, I.d_row_off, &I.d_col, I.stream);
-  I.m_input = m;
-  I.gen_peak_bytes = I.shard_bytes() + ((size_t)(I.hi - I.lo) + 1) * 8;  // + the scatter cursor
+  {
+    devmem::Scope scope(&I.mem);
+    I.mem.reset_peak();
+    devmem::alloc(&I.d_row_off, I.row_off_bytes());
+    I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, I.lo, I.hi, I.d_row_off, &I.d_col, I.stream);
+    I.m_input = m;
+  }
   I.finish_build();
 }
 
@@ -2884,6 +3425,57 @@ void DistBiBfs::barrier() {
   I.wait(I.cstream);
 }
 
+bool DistBiBfs::validate_path(vid_t src, vid_t dst, int64_t hops, const std::vector<vid_t>& path) {
+  auto& I = *p_;
+  BIBFS_REQUIRE(I.n > 0, "no graph loaded");
+  HIP_CHECK(hipSetDevice(I.device));
+  // Shape checks first: every rank holds the same path, so they all decide
+  // alike and either all reach the collective below or none does.
+  if (hops < 0 || path.size() != (size_t)hops + 1 || path.front() != src || path.back() != dst) return false;
+  for (vid_t v : path)
+    if (v >= I.n) return false;
+  if (hops == 0) return src == dst;
+  std::vector<uint32_t> idx;
+  for (size_t i = 0; i + 1 < path.size(); ++i)
+    if (path[i] >= I.lo && path[i] < I.hi) idx.push_back((uint32_t)i);
+  double found = 0;
+  if (!idx.empty()) {
+    I.ensure_path_dev(path.size() + idx.size() + 1);
+    uint32_t* d_path = I.d_pathS;
+    uint32_t* d_idx = I.d_pathT;
+    uint32_t* d_found = I.d_pathT + idx.size();
+    HIP_CHECK(hipMemcpyAsync(d_path, path.data(), path.size() * 4, hipMemcpyHostToDevice, I.cstream));
+    HIP_CHECK(hipMemcpyAsync(d_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, I.cstream));
+    k_path_edges<<<(unsigned)idx.size(), kThreads, 0, I.cstream>>>(I.V, d_path, d_idx, d_found);
+    HIP_CHECK(hipGetLastError());
+    std::vector<uint32_t> f(idx.size());
+    HIP_CHECK(hipMemcpyAsync(f.data(), d_found, f.size() * 4, hipMemcpyDeviceToHost, I.cstream));
+    I.wait(I.cstream);
+    for (uint32_t x : f) found += x;
+  }
+  // every edge's first vertex has exactly one owner: the edges found over all
+  // ranks must be all `hops` of them
+  double y = found;
+  HIP_CHECK(hipMemcpyAsync(I.d_scalar, &y, 8, hipMemcpyHostToDevice, I.cstream));
+  I.comm->allreduce(I.d_scalar, 1, DType::kF64, ROp::kSum, I.cstream);
+  HIP_CHECK(hipMemcpyAsync(&y, I.d_scalar, 8, hipMemcpyDeviceToHost, I.cstream));
+  I.wait(I.cstream);
+  return (int64_t)(y + 0.5) == hops;
+}
+
+SearchResult DistBiBfs::search_unidirectional(vid_t src, vid_t dst) {
+  auto& I = *p_;
+  SearchOptions opt;
+  opt.lockstep = false;
+  opt.want_path = false;
+  I.source_only = true;
+  struct Reset {
+    Impl& I;
+    ~Reset() { I.source_only = false; }
+  } reset{I};
+  return search(src, dst, opt);
+}
+
 double DistBiBfs::allreduce_max(double x) {
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));
@@ -2907,9 +3499,11 @@ void DistBiBfs::set_tuning(const DistTuning& t) {
   BIBFS_REQUIRE(t.spec_rounds >= 0 && t.timeout_s > 0 && t.walk_max >= 1, "bad DistTuning");
   const bool realloc = p_->state && t.walk_max > p_->tune.walk_max;
   p_->tune = t;
+  p_->mem.cap = t.hbm_cap_bytes;
   if (realloc) {  // path-gather blocks are sized from walk_max
     HIP_CHECK(hipSetDevice(p_->device));
-    HIP_CHECK(hipFree(p_->state));
+    devmem::Scope scope(&p_->mem);
+    devmem::release(p_->state, p_->state_bytes);
     p_->state = nullptr;
     p_->alloc_state();
   }
@@ -2927,6 +3521,8 @@ uint64_t DistBiBfs::m_input() const { return p_->m_input; }
 uint64_t DistBiBfs::local_nnz() const { return p_->nnz; }
 size_t DistBiBfs::shard_bytes() const { return p_->shard_bytes(); }
 size_t DistBiBfs::gen_peak_bytes() const { return p_->gen_peak_bytes; }
+size_t DistBiBfs::gen_hbm_peak_bytes() const { return p_->gen_hbm_peak_bytes; }
+size_t DistBiBfs::resident_bytes() const { return p_->mem.cur; }
 uint32_t DistBiBfs::lo() const { return p_->lo; }
 uint32_t DistBiBfs::hi() const { return p_->hi; }
 const DistLevelStats& DistBiBfs::last_stats() const { return p_->stats; }
@@ -3006,12 +3602,14 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
                                                   double arg, uint64_t seed,
                                                   const std::vector<std::pair<vid_t, vid_t>>& queries,
                                                   const SearchOptions& opt, DistLocalTiming* timing,
-                                                  const DistTuning& tuning) {
+                                                  const DistTuning& tuning, int verify) {
   BIBFS_REQUIRE(kind == "gnp" || kind == "rmat", "dist_local_generate_run: kind must be gnp or rmat");
-  std::vector<double> build_ms((size_t)std::max(ranks, 1), 0.0), qms;
-  std::vector<uint64_t> nnz((size_t)std::max(ranks, 1), 0), shard((size_t)std::max(ranks, 1), 0),
-      peak((size_t)std::max(ranks, 1), 0);
+  const size_t R = (size_t)std::max(ranks, 1);
+  std::vector<double> build_ms(R, 0.0), qms;
+  std::vector<uint64_t> nnz(R, 0), shard(R, 0), peak(R, 0), hpeak(R, 0), resident(R, 0);
   std::vector<DistLevelStats> qstats;
+  std::vector<int> valid;
+  std::vector<int64_t> uni;
   auto rs = run_local_ranks(
       "dist_local_generate_run", ranks, device, queries.size(), tuning, DistLocalFault{},
       [&](DistBiBfs& e, int r, std::vector<SearchResult>& out) {
@@ -3024,12 +3622,24 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
         nnz[(size_t)r] = e.local_nnz();
         shard[(size_t)r] = e.shard_bytes();
         peak[(size_t)r] = e.gen_peak_bytes();
-        for (const auto& q : queries) {
+        hpeak[(size_t)r] = e.gen_hbm_peak_bytes();
+        resident[(size_t)r] = e.resident_bytes();
+        for (size_t qi = 0; qi < queries.size(); ++qi) {
+          const auto& q = queries[qi];
           const auto q0 = std::chrono::steady_clock::now();
           out.push_back(e.search(q.first, q.second, opt));
           if (r == 0) {
             qms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count());
             qstats.push_back(e.last_stats());
+          }
+          if (verify > 0) {  // collective checks (every rank), no graph copy anywhere
+            const SearchResult& x = out.back();
+            const int ok = x.found ? (e.validate_path(q.first, q.second, x.hops, x.path) ? 1 : 0) : -1;
+            const int64_t uh = (int)qi < verify ? e.search_unidirectional(q.first, q.second).hops : -2;
+            if (r == 0) {
+              valid.push_back(ok);
+              uni.push_back(uh);
+            }
           }
         }
       });
@@ -3039,7 +3649,11 @@ std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const s
     timing->local_nnz = std::move(nnz);
     timing->shard_bytes = std::move(shard);
     timing->gen_peak_bytes = std::move(peak);
+    timing->gen_hbm_peak_bytes = std::move(hpeak);
+    timing->resident_bytes = std::move(resident);
     timing->stats = std::move(qstats);
+    timing->path_valid = std::move(valid);
+    timing->uni_hops = std::move(uni);
   }
   return rs;
 }

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "bibfs/rng.hpp"
+#include "devmem.hpp"
 #include "device.hpp"
 
 namespace bibfs {
@@ -112,13 +113,13 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(uint64_t* __restric
 void exclusive_scan_u64(uint64_t* d, uint64_t count, hipStream_t s) {
   const uint64_t nb = (count + kScanTile - 1) / kScanTile;
   uint64_t* bsum = nullptr;
-  HIP_CHECK(hipMalloc(&bsum, (nb + 1) * sizeof(uint64_t)));
+  devmem::alloc(&bsum, (nb + 1) * sizeof(uint64_t));  // (counted by the partitioned build's tracker)
   k_scan_reduce<<<(unsigned)nb, kScanThreads, 0, s>>>(d, count, bsum);
   k_scan_bsums<<<1, kScanThreads, 0, s>>>(bsum, nb);
   k_scan_apply<<<(unsigned)nb, kScanThreads, 0, s>>>(d, count, bsum);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(s));
-  HIP_CHECK(hipFree(bsum));
+  devmem::release(bsum, (nb + 1) * sizeof(uint64_t));
 }
 
 __global__ void k_scatter(const uint32_t* __restrict__ uv, uint64_t m, uint32_t lo, uint32_t hi,
@@ -269,14 +270,14 @@ uint64_t finish_rows(uint32_t rows, uint64_t* d_row_off, uint32_t** d_col_out, h
   HIP_CHECK(hipMemcpyAsync(&nnz, d_row_off + rows, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
   uint32_t* col = nullptr;
-  HIP_CHECK(hipMalloc(&col, std::max<uint64_t>(nnz, 1) * 4));
+  devmem::alloc(&col, std::max<uint64_t>(nnz, 1) * 4);
   uint64_t* cursor = nullptr;
-  HIP_CHECK(hipMalloc(&cursor, (rows + 1ULL) * 8));
+  devmem::alloc(&cursor, (rows + 1ULL) * 8);
   k_copy_u64<<<grid_for(rows + 1ULL, 256), 256, 0, s>>>(d_row_off, rows + 1ULL, cursor);
   scatter(reinterpret_cast<unsigned long long*>(cursor), col);
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipStreamSynchronize(s));
-  HIP_CHECK(hipFree(cursor));
+  devmem::release(cursor, (rows + 1ULL) * 8);
   *d_col_out = col;
   return nnz;
 }
@@ -298,7 +299,7 @@ uint64_t gen_rows_gnp(uint32_t n, double p, uint64_t seed, uint32_t lo, uint32_t
   const uint64_t K = gnp_num_chunks(n, p);
   const uint32_t rows = hi - lo;
   unsigned long long* dm = nullptr;
-  HIP_CHECK(hipMalloc(&dm, 8));
+  devmem::alloc(&dm, 8);
   HIP_CHECK(hipMemsetAsync(dm, 0, 8, s));
   HIP_CHECK(hipMemsetAsync(d_row_off, 0, (rows + 1ULL) * 8, s));
   k_gnp_degree<<<grid_for(K, 256), 256, 0, s>>>(n, p, seed, K, lo, hi, d_row_off, dm);
@@ -308,7 +309,7 @@ uint64_t gen_rows_gnp(uint32_t n, double p, uint64_t seed, uint32_t lo, uint32_t
   const uint64_t nnz = finish_rows(rows, d_row_off, d_col_out, s, [&](unsigned long long* cur, uint32_t* col) {
     k_gnp_scatter<<<grid_for(K, 256), 256, 0, s>>>(n, p, seed, K, lo, hi, cur, col);
   });
-  HIP_CHECK(hipFree(dm));
+  devmem::release(dm, 8);
   *m_out = m;
   return nnz;
 }
@@ -367,14 +368,14 @@ __global__ void k_max_degree(const uint64_t* __restrict__ row_off, uint32_t n, u
 
 uint64_t max_degree(const uint64_t* d_row_off, uint32_t n, hipStream_t s) {
   unsigned long long* d = nullptr;
-  HIP_CHECK(hipMalloc(&d, 8));
+  devmem::alloc(&d, 8);
   HIP_CHECK(hipMemsetAsync(d, 0, 8, s));
   k_max_degree<<<(unsigned)std::min<uint64_t>(grid_for(n, 256), 2048), 256, 0, s>>>(d_row_off, n, d);
   HIP_CHECK(hipGetLastError());
   unsigned long long h = 0;
   HIP_CHECK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s));
   HIP_CHECK(hipStreamSynchronize(s));
-  HIP_CHECK(hipFree(d));
+  devmem::release(d, 8);
   return h;
 }
 

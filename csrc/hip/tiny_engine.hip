@@ -205,7 +205,12 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
   }
   // claim, then read the other side's word: the LDS executes one wave's DS
   // instructions in order, so of two same-round claims of a vertex by the two
-  // sides at least one sees the other
+  // sides at least one sees the other.  That needs every claim ISSUED before
+  // the other-side reads; the two are relaxed atomics on different words,
+  // which the C++ model would let the compiler reorder (a store-buffer /
+  // Dekker pattern), so a compiler-only fence pins the order (no instruction:
+  // the hardware order then comes from in-order DS issue).
+  unsigned long long* own[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     old[b] = W.oth[b] = 0ull;
@@ -213,9 +218,15 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
     const uint32_t v = tw_v(W.rec[b]);
     const uint32_t par = W.s1[b] ? R.par[1] : R.par[0];
     const unsigned long long m = W.act[b] ? 1ull << ((v & 31) + (par << 5)) : 0ull;
-    unsigned long long* own = &VIS[W.s1[b] ? 1 : 0][v >> 5];
-    old[b] = __hip_atomic_fetch_or(own, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    W.oth[b] = __hip_atomic_load(W.s1[b] ? own - kTW : own + kTW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    own[b] = &VIS[W.s1[b] ? 1 : 0][v >> 5];
+    old[b] = __hip_atomic_fetch_or(own[b], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b >= nb) continue;
+    W.oth[b] = __hip_atomic_load(W.s1[b] ? own[b] - kTW : own[b] + kTW, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {

@@ -68,6 +68,12 @@ struct DistLevelStats {
   int path_collectives = 0;        // collectives spent reconstructing the path
   int solo_rounds = 0;             // rounds run by the one-workgroup solo kernel (one rank)
   int cont_rounds = 0;             // continuation rounds: candidates that overflowed an owner block re-offered
+  // DistTuning::stamps: the speculative rounds split by device stamps (sums
+  // over the stamped rounds, microseconds): expansion kernel(s), claim kernel,
+  // expansion end -> claim start (candidate exchange + launch gap), claim end
+  // -> next expansion start (status allgather + launch gap)
+  int stamped_rounds = 0;
+  double expand_us = 0.0, claim_us = 0.0, exchange_us = 0.0, status_us = 0.0;
 };
 
 // Knobs of the partitioned engine (defaults are the production settings; the
@@ -86,6 +92,10 @@ struct DistTuning {
                                    // host-planned round (0 = only when the spill lists could overflow)
   bool overlap = false;            // > 1 rank: lockstep rounds expand side 1 on the compute stream while side 0's
                                    // candidates are exchanged (off until measured on a multi-GPU node)
+  size_t hbm_cap_bytes = 0;        // > 0: a build that would make this rank hold more device memory throws
+                                   // (tests: rehearse "does not fit one GPU" at small scale)
+  bool stamps = false;             // per-round device stamps -> DistLevelStats::{expand,claim,exchange,status}_us
+                                   // (adds one host wait + a copy per search: diagnostics, not serving)
 };
 
 class DistBiBfs {
@@ -106,6 +116,15 @@ class DistBiBfs {
   // the full result (hops + path).
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
 
+  // Collective checks that need no copy of the whole graph anywhere:
+  // validate_path -- every edge (path[i], path[i+1]) is looked up in the row
+  // of path[i] by the rank that owns it, one sum-allreduce of the edges found
+  // (plus endpoints and length); search_unidirectional -- a plain
+  // level-synchronous BFS from src over the same partition (side 0 expands
+  // alone, so its hop count is independent of the bidirectional meet rule).
+  bool validate_path(vid_t src, vid_t dst, int64_t hops, const std::vector<vid_t>& path);
+  SearchResult search_unidirectional(vid_t src, vid_t dst);
+
   void barrier();
   double allreduce_max(double x);
   void release();  // free the graph shard and search state (the communicator stays)
@@ -123,7 +142,13 @@ class DistBiBfs {
   uint64_t m_input() const;
   uint64_t local_nnz() const;
   size_t shard_bytes() const;     // owned CSR rows: row offsets + columns
-  size_t gen_peak_bytes() const;  // peak allocation of the last device generation (0: loaded, not generated)
+  // Measured device memory of the last build (devmem.hpp): the most this rank
+  // held at once (shard + generator temporaries + search state), the device's
+  // free-memory drop over the build (hipMemGetInfo low-water mark: equal up to
+  // allocator granularity with one rank per GPU), and what it holds now.
+  size_t gen_peak_bytes() const;
+  size_t gen_hbm_peak_bytes() const;
+  size_t resident_bytes() const;
   uint32_t lo() const;
   uint32_t hi() const;
   const DistLevelStats& last_stats() const;
@@ -158,12 +183,18 @@ struct DistLocalTiming {
   std::vector<double> query_ms;
   std::vector<uint64_t> local_nnz;  // per rank
   std::vector<uint64_t> shard_bytes, gen_peak_bytes;  // per rank
+  std::vector<uint64_t> gen_hbm_peak_bytes, resident_bytes;  // per rank (devmem.hpp)
   std::vector<DistLevelStats> stats;  // rank 0, per query
+  // verify > 0: per query, the distributed path check (1 valid, 0 invalid,
+  // -1 no path), and for the first `verify` queries the hop count of a
+  // unidirectional partitioned BFS (-2 = not run)
+  std::vector<int> path_valid;
+  std::vector<int64_t> uni_hops;
 };
 std::vector<SearchResult> dist_local_generate_run(int ranks, int device, const std::string& kind, uint32_t n,
                                                   double arg, uint64_t seed,
                                                   const std::vector<std::pair<vid_t, vid_t>>& queries,
                                                   const SearchOptions& opt, DistLocalTiming* timing,
-                                                  const DistTuning& tuning = {});
+                                                  const DistTuning& tuning = {}, int verify = 0);
 
 }  // namespace bibfs

@@ -87,6 +87,11 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["exchanged_bytes"] = s.exchanged_bytes;
   d["comm_ms"] = s.comm_ms;
   d["device_ms"] = s.device_ms;
+  d["stamped_rounds"] = s.stamped_rounds;
+  d["expand_us"] = s.expand_us;
+  d["claim_us"] = s.claim_us;
+  d["exchange_us"] = s.exchange_us;
+  d["status_us"] = s.status_us;
   return d;
 }
 
@@ -350,7 +355,9 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("solo_edges", &DistTuning::solo_edges)
       .def_readwrite("owner_cap", &DistTuning::owner_cap)
       .def_readwrite("overlap", &DistTuning::overlap)
-      .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges);
+      .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges)
+      .def_readwrite("stamps", &DistTuning::stamps)
+      .def_readwrite("hbm_cap_bytes", &DistTuning::hbm_cap_bytes);
   py::class_<DistLocalFault>(m, "DistLocalFault")
       .def(py::init<>())
       .def_readwrite("rank", &DistLocalFault::rank)
@@ -371,6 +378,12 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("local_nnz", &DistBiBfs::local_nnz)
       .def_property_readonly("shard_bytes", &DistBiBfs::shard_bytes)
       .def_property_readonly("gen_peak_bytes", &DistBiBfs::gen_peak_bytes)
+      .def_property_readonly("gen_hbm_peak_bytes", &DistBiBfs::gen_hbm_peak_bytes)
+      .def_property_readonly("resident_bytes", &DistBiBfs::resident_bytes)
+      .def("validate_path", &DistBiBfs::validate_path, py::arg("src"), py::arg("dst"), py::arg("hops"),
+           py::arg("path"), py::call_guard<py::gil_scoped_release>())
+      .def("search_unidirectional", &DistBiBfs::search_unidirectional, py::arg("src"), py::arg("dst"),
+           py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("lo", &DistBiBfs::lo)
       .def_property_readonly("hi", &DistBiBfs::hi)
       .def("load_edges", &DistBiBfs::load_edges, py::call_guard<py::gil_scoped_release>())
@@ -409,12 +422,13 @@ PYBIND11_MODULE(_native, m) {
   m.def(
       "dist_local_generate_run",
       [](int ranks, int device, const std::string& kind, uint32_t n, double arg, uint64_t seed,
-         const std::vector<std::pair<vid_t, vid_t>>& queries, const SearchOptions& opt, const DistTuning& tuning) {
+         const std::vector<std::pair<vid_t, vid_t>>& queries, const SearchOptions& opt, const DistTuning& tuning,
+         int verify) {
         DistLocalTiming t;
         std::vector<SearchResult> rs;
         {
           py::gil_scoped_release nogil;
-          rs = dist_local_generate_run(ranks, device, kind, n, arg, seed, queries, opt, &t, tuning);
+          rs = dist_local_generate_run(ranks, device, kind, n, arg, seed, queries, opt, &t, tuning, verify);
         }
         py::dict d;
         d["build_ms"] = t.build_ms;
@@ -422,11 +436,16 @@ PYBIND11_MODULE(_native, m) {
         d["local_nnz"] = t.local_nnz;
         d["shard_bytes"] = t.shard_bytes;
         d["gen_peak_bytes"] = t.gen_peak_bytes;
+        d["gen_hbm_peak_bytes"] = t.gen_hbm_peak_bytes;
+        d["resident_bytes"] = t.resident_bytes;
+        d["path_valid"] = t.path_valid;
+        d["uni_hops"] = t.uni_hops;
         py::list st;
         for (const auto& x : t.stats) st.append(dist_stats_dict(x));
         d["stats"] = st;
         return py::make_tuple(rs, d);
       },
       py::arg("ranks"), py::arg("device"), py::arg("kind"), py::arg("n"), py::arg("arg"), py::arg("seed"),
-      py::arg("queries"), py::arg("options") = SearchOptions{}, py::arg("tuning") = DistTuning{});
+      py::arg("queries"), py::arg("options") = SearchOptions{}, py::arg("tuning") = DistTuning{},
+      py::arg("verify") = 0);
 }

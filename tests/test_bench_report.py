@@ -74,12 +74,22 @@ def test_launcher_command_and_world_check(monkeypatch):
 
 
 def test_world_scaled_partitioned_config():
-    """kron:auto keeps ~17 GB of CSR per GPU: scale 27 on one GPU, +1 per doubling, capped at 30."""
+    """kron:auto: Kronecker 27 on one GPU (the single-GPU engine is its
+    reference); for N >= 2 a graph that does NOT fit one GPU -- its CSR is
+    ~1.35x one GPU's HBM -- while every rank's shard stays within ~70% of it."""
     import bench
 
-    assert [bench.world_scaled("kron:auto", w) for w in (1, 2, 4, 8, 16)] == [
-        "kron:27:16:1", "kron:28:16:1", "kron:29:16:1", "kron:30:16:1", "kron:30:16:1"]
-    assert bench.world_scaled("gnp:1000000::2", 8) == "gnp:1000000::2"
+    H = 288 * 10**9
+    assert bench.world_scaled("kron:auto", 1, H) == "kron:27:16:1"
+    for w in (2, 4, 8):
+        spec = bench.world_scaled("kron:auto", w, H)
+        assert spec.startswith("kron:30:")
+        total = bench.csr_bytes(spec)
+        assert total > 1.25 * H, (spec, total)
+        assert total / w < 0.72 * H, (spec, total / w)
+    assert bench.world_scaled("kron:auto", 8, H) == "kron:30:44:1"
+    assert bench.world_scaled("gnp:1000000::2", 8, H) == "gnp:1000000::2"
+    assert bench.csr_bytes("kron:27:16:1") == 8 * ((1 << 27) + 1) + 8 * (16 << 27)
 
 
 def test_secondary_errors_listed_without_touching_the_headline():

@@ -36,6 +36,40 @@ def test_dist_engine_world1():
     assert r.hops == 19 and len(r.path) == 20
 
 
+def test_dist_engine_distributed_checks_world1():
+    """validate_path accepts the engine's own paths and rejects a broken edge,
+    a wrong length or wrong endpoints; search_unidirectional (a plain
+    partitioned BFS) agrees with the bidirectional hop counts and the oracle,
+    including an unreachable pair."""
+    import torch  # noqa: F401
+
+    from bidirectional_bfs_amd.parallel import DistEngine
+
+    eng = DistEngine(0, 1, 0, DistEngine.unique_id())
+    g = bb.from_spec("rmat:65536:1048576:3")
+    eng.load(g)
+    rnd = random.Random(8)
+    for s, d in [(rnd.randrange(g.n), rnd.randrange(g.n)) for _ in range(8)]:
+        r = eng.search(s, d)
+        oh = native.bfs_oracle(g.csr, s, d).hops
+        assert eng.search_unidirectional(s, d).hops == r.hops == oh
+        if not r.found or r.hops < 2:
+            continue
+        p = list(r.path)
+        assert eng.validate_path(s, d, r.hops, p)
+        bad = p[:]
+        bad[1] = (bad[1] + 1) % g.n
+        while native.bfs_oracle(g.csr, bad[0], bad[1]).hops == 1 and native.bfs_oracle(g.csr, bad[1], bad[2]).hops == 1:
+            bad[1] = (bad[1] + 1) % g.n
+        assert not eng.validate_path(s, d, r.hops, bad)
+        assert not eng.validate_path(s, d, r.hops + 1, p)
+        assert not eng.validate_path(d, s, r.hops, p) or s == d
+    g2 = bb.Graph.from_edges(100, [[0, 1], [1, 2], [50, 51]])
+    eng.load(g2)
+    assert eng.search_unidirectional(0, 2).hops == 2
+    assert eng.search_unidirectional(0, 51).hops == -1
+
+
 def test_bibfs_hip_cli():
     out = subprocess.run([tool_path("bibfs_hip"), "gnp:100000::6", "0", "99999", "--verify", "--repeat", "3"],
                          capture_output=True, text=True, timeout=120)

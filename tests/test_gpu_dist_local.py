@@ -338,3 +338,55 @@ def test_overlap_knob_matches_oracle(ranks):
         for kw in ({}, {"lockstep": False}, {"direction": "bottomup"}):
             rs = dist_local_run(ranks, g, qs, tuning=make_tuning(overlap=True), **kw)
             _check_all(g, qs, rs)
+
+
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_round_stamps_split_kernel_and_exchange(ranks):
+    """DistTuning.stamps: the speculative rounds of a P > 1 search are stamped
+    (expansion / claim kernels, and the gaps the exchanges leave between
+    them); answers unchanged, overlap on and off."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    g = bb.from_spec("gnp:200000::5")
+    qs = _pairs(g.n, 8, 41)
+    for ov in (False, True):
+        rs, st = dist_local_run(ranks, g, qs, tuning=make_tuning(stamps=True, overlap=ov), return_stats=True)
+        _check_all(g, qs, rs)
+        stamped = [x for r, x in zip(rs, st) if r.found and r.hops > 2]
+        assert stamped and all(x["stamped_rounds"] > 0 for x in stamped)
+        for x in stamped:
+            assert x["stamped_rounds"] <= x["spec_rounds"]
+            assert x["expand_us"] > 0 and x["claim_us"] > 0 and x["exchange_us"] >= 0 and x["status_us"] >= 0
+            # microseconds per round, not garbage from a stale ring slot
+            assert (x["expand_us"] + x["claim_us"]) / x["stamped_rounds"] < 50000
+
+
+def test_capped_hbm_graph_only_partitioned_and_verified_without_copy():
+    """A graph that does not fit one rank's (artificially capped) HBM: the
+    one-rank build is refused, the 4-rank build holds it (the shards together
+    exceed the cap), and its answers are verified with no full copy of the
+    graph on the device: paths edge by edge by the owners (validate_path) and
+    hop counts by a unidirectional partitioned BFS -- both also held to the
+    host oracle here.  The build's peak is measured per allocation."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import dist_local_generate_run, make_tuning
+
+    spec = "rmat:65536:16777216:3"  # 33.5M directed entries: ~134 MB of columns
+    cap = 80 << 20
+    qs = _pairs(65536, 6, 53)[2:] + [(0, 65535)]
+    with pytest.raises(RuntimeError, match="HBM cap"):
+        dist_local_generate_run(1, spec, qs[:1], tuning=make_tuning(hbm_cap_bytes=cap))
+    rs, t = dist_local_generate_run(4, spec, qs, tuning=make_tuning(hbm_cap_bytes=cap), verify=4)
+    assert sum(t["shard_bytes"]) > cap, t["shard_bytes"]
+    assert max(t["resident_bytes"]) <= cap
+    for sb, pk, rb in zip(t["shard_bytes"], t["gen_peak_bytes"], t["resident_bytes"]):
+        # measured, not a formula: at least the shard plus the scatter cursor,
+        # at least what the rank holds after the build, within the cap
+        assert pk >= sb + 65536 // 4 * 8 and pk >= rb and pk <= cap, (sb, pk, rb)
+    g = bb.from_spec(spec)
+    for i, ((s, d), r) in enumerate(zip(qs, rs)):
+        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+        assert t["path_valid"][i] == (1 if r.found else -1)
+        if i < 4:
+            assert t["uni_hops"][i] == r.hops
