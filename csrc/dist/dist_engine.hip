@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <thread>
@@ -127,6 +128,10 @@ struct Ctl {
 
 struct Policy {
   double alpha, beta;
+  // alpha, beta in 1/256 steps: the planner's Beamer tests in integer
+  // arithmetic (one lane's f64 conversions and compares cost it ~1k cycles a
+  // round; 14 and 24, the defaults, are exact)
+  unsigned long long alpha_q, beta_q;
   unsigned long long nnz_total;
   uint32_t n;
   int lockstep, side, direction;
@@ -391,10 +396,11 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
       } else if (pol.direction == (int)Direction::kBottomUp) {
         mode = 2;
       } else {
-        // Beamer: m_f > m_u / alpha and n_f < n / beta, multiplied out (no f64 division)
-        const double m_u = (double)pol.nnz_total - (double)c.ved[s];
-        if (c.dir[s] == 1 && (double)c.fed[s] * pol.alpha > m_u) c.dir[s] = 2;
-        else if (c.dir[s] == 2 && (double)c.cnt[s] * pol.beta < (double)pol.n) c.dir[s] = 1;
+        // Beamer: m_f > m_u / alpha and n_f < n / beta, multiplied out, in
+        // 1/256 fixed point (fed < 2^40, alpha_q < 2^20: no overflow)
+        const unsigned long long m_u = pol.nnz_total > c.ved[s] ? pol.nnz_total - c.ved[s] : 0ull;
+        if (c.dir[s] == 1 && c.fed[s] * pol.alpha_q > m_u * 256ull) c.dir[s] = 2;
+        else if (c.dir[s] == 2 && c.cnt[s] * pol.beta_q < (unsigned long long)pol.n * 256ull) c.dir[s] = 1;
         mode = c.dir[s];
       }
       if (mode == 2) wm |= 1u << s;
@@ -787,7 +793,19 @@ __device__ void terminal_walk(const DView& V, unsigned long long key, const Poli
 // Small rounds (P > 1): the whole rank's expansion / claims by one workgroup
 // (defined with the solo kernel's helpers below).  The tests are grid-uniform:
 // every block computed the same plan.
-__device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr);
+// Block (0, 0)'s LDS staging of both frontiers for a small round: filled by
+// waves 1-3 while lane 0 plans the round (small_prefetch), so the frontier's
+// queue and row-offset loads overlap the planner instead of following it.
+struct SmallStage {
+  uint32_t su[2 * kSmallV];            // frontier vertices: side 0's, then side 1's
+  unsigned long long sb[2 * kSmallV];  // their row begins
+  uint32_t se[2 * kSmallV + 1];        // degrees -> exclusive edge prefix
+  uint32_t n0, nv, valid;              // side 0's count, both, staged (both frontiers fit)
+  uint32_t qbase[2], spbase[2], lst[2];
+};
+__device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S, uint32_t t, uint32_t nt);
+__device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
+                             SmallStage& S);
 __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap);
 __device__ __forceinline__ bool small_expand_ok(const Ctl& c, int P) {
   if (c.cont || !c.sides || P > kStageRanks) return false;
@@ -830,9 +848,16 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     fr[k] = k < 2 ? V.st->fbeg[k] : V.st->fend[k - 2];
   }
   __syncthreads();
+  __shared__ SmallStage sm;
   if (threadIdx.x == 0) {
-    reduce_gathered(V.P <= kStageRanks ? gst : V.redg[p ^ 1], V.P, rd);
+    // (two call sites, not one through a conditional pointer: that made every
+    // load of the planner's inputs a flat load)
+    if (V.P <= kStageRanks) reduce_gathered(gst, V.P, rd);
+    else reduce_gathered(V.redg[p ^ 1], V.P, rd);
     plan_round(prev, rd, pol, plan_cap, flags, c);
+  } else if (threadIdx.x >= kWave && ocap && header && nsides == 2 && V.P <= kStageRanks && blockIdx.x == 0 &&
+             blockIdx.y == 0) {
+    small_prefetch(V, fr, sm, threadIdx.x - kWave, kThreads - kWave);  // (a no-op unless the round is small)
   }
   __syncthreads();
   const bool terminal = c.state == kDone || c.state == kDead;
@@ -880,7 +905,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   }
   if (ocap && header && nsides == 2 && small_expand_ok(c, V.P)) {  // small round: one workgroup
     if (blockIdx.x == 0 && blockIdx.y == 0) {
-      small_expand(V, c, it, ocap, fr);
+      small_expand(V, c, it, ocap, fr, sm);
       if (RoundStamp* rs = round_stamp(V, it)) {
         __syncthreads();
         if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
@@ -1516,22 +1541,75 @@ __device__ __forceinline__ void small_emit(const DView& V, SmallCtr& K, const ui
 // The expansion of a small round by block (0, 0): both sides' frontiers
 // staged in LDS (side 0's vertices, then side 1's), one degree prefix, and
 // passes of kSmallU edges per thread (all their loads in flight together).
-__device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr) {
-  __shared__ uint32_t su[2 * kSmallV];
-  __shared__ unsigned long long sb[2 * kSmallV];
-  __shared__ uint32_t se[2 * kSmallV + 1];
+// Stage both sides' frontiers (and the round's state words) into S, threads
+// t of nt.  valid = 0 when a frontier is above kSmallV on this rank (possible
+// for a side that does not expand this round): small_expand then stages the
+// expanding sides itself.
+__device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S, uint32_t t, uint32_t nt) {
+  const uint32_t n0 = fr[2] - fr[0], n1 = fr[3] - fr[1];
+  const uint32_t valid = n0 <= kSmallV && n1 <= kSmallV;
+  if (t == 0) {
+    S.n0 = n0;
+    S.nv = n0 + n1;
+    S.valid = valid;
+  }
+  if (!valid) return;
+  const DState* st = V.st;
+  if (t < 2) {
+    const uint32_t cur = st->spill_cur[t];
+    S.qbase[t] = st->qtail[t];
+    S.lst[t] = cur;
+    S.spbase[t] = st->spill_n[t][cur];
+  }
+  for (uint32_t i = t; i < n0 + n1; i += nt) {
+    const int s = i >= n0;
+    const uint32_t u = pick(V.queue, s)[fr[s] + (s ? i - n0 : i)];
+    const uint32_t li = u - V.lo;
+    const unsigned long long b = V.row_off[li];
+    S.su[i] = u;
+    S.sb[i] = b;
+    S.se[i] = (uint32_t)(V.row_off[li + 1] - b);
+  }
+}
+
+__device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
+                             SmallStage& S) {
   __shared__ SmallCtr K;
-  __shared__ uint32_t qbase[2], spbase[2], lst[2];
+  uint32_t* const su = S.su;
+  unsigned long long* const sb = S.sb;
+  uint32_t* const se = S.se;
   const uint32_t tid = threadIdx.x;
   const int p = it & 1;
   DState* st = V.st;
-  const uint32_t F0 = (c.sides & 1) ? fr[2] - fr[0] : 0u, F1 = (c.sides & 2) ? fr[3] - fr[1] : 0u;
-  const uint32_t nv = F0 + F1;  // <= 2 kSmallV (the plan's vertex bound)
+  if (!S.valid) {  // (a big idle side): stage the expanding sides only
+    const uint32_t F0 = (c.sides & 1) ? fr[2] - fr[0] : 0u, F1 = (c.sides & 2) ? fr[3] - fr[1] : 0u;
+    if (tid == 0) {
+      S.n0 = F0;
+      S.nv = F0 + F1;  // <= 2 kSmallV (the plan's vertex bound)
+    }
+    if (tid < 2) {
+      const uint32_t cur = st->spill_cur[tid];
+      S.qbase[tid] = st->qtail[tid];
+      S.lst[tid] = cur;
+      S.spbase[tid] = st->spill_n[tid][cur];
+    }
+    for (uint32_t i = tid; i < F0 + F1; i += kThreads) {
+      const int s = i >= F0;
+      const uint32_t u = pick(V.queue, s)[fr[s] + (s ? i - F0 : i)];
+      const uint32_t li = u - V.lo;
+      const unsigned long long b = V.row_off[li];
+      su[i] = u;
+      sb[i] = b;
+      se[i] = (uint32_t)(V.row_off[li + 1] - b);
+    }
+    __syncthreads();
+  } else {
+    // staged during the plan: a side that does not expand keeps its entries
+    // with degree 0 (the edge search skips them)
+    for (uint32_t i = tid; i < S.nv; i += kThreads)
+      if (!((c.sides >> (i >= S.n0 ? 1 : 0)) & 1)) se[i] = 0;
+  }
   if (tid < 2) {
-    const uint32_t cur = st->spill_cur[tid];
-    qbase[tid] = st->qtail[tid];
-    lst[tid] = cur;
-    spbase[tid] = st->spill_n[tid][cur];
     K.q[tid] = 0;
     K.ne[tid] = 0;
     K.sp[tid] = 0;
@@ -1541,16 +1619,11 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
     K.best = kNoKey;
     K.found = 0;
   }
-  for (uint32_t i = tid; i < nv; i += kThreads) {
-    const int s = i >= F0;
-    const uint32_t u = pick(V.queue, s)[fr[s] + (s ? i - F0 : i)];
-    const uint32_t li = u - V.lo;
-    const unsigned long long b = V.row_off[li];
-    su[i] = u;
-    sb[i] = b;
-    se[i] = (uint32_t)(V.row_off[li + 1] - b);
-  }
   __syncthreads();
+  const uint32_t nv = S.nv, F0 = S.n0;
+  const uint32_t* const qbase = S.qbase;
+  const uint32_t* const spbase = S.spbase;
+  const uint32_t* const lst = S.lst;
   small_scan(se, nv);
   const uint32_t E = se[nv];
   const uint32_t dn[2] = {c.depth[0] + 1, c.depth[1] + 1};
@@ -1611,7 +1684,8 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
 __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap) {
   __shared__ uint32_t cnt[2 * kStageRanks + 1];
   __shared__ SmallCtr K;
-  __shared__ uint32_t qbase[2];
+  __shared__ uint32_t qbase[2], fend0[2], spn[2], ocm;
+  __shared__ unsigned long long ne0[2];
   const uint32_t tid = threadIdx.x;
   const int p = it & 1;
   const int P = V.P;
@@ -1621,6 +1695,13 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
     qbase[tid] = st->qtail[tid];
     K.q[tid] = 0;
     K.ne[tid] = 0;
+  } else if (tid >= kWave && tid < kWave + 2) {  // the round end's inputs, loaded up front
+    const uint32_t s = tid - kWave;
+    ne0[s] = st->new_edges[s];
+    fend0[s] = st->fend[s];
+    spn[s] = st->spill_n[s][st->spill_cur[s]];
+  } else if (tid == kWave + 2) {
+    ocm = st->ocmax;
   }
   if (tid == 0) {
     K.best = kNoKey;
@@ -1679,23 +1760,23 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
     for (int s = 0; s < 2; ++s) {
       const bool on = (c.sides >> s) & 1;
       const uint32_t qt = qbase[s] + K.q[s];
-      const unsigned long long ne = st->new_edges[s] + K.ne[s];
+      const unsigned long long ne = ne0[s] + K.ne[s];
       st->qtail[s] = qt;
       st->new_edges[s] = 0;
-      V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - st->fend[s]) : 0ull;
+      V.red[p].sums[2 * s] = on ? (unsigned long long)(qt - fend0[s]) : 0ull;
       V.red[p].sums[2 * s + 1] = on ? ne : 0ull;
       V.red[p].nfmax[s] = on ? ~ne : ~0ull;
       if (on) {
-        st->fbeg[s] = st->fend[s];
+        st->fbeg[s] = fend0[s];
         st->fend[s] = qt;
       }
-      const unsigned long long sp = on ? st->spill_n[s][st->spill_cur[s]] : 0ull;
+      const unsigned long long sp = on ? spn[s] : 0ull;
       V.red[p].spill[s] = sp;
       V.red[p].spillmax[s] = (uint32_t)min(sp, 0xffffffffull);
       st->hub_count[s] = 0;
     }
     if (K.found) st->meet_found = 1;
-    V.red[p].nocmax = ~(unsigned long long)st->ocmax;
+    V.red[p].nocmax = ~(unsigned long long)ocm;
     st->ocmax = 0;
     V.red[p].meetkey = min(V.red[p].meetkey, K.best);
     V.red[p ^ 1].meetkey = kNoKey;
@@ -2625,8 +2706,13 @@ struct DistBiBfs::Impl {
       wait(cstream);
     }
     max_deg = (uint64_t)y;
-    // measured, not a formula: the most this rank held at once during the
-    // build (CSR temporaries included) and the device's free-memory drop
+  }
+  // Measured, not a formula: the most this rank held at once while its CSR
+  // shard was built (generator / scan temporaries included), and the
+  // device's free-memory drop over the same span.  Called when the shard is
+  // complete, before the search state is allocated (resident_bytes covers
+  // everything held afterwards).
+  void record_build_peak() {
     gen_peak_bytes = mem.peak;
     gen_hbm_peak_bytes = mem.hbm_peak();
   }
@@ -2645,6 +2731,7 @@ struct DistBiBfs::Impl {
       HIP_CHECK(hipMemcpyAsync(d_col, rows.col.data(), rows.nnz() * 4, hipMemcpyHostToDevice, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
     nnz = rows.nnz();
+    record_build_peak();
   }
 
   // Host wait with a watchdog.  A one-lane kernel at the end of the stream
@@ -2756,6 +2843,11 @@ struct DistBiBfs::Impl {
     Policy p;
     p.alpha = opt.alpha;
     p.beta = opt.beta;
+    auto q8 = [](double x) {
+      return (unsigned long long)std::llround(std::min(std::max(x, 0.0), (double)(1u << 20)) * 256.0);
+    };
+    p.alpha_q = q8(opt.alpha);
+    p.beta_q = q8(opt.beta);
     p.nnz_total = 2 * m_input;
     p.n = n;
     p.lockstep = opt.lockstep ? 1 : 0;
@@ -3380,6 +3472,7 @@ void DistBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
     uint64_t m = 0;
     I.nnz = launch::gen_rows_gnp(n, p, seed, I.lo, I.hi, I.d_row_off, &I.d_col, &m, I.stream);
     I.m_input = m;
+    I.record_build_peak();
   }
   I.finish_build();
 }
@@ -3397,6 +3490,7 @@ void DistBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, d
     devmem::alloc(&I.d_row_off, I.row_off_bytes());
     I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, I.lo, I.hi, I.d_row_off, &I.d_col, I.stream);
     I.m_input = m;
+    I.record_build_peak();
   }
   I.finish_build();
 }

@@ -345,12 +345,23 @@ struct HipBiBfs::Impl {
       _mm_pause();
     }
   }
+  // Host-path stamps of the serving call (set_host_stamps(true)): steady-clock
+  // nanoseconds summed over queries -- entry -> request posted, posted -> first
+  // answer packet seen, -> all packets read, -> return to the binding.
+  bool host_stamps_on = false;
+  uint64_t hs_n = 0, hs_post = 0, hs_wait = 0, hs_read = 0, hs_tail = 0;
+  std::chrono::steady_clock::time_point hs_t0, hs_t1, hs_t2, hs_t3;
+  static uint64_t ns(std::chrono::steady_clock::duration d) {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count();
+  }
   uint32_t tiny_search(uint32_t src, uint32_t dst, std::vector<vid_t>* path, TinyAnswer& a) {
     ensure_server(kSrvTiny);
     const uint32_t qseq = ++seq == 0 ? ++seq : seq;
     post(qseq, src, dst, 0u);
+    if (host_stamps_on) hs_t1 = std::chrono::steady_clock::now();
     TinyPkt p0, p1;
     wait_server(kSrvTiny, qseq, [&] { return read_pkt(h_pkts, qseq, p0); });
+    if (host_stamps_on) hs_t2 = std::chrono::steady_clock::now();
     spin_pkt(h_pkts + 1, qseq, p1);
     a.status = p0.a & 0xffu;
     a.levels = p0.a >> 8;
@@ -372,6 +383,7 @@ struct HipBiBfs::Impl {
         if (3 * j + 2 < plen) out[3 * j + 2] = pk.c;
       }
     }
+    if (host_stamps_on) hs_t3 = std::chrono::steady_clock::now();
     if (tiny_stamp()) {
       unsigned long long s[16];
       HIP_CHECK(hipMemcpy(s, d_stamps, sizeof s, hipMemcpyDeviceToHost));
@@ -1103,11 +1115,19 @@ int64_t HipBiBfs::query(vid_t src, vid_t dst, std::vector<vid_t>* path) {
   }
   static const SearchOptions kDefault{};
   if (I.tiny_usable(kDefault)) {
+    if (I.host_stamps_on) I.hs_t0 = std::chrono::steady_clock::now();
     Impl::TinyAnswer a;
     const uint32_t st = I.tiny_search(src, dst, path, a);
     if (st != kTinyOverflow) {
       I.last_ms = a.ticks * 1e-5;
       I.last_einsp = a.einsp;
+      if (I.host_stamps_on) {
+        ++I.hs_n;
+        I.hs_post += Impl::ns(I.hs_t1 - I.hs_t0);
+        I.hs_wait += Impl::ns(I.hs_t2 - I.hs_t1);
+        I.hs_read += Impl::ns(I.hs_t3 - I.hs_t2);
+        I.hs_tail += Impl::ns(std::chrono::steady_clock::now() - I.hs_t3);
+      }
       if (st == kTinyFound) return a.hops;
       if (path) path->clear();
       return -1;
@@ -1129,6 +1149,15 @@ double HipBiBfs::auto_gate_timeout_us() const { return p_->auto_gate_us; }
 uint64_t HipBiBfs::auto_gate_misses() const { return p_->auto_gate_misses; }
 bool HipBiBfs::auto_handoff() const { return p_->auto_on; }
 uint64_t HipBiBfs::tiny_overflows() const { return p_->tiny_overflows; }
+void HipBiBfs::set_host_stamps(bool on) {
+  p_->host_stamps_on = on;
+  p_->hs_n = p_->hs_post = p_->hs_wait = p_->hs_read = p_->hs_tail = 0;
+}
+std::vector<double> HipBiBfs::host_stamps() const {
+  const double n = p_->hs_n ? (double)p_->hs_n : 1.0;
+  return {(double)p_->hs_n, p_->hs_post / n * 1e-3, p_->hs_wait / n * 1e-3, p_->hs_read / n * 1e-3,
+          p_->hs_tail / n * 1e-3};
+}
 
 SearchResult HipBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   auto& I = *p_;

@@ -75,10 +75,25 @@ constexpr bool kSpecAll = BIBFS_TINY_SPEC_ALL;
 constexpr bool kX4 = BIBFS_TINY_X4;
 typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
 static_assert(kTinyUnroll == 4, "two 16-byte loads per neighbour");
+// 1 = the second 16-byte load (edge words 2, 3) only for a neighbour with
+// more than two edges (at G(n, 2.2/n) ~60% of the vertices have at most
+// two).  Measured no gain: 14.50-14.56 vs 14.38-14.48 us mean query, device
+// 11.48-11.54 vs 11.41-11.47 us (profiles/r4_tiny_lazy2_ab.jsonl, 2 x 1920
+// queries each) -- the masked lines are not what bounds a round.  Off.
+#ifndef BIBFS_TINY_LAZY2
+#define BIBFS_TINY_LAZY2 0
+#endif
+constexpr bool kLazy2 = BIBFS_TINY_LAZY2;
 __device__ __forceinline__ void load_first4(unsigned long long (&w)[kTinyUnroll],
-                                            const unsigned long long* __restrict__ p) {
-  const u64x2a8 a = *reinterpret_cast<const u64x2a8*>(p), b = *reinterpret_cast<const u64x2a8*>(p + 2);
-  w[0] = a.x, w[1] = a.y, w[2] = b.x, w[3] = b.y;
+                                            const unsigned long long* __restrict__ p, uint32_t deg) {
+  if (deg) {  // (exec-masked per lane)
+    const u64x2a8 a = *reinterpret_cast<const u64x2a8*>(p);
+    w[0] = a.x, w[1] = a.y;
+  }
+  if (kLazy2 ? deg > 2 : deg > 0) {
+    const u64x2a8 b = *reinterpret_cast<const u64x2a8*>(p + 2);
+    w[2] = b.x, w[3] = b.y;
+  }
 }
 static_assert(kTinyQ == 1u << kQBits, "queue index width");
 
@@ -195,7 +210,7 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
       if (b >= nb) continue;
       const uint32_t base = tw_base(W.rec[b]), deg = W.act[b] ? tw_deg(W.rec[b]) : 0u;
       if (kX4) {
-        if (deg) load_first4(W.nbw[b], tadj + base);
+        load_first4(W.nbw[b], tadj + base, deg);
         continue;
       }
 #pragma unroll
@@ -246,7 +261,7 @@ __device__ __forceinline__ void round_fetch(Work<NB>& W, int nb, const unsigned 
     if (b >= nb) continue;
     const uint32_t base = tw_base(W.rec[b]);
     if (kX4) {
-      if (W.deg[b]) load_first4(W.nbw[b], tadj + base);
+      load_first4(W.nbw[b], tadj + base, W.deg[b]);
       continue;
     }
 #pragma unroll

@@ -143,9 +143,10 @@ class DistBiBfs {
   uint64_t local_nnz() const;
   size_t shard_bytes() const;     // owned CSR rows: row offsets + columns
   // Measured device memory of the last build (devmem.hpp): the most this rank
-  // held at once (shard + generator temporaries + search state), the device's
-  // free-memory drop over the build (hipMemGetInfo low-water mark: equal up to
-  // allocator granularity with one rank per GPU), and what it holds now.
+  // held at once while building its CSR shard (generator / scan temporaries
+  // included), the device's free-memory drop over that span (hipMemGetInfo
+  // low-water mark: equal up to allocator granularity with one rank per GPU),
+  // and what it holds now (shard + search state).
   size_t gen_peak_bytes() const;
   size_t gen_hbm_peak_bytes() const;
   size_t resident_bytes() const;

@@ -61,6 +61,12 @@ class HipBiBfs {
   uint64_t last_edges_inspected() const;
   bool tiny_engine() const;              // the loaded graph has the tiny server's packed adjacency
   uint64_t tiny_overflows() const;       // queries the tiny server handed back to the general engine (cumulative)
+  // Host-path stamps of query() on the tiny server (diagnostics): on = reset
+  // and start; host_stamps() = {queries, then mean microseconds of: entry ->
+  // request posted, posted -> first answer packet seen, -> every packet
+  // read, -> return}.
+  void set_host_stamps(bool on);
+  std::vector<double> host_stamps() const;
 
   // Throughput serving: answer K queries with one launch, one workgroup (one
   // CU) per query, up to 256 in flight.  Same results as K search() calls.

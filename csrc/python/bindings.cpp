@@ -274,6 +274,17 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("last_edges_inspected", &HipBiBfs::last_edges_inspected)
       .def_property_readonly("tiny_engine", &HipBiBfs::tiny_engine)
       .def_property_readonly("tiny_overflows", &HipBiBfs::tiny_overflows)
+      .def("set_host_stamps", &HipBiBfs::set_host_stamps)
+      .def("host_stamps", [](const HipBiBfs& e) {
+        const auto v = e.host_stamps();
+        py::dict d;
+        d["queries"] = (uint64_t)v[0];
+        d["post_us"] = v[1];
+        d["wait_first_packet_us"] = v[2];
+        d["read_packets_us"] = v[3];
+        d["return_us"] = v[4];
+        return d;
+      })
       .def("release", &HipBiBfs::release, py::call_guard<py::gil_scoped_release>())
       .def("search_batch", &HipBiBfs::search_batch, py::arg("src"), py::arg("dst"),
            py::arg("options") = SearchOptions{}, py::call_guard<py::gil_scoped_release>())
