@@ -69,9 +69,16 @@ def main():
                     "claim_us_per_round": per_round(sts, "claim_us"),
                     "exchange_us_per_round": per_round(sts, "exchange_us"),
                     "status_us_per_round": per_round(sts, "status_us"),
+                    "small_expand_rounds": sum(st["small_expand_rounds"] for st in sts),
+                    "small_claim_rounds": sum(st["small_claim_rounds"] for st in sts),
                     "host_rounds": sum(st["host_rounds"] for st in sts),
                     "solo_rounds": sum(st["solo_rounds"] for st in sts),
                 }
+                for k, nk in (("sx_plan_us", "small_expand_rounds"), ("sx_stage_us", "small_expand_rounds"),
+                              ("sx_edges_us", "small_expand_rounds"), ("sx_end_us", "small_expand_rounds"),
+                              ("sc_claims_us", "small_claim_rounds"), ("sc_end_us", "small_claim_rounds")):
+                    tot, cnt = sum(st[k] for st in sts), sum(st[nk] for st in sts)
+                    rec[k + "_per_small_round"] = round(tot / cnt, 3) if cnt else None
                 if rec["expand_us_per_round"] is not None:
                     rec["kernel_us_per_round"] = round(rec["expand_us_per_round"] + (rec["claim_us_per_round"] or 0), 3)
                 print(json.dumps(rec), flush=True)

@@ -173,7 +173,10 @@ struct RoundRec {
 // the kernels.  eb1/ee1: the side-1 launch of a split (overlap) round.
 struct RoundStamp {
   unsigned long long eb, ee, cb, ce, eb1, ee1;
-  uint32_t tag, pad;
+  // small rounds (block 0): expansion planned, frontier staged + scanned,
+  // edges done; claim: candidates claimed
+  unsigned long long ep, es, ex, cx;
+  uint32_t tag, small;  // small: bit 0 expansion, bit 1 claim ran the one-workgroup path
 };
 
 struct DState {
@@ -805,8 +808,8 @@ struct SmallStage {
 };
 __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S, uint32_t t, uint32_t nt);
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
-                             SmallStage& S);
-__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap);
+                             SmallStage& S, RoundStamp* rs);
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs);
 __device__ __forceinline__ bool small_expand_ok(const Ctl& c, int P) {
   if (c.cont || !c.sides || P > kStageRanks) return false;
   for (int s = 0; s < 2; ++s)
@@ -861,7 +864,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   }
   __syncthreads();
   const bool terminal = c.state == kDone || c.state == kDead;
-  const bool planner = blockIdx.x == 0 && blockIdx.y == 0 && side0 == 0;  // one block publishes
+  // One block publishes the plan: block (0, 1) when the launch has a second
+  // row, so the plan publication (its system-scope stores and fence, several
+  // microseconds on one lane) never delays block (0, 0), which runs a small
+  // round's whole expansion (small_expand).
+  const bool planner = blockIdx.x == 0 && blockIdx.y == (gridDim.y > 1 ? 1u : 0u) && side0 == 0;
   if (planner && threadIdx.x < kWave) {
     if (threadIdx.x == 0) publish(V, p, prev, rd, c);
     // the round that ends the search hands the host its accounted Ctl directly
@@ -898,6 +905,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     if (side0 == 0) {
       rs->eb = t_in;
       rs->tag = plan_tag(pol.epoch, it);
+      rs->small = 0;
       if (nsides == 2) rs->eb1 = rs->ee1 = 0;
     } else {
       rs->eb1 = t_in;
@@ -905,7 +913,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   }
   if (ocap && header && nsides == 2 && small_expand_ok(c, V.P)) {  // small round: one workgroup
     if (blockIdx.x == 0 && blockIdx.y == 0) {
-      small_expand(V, c, it, ocap, fr, sm);
+      if (RoundStamp* rs = round_stamp(V, it); rs && threadIdx.x == 0) {
+        rs->ep = __builtin_amdgcn_s_memrealtime();
+        rs->small = 1;
+      }
+      small_expand(V, c, it, ocap, fr, sm, round_stamp(V, it));
       if (RoundStamp* rs = round_stamp(V, it)) {
         __syncthreads();
         if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
@@ -1476,12 +1488,14 @@ __device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const u
   unsigned long long rb = 0, re = 0, best = kNoKey;
   if (want) {
     const unsigned long long m = 1ull << ((li & 31) + 32 * s);
+    // the row bounds are loaded beside the claim (independent of its result:
+    // one dependent round trip fewer; a loser's load is wasted)
     const unsigned long long old = wg_fetch_or(visw + (li >> 5), m);
+    rb = V.row_off[li];
+    re = V.row_off[li + 1];
     mine = !(old & m);
     const bool other = (old >> ((li & 31) + 32 * (s ^ 1))) & 1ull;
     if (mine) {
-      rb = V.row_off[li];
-      re = V.row_off[li + 1];
       if (other) {
         uint32_t dd = __hip_atomic_load(&pick(V.depth, s ^ 1)[li], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (dd == kEmpty) dd = s ? dcl[1] : dcl[0];
@@ -1573,7 +1587,7 @@ __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S
 }
 
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
-                             SmallStage& S) {
+                             SmallStage& S, RoundStamp* rs) {
   __shared__ SmallCtr K;
   uint32_t* const su = S.su;
   unsigned long long* const sb = S.sb;
@@ -1625,6 +1639,7 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
   const uint32_t* const spbase = S.spbase;
   const uint32_t* const lst = S.lst;
   small_scan(se, nv);
+  if (rs && tid == 0) rs->es = __builtin_amdgcn_s_memrealtime();
   const uint32_t E = se[nv];
   const uint32_t dn[2] = {c.depth[0] + 1, c.depth[1] + 1};
   const uint32_t dcl[2] = {c.depth[1] + 1, c.depth[0] + 1};  // (only this round's claims of the other side read kEmpty)
@@ -1659,6 +1674,7 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
     }
   }
   __syncthreads();
+  if (rs && tid == 0) rs->ex = __builtin_amdgcn_s_memrealtime();
   // owner headers of both sides (count capped to the block), the round's state
   const uint64_t bw = block_words(ocap);
   for (uint32_t t = tid; t < 2u * V.P; t += kThreads) {
@@ -1681,7 +1697,7 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
 // The claims of a small round by block (0, 0) of k_spec_claim: every sender's
 // block of both sides, then the round's end (spec_round_end's bookkeeping,
 // from the LDS counters -- one thread, plain accesses).
-__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap) {
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs) {
   __shared__ uint32_t cnt[2 * kStageRanks + 1];
   __shared__ SmallCtr K;
   __shared__ uint32_t qbase[2], fend0[2], spn[2], ocm;
@@ -1756,6 +1772,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
     }
   }
   __syncthreads();
+  if (rs && tid == 0) rs->cx = __builtin_amdgcn_s_memrealtime();
   if (tid == 0) {  // spec_round_end from the LDS counters (no continuation in a small round)
     for (int s = 0; s < 2; ++s) {
       const bool on = (c.sides >> s) & 1;
@@ -1922,7 +1939,8 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   if (rs && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) rs->cb = t_in;
   if (small_claim_ok(c, V.P)) {  // small round: one workgroup claims and closes it
     if (blockIdx.x == 0 && blockIdx.y == 0) {
-      small_claim_round(V, c, it, cap);
+      if (rs && threadIdx.x == 0) rs->small |= 2u;
+      small_claim_round(V, c, it, cap, rs);
       if (rs) {
         __syncthreads();
         if (threadIdx.x == 0) rs->ce = __builtin_amdgcn_s_memrealtime();
@@ -2893,6 +2911,18 @@ struct DistBiBfs::Impl {
         stats.exchange_us += us(ee, x.cb);
       }
       if (prev && prev_it + 1 == i) stats.status_us += us(prev->ce ? prev->ce : std::max(prev->ee, prev->ee1), x.eb);
+      if (x.small & 1) {
+        stats.small_expand_rounds++;
+        stats.sx_plan_us += us(x.eb, x.ep);
+        stats.sx_stage_us += us(x.ep, x.es);
+        stats.sx_edges_us += us(x.es, x.ex);
+        stats.sx_end_us += us(x.ex, x.ee);
+      }
+      if (x.small & 2) {
+        stats.small_claim_rounds++;
+        stats.sc_claims_us += us(x.cb, x.cx);
+        stats.sc_end_us += us(x.cx, x.ce);
+      }
       prev = &x;
       prev_it = i;
     }

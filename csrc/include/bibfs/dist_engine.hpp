@@ -74,6 +74,12 @@ struct DistLevelStats {
   // -> next expansion start (status allgather + launch gap)
   int stamped_rounds = 0;
   double expand_us = 0.0, claim_us = 0.0, exchange_us = 0.0, status_us = 0.0;
+  // ... of them, the rounds that took the one-workgroup small paths, by phase:
+  // expansion = plan (entry -> planned) + stage (frontier staged, degree
+  // prefix) + edges + end (headers, state); claim = claims + end
+  int small_expand_rounds = 0, small_claim_rounds = 0;
+  double sx_plan_us = 0.0, sx_stage_us = 0.0, sx_edges_us = 0.0, sx_end_us = 0.0;
+  double sc_claims_us = 0.0, sc_end_us = 0.0;
 };
 
 // Knobs of the partitioned engine (defaults are the production settings; the

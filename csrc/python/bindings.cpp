@@ -92,6 +92,14 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["claim_us"] = s.claim_us;
   d["exchange_us"] = s.exchange_us;
   d["status_us"] = s.status_us;
+  d["small_expand_rounds"] = s.small_expand_rounds;
+  d["small_claim_rounds"] = s.small_claim_rounds;
+  d["sx_plan_us"] = s.sx_plan_us;
+  d["sx_stage_us"] = s.sx_stage_us;
+  d["sx_edges_us"] = s.sx_edges_us;
+  d["sx_end_us"] = s.sx_end_us;
+  d["sc_claims_us"] = s.sc_claims_us;
+  d["sc_end_us"] = s.sc_end_us;
   return d;
 }
 
