@@ -520,8 +520,12 @@ def main(argv=None) -> int:
 
         for i in range(warmup):
             query(i)
+        # the engine's own barrier (RCCL allreduce + its streams drained); no
+        # device-wide synchronize: at world size 1 the single-GPU engine's
+        # resident server stays up across it, as in the headline loop
         eng.barrier()
-        barrier()
+        if world > 1:
+            dist.barrier()
         done = []
         qt = []
         t0 = time.perf_counter()
@@ -566,7 +570,22 @@ def main(argv=None) -> int:
             "speculative_rounds_per_query": sum(s["spec_rounds"] for s in st) / steps,
             "dense_levels_per_query": sum(s["dense_levels"] for s in st) / steps,
             "verified": ok, "checked_queries": steps + warmup,
+            "world1_engine": ("single-GPU engine over the rank's own device CSR (DistTuning.world1_single)"
+                              if world == 1 and st and st[0].get("single_engine") else None),
         }
+        if world == 1:
+            # the partitioned rounds at world size 1 (solo workgroup + speculative
+            # rounds), side by side with the default single-engine path
+            eng.set_tuning(world1_single=False)
+            for i in range(3):
+                query(i)
+            eng.barrier()
+            t1 = time.perf_counter()
+            for i in range(steps):
+                query(warmup + i)
+            eng.barrier()
+            out["rounds_engine_ms_per_query"] = round((time.perf_counter() - t1) * 1e3 / steps, 5)
+            eng.set_tuning()
         # distributed verification (untimed, no graph copy anywhere): each
         # checked path edge looked up by the owner of its first vertex, and the
         # hop counts re-derived by a unidirectional partitioned BFS

@@ -41,7 +41,8 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                 walk_max: Optional[int] = None, solo: Optional[bool] = None,
                 solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
                 overlap: Optional[bool] = None, spec_stall_edges: Optional[int] = None,
-                stamps: Optional[bool] = None, hbm_cap_bytes: Optional[int] = None) -> "native.DistTuning":
+                stamps: Optional[bool] = None, hbm_cap_bytes: Optional[int] = None,
+                world1_single: Optional[bool] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
 
     solo (one rank only): run the small rounds in one persistent workgroup
@@ -64,12 +65,17 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
     host wait and a copy per search.
 
     hbm_cap_bytes: a build that would make a rank hold more device memory
-    than this throws (rehearses "does not fit one GPU" at small scale)."""
+    than this throws (rehearses "does not fit one GPU" at small scale).
+
+    world1_single (default on): with ONE rank the shard is the whole graph,
+    so queries are answered by the single-GPU engine over the same device CSR
+    (no copy); off = the partitioned rounds (solo workgroup) at world size 1."""
     t = native.DistTuning()
     for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
                  ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap),
-                 ("spec_stall_edges", spec_stall_edges), ("stamps", stamps), ("hbm_cap_bytes", hbm_cap_bytes)):
+                 ("spec_stall_edges", spec_stall_edges), ("stamps", stamps), ("hbm_cap_bytes", hbm_cap_bytes),
+                 ("world1_single", world1_single)):
         if v is not None:
             setattr(t, k, v)
     return t

@@ -46,6 +46,7 @@
 #include <thread>
 
 #include "bibfs/dist_engine.hpp"
+#include "bibfs/hip_engine.hpp"
 #include "bibfs/io.hpp"
 #include "bibfs/trace.hpp"
 #include "comm.hpp"
@@ -2514,6 +2515,18 @@ struct DistBiBfs::Impl {
   DistLevelStats stats;
   DistTuning tune;
   bool source_only = false;  // the search in progress is search_unidirectional's
+  // World size 1 (DistTuning::world1_single): the rank's shard is the whole
+  // graph, so queries go to the single-GPU engine over the same device CSR
+  // (adopted, not copied) with its resident server; the partitioned rounds
+  // (solo workgroup, speculative rounds) serve search_unidirectional and
+  // world1_single = false.
+  std::unique_ptr<HipBiBfs> single;
+  void ensure_single() {
+    if (single || !d_row_off) return;
+    single = std::make_unique<HipBiBfs>(device);
+    single->adopt_device_csr(n, nnz, m_input, d_row_off, d_col);
+    single->set_resident(true);
+  }
   int fault_at = 0, fault_mode = 0;
 
   void setup(int dev) {
@@ -2564,6 +2577,7 @@ struct DistBiBfs::Impl {
   size_t col_bytes() const { return std::max<uint64_t>(nnz, 1) * 4; }
 
   void free_all() {
+    single.reset();  // (stops its resident server; the CSR it borrowed is freed below)
     devmem::Scope scope(&mem);
     devmem::release(d_row_off, row_off_bytes());
     devmem::release(d_col, col_bytes());
@@ -2724,6 +2738,7 @@ struct DistBiBfs::Impl {
       wait(cstream);
     }
     max_deg = (uint64_t)y;
+    if (size == 1 && tune.world1_single) ensure_single();
   }
   // Measured, not a formula: the most this rank held at once while its CSR
   // shard was built (generator / scan temporaries included), and the
@@ -3046,6 +3061,15 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     r.stats.visited = 1;
     r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return r;
+  }
+  if (size == 1 && tune.world1_single && !source_only) {
+    ensure_single();
+    SearchResult rs = single->search(src, dst, opt);
+    stats.single_engine = 1;
+    stats.levels = rs.stats.levels;
+    stats.device_ms = rs.search_ms;
+    stats.comm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return rs;
   }
   const int P = size;
   hipStream_t cs = cstream;
@@ -3646,7 +3670,16 @@ uint64_t DistBiBfs::local_nnz() const { return p_->nnz; }
 size_t DistBiBfs::shard_bytes() const { return p_->shard_bytes(); }
 size_t DistBiBfs::gen_peak_bytes() const { return p_->gen_peak_bytes; }
 size_t DistBiBfs::gen_hbm_peak_bytes() const { return p_->gen_hbm_peak_bytes; }
-size_t DistBiBfs::resident_bytes() const { return p_->mem.cur; }
+size_t DistBiBfs::resident_bytes() const {
+  // (+ the world-1 single-GPU engine's own arrays; its CSR is this rank's)
+  const auto& I = *p_;
+  size_t extra = 0;
+  if (I.single) {
+    const size_t all = I.single->device_bytes(), csr = I.row_off_bytes() + I.col_bytes();
+    extra = all > csr ? all - csr : 0;
+  }
+  return I.mem.cur + extra;
+}
 uint32_t DistBiBfs::lo() const { return p_->lo; }
 uint32_t DistBiBfs::hi() const { return p_->hi; }
 const DistLevelStats& DistBiBfs::last_stats() const { return p_->stats; }

@@ -430,9 +430,15 @@ struct HipBiBfs::Impl {
     }
   }
 
+  bool borrowed_csr = false;  // d_row_off / d_col belong to the caller (adopt_device_csr)
   void free_graph() {
     stop_server();
     free_batch();
+    if (borrowed_csr) {
+      d_row_off = nullptr;
+      d_col = nullptr;
+      borrowed_csr = false;
+    }
     if (d_row_off) HIP_CHECK(hipFree(d_row_off));
     if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
     if (d_col) HIP_CHECK(hipFree(d_col));
@@ -850,6 +856,21 @@ void HipBiBfs::load_csr(const Csr& g) {
   I.finish_graph(ms);
 }
 
+
+void HipBiBfs::adopt_device_csr(uint32_t n, uint64_t nnz, uint64_t m_input, uint64_t* d_row_off,
+                                uint32_t* d_col) {
+  TraceRange range("bibfs:build");
+  HIP_CHECK(hipSetDevice(p_->device));
+  p_->free_graph();
+  auto& I = *p_;
+  I.n = n;
+  I.nnz = nnz;
+  I.m_input = m_input;
+  I.d_row_off = d_row_off;
+  I.d_col = d_col;
+  I.borrowed_csr = true;
+  I.finish_graph(0.0);
+}
 
 void HipBiBfs::load_edges(const EdgeList& el) {
   TraceRange range("bibfs:build");

@@ -68,6 +68,7 @@ struct DistLevelStats {
   int path_collectives = 0;        // collectives spent reconstructing the path
   int solo_rounds = 0;             // rounds run by the one-workgroup solo kernel (one rank)
   int cont_rounds = 0;             // continuation rounds: candidates that overflowed an owner block re-offered
+  int single_engine = 0;           // world size 1: answered by the single-GPU engine (DistTuning::world1_single)
   // DistTuning::stamps: the speculative rounds split by device stamps (sums
   // over the stamped rounds, microseconds): expansion kernel(s), claim kernel,
   // expansion end -> claim start (candidate exchange + launch gap), claim end
@@ -100,6 +101,9 @@ struct DistTuning {
                                    // candidates are exchanged (off until measured on a multi-GPU node)
   size_t hbm_cap_bytes = 0;        // > 0: a build that would make this rank hold more device memory throws
                                    // (tests: rehearse "does not fit one GPU" at small scale)
+  bool world1_single = true;       // one rank: answer queries with the single-GPU engine over this rank's device
+                                   // CSR (the whole graph; no copy), resident server included; false = the
+                                   // partitioned rounds (solo workgroup + speculative rounds) at world size 1 too
   bool stamps = false;             // per-round device stamps -> DistLevelStats::{expand,claim,exchange,status}_us
                                    // (adds one host wait + a copy per search: diagnostics, not serving)
 };

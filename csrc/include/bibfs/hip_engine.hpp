@@ -39,6 +39,11 @@ class HipBiBfs {
 
   // --- graph ingest -------------------------------------------------------
   void load_csr(const Csr& g);                 // upload a host CSR
+  // Serve a CSR that already lives on this device (u64 row offsets, u32
+  // columns, both directions): no copy; the caller keeps ownership and must
+  // keep it alive until release() / destruction (the partitioned engine at
+  // world size 1 hands its shard -- the whole graph -- to this engine).
+  void adopt_device_csr(uint32_t n, uint64_t nnz, uint64_t m_input, uint64_t* d_row_off, uint32_t* d_col);
   void load_edges(const EdgeList& el);         // upload edges, build CSR on device
   void generate_gnp(uint32_t n, double p, uint64_t seed);                // on device
   void generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a = 0.57, double b = 0.19,

@@ -88,6 +88,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["comm_ms"] = s.comm_ms;
   d["device_ms"] = s.device_ms;
   d["stamped_rounds"] = s.stamped_rounds;
+  d["single_engine"] = s.single_engine;
   d["expand_us"] = s.expand_us;
   d["claim_us"] = s.claim_us;
   d["exchange_us"] = s.exchange_us;
@@ -376,7 +377,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("overlap", &DistTuning::overlap)
       .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges)
       .def_readwrite("stamps", &DistTuning::stamps)
-      .def_readwrite("hbm_cap_bytes", &DistTuning::hbm_cap_bytes);
+      .def_readwrite("hbm_cap_bytes", &DistTuning::hbm_cap_bytes)
+      .def_readwrite("world1_single", &DistTuning::world1_single);
   py::class_<DistLocalFault>(m, "DistLocalFault")
       .def(py::init<>())
       .def_readwrite("rank", &DistLocalFault::rank)

@@ -27,10 +27,14 @@ def test_dist_engine_world1():
         g = bb.from_spec(spec)
         eng.load(g)
         rnd = random.Random(3)
-        for s, d in [(0, g.n - 1)] + [(rnd.randrange(g.n), rnd.randrange(g.n)) for _ in range(10)]:
-            for direction in ("auto", "topdown", "bottomup"):
-                r = eng.search(s, d, direction=direction)
-                check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+        for single in (True, False):  # the single-GPU engine on the rank's CSR, then the partitioned rounds
+            eng.set_tuning(world1_single=single)
+            for s, d in [(0, g.n - 1)] + [(rnd.randrange(g.n), rnd.randrange(g.n)) for _ in range(10)]:
+                for direction in ("auto", "topdown", "bottomup"):
+                    r = eng.search(s, d, direction=direction)
+                    check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+                    assert eng.last_stats["single_engine"] == (1 if single and s != d else 0)
+    eng.set_tuning()
     eng.generate_gnp(1_000_000, None, 2)
     r = eng.search(0, 999_999)
     assert r.hops == 19 and len(r.path) == 20

@@ -114,7 +114,7 @@ def test_tiny_capacities_force_count_sync_and_overflow(ranks):
     import torch  # noqa: F401
     from bidirectional_bfs_amd.parallel import make_tuning
 
-    tune = make_tuning(cap=4, nosync_bytes=0, spec_cap_max=1024, spec_stall_edges=1024)
+    tune = make_tuning(cap=4, nosync_bytes=0, spec_cap_max=1024, spec_stall_edges=1024, world1_single=False)
     seen = {"host_rounds": 0, "count_syncs": 0, "overflow_levels": 0}
     for spec in ("kron:14:16:3", "gnp:20000::6"):
         g = bb.from_spec(spec)
@@ -175,10 +175,12 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
         qs = _pairs(g.n, 6, 13)
         for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False},
                    {"direction": "bottomup"}):
-            for tune in (make_tuning(spec_rounds=spec_rounds), make_tuning(spec_rounds=spec_rounds, cap=4,
-                                                                          nosync_bytes=0, spec_stall_edges=64),
-                         make_tuning(spec_rounds=spec_rounds, owner_cap=2),
-                         make_tuning(spec_rounds=spec_rounds, overlap=True, owner_cap=64)):
+            # (world1_single off: one rank runs the partitioned rounds too)
+            for tune in (make_tuning(spec_rounds=spec_rounds, world1_single=False),
+                         make_tuning(spec_rounds=spec_rounds, cap=4, nosync_bytes=0, spec_stall_edges=64,
+                                     world1_single=False),
+                         make_tuning(spec_rounds=spec_rounds, owner_cap=2, world1_single=False),
+                         make_tuning(spec_rounds=spec_rounds, overlap=True, owner_cap=64, world1_single=False)):
                 rs = dist_local_run(ranks, g, qs, tuning=tune, trace=True, **kw)
                 for (s, d), r in zip(qs, rs):
                     want, hops = round_trace(g.csr, s, d, side=kw.get("side", "edges"),
@@ -247,7 +249,8 @@ def test_world1_solo_matches_oracle_and_hands_off(spec):
     for solo in (True, False):
         for kw in ({}, {"lockstep": False}, {"direction": "bottomup"}, {"side": "alternate"},
                    {"want_path": False}):
-            rs, st = dist_local_run(1, g, qs, tuning=make_tuning(solo=solo), return_stats=True, **kw)
+            rs, st = dist_local_run(1, g, qs, tuning=make_tuning(solo=solo, world1_single=False), return_stats=True,
+                                    **kw)
             for (s, d), r, e in zip(qs, rs, expect):
                 if kw.get("want_path") is False:
                     assert r.hops == e, (s, d, r.hops, e)
@@ -267,7 +270,10 @@ def test_world1_solo_long_path_and_disconnected():
     n = 5000
     line = np.stack([np.arange(n - 1), np.arange(1, n)], 1).astype(np.uint32)
     g = Graph.from_edges(n + 3, np.concatenate([line, np.array([[n, n + 1]], np.uint32)]))
-    rs, st = dist_local_run(1, g, [(0, n - 1), (17, 2900), (0, n + 1), (n + 2, 3)], return_stats=True)
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    rs, st = dist_local_run(1, g, [(0, n - 1), (17, 2900), (0, n + 1), (n + 2, 3)], return_stats=True,
+                            tuning=make_tuning(world1_single=False))
     assert rs[0].hops == n - 1 and list(rs[0].path) == list(range(n))
     assert rs[1].hops == 2900 - 17 and list(rs[1].path) == list(range(17, 2901))
     assert not rs[2].found and not rs[3].found
@@ -282,9 +288,14 @@ def test_world1_back_to_back_queries_keep_state_clean():
     g = bb.from_spec("gnp:30000::4")
     rnd = random.Random(5)
     qs = [(rnd.randrange(g.n), rnd.randrange(g.n)) for _ in range(60)]
-    rs = dist_local_run(1, g, qs)
-    for (s, d), r in zip(qs, rs):
-        check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    for single in (False, True):
+        rs, st = dist_local_run(1, g, qs, tuning=make_tuning(world1_single=single), return_stats=True)
+        for (s, d), r in zip(qs, rs):
+            check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
+        # world1_single: the rank's CSR is served by the single-GPU engine (no rounds)
+        assert all(x["single_engine"] == (1 if single else 0) for x in st if x["levels"])
 
 
 @pytest.mark.parametrize("ranks", [2, 3, 4])
