@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "device.hpp"
 
@@ -73,6 +74,11 @@ constexpr bool kSpecAll = BIBFS_TINY_SPEC_ALL;
 #define BIBFS_TINY_X4 1
 #endif
 constexpr bool kX4 = BIBFS_TINY_X4;
+// 1 = single-wave rounds of at most 64 edges run a one-item body (see the loop)
+#ifndef BIBFS_TINY_SW_SPLIT
+#define BIBFS_TINY_SW_SPLIT 1
+#endif
+constexpr bool kSwSplit = BIBFS_TINY_SW_SPLIT;
 typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
 static_assert(kTinyUnroll == 4, "two 16-byte loads per neighbour");
 // 1 = the second 16-byte load (edge words 2, 3) only for a neighbour with
@@ -467,17 +473,21 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         }
         if (T.E0 == 0 || T.E1 == 0) T.status = kTinyNoPath;  // an isolated endpoint
         if (kStamp) st[1] = stamp();
-        // ---- single-wave rounds: both frontiers together up to 128 edges
-        while (T.status == 0 && T.E0 + T.E1 <= kCapW) {
+        // ---- single-wave rounds: both frontiers together up to 128 edges.
+        // Compiled twice: one item per lane for rounds of at most 64 edges
+        // (the first rounds of a query), two otherwise -- the one-item body
+        // carries none of the second item's selects, ballots and stores.
+        // (Every exit sets T.status, which ends the loop.)
+        auto sw_round = [&](auto nbc) {
+          constexpr int NB = decltype(nbc)::value;
           const uint32_t x0 = T.E0, x1 = T.E1;
           const RoundCtx X = make_ctx(x0, x1, T.cb0, T.cb1, T.d0, T.d1);
-          const int nb = x0 + x1 > 64 ? 2 : 1;
-          Work<2> W;
-          round_issue<2, true>(W, X, lane, 64, nb, P.tadj, VIS);
-          Counts<2> K;
-          round_count<2>(K, W);
+          Work<NB> W;
+          round_issue<NB, true>(W, X, lane, 64, NB, P.tadj, VIS);
+          Counts<NB> K;
+          round_count<NB>(K, W);
           const uint32_t ovf =
-              round_place<2, true>(W, K, X, nb, T.ql0, T.ql1, 0u, 0u, lane, P.tadj, QU, JQ, JR, &C.meet);
+              round_place<NB, true>(W, K, X, NB, T.ql0, T.ql1, 0u, 0u, lane, P.tadj, QU, JQ, JR, &C.meet);
           const bool qovf = __ballot(ovf & kOvfQueue) != 0, rovf = __ballot(ovf & kOvfRec) != 0;
           T.x0 = x0;
           T.x1 = x1;
@@ -487,18 +497,18 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           T.ql1 += K.qt[1];
           if (qovf) {
             T.status = kTinyOverflow;
-            break;
+            return;
           }
           // the wave's own ds_min_u64 precede this read (one wave's LDS ops are in order)
           const unsigned long long m = uni64(__hip_atomic_load(&C.meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
           if (m != ~0ull) {
             T.meet = m;
             T.status = kTinyFound;
-            break;
+            return;
           }
           if (rovf) {  // the next round's records do not fit
             T.status = kTinyOverflow;
-            break;
+            return;
           }
           T.E0 = K.et & 0xffffu;
           T.E1 = K.et >> 16;
@@ -507,6 +517,10 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           ++T.d0;
           ++T.d1;
           if (!T.E0 || !T.E1) T.status = kTinyNoPath;  // a side claimed nothing: its component is exhausted
+        };
+        while (T.status == 0 && T.E0 + T.E1 <= kCapW) {
+          if (kSwSplit && T.E0 + T.E1 <= 64) sw_round(std::integral_constant<int, 1>{});
+          else sw_round(std::integral_constant<int, 2>{});
         }
         if (lane == 0) S = T;
       }
