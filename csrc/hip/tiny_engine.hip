@@ -79,6 +79,11 @@ constexpr bool kX4 = BIBFS_TINY_X4;
 #define BIBFS_TINY_SW_SPLIT 1
 #endif
 constexpr bool kSwSplit = BIBFS_TINY_SW_SPLIT;
+// 1 = all-wave rounds of at most kTT edges run a one-item body
+#ifndef BIBFS_TINY_AW_SPLIT
+#define BIBFS_TINY_AW_SPLIT 1
+#endif
+constexpr bool kAwSplit = BIBFS_TINY_AW_SPLIT;
 typedef unsigned long long u64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
 static_assert(kTinyUnroll == 4, "two 16-byte loads per neighbour");
 // 1 = the second 16-byte load (edge words 2, 3) only for a neighbour with
@@ -561,13 +566,17 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       if (tid == kTT - 64) C.cnt[slot == 2 ? 0 : slot + 1] = 0ull;
       const RoundCtx X = make_ctx(x0, x1, cb0, cb1, d0, d1);
       TINY_PH(0)
-      if (wid * 64 < X.tot) {
-        const int nb = (wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
-        Work<2> W;
-        round_issue<2, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS);
-        if (!kSpecAll) round_fetch<2>(W, nb, P.tadj);
-        Counts<2> K;
-        round_count<2>(K, W);
+      // one item per lane when the round has at most kTT edges (every round
+      // under the lockstep cap), two otherwise: as in the single-wave phase
+      // the one-item body carries none of the second item's instructions
+      auto aw_round = [&](auto nbc) {
+        constexpr int NB = decltype(nbc)::value;
+        const int nb = (NB == 2 && wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
+        Work<NB> W;
+        round_issue<NB, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS);
+        if (!kSpecAll) round_fetch<NB>(W, nb, P.tadj);
+        Counts<NB> K;
+        round_count<NB>(K, W);
         TINY_PH(3)
         if (K.qt[0] | K.qt[1]) {  // uniform
           // ONE ds_add_rtn_u64 on the packed round counter (TinyCtl layout)
@@ -578,12 +587,16 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
                                                (unsigned long long)K.qt[0] << 40 | (unsigned long long)K.qt[1] << 52);
           const uint32_t blo = lane0((uint32_t)base), bhi = lane0((uint32_t)(base >> 32));
           TINY_PH(4)
-          const uint32_t ovf = round_place<2, kSpecAll>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20),
-                                              blo & 0xFFFFFu, ((blo >> 20) | (bhi << 12)) & 0xFFFFFu, lane, P.tadj,
-                                              QU, JQ, JR, &C.meet);
+          const uint32_t ovf = round_place<NB, kSpecAll>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20),
+                                               blo & 0xFFFFFu, ((blo >> 20) | (bhi << 12)) & 0xFFFFFu, lane, P.tadj,
+                                               QU, JQ, JR, &C.meet);
           if (ovf & kOvfQueue) atomicMin(&C.meet, 0ull);  // key 0 = overflow (a meet has length >= 1)
           if (ovf & kOvfRec) C.rovf = 1u;
         }
+      };
+      if (wid * 64 < X.tot) {
+        if (kAwSplit && X.tot <= (uint32_t)kTT) aw_round(std::integral_constant<int, 1>{});
+        else aw_round(std::integral_constant<int, 2>{});
       }
       TINY_PH(5)
       lds_barrier();

@@ -15,7 +15,7 @@
 #   suite    reference suite table (C21): scripts/make_graphs + scripts/benchmark_test.sh
 #            over 1k/10k/50k/100k x v1, v2 (np 4), v3 (--resident), v4 (np 1)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench
-#   stamp    cycle stamps of the 100k single-query server (BIBFS_STAMP builds)
+#   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
@@ -43,8 +43,8 @@ run_task() {
         python3 bench.py --steps 20 --warmup 5 --extra-steps 50 --batch 0 --no-cpu-ref \
         > $O/${TAG}_prof_bench.json 2> $O/${TAG}_prof_bench.err ;;
     stamp)
-      BIBFS_STAMP=1 BIBFS_STAMP_SERVER=1 $T 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999 --verify --trace \
-        --resident --repeat 5 > $O/${TAG}_stamp_100k.txt 2>&1 ;;
+      BIBFS_TINY_STAMP=1 $T 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999 --verify --resident --repeat 8 \
+        > $O/${TAG}_stamp_100k.txt 2>&1 ;;
     distab)
       $T 600 python3 benchmarks/dist_rounds.py > $O/${TAG}_dist_rounds.jsonl 2> $O/${TAG}_dist_rounds.err ;;
     *)
