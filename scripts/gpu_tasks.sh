@@ -15,6 +15,7 @@
 #   suite    reference suite table (C21): scripts/make_graphs + scripts/benchmark_test.sh
 #            over 1k/10k/50k/100k x v1, v2 (np 4), v3 (--resident), v4 (np 1)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench
+#   pmc      one SQ counter pass (rocprofv3 --pmc) over the resident 100k workload
 #   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
 set -o pipefail
@@ -45,6 +46,10 @@ run_task() {
     stamp)
       BIBFS_TINY_STAMP=1 $T 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999 --verify --resident --repeat 8 \
         > $O/${TAG}_stamp_100k.txt 2>&1 ;;
+    pmc)
+      timeout -s KILL 120 rocprofv3 --output-format csv --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
+        SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES -d $O/${TAG}_pmc_sq -- \
+        python3 benchmarks/pmc_100k.py --mode resident > $O/${TAG}_pmc_sq.log 2>&1 ;;
     distab)
       $T 600 python3 benchmarks/dist_rounds.py > $O/${TAG}_dist_rounds.jsonl 2> $O/${TAG}_dist_rounds.err ;;
     *)
