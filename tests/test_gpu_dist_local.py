@@ -401,3 +401,25 @@ def test_capped_hbm_graph_only_partitioned_and_verified_without_copy():
         assert t["path_valid"][i] == (1 if r.found else -1)
         if i < 4:
             assert t["uni_hops"][i] == r.hops
+
+
+def test_eight_rank_rehearsal_of_the_bench_path():
+    """The bench's multi-GPU partitioned path rehearsed with 8 ranks on one GPU:
+    device-generated shards, small and multi-workgroup rounds, stamps, and the
+    distributed checks (path per owner, unidirectional BFS) -- every answer
+    against the host oracle."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import dist_local_generate_run, make_tuning
+
+    for spec in ("gnp:60000::7", "kron:15:16:4"):
+        g = bb.from_spec(spec)
+        qs = _pairs(g.n, 8, 61)[2:]
+        rs, t = dist_local_generate_run(8, spec, qs, tuning=make_tuning(stamps=True), verify=3)
+        assert len(t["local_nnz"]) == 8 and sum(t["local_nnz"]) == g.csr.nnz
+        for i, ((s, d), r) in enumerate(zip(qs, rs)):
+            h = native.bfs_oracle(g.csr, s, d).hops
+            check_result(g.csr, s, d, r.hops, r.path, h)
+            assert t["path_valid"][i] == (1 if r.found else -1)
+            if i < 3:
+                assert t["uni_hops"][i] == h
+        assert any(st["stamped_rounds"] > 0 for st in t["stats"])
