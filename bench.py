@@ -562,7 +562,7 @@ def main(argv=None) -> int:
             "device_ms_per_query": round(sum(r.search_ms for r, _ in done) / steps, 5),
             "mean_hops": sum(r.hops for r, _ in done) / steps,
             "mean_rounds": rounds,
-            "ms_per_round": round(dt * 1e3 / steps / max(rounds, 1e-9), 5),
+            "ms_per_round": round(dt * 1e3 / steps / rounds, 5) if rounds else None,
             "host_syncs_per_query": sum(s["host_syncs"] for s in st) / steps,
             "exchanged_bytes_per_query": sum(s["exchanged_bytes"] for s in st) / steps,
             "collectives_per_query": sum(s["collectives"] for s in st) / steps,

@@ -74,7 +74,8 @@ def main():
                     "host_rounds": sum(st["host_rounds"] for st in sts),
                     "solo_rounds": sum(st["solo_rounds"] for st in sts),
                 }
-                for k, nk in (("sx_plan_us", "small_expand_rounds"), ("sx_stage_us", "small_expand_rounds"),
+                for k, nk in (("sx_plan_us", "small_expand_rounds"), ("sx_staging_us", "small_expand_rounds"),
+                              ("sx_stage_us", "small_expand_rounds"),
                               ("sx_edges_us", "small_expand_rounds"), ("sx_end_us", "small_expand_rounds"),
                               ("sc_claims_us", "small_claim_rounds"), ("sc_end_us", "small_claim_rounds")):
                     tot, cnt = sum(st[k] for st in sts), sum(st[nk] for st in sts)

@@ -80,6 +80,7 @@ struct DistLevelStats {
   // prefix) + edges + end (headers, state); claim = claims + end
   int small_expand_rounds = 0, small_claim_rounds = 0;
   double sx_plan_us = 0.0, sx_stage_us = 0.0, sx_edges_us = 0.0, sx_end_us = 0.0;
+  double sx_staging_us = 0.0;      // ... of sx_plan_us: entry -> previous plan + reductions staged in LDS
   double sc_claims_us = 0.0, sc_end_us = 0.0;
 };
 

@@ -96,6 +96,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["small_expand_rounds"] = s.small_expand_rounds;
   d["small_claim_rounds"] = s.small_claim_rounds;
   d["sx_plan_us"] = s.sx_plan_us;
+  d["sx_staging_us"] = s.sx_staging_us;
   d["sx_stage_us"] = s.sx_stage_us;
   d["sx_edges_us"] = s.sx_edges_us;
   d["sx_end_us"] = s.sx_end_us;
