@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--graph", default="gnp:100000::6")
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--summary", default=None, help="print only one aggregate line, tagged with this label")
     a = ap.parse_args()
     import torch  # noqa: F401  (HIP runtime first)
     import bench
@@ -28,16 +29,37 @@ def main():
     eng = bench.generate(HipEngine(0), a.graph)
     eng.set_resident(True)
     pairs = bench.pick_pairs(eng, n, a.pairs, 12345)
+    agg = []
     for s, d, h in pairs:
-        dev, tot = [], []
+        dev, tot, lds = [], [], []
         for _ in range(a.reps):
             r = eng.search(s, d)
             assert r.hops == h
             dev.append(r.search_ms)
             tot.append(r.total_ms)
-        print(json.dumps({"src": s, "dst": d, "hops": h, "search_us": round(statistics.median(dev) * 1e3, 2),
-                          "query_us": round(statistics.median(tot) * 1e3, 2), "levels": r.levels,
-                          "edges": r.edges_inspected, "visited": r.visited}), flush=True)
+            lds.append(r.stats["lds_ms"])
+        rec = {"src": s, "dst": d, "hops": h, "search_us": round(statistics.median(dev) * 1e3, 2),
+               "query_us": round(statistics.median(tot) * 1e3, 2), "levels": r.levels,
+               "edges": r.edges_inspected, "visited": r.visited, "handoff": r.handoff,
+               "grid_levels": r.stats["grid_levels"], "lds_us": round(statistics.median(lds) * 1e3, 2),
+               "lds_levels": r.stats["lds_levels"]}
+        agg.append(rec)
+        if a.summary is None:
+            print(json.dumps(rec), flush=True)
+    if a.summary is not None:
+        print(json.dumps({"label": a.summary, "graph": a.graph, "pairs": len(agg), "reps": a.reps,
+                          "search_us_mean": round(statistics.mean(x["search_us"] for x in agg), 2),
+                          "query_us_mean": round(statistics.mean(x["query_us"] for x in agg), 2),
+                          "handoff_fraction": round(statistics.mean(float(x["handoff"]) for x in agg), 3),
+                          "grid_levels_mean": round(statistics.mean(x["grid_levels"] for x in agg), 2),
+                          "lds_us_mean": round(statistics.mean(x["lds_us"] for x in agg), 2),
+                          "lds_levels_mean": round(statistics.mean(x["lds_levels"] for x in agg), 2),
+                          "levels_mean": round(statistics.mean(x["levels"] for x in agg), 2),
+                          "handoff_lds_us_mean": round(statistics.mean(
+                              [x["lds_us"] for x in agg if x["handoff"]] or [0.0]), 2),
+                          "handoff_search_us_mean": round(statistics.mean(
+                              [x["search_us"] for x in agg if x["handoff"]] or [0.0]), 2)}),
+              flush=True)
     eng.set_resident(False)
 
 

@@ -321,9 +321,9 @@ __device__ __forceinline__ T uniform_copy(const T& src) {
 
 // The planner on a WHOLE wave (every lane computes the same plan from
 // wave-uniform copies of its inputs, which puts the ~50-field decision chain
-// on the scalar unit); lane 0 writes it.  On one lane of the vector unit the
-// same code took ~5k cycles per round (stamped: RoundStamp::sg -> ep), each
-// dependent 64-bit step paying the vector pipeline's latency.
+// on the scalar unit); lane 0 writes it.  Kept as the kPlanOnWave A/B only:
+// the copies spill ~80 SGPRs to VGPR lanes and the round's planning stamp
+// (RoundStamp::sg -> ep) got ~0.7-1.2 us SLOWER than on one lane.
 __device__ __forceinline__ void plan_round_wave(const Ctl& p, const Reduced& rd, const Policy& pol, uint64_t spec_cap,
                                                 int flags, Ctl& out) {
   const Ctl pl = uniform_copy(p);

@@ -1232,6 +1232,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   SearchStats stats;
   bool grid = opt.force_grid;
   double lds_ms = 0.0;
+  int stats_handoff_levels = -1;  // levels the LDS phase ran before a hand-off
   bool use_auto = false, auto_final = false;  // device hand-off (grid_auto) behind a resident search
   uint32_t pub_auto = 0, auto_ls = 0, auto_tag = 0;
   grid = grid || I.n > 0x7fffffffu;
@@ -1279,6 +1280,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         grid = true;
         stats.handoff = true;
         const uint32_t lv1 = I.h_res->levels;
+        stats_handoff_levels = (int)lv1;
         const auto outcome = I.wait_auto(pub_auto, auto_ls);
         auto_final = outcome == Impl::kAutoFinal;
         if (auto_final) {
@@ -1312,6 +1314,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
       if (I.h_res->status == kHandoff) {
         grid = true;
         stats.handoff = true;
+        stats_handoff_levels = (int)I.h_res->levels;
         I.mirror_valid = true;  // the LDS kernel published the hand-off state
         launch::handoff_scatter(g, I.buf, I.stream);
       }
@@ -1357,6 +1360,8 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   SearchResult r = I.collect(grid ? *I.gres : *I.h_res, opt, std::move(stats));
   r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   r.search_ms = lds_ms;
+  r.stats.lds_ms = lds_ms;
+  if (!grid || stats_handoff_levels >= 0) r.stats.lds_levels = grid ? stats_handoff_levels : r.stats.levels;
   if (grid && !timed_by_events && I.gres->seq == pub_seq)
     r.search_ms = (double)(I.gres->rt_end - I.h_res->rt_begin) * 1e-5;
   // the last grid level's predicated cleanup did the work (its tag is the

@@ -79,6 +79,14 @@ constexpr bool kX4 = BIBFS_TINY_X4;
 #define BIBFS_TINY_SW_SPLIT 1
 #endif
 constexpr bool kSwSplit = BIBFS_TINY_SW_SPLIT;
+// Items per lane of the widest single-wave round (2 or 4): with 4, rounds of
+// 129-256 edges stay on wave 0 (no barrier, SGPR state) instead of starting
+// the all-wave phase.
+#ifndef BIBFS_TINY_SW_NB
+#define BIBFS_TINY_SW_NB 2
+#endif
+constexpr int kSwNB = BIBFS_TINY_SW_NB;
+static_assert(kSwNB == 2 || kSwNB == 4, "single-wave items per lane");
 // 1 = all-wave rounds of at most kTT edges run a one-item body
 #ifndef BIBFS_TINY_AW_SPLIT
 #define BIBFS_TINY_AW_SPLIT 1
@@ -282,16 +290,18 @@ __device__ __forceinline__ void round_fetch(Work<NB>& W, int nb, const unsigned 
 }
 
 // Per-lane and per-wave counts of the new vertices: queue slots from ballots,
-// record slots from ONE DPP scan of the degrees (side 0 [15:0], side 1 [31:16]).
+// record slots from ONE DPP scan of the degrees (side 0 [15:0], side 1
+// [31:16]) while a wave's sum fits 16 bits (NB <= 2), else one scan per side.
 template <int NB>
 struct Counts {
   uint32_t qpre[NB];  // new vertices of this lane's side below this lane (in batches < b, then lanes < lane)
   uint32_t qt[2];     // the wave's new vertices per side (uniform)
-  uint32_t ex, et;    // exclusive / total (uniform) record counts per side
+  uint32_t ex[2], et[2];  // exclusive / total (uniform) record counts per side
 };
 template <int NB>
 __device__ __forceinline__ void round_count(Counts<NB>& K, const Work<NB>& W) {
-  uint32_t ep = 0;
+  uint32_t ep = 0, ep1 = 0;
+  constexpr bool kPacked = 64u * NB * kTinyMaxDeg < 65536u;
   K.qt[0] = K.qt[1] = 0;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -299,11 +309,27 @@ __device__ __forceinline__ void round_count(Counts<NB>& K, const Work<NB>& W) {
     K.qpre[b] = W.s1[b] ? K.qt[1] + mbcnt64(m1) : K.qt[0] + mbcnt64(m0);
     K.qt[0] += (uint32_t)__popcll(m0);
     K.qt[1] += (uint32_t)__popcll(m1);
-    ep += W.deg[b] << (W.s1[b] ? 16 : 0);
+    if (kPacked) {
+      ep += W.deg[b] << (W.s1[b] ? 16 : 0);
+    } else {
+      ep += W.s1[b] ? 0u : W.deg[b];
+      ep1 += W.s1[b] ? W.deg[b] : 0u;
+    }
   }
   const uint32_t ei = wave_scan(ep);
-  K.ex = ei - ep;
-  K.et = lane63(ei);
+  if (kPacked) {
+    K.ex[0] = (ei - ep) & 0xffffu;
+    K.ex[1] = (ei - ep) >> 16;
+    const uint32_t t = lane63(ei);
+    K.et[0] = t & 0xffffu;
+    K.et[1] = t >> 16;
+  } else {
+    const uint32_t ei1 = wave_scan(ep1);
+    K.ex[0] = ei - ep;
+    K.ex[1] = ei1 - ep1;
+    K.et[0] = lane63(ei);
+    K.et[1] = lane63(ei1);
+  }
 }
 
 // Round step 2: queue entries, next-round records (the speculatively loaded
@@ -320,7 +346,7 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
                                                 const unsigned long long* __restrict__ tadj, uint32_t (*QU)[kTinyQ],
                                                 uint32_t* JQ, unsigned long long* JR, unsigned long long* meet) {
   uint32_t ovf = 0;
-  uint32_t e0 = e0b + (K.ex & 0xffffu), e1 = e1b + (K.ex >> 16);
+  uint32_t e0 = e0b + K.ex[0], e1 = e1b + K.ex[1];
   // (!kSpec: the claimed vertices' first edges were fetched by round_fetch,
   // right after the claims, so their latency overlaps the counting)
 #pragma unroll
@@ -367,7 +393,7 @@ template <bool kStamp>
 __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
   static_assert(kTinyB == 2, "two items per lane");
   constexpr uint32_t kCapR = (uint32_t)kTT * kTinyB;  // frontier edges one all-wave round expands
-  constexpr uint32_t kCapW = 64u * kTinyB;             // ... one single-wave round
+  constexpr uint32_t kCapW = 64u * kSwNB;              // ... one single-wave round
   __shared__ unsigned long long VIS[2][kTW];
   __shared__ uint32_t QU[2][kTinyQ];
   __shared__ unsigned long long R[2][2][kTRC];  // [buffer][side][record]
@@ -515,8 +541,8 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
             T.status = kTinyOverflow;
             return;
           }
-          T.E0 = K.et & 0xffffu;
-          T.E1 = K.et >> 16;
+          T.E0 = K.et[0];
+          T.E1 = K.et[1];
           T.cb0 ^= 1;
           T.cb1 ^= 1;
           ++T.d0;
@@ -525,7 +551,8 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         };
         while (T.status == 0 && T.E0 + T.E1 <= kCapW) {
           if (kSwSplit && T.E0 + T.E1 <= 64) sw_round(std::integral_constant<int, 1>{});
-          else sw_round(std::integral_constant<int, 2>{});
+          else if (kSwNB == 2 || T.E0 + T.E1 <= 128) sw_round(std::integral_constant<int, 2>{});
+          else sw_round(std::integral_constant<int, kSwNB>{});
         }
         if (lane == 0) S = T;
       }
@@ -582,8 +609,8 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           // ONE ds_add_rtn_u64 on the packed round counter (TinyCtl layout)
           unsigned long long base = 0;
           if (lane == 0)
-            base = atomicAdd(&C.cnt[slot], (unsigned long long)(K.et & 0xffffu) |
-                                               (unsigned long long)(K.et >> 16) << 20 |
+            base = atomicAdd(&C.cnt[slot], (unsigned long long)K.et[0] |
+                                               (unsigned long long)K.et[1] << 20 |
                                                (unsigned long long)K.qt[0] << 40 | (unsigned long long)K.qt[1] << 52);
           const uint32_t blo = lane0((uint32_t)base), bhi = lane0((uint32_t)(base >> 32));
           TINY_PH(4)

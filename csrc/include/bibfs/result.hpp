@@ -46,6 +46,8 @@ struct SearchStats {
   int grid_levels = 0;         // GPU: levels run by the grid engine
   int bottomup_levels = 0;
   bool handoff = false;        // GPU: persistent engine handed off to the grid engine
+  double lds_ms = 0.0;         // GPU: device time of the one-workgroup (LDS / tiny) phase
+  int lds_levels = 0;          // GPU: levels that phase ran (before a hand-off)
   std::vector<LevelTrace> trace;
 };
 

@@ -42,6 +42,8 @@ py::dict stats_dict(const SearchStats& s) {
   d["grid_levels"] = s.grid_levels;
   d["bottomup_levels"] = s.bottomup_levels;
   d["handoff"] = s.handoff;
+  d["lds_ms"] = s.lds_ms;
+  d["lds_levels"] = s.lds_levels;
   py::list tr;
   for (const auto& t : s.trace) {
     py::dict x;
