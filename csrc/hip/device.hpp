@@ -279,7 +279,7 @@ void bitmap_meet(const SearchBuffers& b, uint32_t* d_flag, hipStream_t s);
 void walk_path(const SearchBuffers& b, const HostSide& h, uint32_t src, uint32_t dst, uint32_t seq,
                uint32_t n, hipStream_t s);
 // if_done: 0 = always; 1 = only once a grid level ended the search; 2 = and
-// only behind an auto level that ran (aux[2] active)
+// only behind an auto chain that took the hand-off (aux[2] bit 0)
 void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
              int if_done, hipStream_t s);
 // Device hand-off: one top-down level enqueued BEFORE the resident LDS search
@@ -289,9 +289,12 @@ void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* h
 // (mirror `seq`, result `res_seq`); a search that ended in LDS, or a first
 // level the Beamer rule sends bottom-up, makes it a no-op (the latter
 // publishes the mirror unchanged, so the host loop takes that level).
+// levels > 1 chains that many device-planned levels: the finisher of each
+// plans the next one into aux (or ends the chain: search over, or a level the
+// Beamer rule declines, which publishes the mirror `seq` for the host).
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
-               unsigned long long gate_ticks,
+               unsigned long long gate_ticks, int levels,
                hipStream_t s);
 
 }  // namespace launch

@@ -1481,7 +1481,53 @@ struct GridParams {
   float alpha;
   uint32_t nparts;     // workgroups taking part in the level (0 = gridDim.x); the rest exit at once
   uint32_t fbase, fcount;  // auto level: the frontier, from the plan (0/0 = read DevState)
+  int chain;           // auto level with another auto level enqueued behind it: its finisher plans that one
 };
+
+// aux[2], the auto chain's word: bit 0 = the chain took the hand-off (its
+// levels dirtied the global state: the predicated cleanup runs), bit 1 = the
+// side of the planned level, bit 3 = a planned level is to run.
+constexpr uint32_t kAuxTook = 1u, kAuxActive = 8u;
+
+// The auto level's plan from the frontier facts, with the host's rules
+// (grid_level / choose_side / choose_mode): the side with fewer frontier
+// edges; declined when the Beamer rule wants bottom-up; hub degree; chunk size.
+struct AutoPlan {
+  uint32_t active, side, F, hub, cv, fb;
+  bool declined;
+};
+template <typename OffT>
+__device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, unsigned long long fe0,
+                                                    unsigned long long fe1, unsigned long long ve0,
+                                                    unsigned long long ve1, uint32_t fb0, uint32_t fb1, uint32_t fd0,
+                                                    uint32_t fd1) {
+  AutoPlan a{1u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false};
+  a.side = fe0 <= fe1 ? 0u : 1u;
+  const unsigned long long fe = a.side ? fe1 : fe0;
+  const double m_u = (double)P.nnz - (double)(a.side ? ve1 : ve0);
+  a.fb = a.side ? fb1 : fb0;
+  a.F = (a.side ? fd1 : fd0) - a.fb;
+  if ((double)fe > m_u / (double)P.alpha) {
+    a.active = 0;
+    a.declined = true;
+    return a;
+  }
+  if (P.max_deg > kHubDegree && fe > kHubDegree) a.hub = kHubDegree;
+  if (a.F <= 4096 && fe > 16384 && P.max_deg > 64) a.hub = 64;
+  if ((a.F + kGridThreads - 1) / kGridThreads < P.cus * 4u && fe > 0)
+    a.cv = (uint32_t)min<uint64_t>(kGridThreads, max<uint64_t>(kGridChunkMin, kGridThreads * (uint64_t)a.F / fe));
+  return a;
+}
+
+// The plan for the kernels behind: [2] the chain word; [3] frontier size;
+// [4] hub degree; [5] chunk size; [6] frontier base
+__device__ __forceinline__ void write_auto_plan(uint32_t* aux, const AutoPlan& a, bool took) {
+  aux[2] = (took ? kAuxTook : 0u) | (a.active ? kAuxActive | a.side << 1 : 0u);
+  aux[3] = a.F;
+  aux[4] = a.hub;
+  aux[5] = a.cv;
+  aux[6] = a.fb;
+}
 
 template <typename OffT>
 __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass);
@@ -1564,8 +1610,7 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
       const bool hand = seen && (uint32_t)g == 1u;
       if (hand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (blockIdx.x == 0) {
-        uint32_t active = hand, side = 0, hub = ~0u, cv = kGridThreads, fb = 0, F = 0;
-        bool declined = false;
+        AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false};
         if (hand) {
           // the whole DevState in one round trip: lane i loads word i
           constexpr uint32_t kW = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
@@ -1578,31 +1623,13 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
             return (unsigned long long)word(field) |
                    (unsigned long long)word(reinterpret_cast<const uint32_t*>(field) + 1) << 32;
           };
-          const unsigned long long fe0 = dword(&st->fedges[0]), fe1 = dword(&st->fedges[1]);
-          side = fe0 <= fe1 ? 0u : 1u;
-          const unsigned long long fe = side ? fe1 : fe0;
-          const double m_u = (double)P.nnz - (double)(side ? dword(&st->vedges[1]) : dword(&st->vedges[0]));
-          fb = side ? word(&st->fbeg[1]) : word(&st->fbeg[0]);
-          F = (side ? word(&st->fend[1]) : word(&st->fend[0])) - fb;
-          if ((double)fe > m_u / (double)P.alpha) {
-            active = 0;
-            declined = true;
-          } else {
-            if (P.max_deg > kHubDegree && fe > kHubDegree) hub = kHubDegree;
-            if (F <= 4096 && fe > 16384 && P.max_deg > 64) hub = 64;
-            if ((F + kGridThreads - 1) / kGridThreads < P.cus * 4u && fe > 0)
-              cv = (uint32_t)min<uint64_t>(kGridThreads, max<uint64_t>(kGridChunkMin, kGridThreads * (uint64_t)F / fe));
-          }
+          ap = plan_auto_level(P, dword(&st->fedges[0]), dword(&st->fedges[1]), dword(&st->vedges[0]),
+                               dword(&st->vedges[1]), word(&st->fbeg[0]), word(&st->fbeg[1]), word(&st->fend[0]),
+                               word(&st->fend[1]));
         }
         if (lane == 0) {
-          // the plan for the kernels behind: [2] bit 0 active, bit 1 side;
-          // [3] frontier size; [4] hub degree; [5] chunk size; [6] frontier base
-          P.b.aux[2] = active | side << 1;
-          P.b.aux[3] = F;
-          P.b.aux[4] = hub;
-          P.b.aux[5] = cv;
-          P.b.aux[6] = fb;
-          if (declined && P.mirror)
+          write_auto_plan(P.b.aux, ap, ap.active != 0);  // a declined level: the chain takes nothing
+          if (ap.declined && P.mirror)
             __hip_atomic_store(&P.mirror->pad[0], P.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
@@ -1628,7 +1655,7 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
 template <typename OffT>
 __device__ bool auto_plan(GridParams<OffT>& P) {
   const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
-  if (!(xp & 1u)) return false;
+  if (!(xp & kAuxActive)) return false;
   P.side = (int)((xp >> 1) & 1u);
   P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
   P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
@@ -1739,7 +1766,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
   DevState* st = P.b.st;
   if constexpr (kAuto) {  // behind an auto level: its plan (written by the kernel before)
     const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
-    if (!(xp & 1u)) return;
+    if (!(xp & kAuxActive)) return;
     P.side = (int)((xp >> 1) & 1u);
     P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
     // the host's hub launch size: 4 workgroups per frontier vertex
@@ -2041,7 +2068,23 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   }
   if (tid < kWords) w[tid] = reinterpret_cast<const uint32_t*>(&sv)[tid];
   if (P.res_seq && sv.status != kRunning) publish_result(b, P.h, sv, P.res_seq, P.n);
-  if (P.mirror && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
+  // an auto level with another one chained behind it plans that level (the
+  // next launch reads aux); the host hears nothing until the chain ends
+  bool next = false;
+  if (P.chain) {
+    __shared__ uint32_t snext;
+    if (tid == 0) {
+      AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false};
+      if (sv.status == kRunning)
+        ap = plan_auto_level(P, sv.fedges[0], sv.fedges[1], sv.vedges[0], sv.vedges[1], sv.fbeg[0], sv.fbeg[1],
+                             sv.fend[0], sv.fend[1]);
+      write_auto_plan(b.aux, ap, true);
+      snext = ap.active;
+    }
+    __syncthreads();
+    next = snext != 0;
+  }
+  if (P.mirror && !next && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
 }
 
 // Seed a search for the grid engine / step-wise API.
@@ -2116,7 +2159,7 @@ __global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t 
 __global__ void k_cleanup(launch::SearchBuffers b, uint32_t* done_ctr, uint32_t* host_tag, uint32_t tag,
                           int if_done) {
   const DevState* st = b.st;
-  if (if_done == 2 && !(load_agent(&b.aux[2]) & 1u)) return;   // no auto level ran (grid-uniform)
+  if (if_done == 2 && !(load_agent(&b.aux[2]) & kAuxTook)) return;  // no auto level ran (grid-uniform)
   if (if_done && load_agent(&st->status) == kRunning) return;  // grid-uniform
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x, t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
   if (((uint64_t)st->qtail[0] + st->qtail[1]) * 32 > b.words) {
@@ -2182,6 +2225,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.alpha = 14.0f;
   P.nparts = 0;
   P.fbase = P.fcount = 0;
+  P.chain = 0;
   return P;
 }
 
@@ -2298,12 +2342,15 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
 
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
-               unsigned long long gate_ticks, hipStream_t s) {
+               unsigned long long gate_ticks, int levels, hipStream_t s) {
   // The grid size is fixed before the frontier exists: cus / 4 workgroups
-  // (a 10M G(n, p) hand-off level is ~17 chunks; every workgroup takes chunk
-  // tickets, and fewer blocks keep the ticket and done counters cheap).  The
-  // hub pass behind is enqueued only when the graph has a vertex above 64.
+  // for the first level (a 10M G(n, p) hand-off level is ~17 chunks; every
+  // workgroup takes chunk tickets, and fewer blocks keep the ticket and done
+  // counters cheap), one per CU for a chained level (a frontier ~2x larger:
+  // the blocks beyond its chunk count leave at once).  The hub pass behind a
+  // level is enqueued only when the graph has a vertex above 64.
   const unsigned blocks = (unsigned)std::max(8, cus / 4);
+  const unsigned cblocks = (unsigned)std::max(8, cus);
   const unsigned hblocks = (unsigned)std::max(8, cus);
   const int scatter = g.n > kBmMaxN ? 1 : 0;
   auto launch_one = [&](auto P) {
@@ -2315,9 +2362,13 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     P.max_deg = max_deg;
     P.nnz = g.nnz;
     P.alpha = (float)alpha;
+    P.chain = 0;
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
-    k_grid_topdown<OffT, true><<<blocks, kGridThreads, 0, s>>>(P);
-    if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
+    for (int l = 0; l < std::max(1, levels); ++l) {
+      P.chain = l + 1 < levels ? 1 : 0;
+      k_grid_topdown<OffT, true><<<l ? cblocks : blocks, kGridThreads, 0, s>>>(P);
+      if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
+    }
   };
   if (g.row_off32) launch_one(gp<uint32_t>(g, b, 0));
   else launch_one(gp<uint64_t>(g, b, 0));

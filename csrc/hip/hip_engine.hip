@@ -73,6 +73,14 @@ struct HipBiBfs::Impl {
     const char* e = std::getenv("BIBFS_AUTO_HANDOFF");
     return !(e && e[0] == '0');
   }();
+  // Device-planned grid levels chained behind the hand-off (the first one
+  // planned by k_handoff, each further one by the finisher of the level before):
+  // BIBFS_AUTO_LEVELS, default 2.
+  int auto_levels = [] {
+    const char* e = std::getenv("BIBFS_AUTO_LEVELS");
+    const int v = e ? std::atoi(e) : 2;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
   bool auto_usable(const SearchOptions& opt) const {
     return auto_on && nnz > 0 && max_deg <= kAutoMaxDeg && !opt.trace && !opt.force_grid &&
            opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
@@ -1259,7 +1267,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
       I.server_post(src, dst, opt, seq);
       if (use_auto) {
         launch::grid_auto(g, I.buf, I.cus, I.max_deg, opt.alpha, I.h_state, auto_ls, hsg(), pub_auto, seq,
-                          (unsigned long long)(std::max(0.0, I.auto_gate_us) * 100.0), I.stream);
+                          (unsigned long long)(std::max(0.0, I.auto_gate_us) * 100.0), I.auto_levels, I.stream);
         auto_tag = I.next_clean_tag();
         launch::cleanup(I.buf, I.n, I.d_flag + 8, I.h_clean, auto_tag, 2, I.stream);
       }
@@ -1284,7 +1292,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         const auto outcome = I.wait_auto(pub_auto, auto_ls);
         auto_final = outcome == Impl::kAutoFinal;
         if (auto_final) {
-          stats.grid_levels = 1;
+          stats.grid_levels = (int)(I.gres->levels - lv1);
           I.clean_tag[I.cur] = auto_tag;  // the cleanup behind the auto level ran (its tag)
         } else if (outcome == Impl::kAutoMissed) {
           // the gate wait gave up before this search handed off: nothing ran
