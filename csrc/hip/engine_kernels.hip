@@ -2351,7 +2351,9 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
   // level is enqueued only when the graph has a vertex above 64.
   const unsigned blocks = (unsigned)std::max(8, cus / 4);
   const unsigned cblocks = (unsigned)std::max(8, cus);
-  const unsigned hblocks = (unsigned)std::max(8, cus);
+  // the hub pass: the host's grid size for a hub level (4 blocks per frontier
+  // vertex up to 4 per CU; k_grid_hubs<auto> leaves the blocks beyond it)
+  const unsigned hblocks = (unsigned)std::max(8, cus * 4);
   const int scatter = g.n > kBmMaxN ? 1 : 0;
   auto launch_one = [&](auto P) {
     using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;

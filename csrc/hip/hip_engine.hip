@@ -64,11 +64,15 @@ struct HipBiBfs::Impl {
 
   // Device hand-off (grid_auto): on by default for resident searches of
   // graphs the general server takes, with the default level policy, when no
-  // vertex has more than kAutoMaxDeg edges; BIBFS_AUTO_HANDOFF=0 turns it off
+  // vertex has more than auto_max_deg edges; BIBFS_AUTO_HANDOFF=0 turns it off
   // (A/B).  Hub graphs keep the host-planned first level: on Kronecker 22 the
   // auto level lost in three A/Bs (0.058-0.060 vs 0.054-0.057 ms) while
   // 10M G(n, p) gains ~1% (profiles/r3_auto_handoff_ab2.jsonl).
-  static constexpr uint64_t kAutoMaxDeg = 64;
+  // (BIBFS_AUTO_MAX_DEG overrides the bound, for A/B on hub graphs)
+  uint64_t auto_max_deg = [] {
+    const char* e = std::getenv("BIBFS_AUTO_MAX_DEG");
+    return e ? std::strtoull(e, nullptr, 10) : 64ull;
+  }();
   bool auto_on = [] {
     const char* e = std::getenv("BIBFS_AUTO_HANDOFF");
     return !(e && e[0] == '0');
@@ -82,7 +86,7 @@ struct HipBiBfs::Impl {
     return v < 1 ? 1 : (v > 8 ? 8 : v);
   }();
   bool auto_usable(const SearchOptions& opt) const {
-    return auto_on && nnz > 0 && max_deg <= kAutoMaxDeg && !opt.trace && !opt.force_grid &&
+    return auto_on && nnz > 0 && max_deg <= auto_max_deg && !opt.trace && !opt.force_grid &&
            opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
   }
   // k_handoff's gate wait limit (microseconds; set_auto_gate_timeout_us).
