@@ -185,6 +185,26 @@ class HipEngine:
         on the host from the LDS engine's mirror."""
         return self._e.auto_gate_misses
 
+    @property
+    def auto_levels(self) -> int:
+        """Device-planned grid levels chained behind the hand-off (1-8): each
+        level's finisher plans the next, so no host round trip between them."""
+        return self._e.auto_levels
+
+    @auto_levels.setter
+    def auto_levels(self, levels: int) -> None:
+        self._e.auto_levels = int(levels)
+
+    @property
+    def auto_max_degree(self) -> int:
+        """The device hand-off runs on graphs whose largest degree is at most
+        this (default 64)."""
+        return self._e.auto_max_degree
+
+    @auto_max_degree.setter
+    def auto_max_degree(self, deg: int) -> None:
+        self._e.auto_max_degree = int(deg)
+
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:
         self._e.begin(int(src), int(dst))

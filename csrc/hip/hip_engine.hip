@@ -1180,6 +1180,13 @@ void HipBiBfs::set_auto_handoff(bool on) { p_->auto_on = on; }
 void HipBiBfs::set_auto_gate_timeout_us(double us) { p_->auto_gate_us = us; }
 double HipBiBfs::auto_gate_timeout_us() const { return p_->auto_gate_us; }
 uint64_t HipBiBfs::auto_gate_misses() const { return p_->auto_gate_misses; }
+void HipBiBfs::set_auto_levels(int levels) {
+  BIBFS_REQUIRE(levels >= 1 && levels <= 8, "auto_levels must be in [1, 8]");
+  p_->auto_levels = levels;
+}
+int HipBiBfs::auto_levels() const { return p_->auto_levels; }
+void HipBiBfs::set_auto_max_degree(uint64_t deg) { p_->auto_max_deg = deg; }
+uint64_t HipBiBfs::auto_max_degree() const { return p_->auto_max_deg; }
 bool HipBiBfs::auto_handoff() const { return p_->auto_on; }
 uint64_t HipBiBfs::tiny_overflows() const { return p_->tiny_overflows; }
 void HipBiBfs::set_host_stamps(bool on) {

@@ -107,6 +107,15 @@ class HipBiBfs {
   void set_auto_gate_timeout_us(double us);
   double auto_gate_timeout_us() const;
   uint64_t auto_gate_misses() const;
+  // Device-planned grid levels chained behind the hand-off (1-8, default 2;
+  // env BIBFS_AUTO_LEVELS): each level's finisher plans the next one, so a
+  // search that needs that many grid levels never waits for the host.
+  void set_auto_levels(int levels);
+  int auto_levels() const;
+  // The device hand-off runs on graphs whose largest degree is at most this
+  // (default 64: hub graphs keep host-planned levels; env BIBFS_AUTO_MAX_DEG).
+  void set_auto_max_degree(uint64_t deg);
+  uint64_t auto_max_degree() const;
 
   // --- step-wise API (parity with the reference's per-level C API,
   //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)

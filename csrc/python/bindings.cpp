@@ -336,6 +336,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property("auto_handoff", &HipBiBfs::auto_handoff, &HipBiBfs::set_auto_handoff)
       .def_property("auto_gate_timeout_us", &HipBiBfs::auto_gate_timeout_us, &HipBiBfs::set_auto_gate_timeout_us)
       .def_property_readonly("auto_gate_misses", &HipBiBfs::auto_gate_misses)
+      .def_property("auto_levels", &HipBiBfs::auto_levels, &HipBiBfs::set_auto_levels)
+      .def_property("auto_max_degree", &HipBiBfs::auto_max_degree, &HipBiBfs::set_auto_max_degree)
       .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
       .def_property_readonly("last_batch_fallbacks", &HipBiBfs::last_batch_fallbacks)
       .def("set_batch_tuning", &HipBiBfs::set_batch_tuning, py::arg("lds_first") = -1, py::arg("threads") = 0)

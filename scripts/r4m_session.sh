@@ -3,7 +3,7 @@
 # (BIBFS_AUTO_LEVELS), then the single-wave 4-item A/B of the tiny server
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 G=${TAG:-r4o}
-timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_engine.py > gpurun_out/${G}_pytest.log 2>&1 || exit 1
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_engine.py tests/test_gpu_dist_and_tools.py > gpurun_out/${G}_pytest.log 2>&1 || exit 1
 O=gpurun_out/${G}_split.jsonl
 for lv in 1 2 3 2 1; do
   BIBFS_AUTO_LEVELS=$lv timeout -k 10 240 python3 benchmarks/pair_latency.py --graph gnp:10000000::1 --pairs 64 --reps 5 --summary levels$lv >> $O 2>>gpurun_out/${G}.err || exit 1

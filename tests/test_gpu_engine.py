@@ -344,6 +344,40 @@ def test_resident_auto_handoff_vs_oracle(gpu_engine, spec):
         gpu_engine.set_resident(False)
 
 
+@pytest.mark.parametrize("spec", ["gnp:3000000::4", "kron:20:16:2"])
+def test_resident_auto_levels_chain_vs_oracle(gpu_engine, spec):
+    """Chained device-planned grid levels (auto_levels): the finisher of each
+    auto level plans the next one into aux, and the host only hears from the
+    chain's end (result, or the mirror when the search goes on or a level is
+    declined).  Chains of 1, 2, 3 and 8 levels, back to back, hub graphs
+    included (auto_max_degree lifted: the hub pass runs behind auto levels);
+    every answer against the oracle, and grid levels are counted from the
+    result's level count."""
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 32, 9)
+    truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
+    gpu_engine.set_resident(True)
+    md0, lv0 = gpu_engine.auto_max_degree, gpu_engine.auto_levels
+    try:
+        gpu_engine.auto_max_degree = 1 << 40
+        for lv in (1, 2, 3, 8, 2):
+            gpu_engine.auto_levels = lv
+            assert gpu_engine.auto_levels == lv
+            grid = 0
+            for (s, d), h in zip(pairs, truth):
+                r = gpu_engine.search(s, d)
+                check_result(g.csr, s, d, r.hops, r.path, h)
+                grid += r.stats["grid_levels"]
+            assert grid > 0, "expected searches with grid levels"
+        with pytest.raises(Exception):
+            gpu_engine.auto_levels = 0
+    finally:
+        gpu_engine.auto_max_degree = md0
+        gpu_engine.auto_levels = lv0
+        gpu_engine.set_resident(False)
+
+
 def test_auto_handoff_gate_timeout_falls_back_to_host(gpu_engine):
     """The gated first grid level gives up when its search has not left LDS in
     time (forced here: a zero wait).  Such a search still hands off later; the
