@@ -1578,6 +1578,9 @@ __device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid
 //  * hash-set searches (n > kBmMaxN): the LDS engine dumped its raw hash
 //    tables (coalesced); every thread scatters one slot into the global
 //    visited bitmaps (a single CU issuing them cost ~7 us on 10M G(n, p)).
+// A gate already holding a later search's seq ends the wait at once (that
+// search ran after ours: ours stayed in LDS; a chain delayed behind earlier
+// launches on the stream used to wait out the whole timeout there).
 // The gate wait gives up after GridParams::gate_ticks (default 6 s of
 // s_memrealtime, 100 MHz -- longer than the host's 5 s server wait).  A wait
 // that gives up runs no level and publishes nothing (aux[2] = 0); the host
@@ -1600,10 +1603,17 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
         g = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         g = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
             __builtin_amdgcn_readfirstlane((uint32_t)g);
-        if ((uint32_t)(g >> 32) == P.gate_seq) {
+        const uint32_t gs = (uint32_t)(g >> 32);
+        if (gs == P.gate_seq) {
           seen = true;
           break;
         }
+        // A LATER search already answered on this state set (the gate word is
+        // per set; sets alternate): ours ended in LDS -- a search that hands
+        // off holds the host in wait_auto until this chain publishes, so no
+        // later search can start -- and this chain was only late behind the
+        // stream's earlier launches.  Nothing to run.
+        if ((int32_t)(gs - P.gate_seq) > 0) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > P.gate_ticks) break;
         __builtin_amdgcn_s_sleep(8);  // ~0.2 us: the pollers must not crowd the LDS search's memory
       }

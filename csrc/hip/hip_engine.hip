@@ -102,6 +102,9 @@ struct HipBiBfs::Impl {
   enum AutoOutcome { kAutoFinal, kAutoMirror, kAutoMissed };
   AutoOutcome wait_auto(uint32_t pub, uint32_t ls) {
     for (uint64_t it = 1;; ++it) {
+      if (dbg() && (it & ((1ull << 26) - 1)) == 0)
+        std::fprintf(stderr, "[auto] waiting: pub %u ls %u gres.seq %u mirror.seq %u levels %u status %u\n", pub, ls,
+                     h_gres->seq, h_state->pad[0], h_state->levels, h_state->status);
       if (__atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub) return kAutoFinal;
       if (__atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) == ls) {
         return __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub ? kAutoFinal : kAutoMirror;
@@ -633,6 +636,8 @@ struct HipBiBfs::Impl {
   // wait for the pinned DevState mirror of the last finished level
   void wait_level() {
     for (uint64_t it = 1; __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != level_seq; ++it) {
+      if (dbg() && (it & ((1ull << 26) - 1)) == 0)
+        std::fprintf(stderr, "[grid] waiting for level seq %u: mirror.seq %u\n", level_seq, h_state->pad[0]);
       if ((it & 8191) == 0) {
         const hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess && __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != level_seq)
@@ -1301,6 +1306,9 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         const uint32_t lv1 = I.h_res->levels;
         stats_handoff_levels = (int)lv1;
         const auto outcome = I.wait_auto(pub_auto, auto_ls);
+        if (I.dbg())
+          std::fprintf(stderr, "[auto] outcome %d lds levels %u gres levels %u mirror levels %u\n", (int)outcome, lv1,
+                       I.h_gres->levels, I.h_state->levels);
         auto_final = outcome == Impl::kAutoFinal;
         if (auto_final) {
           stats.grid_levels = (int)(I.gres->levels - lv1);
