@@ -68,7 +68,9 @@ struct HipBiBfs::Impl {
   // (A/B).  Hub graphs keep the host-planned first level: on Kronecker 22 the
   // auto level lost in three A/Bs (0.058-0.060 vs 0.054-0.057 ms) while
   // 10M G(n, p) gains ~1% (profiles/r3_auto_handoff_ab2.jsonl).
-  // (BIBFS_AUTO_MAX_DEG overrides the bound, for A/B on hub graphs)
+  // (BIBFS_AUTO_MAX_DEG overrides the bound, for A/B on hub graphs: with the
+  // hub pass sized like the host's it still lost on Kronecker 22, 71.6-72.2 vs
+  // 47.2-49.8 us mean search, profiles/r4_auto_chain_ab.jsonl)
   uint64_t auto_max_deg = [] {
     const char* e = std::getenv("BIBFS_AUTO_MAX_DEG");
     return e ? std::strtoull(e, nullptr, 10) : 64ull;
@@ -79,10 +81,14 @@ struct HipBiBfs::Impl {
   }();
   // Device-planned grid levels chained behind the hand-off (the first one
   // planned by k_handoff, each further one by the finisher of the level before):
-  // BIBFS_AUTO_LEVELS, default 2.
+  // BIBFS_AUTO_LEVELS, default 1.  Chains of 2 / 3 measured slower on 10M
+  // G(n, p): 69.3-70.1 / 71.4 vs 67.1-67.2 us mean search -- the LDS phase
+  // itself slows by ~2 us per chained level (the extra launches behind every
+  // query) and the second level saves less than that
+  // (profiles/r4_auto_chain_ab.jsonl).
   int auto_levels = [] {
     const char* e = std::getenv("BIBFS_AUTO_LEVELS");
-    const int v = e ? std::atoi(e) : 2;
+    const int v = e ? std::atoi(e) : 1;
     return v < 1 ? 1 : (v > 8 ? 8 : v);
   }();
   bool auto_usable(const SearchOptions& opt) const {

@@ -81,7 +81,9 @@ constexpr bool kX4 = BIBFS_TINY_X4;
 constexpr bool kSwSplit = BIBFS_TINY_SW_SPLIT;
 // Items per lane of the widest single-wave round (2 or 4): with 4, rounds of
 // 129-256 edges stay on wave 0 (no barrier, SGPR state) instead of starting
-// the all-wave phase.
+// the all-wave phase.  Measured slower: device 11.61-11.75 vs 10.55-10.63 us
+// mean per 100k query (profiles/r4_tiny_sw4_ab.jsonl) -- a 4-item wave-0
+// round costs more than the 16-wave round it replaces.  Off (2).
 #ifndef BIBFS_TINY_SW_NB
 #define BIBFS_TINY_SW_NB 2
 #endif

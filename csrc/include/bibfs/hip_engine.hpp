@@ -107,7 +107,7 @@ class HipBiBfs {
   void set_auto_gate_timeout_us(double us);
   double auto_gate_timeout_us() const;
   uint64_t auto_gate_misses() const;
-  // Device-planned grid levels chained behind the hand-off (1-8, default 2;
+  // Device-planned grid levels chained behind the hand-off (1-8, default 1;
   // env BIBFS_AUTO_LEVELS): each level's finisher plans the next one, so a
   // search that needs that many grid levels never waits for the host.
   void set_auto_levels(int levels);
