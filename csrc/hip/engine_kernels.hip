@@ -1482,6 +1482,7 @@ struct GridParams {
   uint32_t nparts;     // workgroups taking part in the level (0 = gridDim.x); the rest exit at once
   uint32_t fbase, fcount;  // auto level: the frontier, from the plan (0/0 = read DevState)
   int chain;           // auto level with another auto level enqueued behind it: its finisher plans that one
+  int hub_direct;      // k_grid_hubs: the whole frontier is the hub list (no top-down pass before it)
 };
 
 // aux[2], the auto chain's word: bit 0 = the chain took the hand-off (its
@@ -1783,7 +1784,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
     P.nparts = max(1u, min(gridDim.x, 4u * __builtin_amdgcn_readfirstlane(P.b.aux[3])));
     if (blockIdx.x >= P.nparts) return;
   }
-  const uint32_t H = st->hub_count;
+  // the hub list: the vertices k_grid_topdown deferred, or (hub_direct) the
+  // whole frontier -- a small frontier of heavy vertices skips the top-down
+  // pass, which ran it on a handful of workgroups
+  const uint32_t* const hl = P.hub_direct ? P.b.queue[P.side] + st->fbeg[P.side] : P.b.hub_list;
+  const uint32_t H = P.hub_direct ? st->fend[P.side] - st->fbeg[P.side] : st->hub_count;
   if (H == 0) return;  // grid-uniform: the top-down finisher completed the level
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (uint32_t t0 = 0; t0 < H; t0 += kHubTile) {
@@ -1795,7 +1800,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
       const uint32_t j = tid * kPer + k;
       d[k] = 0;
       if (j < nt) {
-        const uint32_t u = P.b.hub_list[t0 + j];
+        const uint32_t u = hl[t0 + j];
         const OffT b = P.row_off[u];
         d[k] = (unsigned long long)(P.row_off[u + 1] - b);
         hu[j] = u;
@@ -2236,6 +2241,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.nparts = 0;
   P.fbase = P.fcount = 0;
   P.chain = 0;
+  P.hub_direct = 0;
   return P;
 }
 
@@ -2336,12 +2342,34 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
     cv = std::min<uint64_t>(kGridThreads, std::max<uint64_t>(kGridChunkMin, kGridThreads * frontier / frontier_edges));
   const uint64_t chunks = (frontier + cv - 1) / cv;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, chunks));
-  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
+  unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
+  // A hub level whose whole frontier fits one hub tile runs as ONE edge-parallel
+  // pass over every frontier edge (k_grid_hubs, hub_direct): the top-down pass
+  // would walk its light vertices on frontier/cv workgroups (one, for a
+  // Kronecker hub level of ~40 vertices: ~10 us) before the hub pass starts.
+  // Measured (profiles/r4_grid_hub_direct_ab.jsonl, mean search): Kronecker 22
+  // 47.4-48.5 -> 40.6-42.1 us, Kronecker 25 60.8 -> 48.7 us.  Sizing that
+  // pass by edges instead (mode 2: up to 1024 workgroups) lost: 57.1 us.
+  // BIBFS_GRID_HUB_DIRECT: 0 off, 1 on (the hub pass's grid), 2 on with one
+  // workgroup per 256 frontier edges (up to 4 per CU)
+  static const int direct_mode = [] {
+    const char* e = std::getenv("BIBFS_GRID_HUB_DIRECT");
+    return e ? std::atoi(e) : 1;
+  }();
+  const bool direct = direct_mode && hub_deg != ~0u && frontier <= (uint64_t)kHubTile;
+  if (direct && direct_mode == 2)
+    hblocks = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>((uint64_t)cus * 4, (frontier_edges + kGridThreads - 1) / kGridThreads));
   auto launch_one = [&](auto P) {
     using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
     P.mirror = mirror, P.seq = seq, P.trace = trace, P.h = h, P.res_seq = res_seq;
     P.hub_deg = hub_deg;  // ~0u: no hub pass
     P.chunk_v = (uint32_t)cv;
+    if (direct) {
+      P.hub_direct = 1;
+      k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
+      return;
+    }
     k_grid_topdown<OffT><<<blocks, kGridThreads, 0, s>>>(P);
     if (hub_deg != ~0u) k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
   };
