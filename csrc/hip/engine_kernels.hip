@@ -1447,6 +1447,7 @@ constexpr uint32_t kHubDegree = 4096;  // deferred to k_grid_hubs
 #define BIBFS_KNOB_GRID_CHUNK_MIN 64
 #endif
 constexpr uint64_t kGridChunkMin = BIBFS_KNOB_GRID_CHUNK_MIN;  // smallest chunk (vertices) of k_grid_topdown
+constexpr int kHubTile = 1024;  // k_grid_hubs: hubs staged in LDS per pass
 // Single-side grid levels stop at their first meet (every meet of such a level
 // has the same length).  The edge loops of k_grid_topdown / k_grid_hubs read
 // the meet word every (mask + 1) batches of 256 edges per workgroup: a
@@ -1487,22 +1488,23 @@ struct GridParams {
 
 // aux[2], the auto chain's word: bit 0 = the chain took the hand-off (its
 // levels dirtied the global state: the predicated cleanup runs), bit 1 = the
-// side of the planned level, bit 3 = a planned level is to run.
-constexpr uint32_t kAuxTook = 1u, kAuxActive = 8u;
+// side of the planned level, bit 2 = it runs as one edge-parallel hub pass
+// over the whole frontier (hub_direct), bit 3 = a planned level is to run.
+constexpr uint32_t kAuxTook = 1u, kAuxDirect = 4u, kAuxActive = 8u;
 
 // The auto level's plan from the frontier facts, with the host's rules
 // (grid_level / choose_side / choose_mode): the side with fewer frontier
 // edges; declined when the Beamer rule wants bottom-up; hub degree; chunk size.
 struct AutoPlan {
   uint32_t active, side, F, hub, cv, fb;
-  bool declined;
+  bool declined, direct;
 };
 template <typename OffT>
 __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, unsigned long long fe0,
                                                     unsigned long long fe1, unsigned long long ve0,
                                                     unsigned long long ve1, uint32_t fb0, uint32_t fb1, uint32_t fd0,
                                                     uint32_t fd1) {
-  AutoPlan a{1u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false};
+  AutoPlan a{1u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false};
   a.side = fe0 <= fe1 ? 0u : 1u;
   const unsigned long long fe = a.side ? fe1 : fe0;
   const double m_u = (double)P.nnz - (double)(a.side ? ve1 : ve0);
@@ -1517,13 +1519,16 @@ __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, u
   if (a.F <= 4096 && fe > 16384 && P.max_deg > 64) a.hub = 64;
   if ((a.F + kGridThreads - 1) / kGridThreads < P.cus * 4u && fe > 0)
     a.cv = (uint32_t)min<uint64_t>(kGridThreads, max<uint64_t>(kGridChunkMin, kGridThreads * (uint64_t)a.F / fe));
+  // grid_topdown's rule: a hub level of at most one hub tile is one
+  // edge-parallel pass (P.hub_direct: allowed on this chain)
+  a.direct = P.hub_direct && a.hub != ~0u && a.F <= (uint32_t)kHubTile;
   return a;
 }
 
 // The plan for the kernels behind: [2] the chain word; [3] frontier size;
 // [4] hub degree; [5] chunk size; [6] frontier base
 __device__ __forceinline__ void write_auto_plan(uint32_t* aux, const AutoPlan& a, bool took) {
-  aux[2] = (took ? kAuxTook : 0u) | (a.active ? kAuxActive | a.side << 1 : 0u);
+  aux[2] = (took ? kAuxTook : 0u) | (a.active ? kAuxActive | a.side << 1 | (a.direct ? kAuxDirect : 0u) : 0u);
   aux[3] = a.F;
   aux[4] = a.hub;
   aux[5] = a.cv;
@@ -1621,7 +1626,7 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
       const bool hand = seen && (uint32_t)g == 1u;
       if (hand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (blockIdx.x == 0) {
-        AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false};
+        AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false};
         if (hand) {
           // the whole DevState in one round trip: lane i loads word i
           constexpr uint32_t kW = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
@@ -1666,7 +1671,7 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
 template <typename OffT>
 __device__ bool auto_plan(GridParams<OffT>& P) {
   const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
-  if (!(xp & kAuxActive)) return false;
+  if (!(xp & kAuxActive) || (xp & kAuxDirect)) return false;  // direct: the hub pass runs the level
   P.side = (int)((xp >> 1) & 1u);
   P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
   P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
@@ -1767,7 +1772,6 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
 // in order in every workgroup).  Enqueued right behind the top-down kernel;
 // a no-op when that level deferred nothing (its finisher reset hub_count),
 // otherwise its last workgroup finishes the level.
-constexpr int kHubTile = 1024;
 template <typename OffT, bool kAuto = false>
 __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) {
   __shared__ uint32_t hu[kHubTile];
@@ -1779,6 +1783,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
     const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
     if (!(xp & kAuxActive)) return;
     P.side = (int)((xp >> 1) & 1u);
+    P.hub_direct = (xp & kAuxDirect) ? 1 : 0;
     P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
     // the host's hub launch size: 4 workgroups per frontier vertex
     P.nparts = max(1u, min(gridDim.x, 4u * __builtin_amdgcn_readfirstlane(P.b.aux[3])));
@@ -2089,7 +2094,7 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   if (P.chain) {
     __shared__ uint32_t snext;
     if (tid == 0) {
-      AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false};
+      AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false};
       if (sv.status == kRunning)
         ap = plan_auto_level(P, sv.fedges[0], sv.fedges[1], sv.vedges[0], sv.vedges[1], sv.fbeg[0], sv.fbeg[1],
                              sv.fend[0], sv.fend[1]);
@@ -2325,6 +2330,16 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
 
 uint32_t grid_hub_degree() { return kHubDegree; }
 
+// BIBFS_GRID_HUB_DIRECT: 0 off, 1 on (the hub pass's grid), 2 on with one
+// workgroup per 256 frontier edges (up to 4 per CU; host-planned levels only)
+static int grid_hub_direct_mode() {
+  static const int mode = [] {
+    const char* e = std::getenv("BIBFS_GRID_HUB_DIRECT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return mode;
+}
+
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
                   uint64_t frontier_edges, dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
                   uint32_t hub_deg, hipStream_t s) {
@@ -2350,12 +2365,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   // Measured (profiles/r4_grid_hub_direct_ab.jsonl, mean search): Kronecker 22
   // 47.4-48.5 -> 40.6-42.1 us, Kronecker 25 60.8 -> 48.7 us.  Sizing that
   // pass by edges instead (mode 2: up to 1024 workgroups) lost: 57.1 us.
-  // BIBFS_GRID_HUB_DIRECT: 0 off, 1 on (the hub pass's grid), 2 on with one
-  // workgroup per 256 frontier edges (up to 4 per CU)
-  static const int direct_mode = [] {
-    const char* e = std::getenv("BIBFS_GRID_HUB_DIRECT");
-    return e ? std::atoi(e) : 1;
-  }();
+  const int direct_mode = grid_hub_direct_mode();
   const bool direct = direct_mode && hub_deg != ~0u && frontier <= (uint64_t)kHubTile;
   if (direct && direct_mode == 2)
     hblocks = (unsigned)std::max<uint64_t>(
@@ -2403,6 +2413,7 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     P.nnz = g.nnz;
     P.alpha = (float)alpha;
     P.chain = 0;
+    P.hub_direct = grid_hub_direct_mode() == 1 ? 1 : 0;  // the planners may choose direct hub levels
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
     for (int l = 0; l < std::max(1, levels); ++l) {
       P.chain = l + 1 < levels ? 1 : 0;

@@ -70,7 +70,11 @@ struct HipBiBfs::Impl {
   // 10M G(n, p) gains ~1% (profiles/r3_auto_handoff_ab2.jsonl).
   // (BIBFS_AUTO_MAX_DEG overrides the bound, for A/B on hub graphs: with the
   // hub pass sized like the host's it still lost on Kronecker 22, 71.6-72.2 vs
-  // 47.2-49.8 us mean search, profiles/r4_auto_chain_ab.jsonl)
+  // 47.2-49.8 us mean search, profiles/r4_auto_chain_ab.jsonl; with direct hub
+  // levels planned on the device too, 50.8-52.6 vs 44.5-44.7 and Kronecker 25
+  // 60.6 vs 51.0, profiles/r4_auto_hub_direct_ab.jsonl -- a gated chain of
+  // k_handoff + top-down + 1024-block hub launches behind EVERY query costs
+  // ~30 us of stream time, which the next query's hand-off queues behind)
   uint64_t auto_max_deg = [] {
     const char* e = std::getenv("BIBFS_AUTO_MAX_DEG");
     return e ? std::strtoull(e, nullptr, 10) : 64ull;
