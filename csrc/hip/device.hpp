@@ -167,6 +167,7 @@ struct GraphView {
   const uint32_t* row_off32;   // n + 1 copy when nnz < 2^32 (else nullptr)
   const uint32_t* col;
   const uint4* padj;           // nnz packed {v, deg(v), row_off[v] lo, hi}, or nullptr
+  uint64_t max_deg = ~0ull;    // largest degree (unknown: ~0)
 };
 
 struct SearchBuffers {

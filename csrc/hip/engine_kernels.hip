@@ -101,6 +101,20 @@ static_assert(kWaveB == 1 || kWaveB == 2 || kWaveB == 4, "batches per wave: 1, 2
 #define BIBFS_KNOB_WAVE_HASH 0
 #endif
 constexpr bool kWaveHash = BIBFS_KNOB_WAVE_HASH;
+// 1 = the all-wave rounds also run with LDS hash visited sets, but claim into
+// the GLOBAL queue and parent arrays (records carry parent ids, as in the
+// wave-0 schedule): no LDS queue, so the record buffers keep their full size
+// and the search hands off no earlier than without the all-wave rounds.  Only
+// on graphs whose largest degree is at most kWaveHashMaxDeg (LdsParams::
+// wave_hash): a hub's edge records are appended by one lane.  Measured
+// (profiles/r4_lds_wave_hash_global_ab.jsonl, mean search): 10M G(n, p)
+// 67.5 -> 63.5-64.0 us, 3M 38.3 -> 34.2, 1M 30.2 -> 26.0; ungated it cost
+// Kronecker 22 +4 us (profiles/r4_lds_wave_hash_global_ungated.jsonl).
+#ifndef BIBFS_KNOB_WAVE_HASH_G
+#define BIBFS_KNOB_WAVE_HASH_G 1
+#endif
+constexpr bool kWaveHashG = BIBFS_KNOB_WAVE_HASH_G;
+constexpr uint64_t kWaveHashMaxDeg = 255;
 // Resident server: the mailbox diagnostics (stage / seen / poll latency) are
 // system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
 // issued them, its first global load of the search would wait for their PCIe
@@ -183,6 +197,9 @@ struct LdsParams {
   // the host alternates sets so a search never shares its global state with
   // the previous search's still-running cleanup
   launch::SearchBuffers b_alt{};
+  // hash-set searches (kWaveHashG): run the all-wave rounds (graphs without
+  // hubs; a hub's records are written by one lane)
+  int wave_hash = 0;
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -292,6 +309,8 @@ template <typename OffT, bool kStamp, bool kBm>
 __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool elected) {
   using Rec = typename LdsRec<OffT>::type;
   constexpr bool kLq = (kBm || kWaveHash) && kWaveRounds && std::is_same<OffT, uint32_t>::value;  // LDS queue + walk
+  // all-wave rounds: with the LDS queue (kLq), or on hash sets with the global queue
+  constexpr bool kWr = kLq || (kWaveHashG && !kBm && kWaveRounds && std::is_same<OffT, uint32_t>::value);
   constexpr uint32_t CAP = kLq ? kCapBm : LdsRec<OffT>::cap;
   __shared__ uint32_t H[2][kHashSize];
   __shared__ Rec R[4][CAP];
@@ -644,10 +663,11 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   __shared__ unsigned long long wmeet[3];    // [slot]: min (len << 32 | side << 31 | vertex)
   bool lq_done = false;                      // replicated: the search ended inside wave_rounds
   auto wave_rounds = [&]() {
-    if constexpr (!kLq) {
+    if constexpr (!kWr) {
       return;
     } else {
       if (!P.padj || !P.lockstep || (P.trace && !kStamp) || s0.ovf || s1.ovf) return;  // uniform
+      if (!kLq && !P.wave_hash) return;
       uint32_t E0 = (uint32_t)s0.fed, E1 = (uint32_t)s1.fed;
       uint32_t d0 = (uint32_t)s0.depth, d1 = (uint32_t)s1.depth;
       uint32_t qe0 = s0.qend, qe1 = s1.qend, c0 = s0.cnt, c1 = s1.cnt, h0 = s0.hcnt, h1 = s1.hcnt;
@@ -662,13 +682,15 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       const uint4* const padj = P.padj;
       if (tid < 6) wctr[tid >> 1][tid & 1] = 0;
       if (tid < 3) wmeet[tid] = ~0ull;
-      if (tid < 2) {  // depth 0: the endpoints at queue index 0
-        LQ[tid][0] = tid ? P.dst : P.src;
-        LP[tid][0] = kEmpty;
-      }
-      for (uint32_t i = tid; i < E0 + E1; i += kLdsThreads) {  // seed records: parent = queue index 0
-        if (i < E0) R[a0][o0 + i].x = 0u;
-        else R[a1][o1 + i - E0].x = 0u;
+      if constexpr (kLq) {
+        if (tid < 2) {  // depth 0: the endpoints at queue index 0
+          LQ[tid][0] = tid ? P.dst : P.src;
+          LP[tid][0] = kEmpty;
+        }
+        for (uint32_t i = tid; i < E0 + E1; i += kLdsThreads) {  // seed records: parent = queue index 0
+          if (i < E0) R[a0][o0 + i].x = 0u;
+          else R[a1][o1 + i - E0].x = 0u;
+        }
       }
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       uint32_t slot = 0, rounds_done = 0;
@@ -769,13 +791,19 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           const uint32_t be = alone ? 0u : __builtin_amdgcn_readlane((uint32_t)pos, 0);
           const uint32_t bn = alone ? 0u : __builtin_amdgcn_readlane((uint32_t)(pos >> 32), 0);
           const uint32_t eb = be + incl - dc;
-          const uint32_t qi = (sd[k] ? qe1 : qe0) + bn + mbcnt64(mask);  // < kQCap (round bound)
-          if (isnew[k]) {
-            (sd[k] ? LP[1] : LP[0])[qi] = u[k];
-            (sd[k] ? LQ[1] : LQ[0])[qi] = v[k];
+          const uint32_t qi = (sd[k] ? qe1 : qe0) + bn + mbcnt64(mask);  // kLq: < kQCap (round bound)
+          if constexpr (kLq) {
+            if (isnew[k]) {
+              (sd[k] ? LP[1] : LP[0])[qi] = u[k];
+              (sd[k] ? LQ[1] : LQ[0])[qi] = v[k];
+            }
+          } else if (isnew[k]) {  // global queue and parents; records carry the parent's id
+            (sd[k] ? par1 : par0)[v[k]] = u[k];
+            if (qi < P.n) (sd[k] ? que1 : que0)[qi] = v[k];
           }
           if (k == 0) sub(2);
-          append_records(sd[k] ? R[x1] : R[x0], isnew[k] && eb + dg[k] <= CAP ? dg[k] : 0u, eb, qi, ob[k]);
+          append_records(sd[k] ? R[x1] : R[x0], isnew[k] && eb + dg[k] <= CAP ? dg[k] : 0u, eb, kLq ? qi : v[k],
+                         ob[k]);
         }
         sub(3);
         return lsub;
@@ -791,8 +819,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         // queue or record bound) then still ends in LDS instead of handing the
         // search to the wave-0 schedule.  The meet rule covers an idle side.
         const uint32_t nb0e = (E0 + kWave - 1) / kWave, nb1e = (E1 + kWave - 1) / kWave;
-        const bool f0 = E0 <= CAP && nb0e <= kMaxBatches && qe0 + E0 <= kQCap && (kBm || h0 + E0 <= kHashLimit);
-        const bool f1 = E1 <= CAP && nb1e <= kMaxBatches && qe1 + E1 <= kQCap && (kBm || h1 + E1 <= kHashLimit);
+        const bool f0 = E0 <= CAP && nb0e <= kMaxBatches && (!kLq || qe0 + E0 <= kQCap) && (kBm || h0 + E0 <= kHashLimit);
+        const bool f1 = E1 <= CAP && nb1e <= kMaxBatches && (!kLq || qe1 + E1 <= kQCap) && (kBm || h1 + E1 <= kHashLimit);
         bool run0 = f0, run1 = f1;
         if (!(f0 && f1 && nb0e + nb1e <= kMaxBatches)) {
           if (!kWaveSingle || !(f0 || f1)) break;
@@ -857,7 +885,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         else if ((run0 && n0 == 0) || (run1 && n1 == 0)) status = kNoPath;
         slot = sn;
       }
-      if (status != kRunning) {
+      if (!kLq) {
+        // global queue and parents all along: nothing to materialise, the path
+        // is walked along the global parent arrays
+      } else if (status != kRunning) {
         lq_done = true;  // the path is walked in LDS
       } else {
         // the wave-0 schedule continues: it needs the global queue and parent
@@ -2268,6 +2299,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   if (g.row_off32) {
     LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
+    P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
       if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -2295,6 +2327,7 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;
+  P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);

@@ -274,7 +274,7 @@ struct HipBiBfs::Impl {
   vid_t step_src = 0, step_dst = 0;
 
   launch::GraphView view() const {
-    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj};
+    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj, max_deg};
   }
 
   bool server_usable() const { return d_row_off32 != nullptr && n > 0 && n <= 0x7fffffffu; }

@@ -17,6 +17,6 @@ wait
 for d in build/var/*/; do
   [ -f $d/engine_kernels.o ] || continue
   /opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $d/libbibfs.so $OBJS $OTHER $d/engine_kernels.o \
-    -L/opt/rocm/lib -lamdhip64 -lhsa-runtime64 -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib -lrccl -pthread
+    -L/opt/rocm/lib -lamdhip64 -lhsa-runtime64 -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -L/opt/rocm/lib -lrccl -pthread
 done
 ls build/var
