@@ -1488,6 +1488,16 @@ constexpr int kHubTile = 1024;  // k_grid_hubs: hubs staged in LDS per pass
 #define BIBFS_KNOB_MEET_CHECK_MASK 0
 #endif
 constexpr uint32_t kMeetCheckMask = BIBFS_KNOB_MEET_CHECK_MASK;
+// 1 = k_grid_topdown's dependent round trips trimmed: each workgroup's first
+// chunk is its block index (no ticket), the ticket and the meet word are read
+// side by side, and a claim reads its visited word before the atomicOr only
+// on levels of more than kGridPrecheckEdges frontier edges (small levels
+// claim mostly unvisited vertices: the read only adds a round trip).
+#ifndef BIBFS_KNOB_GRID_FAST
+#define BIBFS_KNOB_GRID_FAST 1
+#endif
+constexpr bool kGridFast = BIBFS_KNOB_GRID_FAST;
+constexpr uint64_t kGridPrecheckEdges = 1ull << 16;
 
 template <typename OffT>
 struct GridParams {
@@ -1515,27 +1525,28 @@ struct GridParams {
   uint32_t fbase, fcount;  // auto level: the frontier, from the plan (0/0 = read DevState)
   int chain;           // auto level with another auto level enqueued behind it: its finisher plans that one
   int hub_direct;      // k_grid_hubs: the whole frontier is the hub list (no top-down pass before it)
+  int precheck;        // claims read the visited word before the atomicOr (big levels)
 };
 
 // aux[2], the auto chain's word: bit 0 = the chain took the hand-off (its
 // levels dirtied the global state: the predicated cleanup runs), bit 1 = the
 // side of the planned level, bit 2 = it runs as one edge-parallel hub pass
 // over the whole frontier (hub_direct), bit 3 = a planned level is to run.
-constexpr uint32_t kAuxTook = 1u, kAuxDirect = 4u, kAuxActive = 8u;
+constexpr uint32_t kAuxTook = 1u, kAuxDirect = 4u, kAuxActive = 8u, kAuxPrecheck = 16u;
 
 // The auto level's plan from the frontier facts, with the host's rules
 // (grid_level / choose_side / choose_mode): the side with fewer frontier
 // edges; declined when the Beamer rule wants bottom-up; hub degree; chunk size.
 struct AutoPlan {
   uint32_t active, side, F, hub, cv, fb;
-  bool declined, direct;
+  bool declined, direct, precheck;
 };
 template <typename OffT>
 __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, unsigned long long fe0,
                                                     unsigned long long fe1, unsigned long long ve0,
                                                     unsigned long long ve1, uint32_t fb0, uint32_t fb1, uint32_t fd0,
                                                     uint32_t fd1) {
-  AutoPlan a{1u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false};
+  AutoPlan a{1u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false, true};
   a.side = fe0 <= fe1 ? 0u : 1u;
   const unsigned long long fe = a.side ? fe1 : fe0;
   const double m_u = (double)P.nnz - (double)(a.side ? ve1 : ve0);
@@ -1553,13 +1564,16 @@ __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, u
   // grid_topdown's rule: a hub level of at most one hub tile is one
   // edge-parallel pass (P.hub_direct: allowed on this chain)
   a.direct = P.hub_direct && a.hub != ~0u && a.F <= (uint32_t)kHubTile;
+  a.precheck = !kGridFast || fe > kGridPrecheckEdges;
   return a;
 }
 
 // The plan for the kernels behind: [2] the chain word; [3] frontier size;
 // [4] hub degree; [5] chunk size; [6] frontier base
 __device__ __forceinline__ void write_auto_plan(uint32_t* aux, const AutoPlan& a, bool took) {
-  aux[2] = (took ? kAuxTook : 0u) | (a.active ? kAuxActive | a.side << 1 | (a.direct ? kAuxDirect : 0u) : 0u);
+  aux[2] = (took ? kAuxTook : 0u) |
+           (a.active ? kAuxActive | a.side << 1 | (a.direct ? kAuxDirect : 0u) | (a.precheck ? kAuxPrecheck : 0u)
+                     : 0u);
   aux[3] = a.F;
   aux[4] = a.hub;
   aux[5] = a.cv;
@@ -1579,7 +1593,7 @@ __device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid
   DevState* st = P.b.st;
   const uint32_t w = v >> 5, bit = 1u << (v & 31);
   bool mine = false;
-  if (valid && !(P.b.vis[s][w] & bit)) mine = !(atomicOr(&P.b.vis[s][w], bit) & bit);
+  if (valid && (!P.precheck || !(P.b.vis[s][w] & bit))) mine = !(atomicOr(&P.b.vis[s][w], bit) & bit);
   const unsigned long long mask = __ballot(mine);
   if (!mask) return;
   const int lane = __lane_id();
@@ -1657,7 +1671,7 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
       const bool hand = seen && (uint32_t)g == 1u;
       if (hand) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       if (blockIdx.x == 0) {
-        AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false};
+        AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false, true};
         if (hand) {
           // the whole DevState in one round trip: lane i loads word i
           constexpr uint32_t kW = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
@@ -1704,6 +1718,7 @@ __device__ bool auto_plan(GridParams<OffT>& P) {
   const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
   if (!(xp & kAuxActive) || (xp & kAuxDirect)) return false;  // direct: the hub pass runs the level
   P.side = (int)((xp >> 1) & 1u);
+  P.precheck = (xp & kAuxPrecheck) ? 1 : 0;
   P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
   P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
   P.chunk_v = __builtin_amdgcn_readfirstlane(P.b.aux[5]);
@@ -1728,8 +1743,22 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint32_t fbase = kAuto ? P.fbase : st->fbeg[s];
   const uint32_t F = kAuto ? P.fcount : st->fend[s] - fbase;
-  for (;;) {
-    if (tid == 0) schunk = (load_agent(&st->meet) != kEmpty) ? kEmpty : atomicAdd(&st->chunk, 1u);
+  const uint32_t parts = P.nparts ? P.nparts : gridDim.x;
+  for (uint32_t round = 0;; ++round) {
+    if (kGridFast) {
+      // chunk b first (no ticket); then tickets, numbered after the blocks'
+      // own chunks, with the meet word read beside the ticket
+      if (tid == 0) {
+        if (round == 0) {
+          schunk = blockIdx.x;
+        } else {
+          const uint32_t t = atomicAdd(&st->chunk, 1u);
+          schunk = load_agent(&st->meet) != kEmpty ? kEmpty : parts + t;
+        }
+      }
+    } else if (tid == 0) {
+      schunk = (load_agent(&st->meet) != kEmpty) ? kEmpty : atomicAdd(&st->chunk, 1u);
+    }
     __syncthreads();
     const uint32_t c = schunk;
     const uint32_t cv = P.chunk_v;
@@ -1815,6 +1844,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
     if (!(xp & kAuxActive)) return;
     P.side = (int)((xp >> 1) & 1u);
     P.hub_direct = (xp & kAuxDirect) ? 1 : 0;
+    P.precheck = (xp & kAuxPrecheck) ? 1 : 0;
     P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
     // the host's hub launch size: 4 workgroups per frontier vertex
     P.nparts = max(1u, min(gridDim.x, 4u * __builtin_amdgcn_readfirstlane(P.b.aux[3])));
@@ -2125,7 +2155,7 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   if (P.chain) {
     __shared__ uint32_t snext;
     if (tid == 0) {
-      AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false};
+      AutoPlan ap{0u, 0u, 0u, ~0u, (uint32_t)kGridThreads, 0u, false, false, true};
       if (sv.status == kRunning)
         ap = plan_auto_level(P, sv.fedges[0], sv.fedges[1], sv.vedges[0], sv.vedges[1], sv.fbeg[0], sv.fbeg[1],
                              sv.fend[0], sv.fend[1]);
@@ -2278,6 +2308,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.fbase = P.fcount = 0;
   P.chain = 0;
   P.hub_direct = 0;
+  P.precheck = 1;
   return P;
 }
 
@@ -2408,6 +2439,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
     P.mirror = mirror, P.seq = seq, P.trace = trace, P.h = h, P.res_seq = res_seq;
     P.hub_deg = hub_deg;  // ~0u: no hub pass
     P.chunk_v = (uint32_t)cv;
+    P.precheck = (!kGridFast || frontier_edges > kGridPrecheckEdges) ? 1 : 0;
     if (direct) {
       P.hub_direct = 1;
       k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);

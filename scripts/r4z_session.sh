@@ -1,0 +1,11 @@
+# grid top-down latency trims (BIBFS_KNOB_GRID_FAST; build/var gf1 = default, gf0 = off) + engine GPU tests
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 500 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_engine.py > gpurun_out/r5a_pytest.log 2>&1 || exit 1
+O=gpurun_out/r5a_gridfast_ab.jsonl
+for rep in 1 2; do
+  for v in gf1 gf0; do
+    for g in gnp:10000000::1 gnp:3000000::4 kron:22:16:1; do
+      LD_LIBRARY_PATH=build/var/$v timeout -k 10 240 python3 benchmarks/pair_latency.py --graph $g --pairs 64 --reps 5 --summary $v >> $O 2>>gpurun_out/r5a.err || exit 1
+    done
+  done
+done
