@@ -1563,7 +1563,11 @@ __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, u
     a.cv = (uint32_t)min<uint64_t>(kGridThreads, max<uint64_t>(kGridChunkMin, kGridThreads * (uint64_t)a.F / fe));
   // grid_topdown's rule: a hub level of at most one hub tile is one
   // edge-parallel pass (P.hub_direct: allowed on this chain)
-  a.direct = P.hub_direct && a.hub != ~0u && a.F <= (uint32_t)kHubTile;
+  {
+    const uint64_t chunks = ((uint64_t)a.F + a.cv - 1) / a.cv;
+    const uint64_t blocks = min<uint64_t>((uint64_t)P.cus * 4, max<uint64_t>(1, chunks));
+    a.direct = P.hub_direct && a.F <= (uint32_t)kHubTile && (a.hub != ~0u || fe > 2ull * kGridThreads * blocks);
+  }
   a.precheck = !kGridFast || fe > kGridPrecheckEdges;
   return a;
 }
@@ -2429,8 +2433,14 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   // Measured (profiles/r4_grid_hub_direct_ab.jsonl, mean search): Kronecker 22
   // 47.4-48.5 -> 40.6-42.1 us, Kronecker 25 60.8 -> 48.7 us.  Sizing that
   // pass by edges instead (mode 2: up to 1024 workgroups) lost: 57.1 us.
+  // With the hub-free small heavy levels too (profiles/r4_grid_direct_levels_ab.jsonl):
+  // Kronecker 22 46.9-48.1 -> 38.0-38.3 us, Kronecker 25 56.2-57.9 -> 44.0-44.2
+  // us against no direct levels; 10M G(n, p) unchanged.
   const int direct_mode = grid_hub_direct_mode();
-  const bool direct = direct_mode && hub_deg != ~0u && frontier <= (uint64_t)kHubTile;
+  // (also a level without hubs whose top-down pass would walk more than two
+  // 256-edge batches per workgroup: a few heavy-ish vertices on one block)
+  const bool direct = direct_mode && frontier <= (uint64_t)kHubTile &&
+                      (hub_deg != ~0u || frontier_edges > 2ull * kGridThreads * blocks);
   if (direct && direct_mode == 2)
     hblocks = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>((uint64_t)cus * 4, (frontier_edges + kGridThreads - 1) / kGridThreads));
@@ -2478,7 +2488,8 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     P.nnz = g.nnz;
     P.alpha = (float)alpha;
     P.chain = 0;
-    P.hub_direct = grid_hub_direct_mode() == 1 ? 1 : 0;  // the planners may choose direct hub levels
+    // the planners may choose direct hub levels (only with the hub pass enqueued)
+    P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
     for (int l = 0; l < std::max(1, levels); ++l) {
       P.chain = l + 1 < levels ? 1 : 0;
