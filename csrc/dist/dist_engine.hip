@@ -75,6 +75,12 @@ constexpr uint32_t kSpecCapMin = 1024;          // smallest speculative candidat
 // that holds it: it is deferred to a hub list whose edges the whole grid then
 // walks edge-parallel (a degree-10^6 hub would otherwise serialise on one CU).
 constexpr uint64_t kHubDeg = 512;
+// 1 = a frontier of at most one 256-vertex chunk is expanded by every block of
+// the launch, each walking a stride of its edges (td_expand_side)
+#ifndef BIBFS_DIST_SPREAD
+#define BIBFS_DIST_SPREAD 1
+#endif
+constexpr bool kDistSpread = BIBFS_DIST_SPREAD;
 // Levels with more frontier edges than this read the visited word before the
 // claim's atomicOr (ClaimMeet::precheck).
 constexpr uint64_t kPrecheckEdges = 1u << 16;
@@ -673,7 +679,13 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
   __shared__ uint32_t sstop;
   const uint32_t* q = pick(V.queue, s);
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  for (uint64_t c0 = (uint64_t)b0 * kThreads; c0 < F; c0 += (uint64_t)nb * kThreads) {
+  // A frontier of at most one chunk (a Kronecker hub round's few heavy-ish
+  // vertices) would run on block 0 alone, its edges in serial 256-edge
+  // steps: instead EVERY block stages that chunk and walks a stride of its
+  // edges (block 0 alone defers the hubs).
+  const bool spread = kDistSpread && F <= (uint32_t)kThreads && nb > 1;
+  for (uint64_t c0 = spread ? 0 : (uint64_t)b0 * kThreads; c0 < F;
+       c0 += spread ? (uint64_t)F : (uint64_t)nb * kThreads) {
     if (exit_on_meet && c0 != (uint64_t)b0 * kThreads) {  // block-uniform: the flag goes through LDS between barriers
       if (tid == 0) sstop = meet_seen(V) ? 1u : 0u;
       __syncthreads();
@@ -690,7 +702,9 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
     }
     const bool hub = deg > hub_deg;  // expanded by k_td_hubs instead
     const unsigned long long hm = __ballot(hub);
-    if (hm) {
+    if (hm && spread && b0 != 0) {
+      deg = hub ? 0ull : deg;  // block 0 lists them
+    } else if (hm) {
       uint32_t pos = 0;
       const int leader = __ffsll((long long)hm) - 1;
       if (lane == leader) pos = atomicAdd(&V.st->hub_count[s], (uint32_t)__popcll(hm));
@@ -717,7 +731,9 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
     se[tid] = pre + x - deg;
     __syncthreads();
     uint32_t iter = 0;
-    for (unsigned long long base = 0; base < tot; base += kThreads, ++iter) {
+    const unsigned long long ebase = spread ? (unsigned long long)b0 * kThreads : 0ull;
+    const unsigned long long estep = spread ? (unsigned long long)nb * kThreads : (unsigned long long)kThreads;
+    for (unsigned long long base = ebase; base < tot; base += estep, ++iter) {
       // wave-uniform exit (no barrier in this loop)
       if (exit_on_meet && iter > 0 && __builtin_amdgcn_readfirstlane(meet_seen(V) ? 1u : 0u)) break;
       const unsigned long long e = base + tid;
