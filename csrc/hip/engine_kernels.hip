@@ -1498,6 +1498,11 @@ constexpr uint32_t kMeetCheckMask = BIBFS_KNOB_MEET_CHECK_MASK;
 #endif
 constexpr bool kGridFast = BIBFS_KNOB_GRID_FAST;
 constexpr uint64_t kGridPrecheckEdges = 1ull << 16;
+// 1 = small top-down levels read the packed adjacency (GridParams::padj)
+#ifndef BIBFS_KNOB_GRID_PADJ
+#define BIBFS_KNOB_GRID_PADJ 1
+#endif
+constexpr bool kGridPadj = BIBFS_KNOB_GRID_PADJ;
 
 template <typename OffT>
 struct GridParams {
@@ -1526,6 +1531,10 @@ struct GridParams {
   int chain;           // auto level with another auto level enqueued behind it: its finisher plans that one
   int hub_direct;      // k_grid_hubs: the whole frontier is the hub list (no top-down pass before it)
   int precheck;        // claims read the visited word before the atomicOr (big levels)
+  // packed adjacency {v, deg, base}: on small levels (!precheck) an edge's one
+  // 16-byte load brings the neighbour's degree with its id (no row-offset
+  // round trip after the claim); nullptr = col + row_off
+  const uint4* padj;
 };
 
 // aux[2], the auto chain's word: bit 0 = the chain took the hand-off (its
@@ -1591,8 +1600,8 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
 // `valid` masks lanes with no edge).  Appends claimed vertices to the queue
 // with one atomic per wave and checks the other side's bitmap (fused meet).
 template <typename OffT>
-__device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid, uint32_t u,
-                                           uint32_t v) {
+__device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid, uint32_t u, uint32_t v,
+                                           uint32_t vdeg = ~0u) {
   const int s = P.side, o = s ^ 1;
   DevState* st = P.b.st;
   const uint32_t w = v >> 5, bit = 1u << (v & 31);
@@ -1607,7 +1616,7 @@ __device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid
     // write-through (sc1): the level's last workgroup may walk this parent
     // chain in the same kernel, from another XCD, with sc1 loads
     __hip_atomic_store(&P.b.parent[s][v], u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    deg = (uint32_t)(P.row_off[v + 1] - P.row_off[v]);
+    deg = vdeg != ~0u ? vdeg : (uint32_t)(P.row_off[v + 1] - P.row_off[v]);
     if (P.b.vis[o][w] & bit) {
       if (atomicCAS(&st->meet, kEmpty, v) == kEmpty) st->meet_side = (uint32_t)s;
     }
@@ -1723,6 +1732,7 @@ __device__ bool auto_plan(GridParams<OffT>& P) {
   if (!(xp & kAuxActive) || (xp & kAuxDirect)) return false;  // direct: the hub pass runs the level
   P.side = (int)((xp >> 1) & 1u);
   P.precheck = (xp & kAuxPrecheck) ? 1 : 0;
+  if (P.precheck) P.padj = nullptr;  // big level: 4-byte column loads
   P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
   P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
   P.chunk_v = __builtin_amdgcn_readfirstlane(P.b.aux[5]);
@@ -1755,6 +1765,8 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
       if (tid == 0) {
         if (round == 0) {
           schunk = blockIdx.x;
+        } else if ((uint64_t)parts * P.chunk_v >= F) {
+          schunk = kEmpty;  // every chunk went to a block of its own: no ticket to take
         } else {
           const uint32_t t = atomicAdd(&st->chunk, 1u);
           schunk = load_agent(&st->meet) != kEmpty ? kEmpty : parts + t;
@@ -1810,7 +1822,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
         break;
       const uint32_t e = base + tid;
       const bool valid = e < Ec;
-      uint32_t uu = 0, v = 0;
+      uint32_t uu = 0, v = 0, vdeg = ~0u;
       if (valid) {
         uint32_t lo = 0, hi = kGridThreads;
         while (hi - lo > 1) {
@@ -1819,9 +1831,16 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
           else hi = mid;
         }
         uu = sv[lo];
-        v = P.col[sb[lo] + (OffT)(e - sEb[lo])];
+        const OffT k = sb[lo] + (OffT)(e - sEb[lo]);
+        if (P.padj) {  // small level: the neighbour's degree with its id
+          const uint4 q = P.padj[k];
+          v = q.x;
+          vdeg = q.y;
+        } else {
+          v = P.col[k];
+        }
       }
-      grid_claim(P, valid, uu, v);
+      grid_claim(P, valid, uu, v, vdeg);
     }
     __syncthreads();
   }
@@ -2313,6 +2332,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.chain = 0;
   P.hub_direct = 0;
   P.precheck = 1;
+  P.padj = kGridPadj ? g.padj : nullptr;
   return P;
 }
 
@@ -2450,6 +2470,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
     P.hub_deg = hub_deg;  // ~0u: no hub pass
     P.chunk_v = (uint32_t)cv;
     P.precheck = (!kGridFast || frontier_edges > kGridPrecheckEdges) ? 1 : 0;
+    if (P.precheck || !kGridPadj) P.padj = nullptr;
     if (direct) {
       P.hub_direct = 1;
       k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);
