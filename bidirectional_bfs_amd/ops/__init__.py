@@ -45,6 +45,9 @@ class HipEngine:
 
     def __init__(self, device: int = 0):
         self._e = native.HipBiBfs(int(device))
+        # the serving call goes straight to the native method (no Python frame
+        # per query); `query` below documents it
+        self.query = self._e.query
 
     # ---- ingest
     def load(self, graph: Graph, build_on_device: bool = True) -> "HipEngine":

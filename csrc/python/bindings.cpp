@@ -278,7 +278,8 @@ PYBIND11_MODULE(_native, m) {
            py::call_guard<py::gil_scoped_release>())
       // serving entry point: (hops, path); the GIL is kept (a query is ~10 us)
       .def("query", [](HipBiBfs& e, vid_t s, vid_t d) {
-        std::vector<vid_t> p;
+        static thread_local std::vector<vid_t> p;  // reused: no allocation per query
+        p.clear();
         const int64_t h = e.query(s, d, &p);
         return hops_path(h, p);
       })
