@@ -31,18 +31,19 @@ def main():
     pairs = bench.pick_pairs(eng, n, a.pairs, 12345)
     agg = []
     for s, d, h in pairs:
-        dev, tot, lds = [], [], []
+        dev, tot, lds, walk = [], [], [], []
         for _ in range(a.reps):
             r = eng.search(s, d)
             assert r.hops == h
             dev.append(r.search_ms)
             tot.append(r.total_ms)
             lds.append(r.stats["lds_ms"])
+            walk.append(r.stats["walk_ms"])
         rec = {"src": s, "dst": d, "hops": h, "search_us": round(statistics.median(dev) * 1e3, 2),
                "query_us": round(statistics.median(tot) * 1e3, 2), "levels": r.levels,
                "edges": r.edges_inspected, "visited": r.visited, "handoff": r.handoff,
                "grid_levels": r.stats["grid_levels"], "lds_us": round(statistics.median(lds) * 1e3, 2),
-               "lds_levels": r.stats["lds_levels"]}
+               "lds_levels": r.stats["lds_levels"], "walk_us": round(statistics.median(walk) * 1e3, 2)}
         agg.append(rec)
         if a.summary is None:
             print(json.dumps(rec), flush=True)
@@ -58,7 +59,9 @@ def main():
                           "handoff_lds_us_mean": round(statistics.mean(
                               [x["lds_us"] for x in agg if x["handoff"]] or [0.0]), 2),
                           "handoff_search_us_mean": round(statistics.mean(
-                              [x["search_us"] for x in agg if x["handoff"]] or [0.0]), 2)}),
+                              [x["search_us"] for x in agg if x["handoff"]] or [0.0]), 2),
+                          "handoff_walk_us_mean": round(statistics.mean(
+                              [x["walk_us"] for x in agg if x["handoff"]] or [0.0]), 2)}),
               flush=True)
     eng.set_resident(False)
 

@@ -64,6 +64,7 @@ struct HostResult {
   uint32_t pad;
   unsigned long long rt_begin, rt_end;  // s_memrealtime (100 MHz) around the LDS search
   unsigned long long rt_pickup;         // resident server: when the request was seen (0 otherwise)
+  unsigned long long rt_walk;           // grid publish: when its path walk started (0: no grid walk)
 };
 
 // Pinned mailbox of the resident query server (k_lds_server).  The host

@@ -2078,6 +2078,7 @@ __device__ void publish_result(const launch::SearchBuffers& b, const launch::Hos
   const int d0 = sv.depth[0], d1 = sv.depth[1];
   const uint32_t hops = (uint32_t)(d0 + d1);
   uint32_t* out = (hops + 1 <= h.path_cap) ? h.path : b.dpath;
+  const unsigned long long t_walk = __builtin_amdgcn_s_memrealtime();
   if (status == kFound && (tid == 0 || tid == kWave)) {
     walk_side(b.parent[tid ? 1 : 0], n, sv.meet, tid ? 1 : 0, d0, d1, out);
     __threadfence_system();
@@ -2085,6 +2086,7 @@ __device__ void publish_result(const launch::SearchBuffers& b, const launch::Hos
   __syncthreads();
   if (tid == 0) {
     HostResult* Rr = h.res;
+    Rr->rt_walk = t_walk;
     Rr->status = status;
     Rr->hops = status == kFound ? (int32_t)hops : -1;
     Rr->meet = sv.meet;
@@ -2238,6 +2240,7 @@ __global__ void k_publish(launch::SearchBuffers b, launch::HostSide h, uint32_t 
   __syncthreads();
   if (tid == 0) {
     HostResult* R = h.res;
+    R->rt_walk = 0;  // (no rt_end stamp here: the host times this path with events)
     R->status = status;
     R->hops = status == kFound ? (int32_t)hops : -1;
     R->meet = st->meet;

@@ -1399,8 +1399,11 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   r.search_ms = lds_ms;
   r.stats.lds_ms = lds_ms;
   if (!grid || stats_handoff_levels >= 0) r.stats.lds_levels = grid ? stats_handoff_levels : r.stats.levels;
-  if (grid && !timed_by_events && I.gres->seq == pub_seq)
+  if (grid && !timed_by_events && I.gres->seq == pub_seq) {
     r.search_ms = (double)(I.gres->rt_end - I.h_res->rt_begin) * 1e-5;
+    if (I.gres->rt_walk && I.gres->rt_end > I.gres->rt_walk)
+      r.stats.walk_ms = (double)(I.gres->rt_end - I.gres->rt_walk) * 1e-5;
+  }
   // the last grid level's predicated cleanup did the work (its tag is the
   // pending one); a search that ended before any grid level cleans up here
   if (grid && !I.grid_cleaned) I.cleanup_async();

@@ -48,6 +48,7 @@ struct SearchStats {
   bool handoff = false;        // GPU: persistent engine handed off to the grid engine
   double lds_ms = 0.0;         // GPU: device time of the one-workgroup (LDS / tiny) phase
   int lds_levels = 0;          // GPU: levels that phase ran (before a hand-off)
+  double walk_ms = 0.0;        // GPU: the grid publish's path walk + result record (hand-off searches)
   std::vector<LevelTrace> trace;
 };
 

@@ -44,6 +44,7 @@ py::dict stats_dict(const SearchStats& s) {
   d["handoff"] = s.handoff;
   d["lds_ms"] = s.lds_ms;
   d["lds_levels"] = s.lds_levels;
+  d["walk_ms"] = s.walk_ms;
   py::list tr;
   for (const auto& t : s.trace) {
     py::dict x;
