@@ -2491,7 +2491,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
 
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
-               unsigned long long gate_ticks, int levels, hipStream_t s) {
+               unsigned long long gate_ticks, int levels, bool lazy, hipStream_t s) {
   // The grid size is fixed before the frontier exists: cus / 4 workgroups
   // for the first level (a 10M G(n, p) hand-off level is ~17 chunks; every
   // workgroup takes chunk tickets, and fewer blocks keep the ticket and done
@@ -2518,10 +2518,31 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
     for (int l = 0; l < std::max(1, levels); ++l) {
-      P.chain = l + 1 < levels ? 1 : 0;
+      P.chain = (l + 1 < levels || lazy) ? 1 : 0;
       k_grid_topdown<OffT, true><<<l ? cblocks : blocks, kGridThreads, 0, s>>>(P);
       if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
     }
+  };
+  if (g.row_off32) launch_one(gp<uint32_t>(g, b, 0));
+  else launch_one(gp<uint64_t>(g, b, 0));
+  HIP_CHECK(hipGetLastError());
+}
+
+void grid_auto_next(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
+                    dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s) {
+  const unsigned cblocks = (unsigned)std::max(8, cus);
+  const unsigned hblocks = (unsigned)std::max(8, cus * 4);
+  auto launch_one = [&](auto P) {
+    using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
+    P.mirror = mirror, P.seq = seq, P.trace = 0, P.h = h, P.res_seq = res_seq;
+    P.cus = (uint32_t)cus;
+    P.max_deg = max_deg;
+    P.nnz = g.nnz;
+    P.alpha = (float)alpha;
+    P.chain = 0;
+    P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
+    k_grid_topdown<OffT, true><<<cblocks, kGridThreads, 0, s>>>(P);
+    if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
   };
   if (g.row_off32) launch_one(gp<uint32_t>(g, b, 0));
   else launch_one(gp<uint64_t>(g, b, 0));
