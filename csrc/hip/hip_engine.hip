@@ -95,14 +95,15 @@ struct HipBiBfs::Impl {
     const int v = e ? std::atoi(e) : 1;
     return v < 1 ? 1 : (v > 8 ? 8 : v);
   }();
-  // Lazy chain (BIBFS_AUTO_LAZY, default on): the auto level always plans the
-  // next one, and the host enqueues that level only once it has seen its
-  // search hand off -- so a search that stays in LDS enqueues nothing extra
-  // (what made the eager chain above lose), while a two-level hand-off runs
-  // its second level with no host round trip.
+  // Lazy chain (BIBFS_AUTO_LAZY=1): the auto level always plans the next one,
+  // and the host enqueues that level only once it has seen its search hand
+  // off -- so a search that stays in LDS enqueues nothing extra (what made the
+  // eager chain above lose).  Measured slower all the same: 10M 61.3 -> 64.0
+  // us mean search, the LDS phase +0.9 us and hand-off searches +3.6 us
+  // (profiles/r4_auto_lazy_ab.jsonl).  Off.
   bool auto_lazy = [] {
     const char* e = std::getenv("BIBFS_AUTO_LAZY");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   bool auto_usable(const SearchOptions& opt) const {
     return auto_on && nnz > 0 && max_deg <= auto_max_deg && !opt.trace && !opt.force_grid &&
