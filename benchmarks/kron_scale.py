@@ -39,6 +39,7 @@ def main() -> int:
     ap.add_argument("--alpha", type=float, default=14.0, help="Beamer top-down -> bottom-up: m_f > m_u / alpha")
     ap.add_argument("--beta", type=float, default=24.0, help="Beamer bottom-up -> top-down: n_f < n / beta")
     ap.add_argument("--force-grid", action="store_true", help="skip the LDS engine: every level on the grid engine")
+    ap.add_argument("--resident", action="store_true", help="serve the queries through the resident server")
     a = ap.parse_args()
     eng = HipEngine(a.device)
     opt = make_options(direction=a.direction, alpha=a.alpha, beta=a.beta, force_grid=a.force_grid)
@@ -47,6 +48,7 @@ def main() -> int:
         t0 = time.perf_counter()
         eng.generate_rmat(n, m, a.seed)
         build_wall = (time.perf_counter() - t0) * 1e3
+        eng.set_resident(a.resident)
         rnd = random.Random(scale)
         pairs, tries = [], 0
         while len(pairs) < a.queries + 2 and tries < 50 * a.queries:
@@ -76,8 +78,9 @@ def main() -> int:
             "gteps_inspected": round(insp / k / (med * 1e-3) / 1e9, 3), "mean_hops": hops / k,
             "mean_grid_levels": grid / k, "mean_bottomup_levels": bu / k,
             "device_gb": round(eng.device_bytes / 1e9, 2), "direction": a.direction,
-            "alpha": a.alpha, "beta": a.beta, "force_grid": a.force_grid,
+            "alpha": a.alpha, "beta": a.beta, "force_grid": a.force_grid, "resident": a.resident,
         }), flush=True)
+        eng.set_resident(False)
         eng.release()
     return 0
 

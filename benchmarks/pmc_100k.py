@@ -21,10 +21,12 @@ from bidirectional_bfs_amd.ops import HipEngine  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--mode", choices=["oneshot", "resident"], default="oneshot")
 ap.add_argument("--queries", type=int, default=256)
+ap.add_argument("--graph", default="gnp:100000::6", help="any bench spec (e.g. gnp:10000000::1 for the LDS server)")
 a = ap.parse_args()
-eng = bench.generate(HipEngine(0), "gnp:100000::6")
+eng = bench.generate(HipEngine(0), a.graph)
 eng.set_resident(False)
-pairs = bench.pick_pairs(eng, 100000, 64, 12345)
+_, n, _, _ = bench.parse_spec(a.graph)
+pairs = bench.pick_pairs(eng, n, 64, 12345)
 for i in range(128):  # warm: every pair twice
     s, d, _ = pairs[i % len(pairs)]
     eng.search(s, d)
@@ -33,4 +35,4 @@ for i in range(a.queries):
     s, d, h = pairs[i % len(pairs)]
     assert eng.search(s, d).hops == h
 eng.set_resident(False)
-print("pmc_100k done", a.mode, a.queries, flush=True)
+print("pmc workload done", a.graph, a.mode, a.queries, flush=True)
