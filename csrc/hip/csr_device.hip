@@ -160,6 +160,17 @@ __global__ void k_padj(const uint64_t* __restrict__ r, const uint32_t* __restric
   }
 }
 
+// The same in 8 bytes (launch::pack8; the caller checked the bounds).
+__global__ void k_padj8(const uint64_t* __restrict__ r, const uint32_t* __restrict__ col, uint64_t nnz,
+                        unsigned long long* __restrict__ pa) {
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nnz;
+       k += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t v = col[k];
+    const uint64_t b = r[v];
+    pa[k] = launch::pack8(v, b, r[v + 1] - b);
+  }
+}
+
 unsigned grid_for(uint64_t work, int threads) {
   uint64_t b = (work + threads - 1) / threads;
   if (b > 8192) b = 8192;  // 32 blocks per CU on 256 CUs, grid-stride beyond
@@ -345,6 +356,12 @@ void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, c
 void fill_csr(const uint32_t* d_uv, uint64_t m, uint32_t n, const uint64_t* d_row_off,
               uint64_t* d_cursor, uint32_t* d_col, hipStream_t s) {
   fill_csr_rows(d_uv, m, 0, n, d_row_off, d_cursor, d_col, s);
+}
+
+void build_padj8(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, unsigned long long* padj8,
+                 hipStream_t s) {
+  if (nnz) k_padj8<<<grid_for(nnz, 256), 256, 0, s>>>(row_off, col, nnz, padj8);
+  HIP_CHECK(hipGetLastError());
 }
 
 void build_padj(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, uint4* padj, hipStream_t s) {

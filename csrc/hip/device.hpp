@@ -169,7 +169,18 @@ struct GraphView {
   const uint32_t* col;
   const uint4* padj;           // nnz packed {v, deg(v), row_off[v] lo, hi}, or nullptr
   uint64_t max_deg = ~0ull;    // largest degree (unknown: ~0)
+  // 8-byte packed adjacency (pack8): v[63:39] | base[38:10] | deg[9:0], for
+  // graphs with n < 2^25, nnz < 2^29 and every degree < 1023 -- half the
+  // bytes of padj, so a 10M-vertex graph's (176 MB) stays in the MALL
+  const unsigned long long* padj8 = nullptr;
 };
+__host__ __device__ inline unsigned long long pack8(uint32_t v, uint64_t base, uint64_t deg) {
+  return (unsigned long long)v << 39 | base << 10 | deg;
+}
+__host__ __device__ inline uint32_t pack8_v(unsigned long long w) { return (uint32_t)(w >> 39); }
+__host__ __device__ inline uint32_t pack8_base(unsigned long long w) { return (uint32_t)(w >> 10) & 0x1FFFFFFFu; }
+__host__ __device__ inline uint32_t pack8_deg(unsigned long long w) { return (uint32_t)w & 0x3FFu; }
+constexpr uint64_t kPack8MaxN = 1ull << 25, kPack8MaxNnz = 1ull << 29, kPack8MaxDeg = 1022;
 
 struct SearchBuffers {
   uint32_t* vis[2];     // n/32 + 1 words each; all-zero between searches
@@ -211,6 +222,7 @@ uint64_t count_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t 
 void fill_csr_rows(const uint32_t* d_uv, uint64_t m, uint32_t lo, uint32_t hi, const uint64_t* d_row_off,
                    uint64_t* d_cursor, uint32_t* d_col, hipStream_t s);
 void build_padj(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, uint4* padj, hipStream_t s);
+void build_padj8(const uint64_t* row_off, const uint32_t* col, uint64_t nnz, unsigned long long* padj8, hipStream_t s);
 void make_row_off32(const uint64_t* d_row_off, uint32_t n, uint32_t* d_row_off32, hipStream_t s);
 uint64_t max_degree(const uint64_t* d_row_off, uint32_t n, hipStream_t s);  // synchronous
 uint64_t gen_gnp_device(uint32_t n, double p, uint64_t seed, uint32_t** d_uv_out, hipStream_t s);

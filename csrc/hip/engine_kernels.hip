@@ -179,6 +179,7 @@ struct LdsParams {
   const OffT* row_off;
   const uint32_t* col;
   const uint4* padj;  // packed {v, deg, base lo, base hi} per edge, or nullptr
+  const unsigned long long* padj8;  // or its 8-byte form (launch::pack8), or nullptr
   uint32_t n;
   uint32_t src, dst, seq;
   int side_policy;
@@ -360,7 +361,15 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   // The branch is on a kernel argument: wave-uniform.
   auto fetch_edges = [&](auto bc, const OffT* kk, uint32_t* vv, OffT* ob, OffT* oe) {
     constexpr int B = decltype(bc)::value;
-    if (P.padj) {
+    if (P.padj8) {
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const unsigned long long w = P.padj8[kk[k]];
+        vv[k] = launch::pack8_v(w);
+        ob[k] = (OffT)launch::pack8_base(w);
+        oe[k] = ob[k] + (OffT)launch::pack8_deg(w);
+      }
+    } else if (P.padj) {
 #pragma unroll
       for (int k = 0; k < B; ++k) {
         const uint4 q = P.padj[kk[k]];
@@ -666,7 +675,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     if constexpr (!kWr) {
       return;
     } else {
-      if (!P.padj || !P.lockstep || (P.trace && !kStamp) || s0.ovf || s1.ovf) return;  // uniform
+      if ((!P.padj && !P.padj8) || !P.lockstep || (P.trace && !kStamp) || s0.ovf || s1.ovf) return;  // uniform
       if (!kLq && !P.wave_hash) return;
       uint32_t E0 = (uint32_t)s0.fed, E1 = (uint32_t)s1.fed;
       uint32_t d0 = (uint32_t)s0.depth, d1 = (uint32_t)s1.depth;
@@ -721,10 +730,17 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           ok[k] = act[k] && e < (sd[k] ? X1 : X0);
           const Rec r = (sd[k] ? &R[a1][o1] : &R[a0][o0])[ok[k] ? e : 0u];
           u[k] = r.x;
-          const uint4 pq = padj[min(r.y, P.nnz_m1)];
-          v[k] = pq.x;
-          dg[k] = pq.y;
-          ob[k] = pq.z;
+          if (P.padj8) {  // kernel argument: uniform
+            const unsigned long long w = P.padj8[min(r.y, P.nnz_m1)];
+            v[k] = launch::pack8_v(w);
+            dg[k] = launch::pack8_deg(w);
+            ob[k] = launch::pack8_base(w);
+          } else {
+            const uint4 pq = padj[min(r.y, P.nnz_m1)];
+            v[k] = pq.x;
+            dg[k] = pq.y;
+            ob[k] = pq.z;
+          }
         }
         sub(0);
 #pragma unroll
@@ -1537,6 +1553,7 @@ struct GridParams {
   // 16-byte load brings the neighbour's degree with its id (no row-offset
   // round trip after the claim); nullptr = col + row_off
   const uint4* padj;
+  const unsigned long long* padj8;  // its 8-byte form (preferred when set)
 };
 
 // aux[2], the auto chain's word: bit 0 = the chain took the hand-off (its
@@ -1734,7 +1751,7 @@ __device__ bool auto_plan(GridParams<OffT>& P) {
   if (!(xp & kAuxActive) || (xp & kAuxDirect)) return false;  // direct: the hub pass runs the level
   P.side = (int)((xp >> 1) & 1u);
   P.precheck = (xp & kAuxPrecheck) ? 1 : 0;
-  if (P.precheck) P.padj = nullptr;  // big level: 4-byte column loads
+  if (P.precheck) P.padj = nullptr, P.padj8 = nullptr;  // big level: 4-byte column loads
   P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
   P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
   P.chunk_v = __builtin_amdgcn_readfirstlane(P.b.aux[5]);
@@ -1834,7 +1851,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
         }
         uu = sv[lo];
         const OffT k = sb[lo] + (OffT)(e - sEb[lo]);
-        if (P.padj) {  // small level: the neighbour's degree with its id
+        if (P.padj8) {  // small level: the neighbour's degree with its id
+          const unsigned long long w = P.padj8[k];
+          v = launch::pack8_v(w);
+          vdeg = launch::pack8_deg(w);
+        } else if (P.padj) {
           const uint4 q = P.padj[k];
           v = q.x;
           vdeg = q.y;
@@ -2338,6 +2359,7 @@ GridParams<OffT> gp(const launch::GraphView& g, const launch::SearchBuffers& b, 
   P.hub_direct = 0;
   P.precheck = 1;
   P.padj = kGridPadj ? g.padj : nullptr;
+  P.padj8 = kGridPadj ? g.padj8 : nullptr;
   return P;
 }
 
@@ -2357,7 +2379,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   // 16 blocks = 2 per XCD under round-robin dispatch; only the elected one works
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   if (g.row_off32) {
-    LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
+    LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
@@ -2369,7 +2391,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
       else k_lds_bibfs<uint32_t, false, false><<<blocks, kLdsThreads, 0, s>>>(P);
     }
   } else {
-    LdsParams<uint64_t> P{g.row_off, g.col, g.padj, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
+    LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     if (trace == 2)
       k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -2384,7 +2406,7 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
                 unsigned long long idle_ticks, hipStream_t s) {
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   BIBFS_REQUIRE(g.row_off32 != nullptr, "resident server: 32-bit row offsets required");
-  LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
+  LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;
   P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
@@ -2402,7 +2424,7 @@ void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* d_src, uint
                uint32_t k, uint32_t* d_slots, dev::HostResult* h_res, uint32_t* h_path, uint32_t path_cap,
                uint32_t seq, hipStream_t s) {
   BIBFS_REQUIRE(g.row_off32 != nullptr, "batched search: 32-bit row offsets required");
-  LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.n, 0, 0, seq, 0, 0, -1, nullptr, 1,
+  LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, 0, 0, seq, 0, 0, -1, nullptr, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 1, b, HostSide{h_res, h_path, path_cap}};
   BatchArgs A{d_src, d_dst, d_slots, h_res, h_path, path_cap, seq};
   if (g.n <= kBmMaxN)
@@ -2475,7 +2497,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
     P.hub_deg = hub_deg;  // ~0u: no hub pass
     P.chunk_v = (uint32_t)cv;
     P.precheck = (!kGridFast || frontier_edges > kGridPrecheckEdges) ? 1 : 0;
-    if (P.precheck || !kGridPadj) P.padj = nullptr;
+    if (P.precheck || !kGridPadj) P.padj = nullptr, P.padj8 = nullptr;
     if (direct) {
       P.hub_direct = 1;
       k_grid_hubs<OffT><<<hblocks, kGridThreads, 0, s>>>(P);

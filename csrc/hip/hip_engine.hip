@@ -37,6 +37,7 @@ struct HipBiBfs::Impl {
   uint32_t* d_row_off32 = nullptr;
   uint32_t* d_col = nullptr;
   uint4* d_padj = nullptr;   // packed adjacency (LDS engine), when it fits the budget
+  unsigned long long* d_padj8 = nullptr;  // its 8-byte form (launch::pack8), instead of it where it fits
   uint64_t max_deg = 0;      // largest degree: no hub pass when it is below the hub degree
   uint32_t* d_uv = nullptr;  // last generated edge list (kept for small graphs / tests)
   uint64_t uv_m = 0;
@@ -284,7 +285,7 @@ struct HipBiBfs::Impl {
   vid_t step_src = 0, step_dst = 0;
 
   launch::GraphView view() const {
-    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj, max_deg};
+    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj, max_deg, d_padj8};
   }
 
   bool server_usable() const { return d_row_off32 != nullptr && n > 0 && n <= 0x7fffffffu; }
@@ -478,6 +479,7 @@ struct HipBiBfs::Impl {
     if (d_row_off32) HIP_CHECK(hipFree(d_row_off32));
     if (d_col) HIP_CHECK(hipFree(d_col));
     if (d_padj) HIP_CHECK(hipFree(d_padj));
+    if (d_padj8) HIP_CHECK(hipFree(d_padj8));
     if (d_tadj) HIP_CHECK(hipFree(d_tadj));
     if (d_tinfo) HIP_CHECK(hipFree(d_tinfo));
     d_tadj = d_tinfo = nullptr;
@@ -491,6 +493,7 @@ struct HipBiBfs::Impl {
     d_row_off32 = nullptr;
     d_col = nullptr;
     d_padj = nullptr;
+    d_padj8 = nullptr;
     d_uv = nullptr;
     state_block = nullptr;
     n = 0;
@@ -592,11 +595,22 @@ struct HipBiBfs::Impl {
     // where the plain CSR path is used instead.
     const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
     const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
-    if (nnz && nnz * 16 <= budget) {
+    max_deg = launch::max_degree(d_row_off, n, stream);
+    // 8 B per edge (launch::pack8) where ids, bases and degrees fit: half the
+    // bytes, so a 10M-vertex graph's packed adjacency stays in the MALL
+    // (BIBFS_PADJ8=0: the 16-byte form)
+    static const bool p8_on = [] {
+      const char* e = std::getenv("BIBFS_PADJ8");
+      return !(e && e[0] == '0');
+    }();
+    if (p8_on && nnz && n < launch::kPack8MaxN && nnz < launch::kPack8MaxNnz && max_deg <= launch::kPack8MaxDeg &&
+        nnz * 8 <= budget) {
+      HIP_CHECK(hipMalloc(&d_padj8, nnz * 8));
+      launch::build_padj8(d_row_off, d_col, nnz, d_padj8, stream);
+    } else if (nnz && nnz * 16 <= budget) {
       HIP_CHECK(hipMalloc(&d_padj, nnz * 16));
       launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
     }
-    max_deg = launch::max_degree(d_row_off, n, stream);
     // small graphs: the packed 8-byte adjacency of the tiny server (8 (nnz + n) B)
     if (!tiny_disabled() && launch::tiny_supported(n, nnz, max_deg)) {
       HIP_CHECK(hipMalloc(&d_tadj, (std::max<uint64_t>(nnz, 1) + 4) * 8));  // +4: 16-byte first-edge loads
@@ -1144,7 +1158,7 @@ double HipBiBfs::last_build_ms() const { return p_->build_ms; }
 size_t HipBiBfs::device_bytes() const {
   const auto& I = *p_;
   return ((size_t)I.n + 1) * 8 + (I.d_row_off32 ? ((size_t)I.n + 1) * 4 : 0) + I.nnz * 4 +
-         (I.d_padj ? I.nnz * 16 : 0) +
+         (I.d_padj ? I.nnz * 16 : 0) + (I.d_padj8 ? I.nnz * 8 : 0) +
          (I.d_uv ? I.uv_m * 8 : 0) + I.state_bytes + I.state_bytes_alt;
 }
 int HipBiBfs::device() const { return p_->device; }
