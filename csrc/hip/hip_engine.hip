@@ -597,8 +597,10 @@ struct HipBiBfs::Impl {
     const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
     max_deg = launch::max_degree(d_row_off, n, stream);
     // 8 B per edge (launch::pack8) where ids, bases and degrees fit: half the
-    // bytes, so a 10M-vertex graph's packed adjacency stays in the MALL
-    // (BIBFS_PADJ8=0: the 16-byte form)
+    // bytes (10M G(n, p): 176 instead of 352 MB).  The hope was a MALL-resident
+    // adjacency and shorter dependent loads; measured the same search times
+    // (10M 62.8-63.1 vs 62.8-63.2 us, profiles/r4_padj8_ab.jsonl), so what it
+    // buys is the memory.  BIBFS_PADJ8=0: the 16-byte form.
     static const bool p8_on = [] {
       const char* e = std::getenv("BIBFS_PADJ8");
       return !(e && e[0] == '0');
