@@ -213,27 +213,79 @@ __device__ __forceinline__ uint32_t hslot(uint32_t v) {
   return (v * 0x9E3779B1u) >> (32 - kHashBits);
 }
 
+// 1 = the hash sets probe buckets of 4 slots: one 16-byte LDS read per probe,
+// then one CAS into the bucket's first empty slot (a vertex lives in the
+// first bucket, in probe order, that had room when it was inserted; slots are
+// never emptied during a search, so a find stops at the first bucket with an
+// empty slot).  0 = one CAS per slot.  Linear probing near the 75% load limit
+// made a wave's claim wait for its longest probe chain (stamped: ~2.5-3.1k
+// cycles per round late in a 10M search, profiles/r4_lds_stamps_10m.txt).
+#ifndef BIBFS_KNOB_HASH_BUCKET
+#define BIBFS_KNOB_HASH_BUCKET 1
+#endif
+constexpr bool kHashBucket = BIBFS_KNOB_HASH_BUCKET;
+typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
+
 // Insert vertex v with the given key (v | parity); true when v was absent.
 __device__ __forceinline__ bool hash_insert(uint32_t* H, uint32_t v, uint32_t key) {
-  uint32_t h = hslot(v);
-  for (uint32_t probe = 0; probe < kHashSize; ++probe) {  // bounded: the load limit keeps it short
-    const uint32_t old = atomicCAS(&H[h], kEmpty, key);
-    if (old == kEmpty) return true;
-    if ((old & kIdMask) == v) return false;
-    h = (h + 1) & kHashMask;
+  if constexpr (kHashBucket) {
+    uint32_t b = hslot(v) & ~3u;
+    for (uint32_t probe = 0; probe < kHashSize / 4;) {  // bounded: the load limit keeps it short
+      const u32x4b q = *reinterpret_cast<const u32x4b*>(H + b);
+      int e = -1;
+#pragma unroll
+      for (int j = 3; j >= 0; --j) {
+        if (q[j] != kEmpty && (q[j] & kIdMask) == v) return false;
+        if (q[j] == kEmpty) e = j;
+      }
+      if (e < 0) {  // full bucket: the next one
+        b = (b + 4) & kHashMask;
+        ++probe;
+        continue;
+      }
+      const uint32_t old = atomicCAS(&H[b + (uint32_t)e], kEmpty, key);
+      if (old == kEmpty) return true;
+      if ((old & kIdMask) == v) return false;
+      // another vertex took that slot first: read the bucket again
+    }
+    return false;
+  } else {
+    uint32_t h = hslot(v);
+    for (uint32_t probe = 0; probe < kHashSize; ++probe) {  // bounded: the load limit keeps it short
+      const uint32_t old = atomicCAS(&H[h], kEmpty, key);
+      if (old == kEmpty) return true;
+      if ((old & kIdMask) == v) return false;
+      h = (h + 1) & kHashMask;
+    }
+    return false;
   }
-  return false;
 }
 
 // Stored key of v (kEmpty when absent).
 __device__ __forceinline__ uint32_t hash_find(const uint32_t* H, uint32_t v) {
-  uint32_t h = hslot(v);
-  for (uint32_t probe = 0; probe < kHashSize; ++probe) {
-    const uint32_t k = H[h];
-    if (k == kEmpty || (k & kIdMask) == v) return k;
-    h = (h + 1) & kHashMask;
+  if constexpr (kHashBucket) {
+    uint32_t b = hslot(v) & ~3u;
+    for (uint32_t probe = 0; probe < kHashSize / 4; ++probe) {
+      const u32x4b q = *reinterpret_cast<const u32x4b*>(H + b);
+      bool room = false;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (q[j] != kEmpty && (q[j] & kIdMask) == v) return q[j];
+        room = room || q[j] == kEmpty;
+      }
+      if (room) return kEmpty;
+      b = (b + 4) & kHashMask;
+    }
+    return kEmpty;
+  } else {
+    uint32_t h = hslot(v);
+    for (uint32_t probe = 0; probe < kHashSize; ++probe) {
+      const uint32_t k = H[h];
+      if (k == kEmpty || (k & kIdMask) == v) return k;
+      h = (h + 1) & kHashMask;
+    }
+    return kEmpty;
   }
-  return kEmpty;
 }
 
 // ---- bitmap visited sets (graphs with n <= kBmMaxN): the hash area holds,
@@ -313,7 +365,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   // all-wave rounds: with the LDS queue (kLq), or on hash sets with the global queue
   constexpr bool kWr = kLq || (kWaveHashG && !kBm && kWaveRounds && std::is_same<OffT, uint32_t>::value);
   constexpr uint32_t CAP = kLq ? kCapBm : LdsRec<OffT>::cap;
-  __shared__ uint32_t H[2][kHashSize];
+  __shared__ __attribute__((aligned(16))) uint32_t H[2][kHashSize];  // (16-byte bucket reads)
   __shared__ Rec R[4][CAP];
   // kLq: per side, the vertices in claim (queue) order and each one's parent's
   // queue index; a search that ends inside the all-wave rounds walks its path
