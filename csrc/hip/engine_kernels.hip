@@ -220,8 +220,12 @@ __device__ __forceinline__ uint32_t hslot(uint32_t v) {
 // empty slot).  0 = one CAS per slot.  Linear probing near the 75% load limit
 // made a wave's claim wait for its longest probe chain (stamped: ~2.5-3.1k
 // cycles per round late in a 10M search, profiles/r4_lds_stamps_10m.txt).
+// Measured much slower: 10M LDS phase 31.9-32.2 -> 39.3 us, mean search
+// 62.6-62.9 -> 69.6-69.7 us (profiles/r4_lds_hash_bucket_ab.jsonl) -- the
+// 16-byte read and the per-slot selects cost more than the probes they save.
+// Off (0).
 #ifndef BIBFS_KNOB_HASH_BUCKET
-#define BIBFS_KNOB_HASH_BUCKET 1
+#define BIBFS_KNOB_HASH_BUCKET 0
 #endif
 constexpr bool kHashBucket = BIBFS_KNOB_HASH_BUCKET;
 typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
