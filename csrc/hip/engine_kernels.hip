@@ -1551,6 +1551,14 @@ constexpr uint32_t kHubDegree = 4096;  // deferred to k_grid_hubs
 #endif
 constexpr uint64_t kGridChunkMin = BIBFS_KNOB_GRID_CHUNK_MIN;  // smallest chunk (vertices) of k_grid_topdown
 constexpr int kHubTile = 1024;  // k_grid_hubs: hubs staged in LDS per pass
+// a hub-free level of at most one hub tile runs as one edge-parallel pass when
+// its top-down pass would walk more than this many 256-edge batches per block
+// (1 vs 2: Kronecker 25 44.1-45.1 -> 43.4-43.8 us, Kronecker 22 37.5-37.9 ->
+// 36.9-37.3 us mean search, 10M unchanged; profiles/r4_grid_direct_batches_ab.jsonl)
+#ifndef BIBFS_KNOB_GRID_DIRECT_BATCHES
+#define BIBFS_KNOB_GRID_DIRECT_BATCHES 1
+#endif
+constexpr uint64_t kGridDirectBatches = BIBFS_KNOB_GRID_DIRECT_BATCHES;
 // Single-side grid levels stop at their first meet (every meet of such a level
 // has the same length).  The edge loops of k_grid_topdown / k_grid_hubs read
 // the meet word every (mask + 1) batches of 256 edges per workgroup: a
@@ -1650,7 +1658,8 @@ __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, u
   {
     const uint64_t chunks = ((uint64_t)a.F + a.cv - 1) / a.cv;
     const uint64_t blocks = min<uint64_t>((uint64_t)P.cus * 4, max<uint64_t>(1, chunks));
-    a.direct = P.hub_direct && a.F <= (uint32_t)kHubTile && (a.hub != ~0u || fe > 2ull * kGridThreads * blocks);
+    a.direct = P.hub_direct && a.F <= (uint32_t)kHubTile &&
+               (a.hub != ~0u || fe > kGridDirectBatches * kGridThreads * blocks);
   }
   a.precheck = !kGridFast || fe > kGridPrecheckEdges;
   return a;
@@ -2543,7 +2552,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   // (also a level without hubs whose top-down pass would walk more than two
   // 256-edge batches per workgroup: a few heavy-ish vertices on one block)
   const bool direct = direct_mode && frontier <= (uint64_t)kHubTile &&
-                      (hub_deg != ~0u || frontier_edges > 2ull * kGridThreads * blocks);
+                      (hub_deg != ~0u || frontier_edges > kGridDirectBatches * kGridThreads * blocks);
   if (direct && direct_mode == 2)
     hblocks = (unsigned)std::max<uint64_t>(
         1, std::min<uint64_t>((uint64_t)cus * 4, (frontier_edges + kGridThreads - 1) / kGridThreads));
