@@ -2549,8 +2549,9 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   // Kronecker 22 46.9-48.1 -> 38.0-38.3 us, Kronecker 25 56.2-57.9 -> 44.0-44.2
   // us against no direct levels; 10M G(n, p) unchanged.
   const int direct_mode = grid_hub_direct_mode();
-  // (also a level without hubs whose top-down pass would walk more than two
-  // 256-edge batches per workgroup: a few heavy-ish vertices on one block)
+  // (also a level without hubs whose top-down pass would walk more than
+  // kGridDirectBatches 256-edge batches per workgroup: a few heavy-ish
+  // vertices on one block)
   const bool direct = direct_mode && frontier <= (uint64_t)kHubTile &&
                       (hub_deg != ~0u || frontier_edges > kGridDirectBatches * kGridThreads * blocks);
   if (direct && direct_mode == 2)
