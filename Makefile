@@ -44,7 +44,7 @@ PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_
 
 CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp
 HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/tiny_engine.hip csrc/hip/batch_global.hip csrc/hip/hip_engine.hip \
-             csrc/hip/capi.hip csrc/dist/comm.hip csrc/dist/dist_engine.hip
+             csrc/hip/capi.hip csrc/dist/comm.hip csrc/dist/ipc_comm.hip csrc/dist/dist_engine.hip
 MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp
 
 CORE_OBJ  := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(CORE_SRC))

@@ -9,6 +9,12 @@
   ``torch.distributed`` (``from_torch_distributed``) or over MPI by the
   ``mpi_bibfs`` CLI.  An error or a watchdog timeout on any rank aborts the
   communicator (``ncclCommAbort``) so no peer is left hanging.
+* ``dist_proc_run``: the same native engine with P ranks as P separate
+  PROCESSES, exchanging over the HIP-IPC transport (``backend="ipc"``,
+  csrc/dist/ipc_comm.hip).  The processes may share one GPU -- the
+  reference's own v4 launch, 4 MPI ranks on one machine's GPU
+  (single_machine_bench.sh:9,52) -- or sit on different GPUs, where the same
+  transport reads peer HBM over xGMI.
 * ``dist_local_run``: the same native engine with P ranks as P threads on ONE
   GPU, exchanging through an in-process group instead of RCCL -- how the
   partition / exchange logic is tested with P > 1 on a one-GPU box.
@@ -20,8 +26,13 @@
 """
 from __future__ import annotations
 
+import json
 import os
+import shutil
 import subprocess
+import sys
+import tempfile
+import time
 from typing import List, Optional, Sequence
 
 from .._lib import native, tool_path
@@ -84,24 +95,35 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
 class DistEngine:
     """Partitioned multi-GPU bidirectional BFS (collective API: call on every rank)."""
 
-    def __init__(self, rank: int, world: int, device: int, unique_id: bytes):
-        self._e = native.DistBiBfs(int(rank), int(world), int(device), unique_id)
+    def __init__(self, rank: int, world: int, device: int, unique_id: bytes, backend: str = "rccl"):
+        self._e = native.DistBiBfs(int(rank), int(world), int(device), unique_id, backend)
 
     @staticmethod
-    def unique_id() -> bytes:
-        return native.rccl_unique_id()
+    def unique_id(backend: str = "rccl") -> bytes:
+        return native.dist_unique_id(backend)
 
     @classmethod
-    def from_torch_distributed(cls, device: Optional[int] = None) -> "DistEngine":
-        """Bootstrap from an initialised torch.distributed process group."""
+    def from_torch_distributed(cls, device: Optional[int] = None, backend: str = "rccl") -> "DistEngine":
+        """Bootstrap from an initialised torch.distributed process group.
+
+        backend "rccl": one rank per GPU; "ipc": the HIP-IPC transport, where
+        several ranks may share a GPU (device defaults to LOCAL_RANK modulo
+        the visible GPUs)."""
         import torch.distributed as dist
 
         rank, world = dist.get_rank(), dist.get_world_size()
-        obj = [native.rccl_unique_id() if rank == 0 else None]
+        obj = [native.dist_unique_id(backend) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         if device is None:
             device = int(os.environ.get("LOCAL_RANK", rank))
-        return cls(rank, world, device, obj[0])
+            if backend == "ipc":
+                device %= max(1, gpu_count())
+        return cls(rank, world, device, obj[0], backend)
+
+    def query(self, src: int, dst: int):
+        """Lean serving call: ``(hops, path)``, hops = -1 when unreachable
+        (the stats stay in ``last_stats``, read outside any timed loop)."""
+        return self._e.query(int(src), int(dst))
 
     def load(self, graph: Graph) -> "DistEngine":
         self._e.load_edges(graph.edges)
@@ -248,6 +270,122 @@ def dist_local_generate_run(ranks: int, spec: str, queries: Sequence, device: in
                                           tuning if tuning is not None else native.DistTuning(), int(verify))
 
 
+class ProcResult:
+    """One query's answer from :func:`dist_proc_run` (the fields of ``native.SearchResult`` the tests read)."""
+
+    __slots__ = ("hops", "found", "path", "stats", "total_ms")
+
+    def __init__(self, d: dict):
+        self.hops, self.found, self.path = int(d["hops"]), bool(d["found"]), list(d["path"])
+        self.stats, self.total_ms = d.get("stats", {}), float(d.get("total_ms", 0.0))
+
+    def __repr__(self) -> str:
+        return f"ProcResult(found={self.found}, hops={self.hops})"
+
+
+class ProcRunError(RuntimeError):
+    """A multi-process run failed; ``returncodes`` / ``outputs`` / ``elapsed_s`` say how."""
+
+    def __init__(self, msg: str, returncodes, outputs, elapsed_s: float):
+        super().__init__(msg)
+        self.returncodes, self.outputs, self.elapsed_s = returncodes, outputs, elapsed_s
+
+
+def dist_proc_launch(ranks: int, graph, queries: Sequence, runs: Sequence = ((None, None),), device: int = 0,
+                     fault=None, verify: int = 0, backend: str = "ipc", timeout: float = 300.0, env=None):
+    """Run the partitioned engine as ``ranks`` separate processes and return
+    ``(returncodes, outputs, elapsed_s)``: ``outputs[r]`` is rank r's report
+    (build sizes and ``runs[i] = {"results", "last_stats", ...}``, or
+    ``error``).  ``graph`` is a :class:`Graph` (written once as ``.bin``;
+    every rank reads only its shard) or a ``gnp:``/``rmat:``/``kron:`` spec
+    (every rank generates its rows on its GPU).  ``runs``: ``(options,
+    tuning)`` keyword dicts of :func:`make_options` / :func:`make_tuning`,
+    each answering every query on the same shards (tuning None = keep the
+    previous); ``fault``: ``(rank, round, mode)`` for ``inject_fault``
+    (3 = that rank's process kills itself)."""
+    tmp = tempfile.mkdtemp(prefix="bibfs_proc_")
+    try:
+        if isinstance(graph, str):
+            gdesc = {"spec": graph}
+        else:
+            path = os.path.join(tmp, "graph.bin")
+            graph.save_bin(path)
+            gdesc = {"bin": path}
+        job = {"size": int(ranks), "device": int(device), "uid": native.dist_unique_id(backend).hex(),
+               "backend": backend, "graph": gdesc, "queries": [[int(s), int(d)] for s, d in queries],
+               "runs": [{"options": dict(o or {}), "tuning": None if t is None else dict(t)} for o, t in runs],
+               "fault": list(fault) if fault else None,
+               "verify": int(verify), "out_dir": tmp}
+        job_path = os.path.join(tmp, "job.json")
+        with open(job_path, "w") as f:
+            json.dump(job, f)
+        e = dict(os.environ)
+        e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if env:
+            e.update(env)
+        root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        e["PYTHONPATH"] = root + (os.pathsep + e["PYTHONPATH"] if e.get("PYTHONPATH") else "")
+        t0 = time.monotonic()
+        procs = [subprocess.Popen([sys.executable, "-m", "bidirectional_bfs_amd.parallel._proc_worker", job_path,
+                                   str(r)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=e)
+                 for r in range(int(ranks))]
+        logs = []
+        for p in procs:
+            left = max(1.0, timeout - (time.monotonic() - t0))
+            try:
+                logs.append(p.communicate(timeout=left)[0])
+            except subprocess.TimeoutExpired:
+                for q in procs:
+                    q.kill()
+                logs.append(p.communicate()[0])
+        elapsed = time.monotonic() - t0
+        rcs = [p.returncode for p in procs]
+        outs = []
+        for r in range(int(ranks)):
+            fp = os.path.join(tmp, f"rank{r}.json")
+            if os.path.exists(fp):
+                with open(fp) as f:
+                    outs.append(json.load(f))
+            else:
+                outs.append({"rank": r, "error": f"no report (exit status {rcs[r]})", "log": logs[r][-2000:]})
+        return rcs, outs, elapsed
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def dist_proc_matrix(ranks: int, graph, queries: Sequence, runs: Sequence, device: int = 0, verify: int = 0,
+                     backend: str = "ipc", timeout: float = 300.0):
+    """Every ``(options, tuning)`` of ``runs`` over the same ``ranks``-process
+    group (see :func:`dist_proc_launch`).  Returns ``[(results, last_stats,
+    run_report)]`` per run -- rank 0's, after checking that every rank
+    returned the same hop counts and paths -- and the per-rank reports."""
+    rcs, outs, elapsed = dist_proc_launch(ranks, graph, queries, runs, device, None, verify, backend, timeout)
+    if any(rcs):
+        errs = "; ".join(f"rank {o.get('rank')}: {o.get('error', '')}" for o in outs if o.get("error"))
+        raise ProcRunError(f"dist_proc_run failed (exit statuses {rcs}): {errs}", rcs, outs, elapsed)
+    got = []
+    for i, run0 in enumerate(outs[0]["runs"]):
+        for o in outs[1:]:
+            for a, b in zip(run0["results"], o["runs"][i]["results"]):
+                if a["hops"] != b["hops"] or a["path"] != b["path"]:
+                    raise ProcRunError("dist_proc_run: ranks returned different results", rcs, outs, elapsed)
+        got.append(([ProcResult(d) for d in run0["results"]], run0["last_stats"], run0))
+    return got, outs
+
+
+def dist_proc_run(ranks: int, graph, queries: Sequence, device: int = 0, options: Optional[dict] = None,
+                  tuning: Optional[dict] = None, return_stats: bool = False, verify: int = 0,
+                  backend: str = "ipc", timeout: float = 300.0, **kw):
+    """Like :func:`dist_local_run`, with every rank its own process.  Returns
+    rank 0's results; with ``return_stats`` also its per-query
+    ``last_stats`` and the per-rank reports."""
+    opts = dict(options or {})
+    opts.update(kw)
+    got, outs = dist_proc_matrix(ranks, graph, queries, [(opts, tuning or {})], device, verify, backend, timeout)
+    rs, st, _ = got[0]
+    return (rs, st, outs) if return_stats else rs
+
+
 class ReplicatedServer:
     """Query-parallel serving: rank r answers queries r, r+W, r+2W, ... on its own GPU."""
 
@@ -275,5 +413,5 @@ def run_mpi(tool: str, args: Sequence[str], np: int = 2, timeout: float = 300.0,
     return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=e)
 
 
-__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "dist_local_generate_run", "make_tuning", "run_mpi",
-           "MPIEXEC"]
+__all__ = ["DistEngine", "ReplicatedServer", "dist_local_run", "dist_local_generate_run", "dist_proc_launch",
+           "dist_proc_matrix", "dist_proc_run", "ProcResult", "ProcRunError", "make_tuning", "run_mpi", "MPIEXEC"]

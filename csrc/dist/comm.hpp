@@ -1,6 +1,8 @@
 // Collective layer of the multi-GPU engine (internal header).
 //
-// Production: RCCL over xGMI, one process per GPU (make_rccl_comm).  The
+// Production: RCCL over xGMI, one process per GPU (make_rccl_comm).  Separate
+// processes that share a GPU (RCCL refuses that) use the IPC transport
+// (make_ipc_comm), which also runs one process per GPU.  The
 // engine only ever issues the handful of collectives below, always on a HIP
 // stream, so the same engine code also runs over an in-process "local group"
 // (make_local_comm): P host threads that share one GPU.  The local group
@@ -54,10 +56,19 @@ class Comm {
   // (peers blocked in one return with an error).  Idempotent.
   virtual void abort() = 0;
   virtual bool aborted() const = 0;
+  // Watchdog of a transport whose host waits for its peers (ipc).
+  virtual void set_timeout(double seconds) {}
 };
 
 std::vector<uint8_t> rccl_unique_id();
 std::unique_ptr<Comm> make_rccl_comm(int rank, int size, const std::vector<uint8_t>& uid);
+
+// P processes, on one GPU or several, exchanging through IPC-mapped staging
+// buffers (ipc_comm.hip).  The id names the group's shared-memory control
+// segment; rank 0 makes it (ipc_unique_id) and hands it to the other ranks
+// over any channel (MPI_Bcast, torch.distributed), as with an RCCL unique id.
+std::vector<uint8_t> ipc_unique_id();
+std::unique_ptr<Comm> make_ipc_comm(int rank, int size, const std::vector<uint8_t>& uid, double timeout_s = 120.0);
 
 struct LocalGroup;
 // `timeout_s`: a rank waiting longer than this in a rendezvous aborts the group.

@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <csignal>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -2544,7 +2545,11 @@ uint32_t next_pow2(uint64_t x) {
 
 }  // namespace
 
-std::vector<uint8_t> dist_unique_id() { return dist::rccl_unique_id(); }
+std::vector<uint8_t> dist_unique_id(const std::string& backend) {
+  if (backend == "ipc") return dist::ipc_unique_id();
+  BIBFS_REQUIRE(backend == "rccl", "dist: backend must be rccl or ipc, got " + backend);
+  return dist::rccl_unique_id();
+}
 
 int gpu_count() {
   int n = 0;
@@ -2644,6 +2649,7 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
+    comm->set_timeout(tune.timeout_s);
     if (const char* t = std::getenv("BIBFS_DIST_STAMP")) solo_stamp = std::atoi(t) != 0;
     HIP_CHECK(hipMalloc(&d_stamps, 16 * sizeof(unsigned long long)));
   }
@@ -2982,6 +2988,7 @@ struct DistBiBfs::Impl {
     const int mode = fault_mode;
     fault_mode = 0;
     if (mode == 2) std::this_thread::sleep_for(std::chrono::duration<double>(2 * tune.timeout_s));
+    if (mode == 3) ::raise(SIGKILL);  // a rank process dies mid-search (multi-process transports)
     throw Error("dist: injected fault on rank " + std::to_string(rank) + " at round " + std::to_string(it));
   }
 
@@ -3521,9 +3528,15 @@ void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult&
   r.path.insert(r.path.end(), pT.begin() + 1, pT.end());
 }
 
-DistBiBfs::DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& uid) : p_(new Impl) {
+DistBiBfs::DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& uid, const std::string& backend)
+    : p_(new Impl) {
   HIP_CHECK(hipSetDevice(device));
-  p_->comm = dist::make_rccl_comm(rank, size, uid);
+  if (backend == "ipc")
+    p_->comm = dist::make_ipc_comm(rank, size, uid, p_->tune.timeout_s);
+  else if (backend == "rccl")
+    p_->comm = dist::make_rccl_comm(rank, size, uid);
+  else
+    throw Error("dist: backend must be rccl or ipc, got " + backend);
   p_->setup(device);
 }
 
@@ -3732,6 +3745,7 @@ void DistBiBfs::set_tuning(const DistTuning& t) {
   const bool realloc = p_->state && t.walk_max > p_->tune.walk_max;
   p_->tune = t;
   p_->mem.cap = t.hbm_cap_bytes;
+  p_->comm->set_timeout(t.timeout_s);
   if (realloc) {  // path-gather blocks are sized from walk_max
     HIP_CHECK(hipSetDevice(p_->device));
     devmem::Scope scope(&p_->mem);

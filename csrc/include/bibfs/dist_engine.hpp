@@ -45,7 +45,10 @@
 
 namespace bibfs {
 
-std::vector<uint8_t> dist_unique_id();  // ncclGetUniqueId as bytes
+// Group id of a collective backend, made on rank 0 and handed to every rank:
+// "rccl" -> ncclGetUniqueId bytes; "ipc" -> the name of the IPC group's
+// shared-memory control segment (comm.hpp: P processes on one GPU or several).
+std::vector<uint8_t> dist_unique_id(const std::string& backend = "rccl");
 int gpu_count();                         // visible HIP devices (0 when none / no driver)
 
 namespace dist {
@@ -111,7 +114,9 @@ struct DistTuning {
 
 class DistBiBfs {
  public:
-  DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& unique_id);  // RCCL
+  // backend "rccl" (one process per GPU) or "ipc" (processes may share a GPU)
+  DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& unique_id,
+            const std::string& backend = "rccl");
   DistBiBfs(std::unique_ptr<dist::Comm> comm, int device);                          // any backend
   ~DistBiBfs();
   DistBiBfs(const DistBiBfs&) = delete;
@@ -143,8 +148,9 @@ class DistBiBfs {
   void set_tuning(const DistTuning& t);
   const DistTuning& tuning() const;
   // Fault injection (tests): from the `at`-th enqueued round of a search on,
-  // this rank throws (mode 1) or stalls for 2 x timeout_s before throwing
-  // (mode 2).  mode 0 disarms.
+  // this rank throws (mode 1), stalls for 2 x timeout_s before throwing
+  // (mode 2), or kills its own process (mode 3: multi-process backends).
+  // mode 0 disarms.
   void inject_fault(int at, int mode);
 
   int rank() const;
@@ -164,7 +170,7 @@ class DistBiBfs {
   uint32_t lo() const;
   uint32_t hi() const;
   const DistLevelStats& last_stats() const;
-  const char* backend() const;  // "rccl" or "local"
+  const char* backend() const;  // "rccl", "ipc" or "local"
 
  private:
   struct Impl;

@@ -370,6 +370,13 @@ PYBIND11_MODULE(_native, m) {
     auto id = dist_unique_id();
     return py::bytes(reinterpret_cast<const char*>(id.data()), id.size());
   });
+  m.def(
+      "dist_unique_id",
+      [](const std::string& backend) {
+        auto id = dist_unique_id(backend);
+        return py::bytes(reinterpret_cast<const char*>(id.data()), id.size());
+      },
+      py::arg("backend") = "rccl");
   py::class_<DistTuning>(m, "DistTuning")
       .def(py::init<>())
       .def_readwrite("spec_rounds", &DistTuning::spec_rounds)
@@ -392,13 +399,13 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("at", &DistLocalFault::at)
       .def_readwrite("mode", &DistLocalFault::mode);
   py::class_<DistBiBfs>(m, "DistBiBfs")
-      .def(py::init([](int rank, int size, int device, py::bytes uid) {
+      .def(py::init([](int rank, int size, int device, py::bytes uid, const std::string& backend) {
              std::string s = uid;
              std::vector<uint8_t> id(s.begin(), s.end());
              py::gil_scoped_release rel;
-             return new DistBiBfs(rank, size, device, id);
+             return new DistBiBfs(rank, size, device, id, backend);
            }),
-           py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("unique_id"))
+           py::arg("rank"), py::arg("size"), py::arg("device"), py::arg("unique_id"), py::arg("backend") = "rccl")
       .def_property_readonly("rank", &DistBiBfs::rank)
       .def_property_readonly("size", &DistBiBfs::size)
       .def_property_readonly("n", &DistBiBfs::n)
@@ -423,6 +430,16 @@ PYBIND11_MODULE(_native, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("search", &DistBiBfs::search, py::arg("src"), py::arg("dst"), py::arg("options") = SearchOptions{},
            py::call_guard<py::gil_scoped_release>())
+      // lean serving call, the twin of HipBiBfs.query: (hops, path), hops -1 when unreachable
+      .def("query",
+           [](DistBiBfs& e, vid_t s, vid_t d) {
+             SearchResult r;
+             {
+               py::gil_scoped_release rel;
+               r = e.search(s, d);
+             }
+             return hops_path(r.found ? r.hops : -1, r.path);
+           })
       .def("barrier", &DistBiBfs::barrier, py::call_guard<py::gil_scoped_release>())
       .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>())
       .def("release", &DistBiBfs::release, py::call_guard<py::gil_scoped_release>())

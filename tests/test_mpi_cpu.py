@@ -58,13 +58,23 @@ def test_mpi_rmat():
 
 
 def test_mpi_bibfs_more_ranks_than_gpus_fails_clearly():
-    """mpi_bibfs is one rank per GPU: a launch with more ranks on the node than
+    """--comm rccl is one rank per GPU: a launch with more ranks on the node than
     visible GPUs (every rank here: no GPU at all, or np 3 on a 1-GPU box) ends
     with one clear message on the over-subscribed ranks and rc 1 -- no raw HIP
-    error, no rank left waiting in RCCL bootstrap."""
+    error, no rank left waiting in RCCL bootstrap.  (--comm auto / ipc run such
+    a launch over the IPC transport: tests/test_gpu_dist_proc.py.)"""
     from bidirectional_bfs_amd.parallel import gpu_count
 
     np_ = gpu_count() + 2
-    r = run_mpi("mpi_bibfs", ["gnp:1000::1", 0, 999], np=np_, timeout=60)
+    r = run_mpi("mpi_bibfs", ["gnp:1000::1", 0, 999, "--comm", "rccl"], np=np_, timeout=60)
     assert r.returncode != 0
     assert "one rank per GPU" in r.stderr and "ranks on this node > GPUs" in r.stderr
+
+
+def test_mpi_bibfs_without_gpu_fails_clearly():
+    from bidirectional_bfs_amd.parallel import gpu_count
+
+    if gpu_count():
+        pytest.skip("a GPU is visible")
+    r = run_mpi("mpi_bibfs", ["gnp:1000::1", 0, 999], np=2, timeout=60)
+    assert r.returncode != 0 and "no usable GPU" in r.stderr, r.stderr

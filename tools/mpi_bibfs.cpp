@@ -1,5 +1,6 @@
 // mpirun -n <p> mpi_bibfs <graph.bin | gnp:N[:p[:seed]] | rmat:N:M[:seed] | kron:S[:EF[:seed]]> <src> <dst>
 //                         [--repeat R] [--warmup W] [--json] [--verify] [--direction auto|topdown|bottomup]
+//                         [--comm auto|rccl|ipc] [--timeout S] [--fault RANK:ROUND:MODE]
 //
 // v4 capability (reference v4/mpi_bas.cpp + v4/comp.cu): multi-GPU
 // bidirectional BFS, one MPI rank per GPU.  MPI is used only to bootstrap the
@@ -8,18 +9,28 @@
 // reads only its shard of the .bin (or generates the graph on its GPU and
 // keeps its rows); the reference broadcast the whole edge list and every rank
 // expanded the whole frontier (v4/comp.cu:99).
+//
+// --comm ipc runs the ranks as separate processes over the HIP-IPC transport
+// (csrc/dist/ipc_comm.hip), so several ranks may share one GPU -- the
+// reference's own single-machine launch, `mpirun -n 4` with every rank on the
+// one GPU (single_machine_bench.sh:9,52; v4/Makefile:64 uses -np 6).  The
+// default `auto` picks RCCL when every rank on a node has a GPU of its own and
+// IPC otherwise.  --fault arms DistBiBfs::inject_fault on one rank (1 throw,
+// 2 stall past the timeout, 3 kill the process) to check that the other ranks
+// fail instead of hanging.
 #include <mpi.h>
 
 #include "bibfs/dist_engine.hpp"
 #include "bibfs/hip_engine.hpp"
 #include "cli_common.hpp"
 
-static int local_rank_from_env(int rank) {
-  for (const char* k : {"MPI_LOCALRANKID", "OMPI_COMM_WORLD_LOCAL_RANK", "LOCAL_RANK", "SLURM_LOCALID"}) {
-    const char* v = std::getenv(k);
-    if (v) return std::atoi(v);
-  }
-  return rank;
+// rank and rank count among the processes of this node
+static void node_rank(int* local_rank, int* local_size) {
+  MPI_Comm node;
+  MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, 0, MPI_INFO_NULL, &node);
+  MPI_Comm_rank(node, local_rank);
+  MPI_Comm_size(node, local_size);
+  MPI_Comm_free(&node);
 }
 
 int main(int argc, char** argv) {
@@ -27,7 +38,8 @@ int main(int argc, char** argv) {
   int rank, size;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &size);
-  auto a = cli::parse(argc, argv, {"repeat", "warmup", "side", "direction", "alpha", "beta", "device"});
+  auto a = cli::parse(argc, argv,
+                      {"repeat", "warmup", "side", "direction", "alpha", "beta", "device", "comm", "timeout", "fault"});
   if (a.pos.size() != 3) {
     if (rank == 0) std::fprintf(stderr, "Usage: mpirun -n <p> %s <graph.bin> <src> <dst>\n", argv[0]);
     MPI_Finalize();
@@ -35,32 +47,50 @@ int main(int argc, char** argv) {
   }
   int rc = 0;
   try {
-    const int device = a.has("device") ? (int)a.geti("device", 0) : local_rank_from_env(rank);
-    // One rank per GPU (the reference ran 4-6 ranks on 1-2 GPUs, v4/Makefile:64,
-    // README.md:16; here a rank owns a GPU's HBM and its RCCL endpoint).  Every
-    // rank checks its device and the verdict is agreed on before any rank
-    // touches RCCL, so a bad launch fails with one clear message, not a raw
-    // HIP error on some ranks and a hang on the others.
+    int local_rank = 0, local_size = 1, max_local = 1;
+    node_rank(&local_rank, &local_size);
+    MPI_Allreduce(&local_size, &max_local, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
     const int ndev = bibfs::gpu_count();
+    std::string comm = a.has("comm") ? a.get("comm") : "auto";
+    if (comm == "auto") comm = max_local > ndev ? "ipc" : "rccl";
+    if (comm != "rccl" && comm != "ipc") throw bibfs::Error("--comm must be auto, rccl or ipc");
+    // RCCL: one rank per GPU (a rank owns a GPU's HBM and its RCCL endpoint).
+    // IPC: ranks share the node's GPUs round-robin.  Every rank checks its
+    // device and the verdict is agreed on before any rank touches a
+    // communicator, so a bad launch fails with one clear message on every rank.
+    const int device = a.has("device") ? (int)a.geti("device", 0)
+                                       : (comm == "ipc" && ndev > 0 ? local_rank % ndev : local_rank);
     int bad = (device < 0 || device >= ndev) ? 1 : 0, any_bad = 0;
     MPI_Allreduce(&bad, &any_bad, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
     if (any_bad) {
-      if (bad)
+      if (bad && comm == "rccl")
         std::fprintf(stderr,
-                     "[rank %d] mpi_bibfs runs one rank per GPU: this rank maps to device %d but only %d GPU(s) "
-                     "are visible (ranks on this node > GPUs); launch with at most %d ranks per node or pass "
-                     "--device\n",
+                     "[rank %d] --comm rccl runs one rank per GPU: this rank maps to device %d but only %d GPU(s) "
+                     "are visible (ranks on this node > GPUs); launch at most %d ranks per node, pass --device, "
+                     "or use --comm ipc\n",
                      rank, device, ndev, ndev);
+      else if (bad)
+        std::fprintf(stderr, "[rank %d] no usable GPU for this rank (device %d, %d visible)\n", rank, device, ndev);
       MPI_Finalize();
       return 1;
     }
     std::vector<uint8_t> uid(128);
-    if (rank == 0) uid = bibfs::dist_unique_id();
+    if (rank == 0) uid = bibfs::dist_unique_id(comm);
     int len = (int)uid.size();
     MPI_Bcast(&len, 1, MPI_INT, 0, MPI_COMM_WORLD);
     uid.resize((size_t)len);
     MPI_Bcast(uid.data(), len, MPI_BYTE, 0, MPI_COMM_WORLD);
-    bibfs::DistBiBfs eng(rank, size, device, uid);
+    bibfs::DistBiBfs eng(rank, size, device, uid, comm);
+    if (a.has("timeout")) {
+      bibfs::DistTuning t = eng.tuning();
+      t.timeout_s = a.getd("timeout", 120.0);
+      eng.set_tuning(t);
+    }
+    if (a.has("fault")) {
+      auto f = cli::split(a.get("fault"), ':');
+      BIBFS_REQUIRE(f.size() == 3, "--fault RANK:ROUND:MODE");
+      if (std::atoi(f[0].c_str()) == rank) eng.inject_fault(std::atoi(f[1].c_str()), std::atoi(f[2].c_str()));
+    }
     const std::string graph = a.pos[0];
     double tl = MPI_Wtime();
     if (cli::is_spec(graph)) {
@@ -103,6 +133,7 @@ int main(int argc, char** argv) {
         if (r.found) std::printf("Shortest path length = %lld\n", (long long)r.hops);
         else std::printf("No path found\n");
         std::printf("[Time] MPI+HIP BI-BFS = %.9g s\n", med * 1e-3);
+        std::printf("Ranks: %d over %s (%d GPU(s) visible per node)\n", size, eng.backend(), ndev);
         cli::print_path(r);
       }
     }
