@@ -92,15 +92,6 @@ constexpr uint32_t kTraceCap = 4096;            // rounds recorded with SearchOp
 constexpr uint32_t kPlanRing = 64;              // pinned per-round plan words (lookahead < this)
 constexpr int kStageRanks = 16;                 // gathered reductions staged in LDS up to this many ranks
 constexpr uint32_t kOwnerCapMin = 256;          // smallest owner-addressed candidate block (pairs)
-// 1 = the round planner runs on a whole wave with scalar (wave-uniform)
-// inputs, 0 = on one lane (A/B: BIBFS_DIST_PLAN_WAVE).  Measured slower: the
-// planner stamp of a small P = 2/4 round went 3.26/3.38 -> 4.01/4.63 us
-// (G(1M) local group, profiles/r4_dist_plan_wave_ab.jsonl) -- copying Ctl and
-// Reduced into SGPRs spills 80 SGPRs to VGPR lanes and costs 120 readfirstlanes.
-#ifndef BIBFS_DIST_PLAN_WAVE
-#define BIBFS_DIST_PLAN_WAVE 0
-#endif
-constexpr bool kPlanOnWave = BIBFS_DIST_PLAN_WAVE;
 // Small rounds at P > 1 (one workgroup per rank, see small_expand):
 constexpr uint32_t kSmallE = 1024;              // frontier edges per side (any rank)
 constexpr uint32_t kSmallV = 512;               // frontier vertices per side (all ranks) staged in LDS
@@ -312,52 +303,6 @@ __device__ __forceinline__ void plan_round(const Ctl& p, const Reduced& rd, cons
   out = cl;
 }
 
-// A struct read from LDS into wave-uniform registers: every 32-bit word
-// through readfirstlane, so the compiler keeps it in SGPRs and does the
-// arithmetic on it on the scalar unit.
-template <typename T>
-__device__ __forceinline__ T uniform_copy(const T& src) {
-  static_assert(sizeof(T) % 4 == 0, "32-bit words");
-  T dst;
-  const uint32_t* s = reinterpret_cast<const uint32_t*>(&src);
-  uint32_t* d = reinterpret_cast<uint32_t*>(&dst);
-#pragma unroll
-  for (uint32_t i = 0; i < sizeof(T) / 4; ++i) d[i] = __builtin_amdgcn_readfirstlane(s[i]);
-  return dst;
-}
-
-// The planner on a WHOLE wave (every lane computes the same plan from
-// wave-uniform copies of its inputs, which puts the ~50-field decision chain
-// on the scalar unit); lane 0 writes it.  Kept as the kPlanOnWave A/B only:
-// the copies spill ~80 SGPRs to VGPR lanes and the round's planning stamp
-// (RoundStamp::sg -> ep) got ~0.7-1.2 us SLOWER than on one lane.
-__device__ __forceinline__ void plan_round_wave(const Ctl& p, const Reduced& rd, const Policy& pol, uint64_t spec_cap,
-                                                int flags, Ctl& out) {
-  const Ctl pl = uniform_copy(p);
-  const Reduced rl = uniform_copy(rd);
-  Ctl cl;
-  plan_round_regs(pl, rl, pol, spec_cap, flags, cl);
-  if (__lane_id() == 0) out = cl;
-}
-
-// reduce_gathered on a whole wave, the same way (wave-uniform inputs).
-__device__ __forceinline__ void reduce_gathered_wave(const Reduced* g, int P, Reduced& out) {
-  Reduced r = uniform_copy(g[0]);
-  for (int k = 1; k < P; ++k) {
-    const Reduced x = uniform_copy(g[k]);
-    for (int i = 0; i < 4; ++i) r.sums[i] += x.sums[i];
-    r.meetkey = min(r.meetkey, x.meetkey);
-    r.nocmax = min(r.nocmax, x.nocmax);
-    for (int s = 0; s < 2; ++s) {
-      r.spill[s] += x.spill[s];
-      r.nfmax[s] = min(r.nfmax[s], x.nfmax[s]);
-      r.maxsend[s] = max(r.maxsend[s], x.maxsend[s]);
-      r.md[s] = min(r.md[s], x.md[s]);
-      r.spillmax[s] = max(r.spillmax[s], x.spillmax[s]);
-    }
-  }
-  if (__lane_id() == 0) out = r;
-}
 
 __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd, const Policy& pol,
                                                 uint64_t spec_cap, int flags, Ctl& c) {
@@ -929,13 +874,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
   __shared__ SmallStage sm;
   if (threadIdx.x < kWave) {  // wave 0 plans, on wave-uniform (scalar) registers
-    if (kPlanOnWave) {
-      if (V.P <= kStageRanks) reduce_gathered_wave(gst, V.P, rd);
-      else if (threadIdx.x == 0) reduce_gathered(V.redg[p ^ 1], V.P, rd);
-      __builtin_amdgcn_wave_barrier();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // lane 0's rd stores before the wave reads them
-      plan_round_wave(prev, rd, pol, plan_cap, flags, c);
-    } else if (threadIdx.x == 0) {
+    if (threadIdx.x == 0) {
       // (two call sites, not one through a conditional pointer: that made every
       // load of the planner's inputs a flat load)
       if (V.P <= kStageRanks) reduce_gathered(gst, V.P, rd);

@@ -306,17 +306,9 @@ void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* h
 // levels > 1 chains that many device-planned levels: the finisher of each
 // plans the next one into aux (or ends the chain: search over, or a level the
 // Beamer rule declines, which publishes the mirror `seq` for the host).
-// lazy: the LAST enqueued level also plans a next one (the host enqueues it
-// with grid_auto_next once it has seen the search hand off).
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
-               unsigned long long gate_ticks, int levels, bool lazy,
-               hipStream_t s);
-// One more device-planned level behind a grid_auto(lazy) chain: runs the plan
-// the level before left in aux (a no-op when it planned nothing), and ends
-// the chain (mirror `seq` or the result `res_seq`).
-void grid_auto_next(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
-                    dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s);
+               unsigned long long gate_ticks, int levels, hipStream_t s);
 
 }  // namespace launch
 }  // namespace bibfs

@@ -66,14 +66,10 @@ using namespace dev;
 // same vertex are always seen by at least one side: each side completes its
 // own insert (LDS CAS) before reading the other set.
 // Tuning knobs (compile-time; scripts/build_variants.sh builds A/B libraries).
-#ifndef BIBFS_KNOB_WID_UNIFORM
-#define BIBFS_KNOB_WID_UNIFORM 0
-#endif
-#ifndef BIBFS_KNOB_APPEND_BALLOT
-#define BIBFS_KNOB_APPEND_BALLOT 0
-#endif
-constexpr bool kWidUniform = BIBFS_KNOB_WID_UNIFORM;
-constexpr bool kAppendBallot = BIBFS_KNOB_APPEND_BALLOT;
+// Variants measured slower and removed from the code (results and the A/B
+// files: docs/DESIGN.md §8): a readfirstlane'd wave id, ballot-driven record
+// appends, hash-set all-wave rounds with an LDS queue (profiles/r2_wave_hash_ab.txt)
+// and 4-slot hash buckets (profiles/r4_lds_hash_bucket_ab.jsonl).
 // 1 = lockstep rounds of up to kLdsThreads frontier edges run on EVERY wave
 // with one LDS-only barrier per round (wave_rounds); 0 = the wave-0 rounds.
 #ifndef BIBFS_KNOB_WAVE_ROUNDS
@@ -92,16 +88,7 @@ constexpr bool kWaveSingle = BIBFS_KNOB_WAVE_SINGLE;
 #endif
 constexpr uint32_t kWaveB = BIBFS_KNOB_WAVE_B;
 static_assert(kWaveB == 1 || kWaveB == 2 || kWaveB == 4, "batches per wave: 1, 2 or 4");
-// 1 = the all-wave rounds also run with LDS hash visited sets (graphs above
-// 131072 vertices); 0 = bitmap graphs only.  A/B (profiles/r2_wave_hash_ab.txt):
-// 1M G(n,p) 28.9 -> 27.4 us, but 10M 110 -> 122 us -- the LDS queue costs
-// record capacity (2976 -> 1900 per buffer), so big graphs hand off to the
-// grid engine a level earlier.  Off by default.
-#ifndef BIBFS_KNOB_WAVE_HASH
-#define BIBFS_KNOB_WAVE_HASH 0
-#endif
-constexpr bool kWaveHash = BIBFS_KNOB_WAVE_HASH;
-// 1 = the all-wave rounds also run with LDS hash visited sets, but claim into
+// 1 = the all-wave rounds also run with LDS hash visited sets, claiming into
 // the GLOBAL queue and parent arrays (records carry parent ids, as in the
 // wave-0 schedule): no LDS queue, so the record buffers keep their full size
 // and the search hands off no earlier than without the all-wave rounds.  Only
@@ -213,83 +200,27 @@ __device__ __forceinline__ uint32_t hslot(uint32_t v) {
   return (v * 0x9E3779B1u) >> (32 - kHashBits);
 }
 
-// 1 = the hash sets probe buckets of 4 slots: one 16-byte LDS read per probe,
-// then one CAS into the bucket's first empty slot (a vertex lives in the
-// first bucket, in probe order, that had room when it was inserted; slots are
-// never emptied during a search, so a find stops at the first bucket with an
-// empty slot).  0 = one CAS per slot.  Linear probing near the 75% load limit
-// made a wave's claim wait for its longest probe chain (stamped: ~2.5-3.1k
-// cycles per round late in a 10M search, profiles/r4_lds_stamps_10m.txt).
-// Measured much slower: 10M LDS phase 31.9-32.2 -> 39.3 us, mean search
-// 62.6-62.9 -> 69.6-69.7 us (profiles/r4_lds_hash_bucket_ab.jsonl) -- the
-// 16-byte read and the per-slot selects cost more than the probes they save.
-// Off (0).
-#ifndef BIBFS_KNOB_HASH_BUCKET
-#define BIBFS_KNOB_HASH_BUCKET 0
-#endif
-constexpr bool kHashBucket = BIBFS_KNOB_HASH_BUCKET;
-typedef uint32_t u32x4b __attribute__((ext_vector_type(4)));
-
 // Insert vertex v with the given key (v | parity); true when v was absent.
 __device__ __forceinline__ bool hash_insert(uint32_t* H, uint32_t v, uint32_t key) {
-  if constexpr (kHashBucket) {
-    uint32_t b = hslot(v) & ~3u;
-    for (uint32_t probe = 0; probe < kHashSize / 4;) {  // bounded: the load limit keeps it short
-      const u32x4b q = *reinterpret_cast<const u32x4b*>(H + b);
-      int e = -1;
-#pragma unroll
-      for (int j = 3; j >= 0; --j) {
-        if (q[j] != kEmpty && (q[j] & kIdMask) == v) return false;
-        if (q[j] == kEmpty) e = j;
-      }
-      if (e < 0) {  // full bucket: the next one
-        b = (b + 4) & kHashMask;
-        ++probe;
-        continue;
-      }
-      const uint32_t old = atomicCAS(&H[b + (uint32_t)e], kEmpty, key);
-      if (old == kEmpty) return true;
-      if ((old & kIdMask) == v) return false;
-      // another vertex took that slot first: read the bucket again
-    }
-    return false;
-  } else {
-    uint32_t h = hslot(v);
-    for (uint32_t probe = 0; probe < kHashSize; ++probe) {  // bounded: the load limit keeps it short
-      const uint32_t old = atomicCAS(&H[h], kEmpty, key);
-      if (old == kEmpty) return true;
-      if ((old & kIdMask) == v) return false;
-      h = (h + 1) & kHashMask;
-    }
-    return false;
+  uint32_t h = hslot(v);
+  for (uint32_t probe = 0; probe < kHashSize; ++probe) {  // bounded: the load limit keeps it short
+    const uint32_t old = atomicCAS(&H[h], kEmpty, key);
+    if (old == kEmpty) return true;
+    if ((old & kIdMask) == v) return false;
+    h = (h + 1) & kHashMask;
   }
+  return false;
 }
 
 // Stored key of v (kEmpty when absent).
 __device__ __forceinline__ uint32_t hash_find(const uint32_t* H, uint32_t v) {
-  if constexpr (kHashBucket) {
-    uint32_t b = hslot(v) & ~3u;
-    for (uint32_t probe = 0; probe < kHashSize / 4; ++probe) {
-      const u32x4b q = *reinterpret_cast<const u32x4b*>(H + b);
-      bool room = false;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (q[j] != kEmpty && (q[j] & kIdMask) == v) return q[j];
-        room = room || q[j] == kEmpty;
-      }
-      if (room) return kEmpty;
-      b = (b + 4) & kHashMask;
-    }
-    return kEmpty;
-  } else {
-    uint32_t h = hslot(v);
-    for (uint32_t probe = 0; probe < kHashSize; ++probe) {
-      const uint32_t k = H[h];
-      if (k == kEmpty || (k & kIdMask) == v) return k;
-      h = (h + 1) & kHashMask;
-    }
-    return kEmpty;
+  uint32_t h = hslot(v);
+  for (uint32_t probe = 0; probe < kHashSize; ++probe) {
+    const uint32_t k = H[h];
+    if (k == kEmpty || (k & kIdMask) == v) return k;
+    h = (h + 1) & kHashMask;
   }
+  return kEmpty;
 }
 
 // ---- bitmap visited sets (graphs with n <= kBmMaxN): the hash area holds,
@@ -353,7 +284,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 
 
 // Published by wave 0 for the parked waves: the big level to run (or the end).
-// Published by wave 0 for the parked waves: the big level to run (or the end).
 // E[q] = records of side q to expand (0 = side q idle this level).
 struct LevelPlan {
   uint32_t status;
@@ -365,7 +295,7 @@ struct LevelPlan {
 template <typename OffT, bool kStamp, bool kBm>
 __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool elected) {
   using Rec = typename LdsRec<OffT>::type;
-  constexpr bool kLq = (kBm || kWaveHash) && kWaveRounds && std::is_same<OffT, uint32_t>::value;  // LDS queue + walk
+  constexpr bool kLq = kBm && kWaveRounds && std::is_same<OffT, uint32_t>::value;  // LDS queue + walk
   // all-wave rounds: with the LDS queue (kLq), or on hash sets with the global queue
   constexpr bool kWr = kLq || (kWaveHashG && !kBm && kWaveRounds && std::is_same<OffT, uint32_t>::value);
   constexpr uint32_t CAP = kLq ? kCapBm : LdsRec<OffT>::cap;
@@ -381,11 +311,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   __shared__ unsigned long long meetk[2];   // big levels [slot]: min (len << 32 | side << 31 | vertex)
   __shared__ LevelPlan plan;
   __shared__ uint32_t won;
-  __shared__ Rec junk[kWave];            // record writes of finished lanes land here (no divergence)
   __shared__ __attribute__((aligned(16))) uint32_t pub_img[64];  // hand-off DevState [0, 32) / HostResult [32, 64) images
 
   const int tid = threadIdx.x;
-  const int wid = kWidUniform ? (int)__builtin_amdgcn_readfirstlane((uint32_t)tid >> 6) : tid >> 6;
+  const int wid = tid >> 6;
   const uint32_t lane = __lane_id();
   // XCD affinity: the search is latency-bound on dependent CSR loads, so it
   // always runs on the same XCD, whose L2 keeps the graph's hot lines across
@@ -402,15 +331,9 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   uint32_t ticket_old = 0;
   if (tid == 0 && !elected) ticket_old = atomicMax(P.ticket, P.seq);
 
-  // Lane writes its vertex's dl edge records Rn[eb .. eb+dl).  The trip count
-  // is the wave's max dl (ballot-driven, scalar loop); lanes already done
-  // write their own junk slot instead of masking, so the body never diverges.
+  // Lane writes its vertex's dl edge records Rn[eb .. eb+dl) (exec-masked loop).
   auto append_records = [&](Rec* Rn, uint32_t dl, uint32_t eb, uint32_t v, OffT base) {
-    if constexpr (kAppendBallot) {
-      for (uint32_t j = 0; __ballot(j < dl); ++j) rec_set(j < dl ? Rn[eb + j] : junk[lane], v, base + j);
-    } else {
-      for (uint32_t j = 0; j < dl; ++j) rec_set(Rn[eb + j], v, base + j);
-    }
+    for (uint32_t j = 0; j < dl; ++j) rec_set(Rn[eb + j], v, base + j);
   };
   // Edge k -> (neighbour v, its row [ob, oe)): one packed load, or col[k] then
   // the row offsets (a second dependent load) when no packed adjacency exists.
@@ -2579,7 +2502,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
 
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
-               unsigned long long gate_ticks, int levels, bool lazy, hipStream_t s) {
+               unsigned long long gate_ticks, int levels, hipStream_t s) {
   // The grid size is fixed before the frontier exists: cus / 4 workgroups
   // for the first level (a 10M G(n, p) hand-off level is ~17 chunks; every
   // workgroup takes chunk tickets, and fewer blocks keep the ticket and done
@@ -2606,7 +2529,7 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
     for (int l = 0; l < std::max(1, levels); ++l) {
-      P.chain = (l + 1 < levels || lazy) ? 1 : 0;
+      P.chain = l + 1 < levels ? 1 : 0;
       k_grid_topdown<OffT, true><<<l ? cblocks : blocks, kGridThreads, 0, s>>>(P);
       if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
     }
@@ -2616,26 +2539,6 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
   HIP_CHECK(hipGetLastError());
 }
 
-void grid_auto_next(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
-                    dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s) {
-  const unsigned cblocks = (unsigned)std::max(8, cus);
-  const unsigned hblocks = (unsigned)std::max(8, cus * 4);
-  auto launch_one = [&](auto P) {
-    using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
-    P.mirror = mirror, P.seq = seq, P.trace = 0, P.h = h, P.res_seq = res_seq;
-    P.cus = (uint32_t)cus;
-    P.max_deg = max_deg;
-    P.nnz = g.nnz;
-    P.alpha = (float)alpha;
-    P.chain = 0;
-    P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
-    k_grid_topdown<OffT, true><<<cblocks, kGridThreads, 0, s>>>(P);
-    if (max_deg > 64) k_grid_hubs<OffT, true><<<hblocks, kGridThreads, 0, s>>>(P);
-  };
-  if (g.row_off32) launch_one(gp<uint32_t>(g, b, 0));
-  else launch_one(gp<uint64_t>(g, b, 0));
-  HIP_CHECK(hipGetLastError());
-}
 
 void handoff_scatter(const GraphView& g, const SearchBuffers& b, hipStream_t s) {
   if (g.n <= kBmMaxN) return;  // bitmap-mode searches copied their bitmaps themselves

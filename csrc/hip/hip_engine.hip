@@ -96,16 +96,9 @@ struct HipBiBfs::Impl {
     const int v = e ? std::atoi(e) : 1;
     return v < 1 ? 1 : (v > 8 ? 8 : v);
   }();
-  // Lazy chain (BIBFS_AUTO_LAZY=1): the auto level always plans the next one,
-  // and the host enqueues that level only once it has seen its search hand
-  // off -- so a search that stays in LDS enqueues nothing extra (what made the
-  // eager chain above lose).  Measured slower all the same: 10M 61.3 -> 64.0
-  // us mean search, the LDS phase +0.9 us and hand-off searches +3.6 us
-  // (profiles/r4_auto_lazy_ab.jsonl).  Off.
-  bool auto_lazy = [] {
-    const char* e = std::getenv("BIBFS_AUTO_LAZY");
-    return e && e[0] == '1';
-  }();
+  // (A lazy chain -- the host enqueuing the planned next level only after the
+  // search handed off -- measured slower too: 10M 61.3 -> 64.0 us mean search,
+  // profiles/r4_auto_lazy_ab.jsonl; removed.)
   bool auto_usable(const SearchOptions& opt) const {
     return auto_on && nnz > 0 && max_deg <= auto_max_deg && !opt.trace && !opt.force_grid &&
            opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
@@ -1320,19 +1313,11 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
       if (use_auto) {
         launch::grid_auto(g, I.buf, I.cus, I.max_deg, opt.alpha, I.h_state, auto_ls, hsg(), pub_auto, seq,
                           (unsigned long long)(std::max(0.0, I.auto_gate_us) * 100.0), I.auto_levels,
-                          I.auto_lazy, I.stream);
+                          I.stream);
         auto_tag = I.next_clean_tag();
         launch::cleanup(I.buf, I.n, I.d_flag + 8, I.h_clean, auto_tag, 2, I.stream);
       }
       I.server_wait(seq);
-      if (use_auto && I.auto_lazy && I.h_res->status == kHandoff) {
-        // the search left LDS: the level its auto level planned next, and the
-        // predicated cleanup behind it (the one above ran before it)
-        launch::grid_auto_next(g, I.buf, I.cus, I.max_deg, opt.alpha, I.h_state, auto_ls, hsg(), pub_auto,
-                               I.stream);
-        auto_tag = I.next_clean_tag();
-        launch::cleanup(I.buf, I.n, I.d_flag + 8, I.h_clean, auto_tag, 2, I.stream);
-      }
       if (I.dbg())
         std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",
                      I.h_res->seq, I.h_res->status, I.h_res->hops, I.h_res->levels, I.h_box->stage,

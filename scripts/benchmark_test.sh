@@ -11,13 +11,17 @@
 #
 # Differences from the reference, on purpose:
 #   * every tool runs REPEAT timed queries after WARMUP untimed ones and prints
-#     the median (the reference ran once, cold);
+#     the median (the reference ran once, cold).  The repeats are the SAME
+#     (0, N-1) pair, so caches are hot: the `timing` column says so.  MODE=cold
+#     runs each cell once with no warm-up, as the reference did
+#     (benchmark_test.sh:54); bench.py reports rotating pairs instead;
 #   * all times are seconds (the reference's v3 printed ms in a seconds column);
 #   * the hop count printed by each tool is checked against the .json ground
 #     truth (column `hops_ok`), and GTEPS(M/t) is reported next to the time.
 #
 #   scripts/benchmark_test.sh [GRAPH_DIR]            (default graphs/)
-#   TIERS="v1 v3" REPEAT=20 NP=4 NGPU=1 scripts/benchmark_test.sh
+#   TIERS="v1 v3" REPEAT=20 NP=4 V4NP=4 scripts/benchmark_test.sh
+#   MODE=cold scripts/benchmark_test.sh      (one cold run per cell, like the reference)
 #   V3_FLAGS="" scripts/benchmark_test.sh   (v3 one launch per query instead of the resident server)
 set -uo pipefail
 
@@ -26,10 +30,15 @@ GDIR="${1:-$ROOT/graphs}"
 BIN="$ROOT/build/bin"
 TIERS="${TIERS:-v1 v2 v3 v4}"
 GRAPHS="${GRAPHS:-1k 10k 50k 100k}"
+MODE="${MODE:-hot}"
+if [[ "$MODE" == cold ]]; then REPEAT=1; WARMUP=0; fi
 REPEAT="${REPEAT:-10}"
 WARMUP="${WARMUP:-2}"
+TIMING=$([[ "$MODE" == cold ]] && echo "cold x1" || echo "hot median x$REPEAT")
 NP="${NP:-4}"          # MPI ranks for the CPU tier (benchmark_test.sh:47-51 used 4)
-NGPU="${NGPU:-1}"      # ranks (one per GPU) for the multi-GPU tier
+# ranks of the multi-GPU tier: 4 like the reference's v4 rows (benchmark_test.sh:47-51);
+# with more ranks than GPUs they share them over the IPC transport (mpi_bibfs --comm auto)
+V4NP="${V4NP:-${NGPU:-4}}"
 MPIEXEC="${MPIEXEC:-$(command -v mpiexec || echo /opt/conda/bin/mpiexec)}"
 LOGDIR="${LOGDIR:-$ROOT/logs}"
 CSV="${CSV:-$ROOT/benchmark_results.csv}"
@@ -46,12 +55,12 @@ tool_cmd() {  # tier graph.bin src dst -> command line
     v1) echo "$BIN/bibfs_serial $g $s $d --repeat $REPEAT" ;;
     v2) echo "$MPIEXEC -n $NP $BIN/second_try $g $s $d --repeat $REPEAT" ;;
     v3) echo "$BIN/bibfs_hip $g $s $d --repeat $REPEAT --warmup $WARMUP ${V3_FLAGS---resident}" ;;
-    v4) echo "$MPIEXEC -n $NGPU $BIN/mpi_bibfs $g $s $d --repeat $REPEAT --warmup $WARMUP" ;;
+    v4) echo "$MPIEXEC -n $V4NP $BIN/mpi_bibfs $g $s $d --repeat $REPEAT --warmup $WARMUP" ;;
     *) return 1 ;;
   esac
 }
 
-echo "version,graph,time_sec,logfile,hops,hops_expected,hops_ok,gteps" > "$CSV"
+echo "version,graph,time_sec,logfile,hops,hops_expected,hops_ok,gteps,timing,ranks" > "$CSV"
 for tier in $TIERS; do
   mkdir -p "$LOGDIR/$tier"
   for gname in $GRAPHS; do
@@ -82,7 +91,8 @@ EOF
     exp=$(python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('none' if d.get('hop_count') is None else d['hop_count'])" "$js" 2>/dev/null || echo "?")
     ok=$([[ "$hops" == "$exp" ]] && echo yes || echo no)
     gteps=$(python3 -c "import sys; t=sys.argv[1]; print('%.4f' % (int(sys.argv[2]) / float(t) / 1e9) if t not in ('ERROR','0') and float(t) > 0 else '')" "$t" "$M" 2>/dev/null)
-    echo "$tier,$gname,$t,$log,$hops,$exp,$ok,$gteps" >> "$CSV"
+    ranks=$(case $tier in v2) echo "$NP" ;; v4) echo "$V4NP" ;; *) echo 1 ;; esac)
+    echo "$tier,$gname,$t,$log,$hops,$exp,$ok,$gteps,$TIMING,$ranks" >> "$CSV"
   done
 done
 
@@ -91,7 +101,7 @@ import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 if not rows:
     sys.exit(0)
-cols = ["version", "graph", "time_sec", "hops", "hops_ok", "gteps"]
+cols = ["version", "graph", "time_sec", "hops", "hops_ok", "gteps", "timing", "ranks"]
 w = {c: max(len(c), *(len(r[c]) for r in rows)) for c in cols}
 bar = "+" + "+".join("-" * (w[c] + 2) for c in cols) + "+"
 print(bar)

@@ -1,6 +1,7 @@
 #!/bin/bash
-# One entry point for the GPU-box sessions (replaces the per-session r3*.sh
-# scripts of round 3).  Run on the box through gpurun, e.g.
+# One entry point for the GPU-box sessions (replaces the per-session
+# r3*/r4*/r5*_session.sh scripts of rounds 3-4).  Run on the box through
+# gpurun, e.g.
 #
 #   gpurun --timeout 900 -- 'bash scripts/gpu_tasks.sh pytest smoke bench'
 #
@@ -13,15 +14,24 @@
 #   smoke    __graft_entry__.smoke()
 #   bench    driver-style bench: python bench.py --gpus 1 --steps 20 --warmup 5
 #   suite    reference suite table (C21): scripts/make_graphs + scripts/benchmark_test.sh
-#            over 1k/10k/50k/100k x v1, v2 (np 4), v3 (--resident), v4 (np 1)
+#            over 1k/10k/50k/100k x v1, v2 (np 4), v3 (--resident), v4 (np 4: ranks share the GPU over IPC)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench
 #   pmc      one SQ counter pass (rocprofv3 --pmc) over the resident 100k workload
 #   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
+#            (SPECS / RANKS / OVERLAP / QUERIES override benchmarks/dist_rounds.py's defaults)
+#   procs    partitioned engine as separate processes on the one GPU (IPC transport):
+#            tests/test_gpu_dist_proc.py
+#   pairab   A/B of one environment knob over pair latencies: ABENV=<var> ABVALS="<v1> <v2>"
+#            GRAPHS="<spec> ..." [PAIRS=64 REPS=5 ROUNDS=2]; ABLIB="<dir1> <dir2>" instead
+#            A/Bs library builds (LD_LIBRARY_PATH=build/var/<dir>, scripts/build_variants.sh)
+#   trace    rocprofv3 --kernel-trace of pair_latency over GRAPHS (per-query kernel timelines)
+#   kron     benchmarks/kron_scale.py over SCALES (default 20,22,24,26,27,28), resident server
+#   stress   benchmarks/stress_resident.py
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-TAG="${TAG:-r4}"
+TAG="${TAG:-r5}"
 T="timeout -k 10"
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 O=gpurun_out
@@ -51,7 +61,38 @@ run_task() {
         SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES -d $O/${TAG}_pmc_sq -- \
         python3 benchmarks/pmc_100k.py --mode resident > $O/${TAG}_pmc_sq.log 2>&1 ;;
     distab)
-      $T 600 python3 benchmarks/dist_rounds.py > $O/${TAG}_dist_rounds.jsonl 2> $O/${TAG}_dist_rounds.err ;;
+      $T 900 python3 benchmarks/dist_rounds.py ${SPECS:+--specs $SPECS} ${RANKS:+--ranks $RANKS} \
+        ${OVERLAP:+--overlap $OVERLAP} ${QUERIES:+--queries $QUERIES} \
+        > $O/${TAG}_dist_rounds.jsonl 2> $O/${TAG}_dist_rounds.err ;;
+    procs)
+      $T 900 $PT -m gpu tests/test_gpu_dist_proc.py > $O/${TAG}_procs.log 2>&1 ;;
+    pairab)
+      local out=$O/${TAG}_pairab.jsonl
+      for rep in $(seq 1 "${ROUNDS:-2}"); do
+        for v in ${ABVALS:-$ABLIB}; do
+          for g in $GRAPHS; do
+            if [ -n "$ABLIB" ]; then
+              LD_LIBRARY_PATH=build/var/$v $T 240 python3 benchmarks/pair_latency.py --graph "$g" \
+                --pairs "${PAIRS:-64}" --reps "${REPS:-5}" --summary "$v" >> $out 2>> $O/${TAG}_pairab.err || return 1
+            else
+              env "$ABENV=$v" $T 240 python3 benchmarks/pair_latency.py --graph "$g" \
+                --pairs "${PAIRS:-64}" --reps "${REPS:-5}" --summary "$ABENV=$v" >> $out 2>> $O/${TAG}_pairab.err || return 1
+            fi
+          done
+        done
+      done ;;
+    trace)
+      for g in ${GRAPHS:-gnp:10000000::1 kron:22:16:1}; do
+        local t; t=$(echo "$g" | tr ':' '_')
+        $T 300 rocprofv3 --kernel-trace --output-format csv -d $O/${TAG}_tr_$t -o run -- \
+          python3 benchmarks/pair_latency.py --graph "$g" --pairs 32 --reps 3 --summary trace \
+          > $O/${TAG}_tr_$t.jsonl 2> $O/${TAG}_tr_$t.err || return 1
+      done ;;
+    kron)
+      $T 900 python3 benchmarks/kron_scale.py --scales "${SCALES:-20,22,24,26,27,28}" --queries 48 --resident \
+        > $O/${TAG}_kron_scale.jsonl 2> $O/${TAG}_kron_scale.err ;;
+    stress)
+      $T 900 python3 -u benchmarks/stress_resident.py > $O/${TAG}_stress.jsonl 2> $O/${TAG}_stress.err ;;
     *)
       echo "unknown task $1" >&2; return 2 ;;
   esac

@@ -30,4 +30,13 @@ def test_make_graphs_and_harness(tmp_path, native):
         assert row["time_sec"] != "ERROR", row
         assert float(row["time_sec"]) < 1.0
         assert row["hops_ok"] == "yes", row
+        assert row["timing"] == "hot median x3", row
+        assert row["ranks"] == ("2" if row["version"] == "v2" else "1"), row
     assert "| version" in r.stdout
+    # MODE=cold: one run per cell, no warm-up, as the reference harness did
+    env.update(MODE="cold", TIERS="v1")
+    r = subprocess.run([os.path.join(ROOT, "scripts", "benchmark_test.sh"), str(tmp_path)], env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    rows = list(csv.DictReader(open(out)))
+    assert len(rows) == 2 and all(x["timing"] == "cold x1" and x["hops_ok"] == "yes" for x in rows), rows
