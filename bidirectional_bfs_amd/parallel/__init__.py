@@ -53,7 +53,7 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                 solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
                 overlap: Optional[bool] = None, spec_stall_edges: Optional[int] = None,
                 stamps: Optional[bool] = None, hbm_cap_bytes: Optional[int] = None,
-                world1_single: Optional[bool] = None) -> "native.DistTuning":
+                world1_single: Optional[bool] = None, spill_cap: Optional[int] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
 
     solo (one rank only): run the small rounds in one persistent workgroup
@@ -78,6 +78,10 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
     hbm_cap_bytes: a build that would make a rank hold more device memory
     than this throws (rehearses "does not fit one GPU" at small scale).
 
+    spill_cap (test hook, 0 = the allocation): a smaller candidate spill
+    list, so a round overflows it -- the search then raises on every rank
+    and the group keeps serving.
+
     world1_single (default on): with ONE rank the shard is the whole graph,
     so queries are answered by the single-GPU engine over the same device CSR
     (no copy); off = the partitioned rounds (solo workgroup) at world size 1."""
@@ -86,7 +90,7 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
                  ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap),
                  ("spec_stall_edges", spec_stall_edges), ("stamps", stamps), ("hbm_cap_bytes", hbm_cap_bytes),
-                 ("world1_single", world1_single)):
+                 ("world1_single", world1_single), ("spill_cap", spill_cap)):
         if v is not None:
             setattr(t, k, v)
     return t

@@ -64,7 +64,9 @@ def main(job_path: str, rank: int) -> int:
         for run in job["runs"]:  # option / tuning sets, all on the same shards
             if run.get("tuning") is not None:
                 eng.set_tuning(make_tuning(**run["tuning"]))
-            opt = make_options(**run.get("options", {}))
+            o = dict(run.get("options", {}))
+            catch = bool(o.pop("_catch", False))  # a failing query is recorded (hops -3) and the run goes on
+            opt = make_options(**o)
             res, stats, valid, uni, qms = [], [], [], [], []
             for qi, (s, d) in enumerate(job["queries"]):
                 if s >= eng.n or d >= eng.n:  # fails on every rank before any collective
@@ -76,7 +78,15 @@ def main(job_path: str, rank: int) -> int:
                         continue
                     raise RuntimeError("an out-of-range query did not raise")
                 q0 = time.perf_counter()
-                r = eng.search(int(s), int(d), opt)
+                try:
+                    r = eng.search(int(s), int(d), opt)
+                except Exception as e:  # noqa: BLE001
+                    if not catch:
+                        raise
+                    res.append({"hops": -3, "found": False, "path": [], "stats": {}, "total_ms": 0.0,
+                                "error": str(e)})
+                    stats.append({})
+                    continue
                 qms.append((time.perf_counter() - q0) * 1e3)
                 res.append(_result(r))
                 stats.append(eng.last_stats)

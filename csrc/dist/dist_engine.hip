@@ -410,7 +410,8 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
         mode = 2;
       } else {
         // Beamer: m_f > m_u / alpha and n_f < n / beta, multiplied out, in
-        // 1/256 fixed point (fed < 2^40, alpha_q < 2^20: no overflow)
+        // 1/256 fixed point (fed, m_u < 2^40 and alpha_q, beta_q <= 2^20 --
+        // alpha and beta clamped to [0, 4096] by policy(): no u64 overflow)
         const unsigned long long m_u = pol.nnz_total > c.ved[s] ? pol.nnz_total - c.ved[s] : 0ull;
         if (c.dir[s] == 1 && c.fed[s] * pol.alpha_q > m_u * 256ull) c.dir[s] = 2;
         else if (c.dir[s] == 2 && c.cnt[s] * pol.beta_q < (unsigned long long)pol.n * 256ull) c.dir[s] = 1;
@@ -2495,6 +2496,13 @@ int gpu_count() {
   return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
+// An error every rank raises at the same point of the same search (decided
+// from reduced values), with no collective outstanding: it does not abort
+// the communicator, and the next search runs normally.
+struct ConsistentError : Error {
+  using Error::Error;
+};
+
 struct DistBiBfs::Impl {
   int rank = 0, size = 1, device = 0, cus = 256;
   hipStream_t stream = nullptr;   // compute: pre phases of host-planned rounds, graph build
@@ -2553,6 +2561,7 @@ struct DistBiBfs::Impl {
     single = std::make_unique<HipBiBfs>(device);
     single->adopt_device_csr(n, nnz, m_input, d_row_off, d_col);
     single->set_resident(true);
+    check_single_cap();
   }
   int fault_at = 0, fault_mode = 0;
 
@@ -2739,25 +2748,33 @@ struct DistBiBfs::Impl {
   // Largest degree of the whole graph (max over the shards).  No vertex above
   // kHubDeg: no hub is ever deferred, so no speculative round launches the hub pass.
   uint64_t max_deg = 0;
+  // One rank owns every row: the packed adjacency of the single-GPU engine
+  // (16 B per edge) within BIBFS_PADJ_MAX_MB (default 4096 MiB, 0 = off).
+  // G(1M) world-1 query 0.108 -> 0.103 ms (profiles/r3_dist_padj_ab.jsonl).
+  bool padj_tried = false;
+  void ensure_padj() {
+    if (padj_tried) return;
+    padj_tried = true;
+    if (!(size == 1 && lo == 0 && nnz)) return;
+    const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
+    const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
+    if (nnz * 16 > budget) return;
+    devmem::Scope scope(&mem);
+    devmem::alloc(&d_padj, nnz * 16);
+    padj_bytes = nnz * 16;
+    launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
+    HIP_CHECK(hipStreamSynchronize(stream));
+    V.padj = d_padj;
+  }
   void finish_build() {
     devmem::Scope scope(&mem);
     alloc_state();
-    // One rank owns every row: the packed adjacency of the single-GPU engine
-    // (16 B per edge) within BIBFS_PADJ_MAX_MB (default 4096 MiB, 0 = off).
-    // G(1M) world-1 query 0.108 -> 0.103 ms (profiles/r3_dist_padj_ab.jsonl).
     V.padj = nullptr;
-    if (size == 1 && lo == 0 && nnz) {
-      const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
-      const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
-      if (nnz * 16 <= budget) {
-        devmem::Scope scope(&mem);
-        devmem::alloc(&d_padj, nnz * 16);
-        padj_bytes = nnz * 16;
-        launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
-        HIP_CHECK(hipStreamSynchronize(stream));
-        V.padj = d_padj;
-      }
-    }
+    padj_tried = false;
+    // world1_single serves the queries from the single-GPU engine, which
+    // builds its own packed adjacency: the rounds' one is made only if the
+    // partitioned rounds ever run at world size 1 (no duplicate)
+    if (!(size == 1 && tune.world1_single)) ensure_padj();
     double y = (double)launch::max_degree(d_row_off, hi - lo, stream);
     if (size > 1) {
       HIP_CHECK(hipMemcpyAsync(d_scalar, &y, 8, hipMemcpyHostToDevice, cstream));
@@ -2767,6 +2784,17 @@ struct DistBiBfs::Impl {
     }
     max_deg = (uint64_t)y;
     if (size == 1 && tune.world1_single) ensure_single();
+  }
+  // The adopted single-GPU engine allocates outside devmem (its own arrays;
+  // the CSR is this rank's): hold DistTuning::hbm_cap_bytes against
+  // everything this rank holds once it exists.
+  void check_single_cap() {
+    if (!single || !mem.cap) return;
+    const size_t all = single->device_bytes(), csr = row_off_bytes() + col_bytes();
+    const size_t held = mem.cur + (all > csr ? all - csr : 0);
+    if (held > mem.cap)
+      throw Error("dist: HBM cap exceeded: this rank would hold " + std::to_string(held) + " bytes with the " +
+                  "single-GPU engine's arrays (cap " + std::to_string(mem.cap) + ")");
   }
   // Measured, not a formula: the most this rank held at once while its CSR
   // shard was built (generator / scan temporaries included), and the
@@ -2904,8 +2932,13 @@ struct DistBiBfs::Impl {
     Policy p;
     p.alpha = opt.alpha;
     p.beta = opt.beta;
+    // alpha / beta in 1/256 fixed point, clamped to [0, 4096] (the device
+    // products above stay below 2^60).  The single-GPU engine compares in
+    // floating point: an alpha or beta that is not a multiple of 1/256 can
+    // flip a borderline direction decision between the two engines (never the
+    // hop count -- both directions find the same levels).
     auto q8 = [](double x) {
-      return (unsigned long long)std::llround(std::min(std::max(x, 0.0), (double)(1u << 20)) * 256.0);
+      return (unsigned long long)std::llround(std::min(std::max(x, 0.0), 4096.0) * 256.0);
     };
     p.alpha_q = q8(opt.alpha);
     p.beta_q = q8(opt.beta);
@@ -3103,8 +3136,10 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   }
   const int P = size;
   hipStream_t cs = cstream;
+  if (P == 1) ensure_padj();  // (the partitioned rounds at world size 1: built on first use)
   ++epoch;
   const Policy pol = policy(opt);
+  V.spill_cap = size > 1 ? (tune.spill_cap ? std::min(block_cap, tune.spill_cap) : block_cap) : 1;
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
   V.rstamp = tune.stamps ? d_rstamp : nullptr;
@@ -3308,8 +3343,10 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   }
   const Ctl h = *h_ctl;
   if (h.lost) {
+    // every rank decided `lost` from the same reduced values, so every rank
+    // throws here, after the same collectives: the communicator stays usable
     cleanup_enqueue(h);
-    throw Error("dist: a rank's candidate spill list overflowed (" + std::to_string(V.spill_cap) +
+    throw ConsistentError("dist: a rank's candidate spill list overflowed (" + std::to_string(V.spill_cap) +
                 " pairs): candidates were dropped, the search result would not be exact");
   }
   stats.rounds = (int)h.rounds;
@@ -3404,13 +3441,15 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   if (lds > 160 * 1024) return false;
   const uint32_t meet = (uint32_t)(key & 0xffffffffull), hops = (uint32_t)(key >> 32);
   hipStream_t cs = cstream;
+  // sized before the collective (every rank knows `hops`): a failing
+  // allocation aborts the communicator before, not between, collectives
+  ensure_path_dev((size_t)hops + 5);
   k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(V, capS, capT);
   const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
   comm->allgather(V.sendbuf, V.recvbuf, blk * 4, cs);
   stats.collectives++;
   stats.path_collectives++;
   stats.exchanged_bytes += blk * 4 * size;
-  ensure_path_dev((size_t)hops + 5);
   k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, d_walk);
   HIP_CHECK(hipGetLastError());
   const size_t words = 4 + (size_t)hops + 1;
@@ -3439,6 +3478,7 @@ void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult&
   TraceRange range("dist:path_per_hop");
   hipStream_t cs = cstream;
   const uint32_t meet = (uint32_t)(key & 0xffffffffull);
+  ensure_path_dev((size_t)std::max<int64_t>(r.hops, 0) + 1);  // (K <= hops; sized before any collective)
   k_meet_depth<<<1, 64, 0, cs>>>(V, meet, it);
   comm->allreduce(V.red[it & 1].md, 2, DType::kU32, ROp::kMin, cs);
   stats.collectives++;
@@ -3448,7 +3488,6 @@ void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult&
   const int dS = (int)h_red->md[0], dT = (int)h_red->md[1];
   BIBFS_REQUIRE((int64_t)dS + dT == r.hops, "dist: meet depths disagree with the path length");
   const int K = std::max(dS, dT);
-  ensure_path_dev((size_t)K + 1);
   const uint32_t init[2] = {meet, meet};
   HIP_CHECK(hipMemcpyAsync(d_cur, init, 8, hipMemcpyHostToDevice, cs));
   for (int i = 0; i <= K; ++i) {
@@ -3594,6 +3633,8 @@ SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   BIBFS_REQUIRE(src < I.n && dst < I.n, "src/dst out of range");
   try {
     return I.search(src, dst, opt);
+  } catch (const ConsistentError&) {
+    throw;  // every rank raised it at the same point: no peer is left in a collective
   } catch (...) {
     // A rank that fails mid-search would leave its peers blocked in a
     // collective forever: tear the communicator down so they return too.

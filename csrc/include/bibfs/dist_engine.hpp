@@ -108,6 +108,8 @@ struct DistTuning {
   bool world1_single = true;       // one rank: answer queries with the single-GPU engine over this rank's device
                                    // CSR (the whole graph; no copy), resident server included; false = the
                                    // partitioned rounds (solo workgroup + speculative rounds) at world size 1 too
+  uint32_t spill_cap = 0;          // test hook: > 0 caps the candidate spill lists below their allocation
+                                   // (a spill overflow then fails the search on every rank; the group lives on)
   bool stamps = false;             // per-round device stamps -> DistLevelStats::{expand,claim,exchange,status}_us
                                    // (adds one host wait + a copy per search: diagnostics, not serving)
 };

@@ -391,6 +391,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("overlap", &DistTuning::overlap)
       .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges)
       .def_readwrite("stamps", &DistTuning::stamps)
+      .def_readwrite("spill_cap", &DistTuning::spill_cap)
       .def_readwrite("hbm_cap_bytes", &DistTuning::hbm_cap_bytes)
       .def_readwrite("world1_single", &DistTuning::world1_single);
   py::class_<DistLocalFault>(m, "DistLocalFault")

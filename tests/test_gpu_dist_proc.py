@@ -189,3 +189,19 @@ def test_torchrun_ranks_share_one_gpu_over_ipc(repo_root):
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["world"] == 3 and d["backend"] == "ipc" and d["checked"] > 0 and d["bad_total"] == 0, d
+
+
+def test_spill_overflow_fails_every_rank_and_group_keeps_serving():
+    """A candidate spill list shrunk below what a round offers: the
+    search raises on EVERY rank at the same point (no rank left in a
+    collective, the communicator is not aborted), and the same processes then
+    answer the queries exactly with the default sizing."""
+    g = bb.from_spec("gnp:20000::6")
+    qs = _pairs(g.n, 6, 71)
+    got, outs = dist_proc_matrix(3, g, qs, [({"_catch": True}, {"owner_cap": 2, "spill_cap": 1}),
+                                            ({}, {"owner_cap": 0, "spill_cap": 0})])
+    failed = [r for r in outs[0]["runs"][0]["results"] if r["hops"] == -3]
+    assert failed and all("spill list overflowed" in r["error"] for r in failed), outs[0]["runs"][0]["results"]
+    for o in outs[1:]:  # every rank failed the same queries
+        assert [r["hops"] for r in o["runs"][0]["results"]] == [r["hops"] for r in outs[0]["runs"][0]["results"]]
+    _check(g, qs, got[1][0])
