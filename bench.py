@@ -87,8 +87,10 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu-ref", action="store_true", help="skip the CPU serial comparison")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for the bench's own barriers/reductions (nccl = RCCL; "
-                         "gloo lets several ranks share one GPU for rehearsals; the partitioned engine "
-                         "needs one GPU per rank and runs only with nccl)")
+                         "gloo lets several ranks share one GPU for rehearsals)")
+    ap.add_argument("--dist-comm", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="collective transport of the partitioned engine: rccl (one rank per GPU), ipc "
+                         "(HIP-IPC staging buffers; ranks may share a GPU), auto = ipc when ranks share a GPU")
     return ap.parse_args(argv)
 
 
@@ -193,7 +195,8 @@ def pick_pairs(eng, n: int, count: int, seed: int):
     return pairs
 
 
-def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks=None) -> dict:
+def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks=None,
+           comm_init_ms=None) -> dict:
     """The one JSON line rank 0 prints (driver contract)."""
     part = a.mode == "partitioned"
     return {
@@ -234,6 +237,8 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks
             "strong_scaling": "partitioned: one query = one collective search over all GPUs (RCCL over xGMI)",
             "extra": extra,
             "partitioned": partitioned,
+            # the partitioned engine's communicator, made once for every config
+            "partitioned_comm_init_ms": round(comm_init_ms, 3) if comm_init_ms is not None else None,
             # secondary configs that failed, were unverified or hit the watchdog
             "secondary_errors": sorted(
                 k for d in (extra, partitioned) for k, v in d.items()
@@ -255,15 +260,23 @@ def exit_status(partitioned: dict, failed: bool, strict: bool) -> int:
     return 4 if (failed and strict) else 0
 
 
-def cpu_serial_ms(spec: str, pairs, reps: int = 20):
+def cpu_serial_ms(spec: str, pairs, reps: int = 20, oracle_pairs: int = 0):
     """This repo's -O3 serial engine (v1 parity) on the same graph and pairs:
     (median engine-internal search ms, mean of it, mean end-to-end query ms
-    through the same Python call + path access as the GPU loop)."""
+    through the same Python call + path access as the GPU loop, pairs whose
+    GPU hop count a unidirectional host BFS (bfs_oracle) re-derived).  Every
+    pair's hop count is also held to the serial engine's."""
     from bidirectional_bfs_amd import native
 
     kind, n, arg, seed = parse_spec(spec)
     el = native.gen_gnp(n, arg, seed) if kind == "gnp" else native.gen_rmat(n, int(arg), seed, 0.57, 0.19, 0.19)
-    eng = native.SerialBiBfs(native.build_csr(el))
+    csr = native.build_csr(el)
+    del el
+    oracle_ok = 0
+    for s, d, h in pairs[:oracle_pairs]:
+        assert native.bfs_oracle(csr, s, d).hops == h, (spec, s, d, h)
+        oracle_ok += 1
+    eng = native.SerialBiBfs(csr)
     ts = []
     q = reps * len(pairs)
     for i in range(q):
@@ -279,7 +292,15 @@ def cpu_serial_ms(spec: str, pairs, reps: int = 20):
         assert hh == h and len(path) == h + 1 and path[0] == s and path[-1] == d
     e2e = (time.perf_counter() - t0) * 1e3 / q
     ts.sort()
-    return ts[len(ts) // 2], sum(ts) / len(ts), e2e
+    return ts[len(ts) // 2], sum(ts) / len(ts), e2e, oracle_ok
+
+
+def cpu_fields(med: float, mean: float, e2e: float, oracle_ok: int, gpu_ms: float) -> dict:
+    """The CPU comparison of one replicated config (same graph, same pairs)."""
+    return {"cpu_serial_ms": round(med, 6), "cpu_serial_mean_ms": round(mean, 6),
+            "cpu_serial_query_ms": round(e2e, 6),
+            "speedup_vs_cpu_serial_query": round(e2e / gpu_ms, 3) if gpu_ms else None,
+            "cpu_oracle_checked_pairs": oracle_ok}
 
 
 def main(argv=None) -> int:
@@ -451,16 +472,30 @@ def main(argv=None) -> int:
         }
         eng.release()  # free HBM before the next config
         if cpu_ref and not a.no_cpu_ref:
-            med, mean, e2e = cpu_serial_ms(spec, pairs)
-            out["cpu_serial_ms"] = round(med, 6)
-            out["cpu_serial_mean_ms"] = round(mean, 6)
-            out["cpu_serial_query_ms"] = round(e2e, 6)
+            # headline: 20 passes over the pairs; extras (10M, Kronecker): 3,
+            # plus a unidirectional host BFS of their first 4 pairs
+            big = n > 1000000 or m > 10000000
+            out.update(cpu_fields(*cpu_serial_ms(spec, pairs, reps=3 if big else 20, oracle_pairs=4 if big else 0),
+                                  out["ms_per_step"]))
         return out
 
+    comm = a.dist_comm if a.dist_comm != "auto" else ("ipc" if shared_gpu else "rccl")
+    dstate = {}
+
     def dist_engine():
-        if world == 1:
-            return DistEngine(0, 1, local, DistEngine.unique_id())
-        return DistEngine.from_torch_distributed(local)
+        """ONE partitioned engine (one communicator) for every config: its
+        bootstrap -- the first RCCL communicator of the process pays ~3.5 s of
+        library / kernel loading -- is reported once (partitioned_comm_init_ms),
+        not inside the first config; release() frees a config's graph."""
+        if "eng" not in dstate:
+            barrier()
+            t0 = time.perf_counter()
+            if world == 1:
+                dstate["eng"] = DistEngine(0, 1, local, DistEngine.unique_id(comm), comm)
+            else:
+                dstate["eng"] = DistEngine.from_torch_distributed(local, backend=comm)
+            dstate["init_ms"] = max_over_ranks((time.perf_counter() - t0) * 1e3)
+        return dstate["eng"]
 
     def run_partitioned(spec: str, steps: int, warmup: int):
         """Strong scaling: the graph sharded over all ranks, one collective search per query.
@@ -497,9 +532,8 @@ def main(argv=None) -> int:
                              f"({hbm_total / 1e9:.0f} GB): there is no single-GPU run to compare with")
         torch.cuda.synchronize()
         barrier()
-        t0 = time.perf_counter()
-        eng = dist_engine()  # RCCL communicator bootstrap (reported apart from the graph build)
-        comm_init_ms = max_over_ranks((time.perf_counter() - t0) * 1e3)
+        eng = dist_engine()  # (communicator made once, reported apart from every graph build)
+        eng.set_tuning()
         t0 = time.perf_counter()
         generate(eng, spec)
         build_ms = max_over_ranks((time.perf_counter() - t0) * 1e3)
@@ -512,41 +546,54 @@ def main(argv=None) -> int:
         wrong = []
 
         def query(i):
+            # statistics passes: the full SearchResult (stats read after it)
             s, d, h = pairs[i % len(pairs)]
             r = eng.search(s, d)
             if not (r.found and r.hops == h and len(r.path) == h + 1 and r.path[0] == s and r.path[-1] == d):
                 wrong.append((s, d, h, r.hops))
             return r
 
+        def lean(i):
+            # timed loops: the serving call, (hops, path) -- the same shape as the
+            # single-GPU reference loop above; stats are read outside the timing
+            s, d, h = pairs[i % len(pairs)]
+            hh, path = eng.query(s, d)
+            if not (hh == h and len(path) == h + 1 and path[0] == s and path[-1] == d):
+                wrong.append((s, d, h, hh))
+
         for i in range(warmup):
-            query(i)
+            lean(i)
         # the engine's own barrier (RCCL allreduce + its streams drained); no
         # device-wide synchronize: at world size 1 the single-GPU engine's
         # resident server stays up across it, as in the headline loop
         eng.barrier()
         if world > 1:
             dist.barrier()
-        done = []
         qt = []
         t0 = time.perf_counter()
         for i in range(steps):
             q0 = time.perf_counter()
-            done.append((query(warmup + i), eng.last_stats))
+            lean(warmup + i)
             qt.append(time.perf_counter() - q0)
         eng.barrier()
         dt = max_over_ranks(time.perf_counter() - t0)
+        # the same queries again, untimed, for the per-query statistics
+        done = []
+        for i in range(steps):
+            done.append((query(warmup + i), eng.last_stats))
         ok = all_ranks_ok(not wrong)
         st = [s for _, s in done]
         rounds = sum(s["rounds"] for s in st) / steps
         out = {
             "engine": f"DistBiBfs/{eng.backend}", "ranks": world, "rccl_ranks": eng.world,
-            "n": n, "m": m, "seed": seed, "comm_init_ms": round(comm_init_ms, 3), "build_ms": round(build_ms, 3),
+            "n": n, "m": m, "seed": seed, "build_ms": round(build_ms, 3),
             "local_nnz_max": int(max_over_ranks(float(eng.local_nnz))),
             "csr_bytes_total": csr_bytes(spec), "hbm_bytes_per_gpu": int(hbm_total), "fits_one_gpu": fits,
             # per-rank HBM, measured: the CSR shard; the most the rank held at
-            # once during the build (shard + generator temporaries + search
-            # state, counted per allocation) and the device's free-memory drop
-            # over it (hipMemGetInfo low-water mark); what it holds for search
+            # once during the build (shard + generator temporaries, counted per
+            # allocation -- build only, before the search state exists) and the
+            # device's free-memory drop over it (hipMemGetInfo low-water mark);
+            # what it holds for search (shard + search state)
             "shard_bytes_max": int(max_over_ranks(float(eng.shard_bytes))),
             "gen_peak_bytes_max": int(max_over_ranks(float(eng.gen_peak_bytes))),
             "gen_hbm_peak_bytes_max": int(max_over_ranks(float(eng.gen_hbm_peak_bytes))),
@@ -578,11 +625,11 @@ def main(argv=None) -> int:
             # rounds), side by side with the default single-engine path
             eng.set_tuning(world1_single=False)
             for i in range(3):
-                query(i)
+                lean(i)
             eng.barrier()
             t1 = time.perf_counter()
             for i in range(steps):
-                query(warmup + i)
+                lean(warmup + i)
             eng.barrier()
             out["rounds_engine_ms_per_query"] = round((time.perf_counter() - t1) * 1e3 / steps, 5)
             eng.set_tuning()
@@ -602,6 +649,10 @@ def main(argv=None) -> int:
         out["verification"] = {
             "pairs_from": "single-GPU engine" if fits else "partitioned engine",
             "hops_vs_single_gpu": fits,
+            # hop counts held to an independent engine: every timed pair when the
+            # single-GPU engine picked them, else only the unidirectional BFS pairs
+            # (the timed loop's check is then self-consistency: ADVICE r4)
+            "hops_cross_checked": (steps + warmup) if fits else min(nchk, 3),
             "paths_checked_distributed": nchk, "bad_paths": bad_paths,
             "unidirectional_bfs_checked": min(nchk, 3), "bad_hops": bad_hops}
         out["verified"] = ok and dist_ok
@@ -614,12 +665,12 @@ def main(argv=None) -> int:
             # overlapping side 1's expansion), side by side with the default
             eng.set_tuning(overlap=True)
             for i in range(2):
-                query(i)
+                lean(i)
             eng.barrier()
             barrier()
             t1 = time.perf_counter()
             for i in range(steps):
-                query(warmup + i)
+                lean(warmup + i)
             eng.barrier()
             dto = max_over_ranks(time.perf_counter() - t1)
             ov = {"ms_per_query": round(dto * 1e3 / steps, 5),
@@ -632,6 +683,7 @@ def main(argv=None) -> int:
             out["overlap_on"] = None  # one rank: nothing is exchanged, nothing to overlap
         if wrong:
             out["mismatch"] = wrong[:4]
+        out["comm"] = eng.backend
         eng.release()
         return out, eng.world
 
@@ -670,7 +722,8 @@ def main(argv=None) -> int:
 
     def emit():
         if rank == 0 and printed.acquire(blocking=False):
-            print(json.dumps(report(a, world, head, extra, partitioned, state["rccl_ranks"])), flush=True)
+            print(json.dumps(report(a, world, head, extra, partitioned, state["rccl_ranks"],
+                                    state.get("comm_init_ms"))), flush=True)
 
     def watchdog():
         # A secondary config that hangs (e.g. a collective that never completes
@@ -697,7 +750,7 @@ def main(argv=None) -> int:
         except Exception as exc:  # report, never hide, a failing secondary config
             extra[spec] = {"error": repr(exc)}
             failed = True
-    if a.mode == "replicated" and (world == 1 or (a.dist_backend == "nccl" and not shared_gpu)):
+    if a.mode == "replicated" and (world == 1 or comm == "ipc" or (a.dist_backend == "nccl" and not shared_gpu)):
         for spec in filter(None, a.dist_graphs.split(",")):
             spec = world_scaled(spec, world, torch.cuda.mem_get_info(dev)[1])
             partitioned[spec] = None
@@ -708,6 +761,7 @@ def main(argv=None) -> int:
             except Exception as exc:
                 partitioned[spec] = {"error": repr(exc)}
                 failed = True
+    state["comm_init_ms"] = dstate.get("init_ms")
 
     emit()
     if world > 1:

@@ -108,12 +108,45 @@ def test_reporting_hygiene_fields_and_exit_status():
     server fallbacks; a partitioned entry reports communicator bootstrap
     apart from the graph build; wrong answers always fail the run."""
     head = dict(_head(), tiny_overflows=3)
-    part = {"gnp:1000000::2": {"verified": True, "comm_init_ms": 3650.0, "build_ms": 70.0}}
-    out = bench.report(_args(), 1, head, {}, part)
+    part = {"gnp:1000000::2": {"verified": True, "build_ms": 70.0}}
+    out = bench.report(_args(), 1, head, {}, part, comm_init_ms=3650.0)
     assert out["detail"]["tiny_overflows"] == 3
     p = out["detail"]["partitioned"]["gnp:1000000::2"]
-    assert "comm_init_ms" in p and "build_ms" in p
+    assert "build_ms" in p
+    # one communicator for every partitioned config, its bootstrap reported once
+    assert out["detail"]["partitioned_comm_init_ms"] == 3650.0
     assert bench.exit_status(part, False, False) == 0
     assert bench.exit_status({"x": {"verified": False}}, False, False) == 5
     assert bench.exit_status({"x": {"error": "timeout"}}, True, False) == 0
     assert bench.exit_status({"x": {"error": "timeout"}}, True, True) == 4
+
+
+def test_cpu_comparison_fields_for_every_replicated_config():
+    """Round-5 fields: every replicated config (headline and extras) carries
+    the serial CPU engine's time on the SAME graph and pairs, the speedup over
+    it, and how many of its pairs a unidirectional host BFS re-derived."""
+    f = bench.cpu_fields(0.9, 1.0, 1.2, 4, 0.06)
+    assert f == {"cpu_serial_ms": 0.9, "cpu_serial_mean_ms": 1.0, "cpu_serial_query_ms": 1.2,
+                 "speedup_vs_cpu_serial_query": 20.0, "cpu_oracle_checked_pairs": 4}
+    extra = {"gnp:10000000::1": dict({"ms_per_step": 0.06}, **f)}
+    out = bench.report(_args(), 1, _head(), extra, {})
+    e = out["detail"]["extra"]["gnp:10000000::1"]
+    assert e["cpu_serial_query_ms"] == 1.2 and e["cpu_oracle_checked_pairs"] == 4
+
+
+def test_cpu_serial_reference_on_small_graph():
+    """cpu_serial_ms runs the serial engine on the bench's graph and pairs and
+    holds every hop count to it (and the first pairs to bfs_oracle)."""
+    from bidirectional_bfs_amd import native
+
+    spec = "gnp:20000::4"
+    kind, n, p, seed = bench.parse_spec(spec)
+    csr = native.build_csr(native.gen_gnp(n, p, seed))
+    eng = native.SerialBiBfs(csr)
+    pairs = []
+    for s, d in [(0, n - 1), (5, 77), (100, 9000), (3, 19999)]:
+        r = eng.search(s, d)
+        if r.found and r.hops > 0:
+            pairs.append((s, d, int(r.hops)))
+    med, mean, e2e, ok = bench.cpu_serial_ms(spec, pairs, reps=2, oracle_pairs=2)
+    assert med > 0 and mean > 0 and e2e > 0 and ok == min(2, len(pairs))
