@@ -27,7 +27,8 @@ def main(job_path: str, rank: int) -> int:
     out_path = os.path.join(job["out_dir"], f"rank{rank}.json")
     out = {"rank": rank, "pid": os.getpid()}
     try:
-        import torch  # noqa: F401  (binds the HIP runtime first, as every GPU test does)
+        if os.environ.get("BIBFS_PROC_TORCH", "1") != "0":
+            import torch  # noqa: F401  (binds the HIP runtime first, as every GPU test does)
 
         from .. import native
         from ..ops import make_options

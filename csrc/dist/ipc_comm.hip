@@ -363,7 +363,9 @@ class IpcComm final : public Comm {
     // The old buffer may still be mapped by peers until they see the new
     // generation (at this collective); it is freed after the next rendezvous.
     if (stage_[slot]) retired_.push_back({stage_[slot], seq_ + 1});
-    size_t cap = 4096;
+    // >= 2 MiB: a small hipMalloc can be a sub-allocation of a larger block,
+    // whose IPC handle some runtimes (torch's bundled HIP 7.0) refuse to open
+    size_t cap = 2u << 20;
     while (cap < bytes) cap <<= 1;
     HIP_CHECK(hipMalloc(&stage_[slot], cap));
     IpcRankSlot& me = shm_->r[rank_];
@@ -430,7 +432,13 @@ class IpcComm final : public Comm {
         if (p.ptr) HIP_CHECK(hipIpcCloseMemHandle(p.ptr));
         p.ptr = nullptr;
         hipIpcMemHandle_t h = ps.handle[slot];
-        HIP_CHECK(hipIpcOpenMemHandle(&p.ptr, h, hipIpcMemLazyEnablePeerAccess));
+        const hipError_t e = hipIpcOpenMemHandle(&p.ptr, h, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess) {
+          p.ptr = nullptr;
+          throw Error(std::string("ipc comm: rank ") + std::to_string(rank_) + " cannot map rank " +
+                      std::to_string(r) + "'s staging buffer (device " + std::to_string(ps.device) +
+                      "): hipIpcOpenMemHandle: " + hipGetErrorString(e));
+        }
         p.gen = ps.gen[slot];
       }
       src.p[r] = static_cast<const unsigned char*>(p.ptr);

@@ -196,7 +196,7 @@ def test_spill_overflow_fails_every_rank_and_group_keeps_serving():
     search raises on EVERY rank at the same point (no rank left in a
     collective, the communicator is not aborted), and the same processes then
     answer the queries exactly with the default sizing."""
-    g = bb.from_spec("gnp:20000::6")
+    g = bb.from_spec("rmat:16384:262144:3")  # dense: many candidates per owner and round
     qs = _pairs(g.n, 6, 71)
     got, outs = dist_proc_matrix(3, g, qs, [({"_catch": True}, {"owner_cap": 2, "spill_cap": 1}),
                                             ({}, {"owner_cap": 0, "spill_cap": 0})])
