@@ -20,6 +20,11 @@ share the GPU's CUs, so kernel times are an upper bound for one rank per
 GPU; the exchange column is the local group's copies, not xGMI.
 
     python benchmarks/dist_rounds.py --specs gnp:1000000::2,kron:22 --ranks 1,2,4 --overlap 0,1
+
+--procs runs the ranks as separate PROCESSES over the HIP-IPC transport
+(csrc/dist/ipc_comm.hip, parallel.dist_proc_matrix) instead of threads of one
+process: every collective is then a host rendezvous between processes plus a
+pull kernel, the cost a round pays between processes on one GPU.
 """
 import argparse
 import json
@@ -31,7 +36,7 @@ import torch  # noqa: F401  (binds the HIP runtime first)
 
 sys.path.insert(0, __file__.rsplit("/benchmarks/", 1)[0])
 from bidirectional_bfs_amd.models import parse_spec  # noqa: E402
-from bidirectional_bfs_amd.parallel import dist_local_generate_run, make_tuning  # noqa: E402
+from bidirectional_bfs_amd.parallel import dist_local_generate_run, dist_proc_matrix, make_tuning  # noqa: E402
 
 
 def per_round(stats, key):
@@ -47,6 +52,7 @@ def main():
     ap.add_argument("--queries", type=int, default=24)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--solo", type=int, default=1, help="P = 1: 0 runs the multi-workgroup rounds (stampable)")
+    ap.add_argument("--procs", action="store_true", help="ranks as processes over the IPC transport")
     a = ap.parse_args()
     for spec in a.specs.split(","):
         _, n, _, _ = parse_spec(spec)
@@ -56,12 +62,19 @@ def main():
             for ov in [int(x) for x in a.overlap.split(",")]:
                 if ov and ranks == 1:
                     continue
-                tun = make_tuning(stamps=True, overlap=bool(ov), solo=bool(a.solo))
-                rs, t = dist_local_generate_run(ranks, spec, qs, tuning=tun)
+                if a.procs:
+                    tk = {"stamps": True, "overlap": bool(ov), "solo": bool(a.solo)}
+                    got, _ = dist_proc_matrix(ranks, spec, qs, [({}, tk)])
+                    rs, st0, run = got[0]
+                    t = {"query_ms": run["query_ms"], "stats": st0}
+                else:
+                    tun = make_tuning(stamps=True, overlap=bool(ov), solo=bool(a.solo))
+                    rs, t = dist_local_generate_run(ranks, spec, qs, tuning=tun)
                 keep = [(r, ms, st) for r, ms, st in zip(rs, t["query_ms"], t["stats"]) if r.found and r.hops > 0]
                 sts = [st for _, _, st in keep]
                 rec = {
                     "spec": spec, "ranks": ranks, "overlap": bool(ov), "queries": len(keep),
+                    "transport": "ipc-processes" if a.procs else "local-threads",
                     "median_query_ms": round(statistics.median(ms for _, ms, _ in keep), 4) if keep else None,
                     "mean_rounds": round(statistics.mean(st["rounds"] for st in sts), 2) if sts else None,
                     "mean_stamped_rounds": round(statistics.mean(st["stamped_rounds"] for st in sts), 2) if sts else None,
