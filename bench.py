@@ -746,7 +746,7 @@ def main(argv=None) -> int:
     for spec in filter(None, a.extra_graph.split(",")):
         extra[spec] = None
         try:
-            extra[spec] = run_replicated(spec, a.extra_steps, min(a.warmup, 10))
+            extra[spec] = run_replicated(spec, a.extra_steps, min(a.warmup, 10), cpu_ref=True)
         except Exception as exc:  # report, never hide, a failing secondary config
             extra[spec] = {"error": repr(exc)}
             failed = True

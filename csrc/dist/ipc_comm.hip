@@ -17,9 +17,10 @@
 // reduces them element-wise (allreduce).  Nothing goes through host memory.
 //
 // Control plane: a POSIX shared-memory segment (name = the group's unique id)
-// with one cache line per rank.  A collective is: stage, host-wait for the
-// caller's stream to reach the staged copy, publish "arrived at collective k",
-// wait until every rank arrived at k, launch the pull kernel.  The device
+// with one cache line per rank.  A collective is: stage (one kernel that
+// copies and then writes the collective's tag into pinned host memory),
+// host-spin on that tag, publish "arrived at collective k", wait until every
+// rank arrived at k, launch the pull kernel.  The device
 // never spins on another process's work (a waiting rank is a host thread).
 // The ping-pong slot makes one rendezvous per collective enough: slot k%2 is
 // rewritten at collective k+2, after every peer arrived at k+1, and a peer
@@ -102,6 +103,24 @@ __global__ void k_ipc_gather(IpcSrc src, uint64_t off, unsigned char* __restrict
   }
 }
 
+// Stage a collective's payload into this rank's exported buffer, then tell the
+// host: one workgroup copies, and after a system-scope release (the staged
+// bytes reach memory every agent and XCD reads) thread 0 writes the
+// collective's tag into pinned host memory, where the host spins -- the stream
+// position is seen one PCIe write after it is reached (an event query sees
+// it much later).  Larger payloads: hipMemcpyAsync, then this kernel with 0 bytes.
+__global__ void k_ipc_stage(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n16,
+                            const unsigned char* __restrict__ src_tail, unsigned char* __restrict__ dst_tail,
+                            uint32_t tail, uint64_t* host_tag, uint64_t tag) {
+  for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  if (threadIdx.x < tail) dst_tail[threadIdx.x] = src_tail[threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(host_tag, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <typename T>
 __global__ void k_ipc_reduce(IpcSrc src, T* out, uint64_t count, int P, int op) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -140,8 +159,10 @@ class IpcComm final : public Comm {
     BIBFS_REQUIRE(!name.empty() && name[0] == '/' && name.size() < 200, "ipc comm: bad group id");
     HIP_CHECK(hipGetDevice(&device_));
     attach();
-    HIP_CHECK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_tag_), 64, hipHostMallocDefault));
+    *h_tag_ = 0;
+    if (const char* e = std::getenv("BIBFS_IPC_STATS")) stats_on_ = e[0] == '1';
   }
 
   ~IpcComm() override {
@@ -160,8 +181,14 @@ class IpcComm final : public Comm {
     for (auto& x : retired_) (void)hipFree(x.ptr);
     for (int s = 0; s < 2; ++s)
       if (stage_[s]) (void)hipFree(stage_[s]);
-    if (ready_) (void)hipEventDestroy(ready_);
     if (done_) (void)hipEventDestroy(done_);
+    if (h_tag_) (void)hipHostFree(h_tag_);
+    if (stats_on_ && n_coll_)
+      std::fprintf(stderr,
+                   "[ipc rank %d] %llu collectives: %.2f us mean stream wait, %.2f us mean rendezvous, %.2f us mean "
+                   "host time per collective\n",
+                   rank_, (unsigned long long)n_coll_, ns_stream_ * 1e-3 / n_coll_, ns_meet_ * 1e-3 / n_coll_,
+                   ns_total_ * 1e-3 / n_coll_);
     if (shm_) munmap(shm_, sizeof(IpcShm));
     if (rank_ == 0 && !unlinked_) shm_unlink(name_.c_str());
   }
@@ -341,20 +368,23 @@ class IpcComm final : public Comm {
     return true;
   }
 
-  // Host wait for `e` (an event on this rank's own stream), with the group's watchdog.
-  void host_wait(hipEvent_t e, const clock::time_point& deadline) {
+  // Host wait for the stage kernel's tag (this rank's own stream reached the
+  // collective), with the group's watchdog.
+  void wait_tag(uint64_t tag, hipStream_t s, const clock::time_point& deadline) {
     for (uint64_t spin = 0;; ++spin) {
-      const hipError_t q = hipEventQuery(e);
-      if (q == hipSuccess) return;
-      if (q != hipErrorNotReady) HIP_CHECK(q);
-      if ((spin & 255) == 255) {
+      if (__atomic_load_n(h_tag_, __ATOMIC_ACQUIRE) == tag) return;
+      if ((spin & 1023) == 1023) {
         live();
+        const hipError_t q = hipStreamQuery(s);
+        if (q != hipSuccess && q != hipErrorNotReady) HIP_CHECK(q);
+        if (q == hipSuccess && __atomic_load_n(h_tag_, __ATOMIC_ACQUIRE) != tag)
+          throw Error("ipc comm: stream drained without the stage tag");
         if (clock::now() > deadline) {
           abort_with("rank " + std::to_string(rank_) + " timed out waiting for its own stream");
           throw Error("ipc comm: rank " + std::to_string(rank_) + " waited " + std::to_string(timeout_s_) +
                       " s for its stream; group aborted");
         }
-        if (spin > 4096) sched_yield();
+        if (spin > (1u << 16)) sched_yield();
       }
     }
   }
@@ -378,14 +408,29 @@ class IpcComm final : public Comm {
   // Stage `bytes` of `src`, wait for them (and for the previous collective's
   // pull), rendezvous.  Returns the staging slot of this collective.
   int enter(const void* src, size_t bytes, hipStream_t s) {
+    const clock::time_point t0 = clock::now();
     const int slot = (int)(seq_ & 1);
     if (bytes > stage_cap_[slot]) grow_stage(slot, bytes);
-    if (bytes) HIP_CHECK(hipMemcpyAsync(stage_[slot], src, bytes, hipMemcpyDeviceToDevice, s));
-    HIP_CHECK(hipEventRecord(ready_, s));
+    // the previous collective's pull must be complete before this rank
+    // arrives (peers then rewrite what it read): on another stream, this
+    // stream waits for it, so the stage tag below implies it
+    if (done_recorded_ && done_stream_ != s) HIP_CHECK(hipStreamWaitEvent(s, done_, 0));
+    const uint64_t tag = ++tag_seq_;
+    const unsigned char* sc = static_cast<const unsigned char*>(src);
+    unsigned char* dc = static_cast<unsigned char*>(stage_[slot]);
+    const bool aligned = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(stage_[slot])) & 15) == 0;
+    if (bytes <= kStageOneBlock && aligned) {
+      k_ipc_stage<<<1, 1024, 0, s>>>(reinterpret_cast<const uint4*>(sc), reinterpret_cast<uint4*>(dc), bytes / 16,
+                                     sc + bytes / 16 * 16, dc + bytes / 16 * 16, (uint32_t)(bytes % 16), h_tag_, tag);
+    } else {
+      if (bytes) HIP_CHECK(hipMemcpyAsync(dc, sc, bytes, hipMemcpyDeviceToDevice, s));
+      k_ipc_stage<<<1, 64, 0, s>>>(nullptr, nullptr, 0, nullptr, nullptr, 0, h_tag_, tag);
+    }
+    HIP_CHECK(hipGetLastError());
     const clock::time_point deadline =
-        clock::now() + std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(timeout_s_));
-    if (done_recorded_) host_wait(done_, deadline);  // previous pull complete: peers may rewrite what it read
-    host_wait(ready_, deadline);
+        t0 + std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(timeout_s_));
+    wait_tag(tag, s, deadline);
+    const clock::time_point t1 = clock::now();
     ++seq_;
     shm_->r[rank_].arrived.store(seq_, std::memory_order_release);
     for (uint64_t spin = 0;; ++spin) {
@@ -407,6 +452,13 @@ class IpcComm final : public Comm {
         }
         if (spin > 2048) sched_yield();
       }
+    }
+    if (stats_on_) {
+      const clock::time_point t2 = clock::now();
+      ++n_coll_;
+      ns_stream_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+      ns_meet_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count();
+      t_enter_ = t0;
     }
     // every rank has passed the rendezvous before this one: buffers retired
     // before it are unmapped everywhere
@@ -457,6 +509,9 @@ class IpcComm final : public Comm {
   void leave(hipStream_t s) {
     HIP_CHECK(hipEventRecord(done_, s));
     done_recorded_ = true;
+    done_stream_ = s;
+    if (stats_on_)
+      ns_total_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clock::now() - t_enter_).count();
   }
 
   int rank_, size_;
@@ -471,8 +526,15 @@ class IpcComm final : public Comm {
   size_t stage_cap_[2] = {0, 0};
   Peer peer_[kIpcMax][2];
   std::vector<Retired> retired_;
-  hipEvent_t ready_ = nullptr, done_ = nullptr;
+  static constexpr size_t kStageOneBlock = 256u << 10;  // one-workgroup stage kernel up to this many bytes
+  hipEvent_t done_ = nullptr;
   bool done_recorded_ = false;
+  hipStream_t done_stream_ = nullptr;
+  uint64_t* h_tag_ = nullptr;  // pinned: the last stage tag the device wrote
+  uint64_t tag_seq_ = 0;
+  bool stats_on_ = false;      // BIBFS_IPC_STATS=1: per-collective host timings on teardown
+  uint64_t n_coll_ = 0, ns_stream_ = 0, ns_meet_ = 0, ns_total_ = 0;
+  clock::time_point t_enter_{};
   clock::time_point last_alive_check_{};
 };
 

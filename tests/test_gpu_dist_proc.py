@@ -198,7 +198,9 @@ def test_spill_overflow_fails_every_rank_and_group_keeps_serving():
     answer the queries exactly with the default sizing."""
     g = bb.from_spec("rmat:16384:262144:3")  # dense: many candidates per owner and round
     qs = _pairs(g.n, 6, 71)
-    got, outs = dist_proc_matrix(3, g, qs, [({"_catch": True}, {"owner_cap": 2, "spill_cap": 1}),
+    # (top-down: a bottom-up level exchanges bitmaps, not candidates)
+    got, outs = dist_proc_matrix(3, g, qs, [({"_catch": True, "direction": "topdown"},
+                                             {"owner_cap": 2, "spill_cap": 1}),
                                             ({}, {"owner_cap": 0, "spill_cap": 0})])
     failed = [r for r in outs[0]["runs"][0]["results"] if r["hops"] == -3]
     assert failed and all("spill list overflowed" in r["error"] for r in failed), outs[0]["runs"][0]["results"]
