@@ -829,7 +829,7 @@ struct SmallStage {
 };
 __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S, uint32_t t, uint32_t nt);
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
-                             SmallStage& S, RoundStamp* rs);
+                             SmallStage& S, RoundStamp* rs, int only = -1);
 __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs);
 __device__ __forceinline__ bool small_expand_ok(const Ctl& c, int P) {
   if (c.cont || !c.sides || P > kStageRanks) return false;
@@ -935,17 +935,18 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
       rs->eb1 = t_in;
     }
   }
-  if (ocap && header && nsides == 2 && small_expand_ok(c, V.P)) {  // small round: one workgroup
+  // small round: one workgroup (an overlap round's one-side launch: one per side)
+  if (ocap && header && small_expand_ok(c, V.P)) {
     if (blockIdx.x == 0 && blockIdx.y == 0) {
-      if (RoundStamp* rs = round_stamp(V, it); rs && threadIdx.x == 0) {
+      if (RoundStamp* rs = round_stamp(V, it); rs && threadIdx.x == 0 && side0 == 0) {
         rs->ep = __builtin_amdgcn_s_memrealtime();
         rs->sg = t_staged;
         rs->small = 1;
       }
-      small_expand(V, c, it, ocap, fr, sm, round_stamp(V, it));
+      small_expand(V, c, it, ocap, fr, sm, side0 == 0 ? round_stamp(V, it) : nullptr, nsides == 2 ? -1 : side0);
       if (RoundStamp* rs = round_stamp(V, it)) {
         __syncthreads();
-        if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) (side0 == 0 ? rs->ee : rs->ee1) = __builtin_amdgcn_s_memrealtime();
       }
     }
     return;
@@ -1504,6 +1505,10 @@ __device__ void small_scan(uint32_t* X, uint32_t cnt) {
 // LDS.  Wave-cooperative (every lane calls it); the side is per lane, so one
 // call serves both sides of a lockstep round.  dcl[s]: the depth a claim of
 // the other side made in THIS round has (its depth store may not be visible).
+// kAgent: the claim's atomicOr at agent scope -- a one-side expansion of an
+// overlap round, while the other side's launch may claim in the same words
+// from another XCD; one workgroup alone keeps it at workgroup scope (its L2).
+template <bool kAgent = false>
 __device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const uint32_t* qbase, bool want, int s,
                                             uint32_t v, uint32_t u, const uint32_t* dn, const uint32_t* dcl,
                                             bool single) {
@@ -1515,7 +1520,9 @@ __device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const u
     const unsigned long long m = 1ull << ((li & 31) + 32 * s);
     // the row bounds are loaded beside the claim (independent of its result:
     // one dependent round trip fewer; a loser's load is wasted)
-    const unsigned long long old = wg_fetch_or(visw + (li >> 5), m);
+    const unsigned long long old =
+        kAgent ? __hip_atomic_fetch_or(visw + (li >> 5), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+               : wg_fetch_or(visw + (li >> 5), m);
     rb = V.row_off[li];
     re = V.row_off[li + 1];
     mine = !(old & m);
@@ -1611,8 +1618,10 @@ __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S
   }
 }
 
+// only >= 0: an overlap round's one-side launch -- that side alone (the other
+// side's launch runs beside it), claims at agent scope, only its headers.
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
-                             SmallStage& S, RoundStamp* rs) {
+                             SmallStage& S, RoundStamp* rs, int only) {
   __shared__ SmallCtr K;
   uint32_t* const su = S.su;
   unsigned long long* const sb = S.sb;
@@ -1620,8 +1629,9 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
   const uint32_t tid = threadIdx.x;
   const int p = it & 1;
   DState* st = V.st;
-  if (!S.valid) {  // (a big idle side): stage the expanding sides only
-    const uint32_t F0 = (c.sides & 1) ? fr[2] - fr[0] : 0u, F1 = (c.sides & 2) ? fr[3] - fr[1] : 0u;
+  const uint32_t mine_sides = only < 0 ? c.sides : (c.sides & (1u << only));
+  if (only >= 0 || !S.valid) {  // (a big idle side, or one side of an overlap round): stage the expanding sides only
+    const uint32_t F0 = (mine_sides & 1) ? fr[2] - fr[0] : 0u, F1 = (mine_sides & 2) ? fr[3] - fr[1] : 0u;
     if (tid == 0) {
       S.n0 = F0;
       S.nv = F0 + F1;  // <= 2 kSmallV (the plan's vertex bound)
@@ -1694,22 +1704,25 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
 #pragma unroll
     for (int k = 0; k < kSmallU; ++k) {
       const bool own = ok[k] && vv[k] >= V.lo && vv[k] < V.hi;
-      small_claim(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
+      if (only >= 0) small_claim<true>(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
+      else small_claim(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
       small_emit(V, K, spbase, lst, ok[k] && !own, ss[k], vv[k], uu[k], ocap);
     }
   }
   __syncthreads();
   if (rs && tid == 0) rs->ex = __builtin_amdgcn_s_memrealtime();
-  // owner headers of both sides (count capped to the block), the round's state
+  // owner headers of its sides (count capped to the block), the round's state
   const uint64_t bw = block_words(ocap);
   for (uint32_t t = tid; t < 2u * V.P; t += kThreads) {
     const uint32_t s = t / V.P, o = t % V.P;
+    if (only >= 0 && (int)s != only) continue;
     const uint32_t cnt = K.oc[s][o];
     V.sendbuf[((uint64_t)s * V.P + o) * bw] = min(cnt, ocap);
     if (cnt) atomicMax(&st->ocmax, cnt);
   }
   if (tid == 0) {
     for (int s = 0; s < 2; ++s) {
+      if (only >= 0 && s != only) continue;
       st->qtail[s] = qbase[s] + K.q[s];
       st->new_edges[s] += K.ne[s];
       st->spill_n[s][lst[s]] = spbase[s] + K.sp[s];
