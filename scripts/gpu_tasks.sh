@@ -46,7 +46,7 @@ run_task() {
       $T 600 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/${TAG}_bench.json 2> $O/${TAG}_bench.err ;;
     suite)
       SIZES="1000 10000 50000 100000" SEED=1 bash scripts/make_graphs $O/${TAG}_graphs > $O/${TAG}_make_graphs.log 2>&1 &&
-      TIERS="v1 v2 v3 v4" REPEAT=20 WARMUP=5 NP=4 NGPU=1 PER_RUN_TIMEOUT=120 \
+      TIERS="v1 v2 v3 v4" REPEAT=20 WARMUP=5 NP=4 V4NP=4 PER_RUN_TIMEOUT=120 \
         LOGDIR=$O/${TAG}_suite_logs CSV=$O/${TAG}_benchmark_results.csv \
         $T 900 bash scripts/benchmark_test.sh $O/${TAG}_graphs > $O/${TAG}_benchmark_table.txt 2>&1 ;;
     prof)
