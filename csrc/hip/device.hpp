@@ -306,14 +306,6 @@ void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* h
 // levels > 1 chains that many device-planned levels: the finisher of each
 // plans the next one into aux (or ends the chain: search over, or a level the
 // Beamer rule declines, which publishes the mirror `seq` for the host).
-// Small top-down levels in one workgroup (k_wg_levels): level after level
-// while the side with fewer frontier edges has at most max_fe of them (and,
-// with beamer, the Beamer rule keeps it top-down); publishes the mirror `seq`
-// (and the result `res_seq` when the search ends) like a grid level.
-// wg_max_edges(): BIBFS_WG_MAX_EDGES, default 16384 (0 = never).
-void wg_levels(const GraphView& g, const SearchBuffers& b, uint64_t max_fe, bool beamer, double alpha,
-               dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s);
-uint64_t wg_max_edges();
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
                unsigned long long gate_ticks, int levels, hipStream_t s);

@@ -2204,169 +2204,6 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   if (P.mirror && !next && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
 }
 
-// ============================================================================
-// Small grid levels in ONE workgroup (round 5)
-// ============================================================================
-// A 10M G(n, p) search leaves LDS with frontiers of ~2k vertices / ~5k edges.
-// A grid level over them is a chain of ~10 dependent device-scope round trips
-// -- the queue and row loads, claim atomics at agent scope (performed past the
-// XCD's L2 to stay coherent across XCDs), the append and done-counter atomics,
-// the finisher's state reads -- plus a launch and a host hand-off: 15-22 us
-// per level (profiles/r4_grid_timelines_final.txt).  Here one 1024-thread
-// workgroup runs level after level itself: the level belongs to it alone, so
-// its claims are WORKGROUP-scope atomics done in its XCD's L2, the append and
-// degree counters live in LDS, a level seam is a __syncthreads, each thread
-// keeps kWgU edges' loads in flight, and the host hears from it only when the
-// search ends or a level outgrows kWgMaxEdges (the grid kernels then take the
-// search over from the state it leaves, exactly as after a grid level).
-// Side and direction follow grid_loop's rules (fewer frontier edges; it stops
-// where the Beamer test would go bottom-up).
-constexpr int kWgThreads = 1024;
-constexpr int kWgU = 4;                 // edges per thread in flight per pass
-constexpr uint32_t kWgMaxLevels = 4096;  // per launch (a long chain returns to the host now and then)
-
-template <typename OffT, bool kAuto>
-__global__ __launch_bounds__(kWgThreads, 1) void k_wg_levels(GridParams<OffT> P, unsigned long long max_fe,
-                                                             int beamer) {
-  __shared__ DevState sv;
-  __shared__ uint32_t fu[kWgThreads];       // frontier chunk: vertices
-  __shared__ OffT fb[kWgThreads];           // their row begins
-  __shared__ uint32_t fp[kWgThreads + 1];   // exclusive degree prefix (+ the chunk's total)
-  __shared__ uint32_t wsum[kWgThreads / kWave];
-  __shared__ uint32_t sq, smeet;            // appended this level; a meet vertex found this level
-  __shared__ unsigned long long sne;        // degree sum of the vertices claimed this level
-  constexpr uint32_t kWords = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
-  static_assert(kWords <= kWgThreads, "one thread per state word");
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const launch::SearchBuffers& b = P.b;
-  uint32_t* const w = reinterpret_cast<uint32_t*>(b.st);
-  if constexpr (kAuto) {  // behind k_handoff: only a planned, small, non-direct level
-    const uint32_t xp = __builtin_amdgcn_readfirstlane(b.aux[2]);
-    if (!(xp & kAuxActive) || (xp & kAuxDirect)) return;
-  }
-  if (tid < kWords) reinterpret_cast<uint32_t*>(&sv)[tid] = load_agent(&w[tid]);
-  __syncthreads();
-  if constexpr (kAuto) {
-    const uint32_t xp = __builtin_amdgcn_readfirstlane(b.aux[2]);
-    const int s = (int)((xp >> 1) & 1u);
-    if (sv.fedges[s] > max_fe) return;  // the grid kernels behind run it
-    __syncthreads();                    // (every wave has read aux)
-    if (tid == 0) b.aux[2] = xp & ~kAuxActive;  // they have nothing to run now
-  }
-  for (uint32_t lv = 0; lv < kWgMaxLevels; ++lv) {
-    if (sv.status != kRunning || sv.meet != kEmpty) break;
-    const int s = sv.fedges[0] <= sv.fedges[1] ? 0 : 1, o = s ^ 1;
-    const unsigned long long fe = sv.fedges[s];
-    if (fe > max_fe) break;
-    if (beamer && (double)fe > ((double)P.nnz - (double)sv.vedges[s]) / (double)P.alpha) break;
-    const uint32_t fbeg = sv.fbeg[s], F = sv.fend[s] - fbeg, qt0 = sv.qtail[s];
-    if (tid == 0) {
-      sq = 0;
-      smeet = kEmpty;
-      sne = 0;
-    }
-    for (uint32_t c0 = 0; c0 < F; c0 += kWgThreads) {
-      const uint32_t i = c0 + tid, nv = min(F - c0, (uint32_t)kWgThreads);
-      uint32_t u = 0, deg = 0;
-      OffT rb = 0;
-      if (i < F) {
-        u = b.queue[s][fbeg + i];
-        rb = P.row_off[u];
-        deg = (uint32_t)(P.row_off[u + 1] - rb);
-      }
-      fu[tid] = u;
-      fb[tid] = rb;
-      const uint32_t x = wave_incl_scan(deg);
-      if (lane == 63) wsum[wid] = x;
-      __syncthreads();
-      if (wid == 0) {
-        const uint32_t y = lane < kWgThreads / kWave ? wsum[lane] : 0u;
-        const uint32_t yi = wave_incl_scan(y);
-        if (lane < kWgThreads / kWave) wsum[lane] = yi - y;
-        if (lane == kWgThreads / kWave - 1) fp[kWgThreads] = yi;
-      }
-      __syncthreads();
-      fp[tid] = x - deg + wsum[wid];
-      __syncthreads();
-      const uint32_t Ec = fp[kWgThreads];
-      for (uint32_t base = 0; base < Ec; base += kWgThreads * kWgU) {
-        uint32_t vv[kWgU], uu[kWgU], vd[kWgU];
-        bool ok[kWgU];
-#pragma unroll
-        for (int k = 0; k < kWgU; ++k) {
-          const uint32_t e = base + (uint32_t)k * kWgThreads + tid;
-          ok[k] = e < Ec;
-          vv[k] = uu[k] = 0;
-          vd[k] = ~0u;
-          if (ok[k]) {
-            uint32_t lo = 0, hi = nv;  // last frontier vertex whose edges start at or before e
-            while (hi - lo > 1) {
-              const uint32_t mid = (lo + hi) >> 1;
-              if (fp[mid] <= e) lo = mid;
-              else hi = mid;
-            }
-            uu[k] = fu[lo];
-            const OffT kk = fb[lo] + (OffT)(e - fp[lo]);
-            if (P.padj8) {
-              const unsigned long long pw = P.padj8[kk];
-              vv[k] = launch::pack8_v(pw);
-              vd[k] = launch::pack8_deg(pw);
-            } else if (P.padj) {
-              const uint4 q = P.padj[kk];
-              vv[k] = q.x;
-              vd[k] = q.y;
-            } else {
-              vv[k] = P.col[kk];
-            }
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < kWgU; ++k) {
-          const uint32_t v = vv[k], wd = v >> 5, bit = 1u << (v & 31);
-          bool mine = false;
-          if (ok[k])
-            mine = !(__hip_atomic_fetch_or(&b.vis[s][wd], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit);
-          const unsigned long long mask = __ballot(mine);
-          if (!mask) continue;  // wave-uniform
-          uint32_t dg = 0;
-          if (mine) {
-            b.parent[s][v] = uu[k];
-            dg = vd[k] != ~0u ? vd[k] : (uint32_t)(P.row_off[v + 1] - P.row_off[v]);
-            // a single-side level: every meet it finds has the same length
-            if (b.vis[o][wd] & bit) atomicCAS(&smeet, kEmpty, v);
-          }
-          const int leader = __ffsll((long long)mask) - 1;
-          uint32_t pos = 0;
-          if ((int)lane == leader) pos = atomicAdd(&sq, (uint32_t)__popcll(mask));
-          pos = __shfl(pos, leader);
-          if (mine) b.queue[s][qt0 + pos + mbcnt64(mask)] = v;
-          const unsigned long long ds = wave_sum((unsigned long long)dg);
-          if ((int)lane == leader) atomicAdd(&sne, ds);
-        }
-      }
-      __syncthreads();  // (fu / fb / fp are rewritten by the next chunk; sq, sne complete)
-    }
-    if (tid == 0) {
-      sv.qtail[s] = qt0 + sq;
-      sv.nedges = sne;
-      if (smeet != kEmpty) {
-        sv.meet = smeet;
-        sv.meet_side = (uint32_t)s;
-      }
-      finish_state(sv, b, s, 1, 0);
-    }
-    __syncthreads();
-  }
-  // the state back for the kernels / host after this one (a new launch reads
-  // it), then the host: the result when the search ended, and the mirror
-  if (tid < kWords) w[tid] = reinterpret_cast<const uint32_t*>(&sv)[tid];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __threadfence();
-  __syncthreads();
-  if (P.res_seq && sv.status != kRunning) publish_result(b, P.h, sv, P.res_seq, P.n);
-  if (P.mirror && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
-}
-
 // Seed a search for the grid engine / step-wise API.
 template <typename OffT>
 __global__ void k_seed(const OffT* row_off, launch::SearchBuffers b, uint32_t src, uint32_t dst) {
@@ -2663,27 +2500,6 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   HIP_CHECK(hipGetLastError());
 }
 
-void wg_levels(const GraphView& g, const SearchBuffers& b, uint64_t max_fe, bool beamer, double alpha,
-               dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s) {
-  auto launch_one = [&](auto P) {
-    using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
-    P.mirror = mirror, P.seq = seq, P.trace = 0, P.h = h, P.res_seq = res_seq;
-    P.alpha = (float)alpha;
-    k_wg_levels<OffT, false><<<1, kWgThreads, 0, s>>>(P, (unsigned long long)max_fe, beamer ? 1 : 0);
-  };
-  if (g.row_off32) launch_one(gp<uint32_t>(g, b, 0));
-  else launch_one(gp<uint64_t>(g, b, 0));
-  HIP_CHECK(hipGetLastError());
-}
-
-uint64_t wg_max_edges() {
-  static const uint64_t v = [] {
-    const char* e = std::getenv("BIBFS_WG_MAX_EDGES");
-    return e ? std::strtoull(e, nullptr, 10) : 16384ull;
-  }();
-  return v;
-}
-
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
                unsigned long long gate_ticks, int levels, hipStream_t s) {
@@ -2712,9 +2528,6 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     // the planners may choose direct hub levels (only with the hub pass enqueued)
     P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
-    // small planned levels run in one workgroup, level after level; a bigger
-    // one (or none) leaves the plan to the grid kernels behind it
-    if (wg_max_edges()) k_wg_levels<OffT, true><<<1, kWgThreads, 0, s>>>(P, (unsigned long long)wg_max_edges(), 1);
     for (int l = 0; l < std::max(1, levels); ++l) {
       P.chain = l + 1 < levels ? 1 : 0;
       k_grid_topdown<OffT, true><<<l ? cblocks : blocks, kGridThreads, 0, s>>>(P);

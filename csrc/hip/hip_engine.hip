@@ -753,30 +753,10 @@ struct HipBiBfs::Impl {
     fbits_valid[0] = fbits_valid[1] = false;
     int turn = 0;
     const int trace = opt.trace ? 1 : 0;
-    const uint64_t wg_max = launch::wg_max_edges();
     for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
       if (guard == 0 && !mirror_valid) sync_state();  // state left by the seed
       if (h_state->status != kRunning || h_state->meet != kEmpty) break;
       const int s = choose_side(opt, turn);
-      // small top-down levels: one workgroup runs them back to back
-      // (k_wg_levels), with the same side rule and Beamer test as this loop
-      if (wg_max && !trace && !opt.force_grid && opt.side == SidePolicy::kSmallerEdges &&
-          opt.direction != Direction::kBottomUp &&
-          dir[s] == 1 && h_state->fedges[s] <= wg_max) {
-        const bool beamer = opt.direction == Direction::kAuto;
-        if (!beamer || (double)h_state->fedges[s] <= ((double)nnz - (double)h_state->vedges[s]) / opt.alpha) {
-          const uint32_t lv0 = h_state->levels;
-          const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
-          launch::wg_levels(view(), buf, wg_max, beamer, opt.alpha, h_state, ls,
-                            launch::HostSide{gres, h_path, h_path_cap, h_state}, res_seq, stream);
-          if (res_seq) cleanup_async(true);
-          wait_level();
-          stats.grid_levels += (int)(h_state->levels - lv0);
-          stats.wg_levels += (int)(h_state->levels - lv0);
-          fbits_valid[0] = fbits_valid[1] = false;
-          if (h_state->levels != lv0) continue;
-        }
-      }
       const int mode = choose_mode(s, opt);
       grid_level(s, mode, trace);
       stats.grid_levels++;

@@ -40,7 +40,6 @@ py::dict stats_dict(const SearchStats& s) {
   d["edges_inspected"] = s.edges_inspected;
   d["visited"] = s.visited;
   d["grid_levels"] = s.grid_levels;
-  d["wg_levels"] = s.wg_levels;
   d["bottomup_levels"] = s.bottomup_levels;
   d["handoff"] = s.handoff;
   d["lds_ms"] = s.lds_ms;

@@ -41,26 +41,6 @@ def test_lds_and_grid_vs_oracle(gpu_engine, spec):
     assert_engine(gpu_engine, g, pairs[:8], lockstep=False)
 
 
-@pytest.mark.parametrize("spec", ["gnp:3000000::4", "gnp:10000000::1", "kron:18:16:3"])
-def test_one_workgroup_levels_vs_oracle(gpu_engine, spec):
-    """Small top-down levels after a hand-off run level after level in one
-    workgroup (k_wg_levels): host loop and device (auto) chain, against the
-    oracle; on the G(n, p) graphs at least some levels take that path."""
-    g = bb.from_spec(spec)
-    gpu_engine.load(g)
-    pairs = pairs_for(g.n, 16, 11)
-    wg = 0
-    for resident in (False, True):
-        gpu_engine.set_resident(resident)
-        for s, d in pairs:
-            r = gpu_engine.search(s, d)
-            check_result(g.csr, s, d, r.hops, r.path, native.bfs_oracle(g.csr, s, d).hops)
-            wg += r.stats["wg_levels"]
-    gpu_engine.set_resident(False)
-    if spec.startswith("gnp"):
-        assert wg > 0
-
-
 def test_device_csr_equals_host(gpu_engine):
     g = gnp(50000, seed=3)
     gpu_engine.load(g)
