@@ -85,9 +85,10 @@ def parse_args(argv=None):
     ap.add_argument("--batch", type=int, default=256,
                     help="also measure batched serving: K queries per launch, one CU each (0 = skip)")
     ap.add_argument("--no-cpu-ref", action="store_true", help="skip the CPU serial comparison")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend for the bench's own barriers/reductions (nccl = RCCL; "
-                         "gloo lets several ranks share one GPU for rehearsals)")
+                         "gloo lets several ranks share one GPU for rehearsals; auto = gloo exactly when "
+                         "the ranks on a node outnumber its GPUs)")
     ap.add_argument("--dist-comm", default="auto", choices=["auto", "rccl", "ipc"],
                     help="collective transport of the partitioned engine: rccl (one rank per GPU), ipc "
                          "(HIP-IPC staging buffers; ranks may share a GPU), auto = ipc when ranks share a GPU")
@@ -320,7 +321,11 @@ def main(argv=None) -> int:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = max(1, torch.cuda.device_count())
-    shared_gpu = local >= ndev  # gloo rehearsal: several ranks on one GPU
+    # several ranks on one GPU (a gloo / IPC rehearsal): decided alike on every
+    # rank from the launcher's ranks-per-node, never from this rank's index
+    shared_gpu = int(os.environ.get("LOCAL_WORLD_SIZE", world)) > ndev
+    if a.dist_backend == "auto":
+        a.dist_backend = "gloo" if shared_gpu else "nccl"
     local = local % ndev
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -752,7 +757,9 @@ def main(argv=None) -> int:
             failed = True
     if a.mode == "replicated" and (world == 1 or comm == "ipc" or (a.dist_backend == "nccl" and not shared_gpu)):
         for spec in filter(None, a.dist_graphs.split(",")):
-            spec = world_scaled(spec, world, torch.cuda.mem_get_info(dev)[1])
+            # (ranks sharing one GPU -- an IPC rehearsal -- share its HBM: no
+            # "bigger than one GPU" graph there)
+            spec = world_scaled(spec, 1 if shared_gpu else world, torch.cuda.mem_get_info(dev)[1])
             partitioned[spec] = None
             try:
                 partitioned[spec], state["rccl_ranks"] = run_partitioned(spec, a.dist_steps, 3)
