@@ -42,7 +42,7 @@ PY_INC    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_paths()
 PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11; print(pybind11.get_include())")
 PY_EXT    := $(shell $(PYTHON) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
 
-CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp
+CORE_SRC  := csrc/io/io.cpp csrc/gen/gen.cpp csrc/csr/csr.cpp csrc/cpu/serial_bibfs.cpp csrc/dist/ipc_group.cpp
 HIP_SRC   := csrc/hip/csr_device.hip csrc/hip/engine_kernels.hip csrc/hip/tiny_engine.hip csrc/hip/batch_global.hip csrc/hip/hip_engine.hip \
              csrc/hip/capi.hip csrc/dist/comm.hip csrc/dist/ipc_comm.hip csrc/dist/dist_engine.hip
 MPI_SRC   := csrc/cpu/mpi_bitmap_bibfs.cpp csrc/cpu/mpi_queue_bibfs.cpp
@@ -53,7 +53,7 @@ MPI_OBJ   := $(patsubst csrc/%.cpp,$(OBJ)/%.o,$(MPI_SRC))
 
 HEADERS   := $(wildcard csrc/include/bibfs/*.hpp csrc/include/bibfs/*.h csrc/hip/*.hpp csrc/dist/*.hpp)
 
-CPU_TOOLS := $(BIN)/bibfs_serial $(BIN)/show_matrix $(BIN)/bibfs_gen
+CPU_TOOLS := $(BIN)/bibfs_serial $(BIN)/show_matrix $(BIN)/bibfs_gen $(BIN)/ipc_group_check
 MPI_TOOLS := $(BIN)/second_try $(BIN)/mpi_queue_bibfs
 GPU_TOOLS := $(BIN)/bibfs_selftest $(BIN)/bibfs_hip $(BIN)/mpi_bibfs $(BIN)/bibfs_bench
 
@@ -106,6 +106,9 @@ $(BIN)/bibfs_serial: tools/bibfs_serial.cpp tools/cli_common.hpp $(LIB)/libbibfs
 	@mkdir -p $(BIN)
 	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib'
 $(BIN)/show_matrix: tools/show_matrix.cpp $(LIB)/libbibfs_core.so
+	@mkdir -p $(BIN)
+	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib'
+$(BIN)/ipc_group_check: tools/ipc_group_check.cpp csrc/dist/ipc_group.hpp $(LIB)/libbibfs_core.so
 	@mkdir -p $(BIN)
 	$(TOOL_CXX) $< -o $@ -L$(LIB) -lbibfs_core -Wl,-rpath,'$$ORIGIN/../lib'
 $(BIN)/bibfs_gen: tools/bibfs_gen.cpp tools/cli_common.hpp $(LIB)/libbibfs_core.so

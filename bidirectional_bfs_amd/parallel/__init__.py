@@ -351,7 +351,8 @@ def dist_proc_launch(ranks: int, graph, queries: Sequence, runs: Sequence = ((No
                 with open(fp) as f:
                     outs.append(json.load(f))
             else:
-                outs.append({"rank": r, "error": f"no report (exit status {rcs[r]})", "log": logs[r][-2000:]})
+                outs.append({"rank": r, "error": f"no report (exit status {rcs[r]})"})
+            outs[-1]["log"] = (logs[r] or "")[-4000:]
         return rcs, outs, elapsed
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

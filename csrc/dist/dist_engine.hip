@@ -3151,8 +3151,10 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   hipStream_t cs = cstream;
   if (P == 1) ensure_padj();  // (the partitioned rounds at world size 1: built on first use)
   ++epoch;
-  const Policy pol = policy(opt);
+  // (before policy(): the plan's overflow test and the kernels' spill bound
+  // must be the same number)
   V.spill_cap = size > 1 ? (tune.spill_cap ? std::min(block_cap, tune.spill_cap) : block_cap) : 1;
+  const Policy pol = policy(opt);
   V.cap = cap();
   V.trace = opt.trace ? d_trace : nullptr;
   V.rstamp = tune.stamps ? d_rstamp : nullptr;

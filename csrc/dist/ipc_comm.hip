@@ -16,8 +16,8 @@
 // block straight out of the peers' staging buffers (allgather / alltoall) or
 // reduces them element-wise (allreduce).  Nothing goes through host memory.
 //
-// Control plane: a POSIX shared-memory segment (name = the group's unique id)
-// with one cache line per rank.  A collective is: stage (one kernel that
+// Control plane (IpcGroup, ipc_group.cpp -- host-only, CPU-tested): a POSIX
+// shared-memory segment (name = the group's unique id) with one cache line per rank.  A collective is: stage (one kernel that
 // copies and then writes the collective's tag into pinned host memory),
 // host-spin on that tag, publish "arrived at collective k", wait until every
 // rank arrived at k, launch the pull kernel.  The device
@@ -32,50 +32,22 @@
 // within milliseconds instead of at the timeout).
 #include "comm.hpp"
 
-#include <fcntl.h>
 #include <sched.h>
-#include <signal.h>
-#include <sys/mman.h>
-#include <sys/stat.h>
-#include <unistd.h>
 
-#include <atomic>
-#include <cerrno>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <random>
 #include <string>
-#include <thread>
+#include <vector>
 
 #include "device.hpp"
+#include "ipc_group.hpp"
 
 namespace bibfs {
 namespace dist {
 
 namespace {
-
-constexpr int kIpcMax = 16;
-constexpr uint64_t kIpcMagic = 0x4942465349504331ull;  // "1CPISFBI"
-
-struct alignas(64) IpcRankSlot {
-  std::atomic<uint64_t> arrived;  // collectives this rank has entered
-  std::atomic<int32_t> pid;
-  int32_t device;
-  uint64_t gen[2];                // staging generation per slot (0 = none yet)
-  uint64_t cap[2];
-  hipIpcMemHandle_t handle[2];
-};
-
-struct IpcShm {
-  std::atomic<uint64_t> magic;
-  int32_t P;
-  std::atomic<int32_t> attached;
-  std::atomic<int32_t> aborted;   // 0, or 1 + the rank that aborted first
-  std::atomic<int32_t> detached;  // ranks that closed their peer mappings (teardown)
-  char why[240];
-  IpcRankSlot r[kIpcMax];
-};
 
 struct IpcSrc {
   const unsigned char* p[kIpcMax];
@@ -135,30 +107,11 @@ __global__ void k_ipc_reduce(IpcSrc src, T* out, uint64_t count, int P, int op) 
 
 size_t tsize(DType t) { return t == DType::kU32 ? 4 : 8; }
 
-bool pid_dead(int pid) {
-  if (pid <= 0) return false;
-  if (kill(pid, 0) != 0 && errno == ESRCH) return true;
-  // a killed rank stays a zombie until its launcher reaps it
-  char path[64];
-  std::snprintf(path, sizeof(path), "/proc/%d/stat", pid);
-  FILE* f = std::fopen(path, "r");
-  if (!f) return false;
-  char buf[256] = {0};
-  const size_t n = std::fread(buf, 1, sizeof(buf) - 1, f);
-  std::fclose(f);
-  const char* rp = std::strrchr(buf, ')');  // "pid (comm) S ..."
-  return n > 0 && rp && rp[1] == ' ' && (rp[2] == 'Z' || rp[2] == 'X');
-}
-
 class IpcComm final : public Comm {
  public:
   IpcComm(int rank, int size, const std::string& name, double timeout_s)
-      : rank_(rank), size_(size), name_(name), timeout_s_(timeout_s) {
-    BIBFS_REQUIRE(size >= 1 && size <= kIpcMax, "ipc comm: 1.." + std::to_string(kIpcMax) + " ranks");
-    BIBFS_REQUIRE(rank >= 0 && rank < size, "ipc comm: bad rank");
-    BIBFS_REQUIRE(!name.empty() && name[0] == '/' && name.size() < 200, "ipc comm: bad group id");
-    HIP_CHECK(hipGetDevice(&device_));
-    attach();
+      : rank_(rank), size_(size), group_(rank, size, name, timeout_s, current_device()) {
+    static_assert(sizeof(hipIpcMemHandle_t) == sizeof(IpcGroup::Blob::handle), "IPC handle size");
     HIP_CHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_tag_), 64, hipHostMallocDefault));
     *h_tag_ = 0;
@@ -169,15 +122,9 @@ class IpcComm final : public Comm {
     for (int r = 0; r < size_; ++r)
       for (int s = 0; s < 2; ++s)
         if (peer_[r][s].ptr) (void)hipIpcCloseMemHandle(peer_[r][s].ptr);
-    if (shm_) {
-      // An exported buffer is freed only after every peer unmapped it (or the
-      // group failed, or a bounded wait for peers that are gone ran out).
-      shm_->detached.fetch_add(1, std::memory_order_acq_rel);
-      const auto deadline = clock::now() + std::chrono::seconds(2);
-      while (shm_->detached.load(std::memory_order_acquire) < size_ && !aborted() && clock::now() < deadline &&
-             peers_alive())
-        std::this_thread::sleep_for(std::chrono::microseconds(200));
-    }
+    // an exported buffer is freed only after every peer unmapped it (or the
+    // group failed, or a bounded wait for peers that are gone ran out)
+    group_.detach_wait(2.0);
     for (auto& x : retired_) (void)hipFree(x.ptr);
     for (int s = 0; s < 2; ++s)
       if (stage_[s]) (void)hipFree(stage_[s]);
@@ -189,16 +136,12 @@ class IpcComm final : public Comm {
                    "host time per collective\n",
                    rank_, (unsigned long long)n_coll_, ns_stream_ * 1e-3 / n_coll_, ns_meet_ * 1e-3 / n_coll_,
                    ns_total_ * 1e-3 / n_coll_);
-    if (shm_) munmap(shm_, sizeof(IpcShm));
-    if (rank_ == 0 && !unlinked_) shm_unlink(name_.c_str());
   }
 
   int rank() const override { return rank_; }
   int size() const override { return size_; }
   const char* name() const override { return "ipc"; }
-  void set_timeout(double s) override {
-    if (s > 0) timeout_s_ = s;
-  }
+  void set_timeout(double s) override { group_.set_timeout(s); }
 
   void allreduce(void* buf, size_t count, DType t, ROp op, hipStream_t s) override {
     live();
@@ -253,16 +196,9 @@ class IpcComm final : public Comm {
     leave(s);
   }
 
-  void check() override {
-    live();
-    if (!peers_alive()) {
-      abort_with("a peer process died");
-      throw Error(abort_message());
-    }
-  }
-
-  void abort() override { abort_with("aborted by rank " + std::to_string(rank_)); }
-  bool aborted() const override { return aborted_ || (shm_ && shm_->aborted.load(std::memory_order_acquire) != 0); }
+  void check() override { group_.check(); }
+  void abort() override { group_.abort("aborted by rank " + std::to_string(rank_)); }
+  bool aborted() const override { return group_.aborted(); }
 
  private:
   struct Peer {
@@ -276,96 +212,18 @@ class IpcComm final : public Comm {
 
   using clock = std::chrono::steady_clock;
 
-  void attach() {
-    const auto deadline = clock::now() + std::chrono::duration<double>(timeout_s_);
-    int fd = -1;
-    if (rank_ == 0) {
-      fd = shm_open(name_.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
-      if (fd < 0) throw Error("ipc comm: shm_open(" + name_ + ") failed: " + std::strerror(errno));
-      if (ftruncate(fd, sizeof(IpcShm)) != 0) {
-        close(fd);
-        shm_unlink(name_.c_str());
-        throw Error(std::string("ipc comm: ftruncate failed: ") + std::strerror(errno));
-      }
-    } else {
-      for (;;) {
-        fd = shm_open(name_.c_str(), O_RDWR, 0600);
-        if (fd >= 0) {
-          struct stat st;
-          if (fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(IpcShm)) break;
-          close(fd);
-          fd = -1;
-        } else if (errno != ENOENT) {
-          throw Error("ipc comm: shm_open(" + name_ + ") failed: " + std::strerror(errno));
-        }
-        if (clock::now() > deadline) throw Error("ipc comm: rank 0 never created group " + name_);
-        std::this_thread::sleep_for(std::chrono::milliseconds(1));
-      }
-    }
-    void* m = mmap(nullptr, sizeof(IpcShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (m == MAP_FAILED) {
-      if (rank_ == 0) shm_unlink(name_.c_str());
-      throw Error(std::string("ipc comm: mmap failed: ") + std::strerror(errno));
-    }
-    shm_ = static_cast<IpcShm*>(m);  // (fresh segments are zero-filled)
-    if (rank_ == 0) {
-      shm_->P = size_;
-      shm_->magic.store(kIpcMagic, std::memory_order_release);
-    } else {
-      while (shm_->magic.load(std::memory_order_acquire) != kIpcMagic) {
-        if (clock::now() > deadline) throw Error("ipc comm: group " + name_ + " never initialised");
-        std::this_thread::sleep_for(std::chrono::microseconds(100));
-      }
-      BIBFS_REQUIRE(shm_->P == size_, "ipc comm: group " + name_ + " has " + std::to_string(shm_->P) +
-                                          " ranks, this rank expected " + std::to_string(size_));
-    }
-    IpcRankSlot& me = shm_->r[rank_];
-    me.device = device_;
-    me.pid.store((int32_t)getpid(), std::memory_order_release);
-    shm_->attached.fetch_add(1, std::memory_order_acq_rel);
-    while (shm_->attached.load(std::memory_order_acquire) < size_) {
-      if (shm_->aborted.load(std::memory_order_acquire)) throw Error(abort_message());
-      if (clock::now() > deadline) {
-        abort_with("not every rank attached within the timeout");
-        throw Error("ipc comm: only " + std::to_string(shm_->attached.load()) + " of " + std::to_string(size_) +
-                    " ranks attached to " + name_);
-      }
-      std::this_thread::sleep_for(std::chrono::microseconds(100));
-    }
-    if (rank_ == 0) {  // every rank has it mapped: the name is no longer needed (no leak on a crash)
-      shm_unlink(name_.c_str());
-      unlinked_ = true;
-    }
+  static int current_device() {
+    int d = 0;
+    HIP_CHECK(hipGetDevice(&d));
+    return d;
   }
 
   void live() const {
-    if (aborted()) throw Error(abort_message());
+    if (group_.aborted()) throw Error(group_.abort_message());
   }
 
-  std::string abort_message() const {
-    const int who = shm_ ? shm_->aborted.load(std::memory_order_acquire) : 0;
-    std::string why = shm_ && who ? std::string(shm_->why, strnlen(shm_->why, sizeof(shm_->why))) : "";
-    return "ipc group aborted" + (who ? " (first by rank " + std::to_string(who - 1) + ": " + why + ")" : std::string());
-  }
-
-  void abort_with(const std::string& why) {
-    aborted_ = true;
-    if (!shm_) return;
-    int expect = 0;
-    if (shm_->aborted.compare_exchange_strong(expect, rank_ + 1, std::memory_order_acq_rel)) {
-      std::snprintf(shm_->why, sizeof(shm_->why), "%s", why.c_str());
-      std::atomic_thread_fence(std::memory_order_release);
-    }
-  }
-
-  bool peers_alive() {
-    const auto now = clock::now();
-    if (now - last_alive_check_ < std::chrono::milliseconds(5)) return true;
-    last_alive_check_ = now;
-    for (int r = 0; r < size_; ++r)
-      if (r != rank_ && pid_dead(shm_->r[r].pid.load(std::memory_order_acquire))) return false;
-    return true;
+  clock::time_point deadline_from(clock::time_point t0) const {
+    return t0 + std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(group_.timeout()));
   }
 
   // Host wait for the stage kernel's tag (this rank's own stream reached the
@@ -380,8 +238,8 @@ class IpcComm final : public Comm {
         if (q == hipSuccess && __atomic_load_n(h_tag_, __ATOMIC_ACQUIRE) != tag)
           throw Error("ipc comm: stream drained without the stage tag");
         if (clock::now() > deadline) {
-          abort_with("rank " + std::to_string(rank_) + " timed out waiting for its own stream");
-          throw Error("ipc comm: rank " + std::to_string(rank_) + " waited " + std::to_string(timeout_s_) +
+          group_.abort("rank " + std::to_string(rank_) + " timed out waiting for its own stream");
+          throw Error("ipc comm: rank " + std::to_string(rank_) + " waited " + std::to_string(group_.timeout()) +
                       " s for its stream; group aborted");
         }
         if (spin > (1u << 16)) sched_yield();
@@ -398,10 +256,12 @@ class IpcComm final : public Comm {
     size_t cap = 2u << 20;
     while (cap < bytes) cap <<= 1;
     HIP_CHECK(hipMalloc(&stage_[slot], cap));
-    IpcRankSlot& me = shm_->r[rank_];
-    HIP_CHECK(hipIpcGetMemHandle(&me.handle[slot], stage_[slot]));
-    me.cap[slot] = cap;
-    me.gen[slot] = ++gen_;
+    IpcGroup::Blob& me = group_.mine(slot);
+    hipIpcMemHandle_t h;
+    HIP_CHECK(hipIpcGetMemHandle(&h, stage_[slot]));
+    std::memcpy(me.handle, &h, sizeof(h));
+    me.cap = cap;
+    me.gen = ++gen_;
     stage_cap_[slot] = cap;
   }
 
@@ -427,32 +287,11 @@ class IpcComm final : public Comm {
       k_ipc_stage<<<1, 64, 0, s>>>(nullptr, nullptr, 0, nullptr, nullptr, 0, h_tag_, tag);
     }
     HIP_CHECK(hipGetLastError());
-    const clock::time_point deadline =
-        t0 + std::chrono::duration_cast<clock::duration>(std::chrono::duration<double>(timeout_s_));
+    const clock::time_point deadline = deadline_from(t0);
     wait_tag(tag, s, deadline);
     const clock::time_point t1 = clock::now();
     ++seq_;
-    shm_->r[rank_].arrived.store(seq_, std::memory_order_release);
-    for (uint64_t spin = 0;; ++spin) {
-      int behind = 0;
-      for (int r = 0; r < size_; ++r)
-        if (shm_->r[r].arrived.load(std::memory_order_acquire) < seq_) ++behind;
-      if (!behind) break;
-      if ((spin & 127) == 127) {
-        live();
-        if (!peers_alive()) {
-          abort_with("a peer process died while rank " + std::to_string(rank_) + " waited at collective " +
-                     std::to_string(seq_));
-          throw Error(abort_message());
-        }
-        if (clock::now() > deadline) {
-          abort_with("rank " + std::to_string(rank_) + " timed out at collective " + std::to_string(seq_));
-          throw Error("ipc comm: rank " + std::to_string(rank_) + " waited " + std::to_string(timeout_s_) +
-                      " s for its peers at collective " + std::to_string(seq_) + "; group aborted");
-        }
-        if (spin > 2048) sched_yield();
-      }
-    }
+    group_.arrive_and_wait(seq_, deadline);
     if (stats_on_) {
       const clock::time_point t2 = clock::now();
       ++n_coll_;
@@ -478,20 +317,21 @@ class IpcComm final : public Comm {
     IpcSrc src{};
     for (int r = 0; r < size_; ++r) {
       if (r == rank_) continue;
-      const IpcRankSlot& ps = shm_->r[r];
+      const IpcGroup::Blob& pb = group_.peer(r, slot);
       Peer& p = peer_[r][slot];
-      if (p.gen != ps.gen[slot]) {
+      if (p.gen != pb.gen) {
         if (p.ptr) HIP_CHECK(hipIpcCloseMemHandle(p.ptr));
         p.ptr = nullptr;
-        hipIpcMemHandle_t h = ps.handle[slot];
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, pb.handle, sizeof(h));
         const hipError_t e = hipIpcOpenMemHandle(&p.ptr, h, hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess) {
           p.ptr = nullptr;
           throw Error(std::string("ipc comm: rank ") + std::to_string(rank_) + " cannot map rank " +
-                      std::to_string(r) + "'s staging buffer (device " + std::to_string(ps.device) +
+                      std::to_string(r) + "'s staging buffer (device " + std::to_string(group_.peer_device(r)) +
                       "): hipIpcOpenMemHandle: " + hipGetErrorString(e));
         }
-        p.gen = ps.gen[slot];
+        p.gen = pb.gen;
       }
       src.p[r] = static_cast<const unsigned char*>(p.ptr);
     }
@@ -514,19 +354,14 @@ class IpcComm final : public Comm {
       ns_total_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(clock::now() - t_enter_).count();
   }
 
+  static constexpr size_t kStageOneBlock = 256u << 10;  // one-workgroup stage kernel up to this many bytes
   int rank_, size_;
-  std::string name_;
-  double timeout_s_;
-  int device_ = 0;
-  IpcShm* shm_ = nullptr;
-  bool unlinked_ = false;
-  bool aborted_ = false;
+  IpcGroup group_;
   uint64_t seq_ = 0, gen_ = 0;
   void* stage_[2] = {nullptr, nullptr};
   size_t stage_cap_[2] = {0, 0};
   Peer peer_[kIpcMax][2];
   std::vector<Retired> retired_;
-  static constexpr size_t kStageOneBlock = 256u << 10;  // one-workgroup stage kernel up to this many bytes
   hipEvent_t done_ = nullptr;
   bool done_recorded_ = false;
   hipStream_t done_stream_ = nullptr;
@@ -535,17 +370,13 @@ class IpcComm final : public Comm {
   bool stats_on_ = false;      // BIBFS_IPC_STATS=1: per-collective host timings on teardown
   uint64_t n_coll_ = 0, ns_stream_ = 0, ns_meet_ = 0, ns_total_ = 0;
   clock::time_point t_enter_{};
-  clock::time_point last_alive_check_{};
 };
 
 }  // namespace
 
 std::vector<uint8_t> ipc_unique_id() {
-  std::random_device rd;
-  const uint64_t x = ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
-  char buf[96];
-  std::snprintf(buf, sizeof(buf), "/bibfs_ipc_%d_%016llx", (int)getpid(), (unsigned long long)x);
-  return std::vector<uint8_t>(buf, buf + std::strlen(buf));
+  const std::string n = IpcGroup::make_name();
+  return std::vector<uint8_t>(n.begin(), n.end());
 }
 
 std::unique_ptr<Comm> make_ipc_comm(int rank, int size, const std::vector<uint8_t>& uid, double timeout_s) {

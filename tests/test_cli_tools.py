@@ -99,3 +99,22 @@ def test_visual(tmp_path):
 
     png = draw(str(tmp_path / "v.bin"), str(tmp_path / "v.json"), str(tmp_path / "v.png"), layout="spring")
     assert (tmp_path / "v.png").stat().st_size > 1000 and png.endswith(".png")
+
+
+def test_ipc_group_control_plane_with_processes():
+    """The IPC transport's control plane (csrc/dist/ipc_group.cpp), host only,
+    with real processes: 4 ranks rendezvous 2000 times exchanging ping-pong
+    values, and a rank that is SIGKILLed, hangs past the timeout or aborts
+    makes every other rank fail (not hang)."""
+    import json
+    import subprocess
+
+    from bidirectional_bfs_amd._lib import tool_path
+
+    for mode, n in (("ok", 2000), ("kill", 50), ("hang", 50), ("abort", 50)):
+        r = subprocess.run([tool_path("ipc_group_check"), mode, "4", str(n)], capture_output=True, text=True,
+                           timeout=60)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert r.returncode == 0 and d["ok"], (mode, r.stdout, r.stderr)
+        if mode == "kill":
+            assert d["status"][1] == -9 and all(x == 10 for i, x in enumerate(d["status"]) if i != 1), d
