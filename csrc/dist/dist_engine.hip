@@ -2848,8 +2848,11 @@ struct DistBiBfs::Impl {
   // bounds it; more ranks' candidates (at most their frontier edges) must fit
   // the spill lists.  DistTuning::spec_stall_edges lowers it (tests force
   // host-planned rounds with it).
+  // (from the spill lists' allocation, not V.spill_cap: DistTuning::spill_cap
+  // shrinks the lists below what this guard assumes, which is how the tests
+  // make a round overflow them)
   uint32_t round_edge_cap() const {
-    const uint32_t hard = size == 1 ? 0xFFFFFFFFu : V.spill_cap;
+    const uint32_t hard = size == 1 ? 0xFFFFFFFFu : block_cap;
     return tune.spec_stall_edges ? std::min<uint32_t>(tune.spec_stall_edges, hard) : hard;
   }
 

@@ -108,8 +108,9 @@ struct DistTuning {
   bool world1_single = true;       // one rank: answer queries with the single-GPU engine over this rank's device
                                    // CSR (the whole graph; no copy), resident server included; false = the
                                    // partitioned rounds (solo workgroup + speculative rounds) at world size 1 too
-  uint32_t spill_cap = 0;          // test hook: > 0 caps the candidate spill lists below their allocation
-                                   // (a spill overflow then fails the search on every rank; the group lives on)
+  uint32_t spill_cap = 0;          // test hook: > 0 caps the candidate spill lists below their allocation while
+                                   // the round-size guard keeps assuming the allocation -- a round can then
+                                   // overflow them, which fails the search on every rank (the group lives on)
   bool stamps = false;             // per-round device stamps -> DistLevelStats::{expand,claim,exchange,status}_us
                                    // (adds one host wait + a copy per search: diagnostics, not serving)
 };
