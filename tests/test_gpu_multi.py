@@ -60,3 +60,17 @@ def test_dist_engine_torchrun_matches_oracle(repo_root):
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["world"] == world and d["checked"] > 0 and d["bad_total"] == 0, d
+
+
+@needs_multi
+@pytest.mark.skipif(not os.path.exists(MPIEXEC), reason="MPICH not installed")
+@pytest.mark.parametrize("np_", [2, 4])
+def test_mpi_bibfs_ipc_transport_across_gpus(np_):
+    """The HIP-IPC transport with one rank per GPU: every pull kernel reads the
+    peers' staging buffers over xGMI (peer access from hipIpcOpenMemHandle)."""
+    if np_ > _ngpus():
+        pytest.skip(f"needs {np_} GPUs")
+    r = run_mpi("mpi_bibfs", ["gnp:1000000::2", 0, 999999, "--verify", "--repeat", "2", "--comm", "ipc"], np=np_,
+                timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "Verify: OK" in r.stdout and f"Ranks: {np_} over ipc" in r.stdout, r.stdout
