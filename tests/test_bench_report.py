@@ -125,9 +125,9 @@ def test_cpu_comparison_fields_for_every_replicated_config():
     """Round-5 fields: every replicated config (headline and extras) carries
     the serial CPU engine's time on the SAME graph and pairs, the speedup over
     it, and how many of its pairs a unidirectional host BFS re-derived."""
-    f = bench.cpu_fields(0.9, 1.0, 1.2, 4, 0.06)
+    f = bench.cpu_fields(0.9, 1.0, 1.2, 4, 2.5, 0.06)
     assert f == {"cpu_serial_ms": 0.9, "cpu_serial_mean_ms": 1.0, "cpu_serial_query_ms": 1.2,
-                 "speedup_vs_cpu_serial_query": 20.0, "cpu_oracle_checked_pairs": 4}
+                 "cpu_serial_first_pass_ms": 2.5, "speedup_vs_cpu_serial_query": 20.0, "cpu_oracle_checked_pairs": 4}
     extra = {"gnp:10000000::1": dict({"ms_per_step": 0.06}, **f)}
     out = bench.report(_args(), 1, _head(), extra, {})
     e = out["detail"]["extra"]["gnp:10000000::1"]
@@ -148,5 +148,5 @@ def test_cpu_serial_reference_on_small_graph():
         r = eng.search(s, d)
         if r.found and r.hops > 0:
             pairs.append((s, d, int(r.hops)))
-    med, mean, e2e, ok = bench.cpu_serial_ms(spec, pairs, reps=2, oracle_pairs=2)
-    assert med > 0 and mean > 0 and e2e > 0 and ok == min(2, len(pairs))
+    med, mean, e2e, ok, first = bench.cpu_serial_ms(spec, pairs, reps=2, oracle_pairs=2)
+    assert med > 0 and mean > 0 and e2e > 0 and first > 0 and ok == min(2, len(pairs))
