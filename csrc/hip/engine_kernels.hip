@@ -2218,7 +2218,7 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
 // XCD's L2, LDS counters -- and checks for a meet after every pass:
 //   * a meet, or the whole frontier walked: the level is finished here
 //     (state, mirror, and the result when the search ends);
-//   * no meet within `budget` edges (whole passes): it stops, leaves its claims in
+//   * `budget` edges walked without a meet: it stops, leaves its claims in
 //     place and publishes the mirror with the level NOT advanced; the grid
 //     kernels then run the whole level (a vertex this probe claimed is
 //     visited and was meet-checked here, so redoing its edges claims nothing
@@ -2275,7 +2275,7 @@ __global__ __launch_bounds__(kProbeThreads, 1) void k_probe_level(GridParams<Off
     __syncthreads();
     const uint32_t Ec = fp[kProbeThreads];
     for (uint32_t base = 0; base < Ec; base += kProbeThreads * kProbeU) {
-      if (walked + min((uint32_t)(kProbeThreads * kProbeU), Ec - base) > budget) {  // (uniform)
+      if (walked >= budget) {
         stop = true;
         break;
       }
