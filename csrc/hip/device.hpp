@@ -306,13 +306,6 @@ void cleanup(const SearchBuffers& b, uint32_t n, uint32_t* done_ctr, uint32_t* h
 // levels > 1 chains that many device-planned levels: the finisher of each
 // plans the next one into aux (or ends the chain: search over, or a level the
 // Beamer rule declines, which publishes the mirror `seq` for the host).
-// Meet probe (k_probe_level): one workgroup walks a top-down level of `side`
-// up to its first meet, at most `budget` edges; finishes the level (mirror
-// `seq`, result `res_seq` when the search ends) or leaves it unadvanced for
-// the grid kernels.  probe_budget(): BIBFS_PROBE_EDGES, default 16384 (0 = off).
-void probe_level(const GraphView& g, const SearchBuffers& b, int side, uint32_t budget, dev::DevState* mirror,
-                 uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s);
-uint32_t probe_budget();
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,
                dev::DevState* mirror, uint32_t seq, const HostSide& h, uint32_t res_seq, uint32_t gate_seq,
                unsigned long long gate_ticks, int levels, hipStream_t s);

@@ -2204,163 +2204,6 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   if (P.mirror && !next && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
 }
 
-// ============================================================================
-// Meet probe: a top-down level in ONE workgroup, up to its first meet (round 5)
-// ============================================================================
-// On hub graphs a bidirectional search meets after a few thousand inspected
-// edges (the serial CPU engine on Kronecker 22: mean 7.2k, median 3.2k per
-// query), but the level it meets in is a hub level of 10^5-10^7 frontier
-// edges, and a grid level costs 20+ us even when its first batch finds the
-// meet (launch, chunk set-up, device-scope round trips, the finisher).  Every
-// meet of a single-side level has the same length, so the level may stop at
-// its first one.  This kernel walks the level's frontier edges in passes of
-// kProbeThreads x kProbeU on one workgroup -- workgroup-scope claims in its
-// XCD's L2, LDS counters -- and checks for a meet after every pass:
-//   * a meet, or the whole frontier walked: the level is finished here
-//     (state, mirror, and the result when the search ends);
-//   * `budget` edges walked without a meet: it stops, leaves its claims in
-//     place and publishes the mirror with the level NOT advanced; the grid
-//     kernels then run the whole level (a vertex this probe claimed is
-//     visited and was meet-checked here, so redoing its edges claims nothing
-//     twice and misses no meet).  The cost of a miss is ~budget edges on one CU.
-constexpr int kProbeThreads = 1024;
-constexpr int kProbeU = 4;  // edges per thread in flight per pass
-
-template <typename OffT>
-__global__ __launch_bounds__(kProbeThreads, 1) void k_probe_level(GridParams<OffT> P, uint32_t budget) {
-  __shared__ DevState sv;
-  __shared__ uint32_t fu[kProbeThreads];      // frontier chunk: vertices
-  __shared__ OffT fb[kProbeThreads];          // their row begins
-  __shared__ uint32_t fp[kProbeThreads + 1];  // exclusive degree prefix (+ the chunk's total)
-  __shared__ uint32_t wsum[kProbeThreads / kWave];
-  __shared__ uint32_t sq, smeet;              // appended by this probe; a meet vertex
-  __shared__ unsigned long long sne;          // degree sum of the vertices it claimed
-  constexpr uint32_t kWords = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const launch::SearchBuffers& b = P.b;
-  uint32_t* const w = reinterpret_cast<uint32_t*>(b.st);
-  if (tid < kWords) reinterpret_cast<uint32_t*>(&sv)[tid] = load_agent(&w[tid]);
-  if (tid == 0) {
-    sq = 0;
-    smeet = kEmpty;
-    sne = 0;
-  }
-  __syncthreads();
-  const int s = P.side, o = s ^ 1;
-  const uint32_t fbeg = sv.fbeg[s], F = sv.fend[s] - fbeg, qt0 = sv.qtail[s];
-  uint32_t walked = 0;  // (uniform)
-  bool stop = false;
-  for (uint32_t c0 = 0; c0 < F && !stop; c0 += kProbeThreads) {
-    const uint32_t i = c0 + tid, nv = min(F - c0, (uint32_t)kProbeThreads);
-    uint32_t u = 0, deg = 0;
-    OffT rb = 0;
-    if (i < F) {
-      u = b.queue[s][fbeg + i];
-      rb = P.row_off[u];
-      deg = (uint32_t)(P.row_off[u + 1] - rb);
-    }
-    fu[tid] = u;
-    fb[tid] = rb;
-    const uint32_t x = wave_incl_scan(deg);
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    if (wid == 0) {
-      const uint32_t y = lane < kProbeThreads / kWave ? wsum[lane] : 0u;
-      const uint32_t yi = wave_incl_scan(y);
-      if (lane < kProbeThreads / kWave) wsum[lane] = yi - y;
-      if (lane == kProbeThreads / kWave - 1) fp[kProbeThreads] = yi;
-    }
-    __syncthreads();
-    fp[tid] = x - deg + wsum[wid];
-    __syncthreads();
-    const uint32_t Ec = fp[kProbeThreads];
-    for (uint32_t base = 0; base < Ec; base += kProbeThreads * kProbeU) {
-      if (walked >= budget) {
-        stop = true;
-        break;
-      }
-      uint32_t vv[kProbeU], uu[kProbeU], vd[kProbeU];
-      bool ok[kProbeU];
-#pragma unroll
-      for (int k = 0; k < kProbeU; ++k) {
-        const uint32_t e = base + (uint32_t)k * kProbeThreads + tid;
-        ok[k] = e < Ec;
-        vv[k] = uu[k] = 0;
-        vd[k] = ~0u;
-        if (ok[k]) {
-          uint32_t lo = 0, hi = nv;  // last frontier vertex whose edges start at or before e
-          while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (fp[mid] <= e) lo = mid;
-            else hi = mid;
-          }
-          uu[k] = fu[lo];
-          const OffT kk = fb[lo] + (OffT)(e - fp[lo]);
-          if (P.padj8) {
-            const unsigned long long pw = P.padj8[kk];
-            vv[k] = launch::pack8_v(pw);
-            vd[k] = launch::pack8_deg(pw);
-          } else if (P.padj) {
-            const uint4 q = P.padj[kk];
-            vv[k] = q.x;
-            vd[k] = q.y;
-          } else {
-            vv[k] = P.col[kk];
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kProbeU; ++k) {
-        const uint32_t v = vv[k], wd = v >> 5, bit = 1u << (v & 31);
-        bool mine = false;
-        if (ok[k])
-          mine = !(__hip_atomic_fetch_or(&b.vis[s][wd], bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & bit);
-        const unsigned long long mask = __ballot(mine);
-        if (!mask) continue;  // wave-uniform
-        uint32_t dg = 0;
-        if (mine) {
-          b.parent[s][v] = uu[k];
-          dg = vd[k] != ~0u ? vd[k] : (uint32_t)(P.row_off[v + 1] - P.row_off[v]);
-          if (b.vis[o][wd] & bit) atomicCAS(&smeet, kEmpty, v);  // (every meet of the level: one length)
-        }
-        const int leader = __ffsll((long long)mask) - 1;
-        uint32_t pos = 0;
-        if ((int)lane == leader) pos = atomicAdd(&sq, (uint32_t)__popcll(mask));
-        pos = __shfl(pos, leader);
-        if (mine) b.queue[s][qt0 + pos + mbcnt64(mask)] = v;
-        const unsigned long long ds = wave_sum((unsigned long long)dg);
-        if ((int)lane == leader) atomicAdd(&sne, ds);
-      }
-      walked += min((uint32_t)(kProbeThreads * kProbeU), Ec - base);
-      __syncthreads();
-      if (smeet != kEmpty) {  // uniform (after the barrier)
-        stop = true;
-        break;
-      }
-    }
-    __syncthreads();  // (fu / fb / fp are rewritten by the next chunk)
-  }
-  const bool complete = smeet != kEmpty || !stop;
-  if (tid == 0) {
-    sv.qtail[s] = qt0 + sq;
-    sv.nedges = sne;  // (a grid level that redoes it adds its own claims to this)
-    if (complete) {
-      if (smeet != kEmpty) {
-        sv.meet = smeet;
-        sv.meet_side = (uint32_t)s;
-      }
-      finish_state(sv, b, s, 1, 0);
-    }
-  }
-  __syncthreads();
-  if (tid < kWords) w[tid] = reinterpret_cast<const uint32_t*>(&sv)[tid];
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __threadfence();
-  __syncthreads();
-  if (complete && P.res_seq && sv.status != kRunning) publish_result(b, P.h, sv, P.res_seq, P.n);
-  if (P.mirror && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
-}
-
 // Seed a search for the grid engine / step-wise API.
 template <typename OffT>
 __global__ void k_seed(const OffT* row_off, launch::SearchBuffers b, uint32_t src, uint32_t dst) {
@@ -2655,26 +2498,6 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   if (g.row_off32) launch_one(gp<uint32_t>(g, b, side));
   else launch_one(gp<uint64_t>(g, b, side));
   HIP_CHECK(hipGetLastError());
-}
-
-void probe_level(const GraphView& g, const SearchBuffers& b, int side, uint32_t budget, dev::DevState* mirror,
-                 uint32_t seq, const HostSide& h, uint32_t res_seq, hipStream_t s) {
-  auto launch_one = [&](auto P) {
-    using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
-    P.mirror = mirror, P.seq = seq, P.trace = 0, P.h = h, P.res_seq = res_seq;
-    k_probe_level<OffT><<<1, kProbeThreads, 0, s>>>(P, budget);
-  };
-  if (g.row_off32) launch_one(gp<uint32_t>(g, b, side));
-  else launch_one(gp<uint64_t>(g, b, side));
-  HIP_CHECK(hipGetLastError());
-}
-
-uint32_t probe_budget() {
-  static const uint32_t v = [] {
-    const char* e = std::getenv("BIBFS_PROBE_EDGES");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 16384u;
-  }();
-  return v;
 }
 
 void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max_deg, double alpha,

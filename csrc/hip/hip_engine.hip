@@ -753,30 +753,11 @@ struct HipBiBfs::Impl {
     fbits_valid[0] = fbits_valid[1] = false;
     int turn = 0;
     const int trace = opt.trace ? 1 : 0;
-    // hub graphs: a top-down level is first probed by one workgroup up to
-    // its first meet (k_probe_level); the grid runs it only if the probe
-    // walked its edge budget without one
-    const uint32_t probe = max_deg > 64 && !trace && !opt.force_grid ? launch::probe_budget() : 0u;
     for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
       if (guard == 0 && !mirror_valid) sync_state();  // state left by the seed
       if (h_state->status != kRunning || h_state->meet != kEmpty) break;
       const int s = choose_side(opt, turn);
       const int mode = choose_mode(s, opt);
-      if (probe && mode == 1) {
-        const uint32_t lv0 = h_state->levels;
-        const uint32_t ls = ++level_seq == 0 ? ++level_seq : level_seq;
-        launch::probe_level(view(), buf, s, probe, h_state, ls, launch::HostSide{gres, h_path, h_path_cap, h_state},
-                            res_seq, stream);
-        if (res_seq) cleanup_async(true);
-        wait_level();
-        stats.probe_levels++;
-        if (h_state->levels != lv0) {  // the probe finished the level (met, or walked it all)
-          stats.grid_levels++;
-          stats.probe_hits++;
-          fbits_valid[s] = false;
-          continue;
-        }
-      }
       grid_level(s, mode, trace);
       stats.grid_levels++;
       if (mode == 2) stats.bottomup_levels++;

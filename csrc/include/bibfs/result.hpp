@@ -44,8 +44,6 @@ struct SearchStats {
   uint64_t edges_inspected = 0;
   uint64_t visited = 0;        // vertices claimed by both sides (incl. src/dst)
   int grid_levels = 0;         // GPU: levels run by the grid engine
-  int probe_levels = 0;        // GPU: hub-graph levels first probed by one workgroup (k_probe_level) ...
-  int probe_hits = 0;          // ... and finished by it (met early, or walked whole within its budget)
   int bottomup_levels = 0;
   bool handoff = false;        // GPU: persistent engine handed off to the grid engine
   double lds_ms = 0.0;         // GPU: device time of the one-workgroup (LDS / tiny) phase

@@ -40,8 +40,6 @@ py::dict stats_dict(const SearchStats& s) {
   d["edges_inspected"] = s.edges_inspected;
   d["visited"] = s.visited;
   d["grid_levels"] = s.grid_levels;
-  d["probe_levels"] = s.probe_levels;
-  d["probe_hits"] = s.probe_hits;
   d["bottomup_levels"] = s.bottomup_levels;
   d["handoff"] = s.handoff;
   d["lds_ms"] = s.lds_ms;
