@@ -105,19 +105,6 @@ static_assert(kTinyUnroll == 4, "two 16-byte loads per neighbour");
 #define BIBFS_TINY_LAZY2 0
 #endif
 constexpr bool kLazy2 = BIBFS_TINY_LAZY2;
-// 1 = a new vertex's records leave out the edge back to the vertex it was
-// reached from.  The CSR is symmetric (graph.hpp), so that edge is always
-// there, and its target is visited by the same side: claiming it again can
-// neither add a vertex nor find a meet.  On G(n, 2.2/n) a reached vertex has
-// 1 + 2.2 edges on average (size-biased Poisson), so ~30% of all records --
-// their claims, their speculative loads and their share of the round size
-// that decides single-wave vs all-wave rounds -- go.  A record slot is kept
-// for deg - 1 words whatever the input, so an asymmetric CSR loses a word,
-// never overruns the buffer.
-#ifndef BIBFS_TINY_PRUNE
-#define BIBFS_TINY_PRUNE 1
-#endif
-constexpr bool kPrune = BIBFS_TINY_PRUNE;
 __device__ __forceinline__ void load_first4(unsigned long long (&w)[kTinyUnroll],
                                             const unsigned long long* __restrict__ p, uint32_t deg) {
   if (deg) {  // (exec-masked per lane)
@@ -218,8 +205,7 @@ struct Work {
   unsigned long long nbw[NB][kTinyUnroll];  // the neighbour's first edges' words (speculative)
   unsigned long long oth[NB];        // the other side's visited word of the neighbour
   bool act[NB], s1[NB], nw[NB];
-  uint32_t deg[NB];                  // records of the neighbour when this lane claimed it (else 0)
-  uint32_t pv[NB];                   // (kPrune) the vertex the item was reached from
+  uint32_t deg[NB];                  // degree of the neighbour when this lane claimed it (else 0)
 };
 
 // Round step 1: read the records, and at once issue the loads of each
@@ -229,7 +215,7 @@ struct Work {
 template <int NB, bool kSpec>
 __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint32_t i0, uint32_t stride, int nb,
                                             const unsigned long long* __restrict__ tadj,
-                                            unsigned long long (*VIS)[kTW], const uint32_t (*QU)[kTinyQ]) {
+                                            unsigned long long (*VIS)[kTW]) {
   unsigned long long old[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -238,8 +224,6 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
     W.s1[b] = i >= R.x0;
     W.rec[b] = 1ull;  // an idle lane: vertex 0, base 0, degree 1
     if (b < nb && W.act[b]) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
-    // (an idle lane reads entry 0, the root)
-    W.pv[b] = kPrune && b < nb ? QU[W.s1[b] ? 1 : 0][tw_pq(W.rec[b])] >> kQBits : 0u;
   }
   if (kSpec) {
 #pragma unroll
@@ -284,8 +268,7 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
   for (int b = 0; b < NB; ++b) {
     const uint32_t bt = tw_v(W.rec[b]) & 31;
     W.nw[b] = b < nb && W.act[b] && ((((uint32_t)old[b] | (uint32_t)(old[b] >> 32)) >> bt) & 1u) == 0;
-    const uint32_t d = tw_deg(W.rec[b]);
-    W.deg[b] = W.nw[b] ? (kPrune ? max(d, 1u) - 1u : d) : 0u;
+    W.deg[b] = W.nw[b] ? tw_deg(W.rec[b]) : 0u;
   }
 }
 
@@ -298,14 +281,13 @@ __device__ __forceinline__ void round_fetch(Work<NB>& W, int nb, const unsigned 
   for (int b = 0; b < NB; ++b) {
     if (b >= nb) continue;
     const uint32_t base = tw_base(W.rec[b]);
-    const uint32_t fd = W.nw[b] ? tw_deg(W.rec[b]) : 0u;  // every edge word (kPrune drops one after the load)
     if (kX4) {
-      load_first4(W.nbw[b], tadj + base, fd);
+      load_first4(W.nbw[b], tadj + base, W.deg[b]);
       continue;
     }
 #pragma unroll
     for (uint32_t j = 0; j < kTinyUnroll; ++j)
-      if (j < fd) W.nbw[b][j] = tadj[base + j];
+      if (j < W.deg[b]) W.nbw[b][j] = tadj[base + j];
   }
 }
 
@@ -389,34 +371,11 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
     const uint32_t dd = rok ? deg : 0u;
     const unsigned long long tag = (unsigned long long)q << 52;
     // past the degree (or with nothing to store) a store goes to the lane's junk slot
-    if (!kPrune) {
 #pragma unroll
-      for (uint32_t j = 0; j < kTinyUnroll; ++j) *(j < dd ? out + j : junk) = W.nbw[b][j] | tag;
-      if (__ballot(rok && deg > kTinyUnroll)) {  // rare: a vertex of degree > 4
-        const uint32_t base = tw_base(W.rec[b]);
-        for (uint32_t j = kTinyUnroll; rok && j < deg; ++j) out[j] = tadj[base + j] | tag;
-      }
-    } else {  // the same, compacted past the first word that leads back to pv
-      const uint32_t fdeg = tw_deg(W.rec[b]), u = W.pv[b];
-      uint32_t k = 0;
-      bool found = false;
-#pragma unroll
-      for (uint32_t j = 0; j < kTinyUnroll; ++j) {
-        const bool back = j < fdeg && !found && tw_v(W.nbw[b][j]) == u;
-        found |= back;
-        const bool st = j < fdeg && !back && k < dd;
-        *(st ? out + k : junk) = W.nbw[b][j] | tag;
-        k += st;
-      }
-      if (__ballot(rok && fdeg > kTinyUnroll)) {  // rare: a vertex of degree > 4
-        const uint32_t base = tw_base(W.rec[b]);
-        for (uint32_t j = kTinyUnroll; rok && j < fdeg; ++j) {
-          const unsigned long long w = tadj[base + j];
-          const bool back = !found && tw_v(w) == u;
-          found |= back;
-          if (!back && k < dd) out[k++] = w | tag;
-        }
-      }
+    for (uint32_t j = 0; j < kTinyUnroll; ++j) *(j < dd ? out + j : junk) = W.nbw[b][j] | tag;
+    if (__ballot(rok && deg > kTinyUnroll)) {  // rare: a vertex of degree > 4
+      const uint32_t base = tw_base(W.rec[b]);
+      for (uint32_t j = kTinyUnroll; rok && j < deg; ++j) out[j] = tadj[base + j] | tag;
     }
     const uint32_t bt = v & 31;
     const uint32_t ost = (uint32_t)((W.oth[b] >> bt) & 1ull) | (uint32_t)((W.oth[b] >> (bt + 32)) & 1ull) << 1;
@@ -557,7 +516,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           const uint32_t x0 = T.E0, x1 = T.E1;
           const RoundCtx X = make_ctx(x0, x1, T.cb0, T.cb1, T.d0, T.d1);
           Work<NB> W;
-          round_issue<NB, true>(W, X, lane, 64, NB, P.tadj, VIS, QU);
+          round_issue<NB, true>(W, X, lane, 64, NB, P.tadj, VIS);
           Counts<NB> K;
           round_count<NB>(K, W);
           const uint32_t ovf =
@@ -643,7 +602,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         constexpr int NB = decltype(nbc)::value;
         const int nb = (NB == 2 && wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
         Work<NB> W;
-        round_issue<NB, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS, QU);
+        round_issue<NB, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS);
         if (!kSpecAll) round_fetch<NB>(W, nb, P.tadj);
         Counts<NB> K;
         round_count<NB>(K, W);
