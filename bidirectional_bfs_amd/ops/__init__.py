@@ -208,6 +208,19 @@ class HipEngine:
     def auto_max_degree(self, deg: int) -> None:
         self._e.auto_max_degree = int(deg)
 
+    @property
+    def lds_probe_edges(self) -> int:
+        """Meet probe of the LDS engine on hub graphs: frontier edges of a level
+        that does not fit LDS tested against the other side's visited set
+        before the level is handed to the grid engine (default 16384, env
+        BIBFS_LDS_PROBE_EDGES; 0 = off).  ``stats["probe_edges"]`` /
+        ``stats["probe_hit"]`` report it per search."""
+        return self._e.lds_probe_edges
+
+    @lds_probe_edges.setter
+    def lds_probe_edges(self, edges: int) -> None:
+        self._e.lds_probe_edges = int(edges)
+
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:
         self._e.begin(int(src), int(dst))

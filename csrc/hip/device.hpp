@@ -61,7 +61,7 @@ struct HostResult {
   uint32_t path_len;      // hops + 1 when found
   uint32_t path_on_device;// 1 when the path did not fit the pinned buffer
   uint32_t lds_levels;
-  uint32_t pad;
+  uint32_t probe;         // LDS meet probe: frontier edges it read | 1 << 31 when it found the meet
   unsigned long long rt_begin, rt_end;  // s_memrealtime (100 MHz) around the LDS search
   unsigned long long rt_pickup;         // resident server: when the request was seen (0 otherwise)
   unsigned long long rt_walk;           // grid publish: when its path walk started (0: no grid walk)
@@ -173,6 +173,9 @@ struct GraphView {
   // graphs with n < 2^25, nnz < 2^29 and every degree < 1023 -- half the
   // bytes of padj, so a 10M-vertex graph's (176 MB) stays in the MALL
   const unsigned long long* padj8 = nullptr;
+  // LDS meet probe before a hand-off: frontier edges it may read (hub graphs
+  // only; HipBiBfs::set_lds_probe_edges, 0 = off)
+  uint32_t probe_edges = 0;
 };
 __host__ __device__ inline unsigned long long pack8(uint32_t v, uint64_t base, uint64_t deg) {
   return (unsigned long long)v << 39 | base << 10 | deg;
@@ -260,6 +263,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
                 uint32_t dst, uint32_t seq, int side_policy, int trace, int pin_xcc, uint32_t* ticket,
                 int lockstep, hipStream_t s);
 int lds_threads();
+uint32_t lds_probe_budget();  // BIBFS_LDS_PROBE_EDGES (default 16384; 0 = no meet probe before a hand-off)
 size_t lds_bytes(bool wide);
 void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers& b_alt, const HostSide& h,
                 dev::ServerBox* box, uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,

@@ -188,6 +188,9 @@ struct LdsParams {
   // hash-set searches (kWaveHashG): run the all-wave rounds (graphs without
   // hubs; a hub's records are written by one lane)
   int wave_hash = 0;
+  // meet probe before a hand-off: frontier edges it may read (0 = off; see
+  // lds_meet_probe)
+  uint32_t probe = 0;
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -288,7 +291,122 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 struct LevelPlan {
   uint32_t status;
   uint32_t E[2], cur[2], off[2], nxt[2], qbase[2], depth[2];
+  uint32_t pside, pfb, pcnt;  // kProbing: the side that does not fit, its frontier in the global queue
 };
+
+// Internal plan status: probe the level that does not fit LDS for a meet
+// before handing it to the grid (never published).
+constexpr uint32_t kProbing = 7;
+constexpr uint32_t kProbeU = 4;  // frontier edges per thread per probe pass
+
+// Meet probe (all waves of the LDS engine, read-only).  The next level of
+// side q does not fit LDS, so the search would hand off to the grid engine.
+// No meet has been found yet, so every vertex of the other side adjacent to
+// q's frontier sits at that side's frontier depth (a shallower one would
+// have claimed -- or been claimed from -- the frontier vertex already, and
+// the claim would have seen the meet): EVERY such edge ends the search with
+// the same, shortest, length dq + 1 + do.  The CPU engine stops at the first
+// one, after a few thousand edges on hub graphs; the grid level reads them
+// all.  So before handing off, the frontier's edges are read in passes of
+// kLdsThreads * kProbeU (queue order, edge-parallel over a chunk of 1024
+// frontier vertices: block scan of their degrees, binary search per edge)
+// and tested against the other side's LDS visited set -- no claims, no
+// state written -- until an edge hits or `budget` edges were read.
+// Returns (u << 32) | v of a hit (u in q's frontier, v visited by the other
+// side), or ~0; *walked = edges read.  Every wave calls it (barriers inside).
+template <typename OffT, bool kBm>
+__device__ unsigned long long lds_meet_probe(const LdsParams<OffT>& P, int q, uint32_t fb, uint32_t F,
+                                             uint32_t budget, const uint32_t* Ho,
+                                             const unsigned long long* Wo, void* scratch, uint32_t* walked_out) {
+  __shared__ unsigned long long pr_hit;
+  __shared__ uint32_t pr_wsum[kLdsThreads / kWave], pr_total;
+  const int tid = threadIdx.x, wid = tid >> 6;
+  const uint32_t lane = __lane_id();
+  uint32_t* su = static_cast<uint32_t*>(scratch);                 // [kLdsThreads] frontier vertex
+  OffT* sbp = reinterpret_cast<OffT*>(su + kLdsThreads);           // its row base
+  uint32_t* sEb = reinterpret_cast<uint32_t*>(sbp + kLdsThreads);  // exclusive prefix of the (clamped) degrees
+  const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
+  if (tid == 0) pr_hit = ~0ull;
+  uint32_t walked = 0;
+  bool stop = false;
+  for (uint32_t c0 = 0; c0 < F && !stop; c0 += kLdsThreads) {
+    const uint32_t i = c0 + (uint32_t)tid;
+    uint32_t u = 0, d = 0;
+    OffT b = 0;
+    if (i < F) {
+      u = load_agent(&qu[fb + i]);  // queue entries were written by this search (L2)
+      b = P.row_off[u];
+      d = (uint32_t)min((OffT)(P.row_off[u + 1] - b), (OffT)(1u << 20));  // sums stay < 2^31
+    }
+    su[tid] = u;
+    sbp[tid] = b;
+    const uint32_t incl = wave_incl_scan(d);
+    if (lane == kWave - 1) pr_wsum[wid] = incl;
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t a = 0;
+      for (int k = 0; k < kLdsThreads / kWave; ++k) {
+        const uint32_t t = pr_wsum[k];
+        pr_wsum[k] = a;
+        a += t;
+      }
+      pr_total = a;
+    }
+    __syncthreads();
+    sEb[tid] = incl - d + pr_wsum[wid];
+    const uint32_t Ec = uni(pr_total);
+    __syncthreads();
+    for (uint32_t base = 0; base < Ec; base += kLdsThreads * kProbeU) {
+      const uint32_t pass = min(kLdsThreads * kProbeU, Ec - base);
+      if (walked + pass > budget) {  // (uniform)
+        stop = true;
+        break;
+      }
+      walked += pass;
+      uint32_t v[kProbeU], uu[kProbeU];
+      bool ok[kProbeU];
+#pragma unroll
+      for (uint32_t j = 0; j < kProbeU; ++j) {
+        const uint32_t e = base + j * kLdsThreads + (uint32_t)tid;
+        ok[j] = e < Ec;
+        uint32_t lo = 0, hi = kLdsThreads;
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (sEb[mid] <= e) lo = mid;
+          else hi = mid;
+        }
+        uu[j] = su[lo];
+        v[j] = ok[j] ? P.col[sbp[lo] + (OffT)(e - sEb[lo])] : 0u;  // every pass's loads in flight together
+      }
+      unsigned long long best = ~0ull;
+#pragma unroll
+      for (uint32_t j = 0; j < kProbeU; ++j) {
+        bool hit;
+        if constexpr (kBm) hit = ok[j] && bm_state(Wo, v[j]) != 0u;
+        else hit = ok[j] && hash_find(Ho, v[j]) != kEmpty;
+        const unsigned long long key = ((unsigned long long)uu[j] << 32) | v[j];
+        if (hit && key < best) best = key;
+      }
+      if (__ballot(best != ~0ull)) {
+        unsigned long long m = best;
+        for (int off = 32; off >= 1; off >>= 1) {
+          const unsigned long long y = __shfl_xor(m, off);
+          m = y < m ? y : m;
+        }
+        if (lane == 0) atomicMin(&pr_hit, m);
+      }
+      __syncthreads();
+      if (uni((uint32_t)(pr_hit >> 32)) != 0xffffffffu) {
+        stop = true;
+        break;
+      }
+    }
+    __syncthreads();  // the chunk's LDS arrays are read until here
+  }
+  *walked_out = walked;
+  const unsigned long long r = pr_hit;
+  return ((unsigned long long)uni((uint32_t)(r >> 32)) << 32) | uni((uint32_t)r);
+}
 
 // One whole search by one workgroup.  `elected`: the caller already owns the
 // search (the resident server); otherwise the block runs the XCD election.
@@ -919,6 +1037,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
   wave_rounds();  // every wave; the replicated state continues below
   uint32_t fstatus = kRunning;
+  bool probed = false, probe_hit = false;
+  uint32_t probe_walked = 0;
   for (;;) {
     if (wid == 0) {
       // ---- wave 0 alone: dual-side (lockstep) and single-side rounds while
@@ -934,8 +1054,9 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         const bool fq = q ? f1 : f0;
         const unsigned long long eq = q ? s1.fed : s0.fed;
         if (!dual && (!fq || eq > kSmallEdges)) {
-          if (!fq) status = kHandoff;
-          break;  // big level (all waves) or hand-off
+          // a level that does not fit: probe it for a meet first (hub graphs)
+          if (!fq) status = (P.probe && !P.batch && !probed) ? kProbing : kHandoff;
+          break;  // big level (all waves), probe or hand-off
         }
         unsigned long long ts0 = 0;
         if (kStamp && tid == 0) ts0 = stamp();
@@ -991,6 +1112,9 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         p.nxt[1] = both ? fb : fa;
         p.qbase[0] = s0.qend, p.qbase[1] = s1.qend;
         p.depth[0] = (uint32_t)s0.depth, p.depth[1] = (uint32_t)s1.depth;
+        p.pside = (uint32_t)q;
+        p.pfb = q ? s1.fbeg : s0.fbeg;
+        p.pcnt = q ? s1.cnt : s0.cnt;
         plan = p;
       }
     }
@@ -998,6 +1122,33 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     unsigned long long ts0 = 0, ts1 = 0, ts2 = 0;
     if (kStamp && tid == 0) ts0 = stamp();
     fstatus = uni(plan.status);
+    if (fstatus == kProbing) {
+      const int pq = (int)uni(plan.pside);
+      uint32_t walked = 0;
+      const unsigned long long hit =
+          lds_meet_probe<OffT, kBm>(P, pq, uni(plan.pfb), uni(plan.pcnt), P.probe, pq ? H[0] : H[1],
+                                    W(pq ^ 1), &R[0][0], &walked);
+      probed = true;
+      probe_walked = walked;
+      if (wid == 0) {
+        if (hit != ~0ull) {
+          const uint32_t u = (uint32_t)(hit >> 32), v = (uint32_t)hit;
+          const uint32_t dq = pq ? (uint32_t)s1.depth : (uint32_t)s0.depth;
+          const uint32_t dob = pq ? (uint32_t)s0.depth : (uint32_t)s1.depth;
+          if (lane == 0) (pq ? P.b.parent[1] : P.b.parent[0])[v] = u;  // the claim the probe did not make
+          meet = v;
+          md0 = pq ? dob : dq + 1;
+          md1 = pq ? dq + 1 : dob;
+          ++levels;  // the probed level ended the search
+          einsp += walked;
+          status = kFound;
+          probe_hit = true;
+        } else {
+          status = kHandoff;
+        }
+      }
+      continue;  // wave 0 publishes the final plan at the top of the loop
+    }
     if (fstatus != kRunning) break;
     // ---- big level: every wave, one edge per lane; side 0's records then side
     // 1's (virtual list as in dual_level); per-side LDS counters place the
@@ -1222,6 +1373,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       rv.depth[1] = status == kFound ? (int32_t)md1 : s1.depth;
       rv.path_len = path_len;
       rv.path_on_device = path_dev ? 1u : path_skip ? 2u : 0u;
+      rv.probe = min(probe_walked, 0x7fffffffu) | (probe_hit ? 0x80000000u : 0u);
       rv.rt_begin = rt0;
       rv.rt_end = __builtin_amdgcn_s_memrealtime();
     }
@@ -1237,7 +1389,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     if (kStamp && tid == 0) e5 = __builtin_amdgcn_s_memtime();
     // write-through (system-scope) stores: no L2 writeback needed for the host;
     // seq (word 0) is written last, below
-    if (lane >= 1 && lane < kResW && lane != offsetof(HostResult, pad) / 4)
+    if (lane >= 1 && lane < kResW)
       __hip_atomic_store(reinterpret_cast<uint32_t*>(Rr) + lane, pub_img[32 + lane], __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -2357,6 +2509,23 @@ namespace launch {
 
 int lds_threads() { return kLdsThreads; }
 
+uint32_t lds_probe_budget() {
+  // BIBFS_LDS_PROBE_EDGES: frontier edges the meet probe may read before a
+  // hand-off (0 = off)
+  static const uint32_t b = [] {
+    const char* e = std::getenv("BIBFS_LDS_PROBE_EDGES");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 16384u;
+  }();
+  return b;
+}
+
+// hub graphs only: on a graph without hubs (G(n, p)) the other side holds a
+// vanishing share of the vertices when a level leaves LDS, so a probe of a
+// few thousand edges almost never hits
+static uint32_t probe_for(const GraphView& g, int trace) {
+  return (trace == 0 && g.max_deg > 64) ? g.probe_edges : 0u;
+}
+
 size_t lds_bytes(bool wide) {
   return 2 * kHashSize * 4 + 4 * (wide ? LdsRec<uint64_t>::cap * 16 : LdsRec<uint32_t>::cap * 8) + 128;
 }
@@ -2370,6 +2539,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
     LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
+    P.probe = probe_for(g, trace);
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
       if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -2381,6 +2551,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   } else {
     LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
+    P.probe = probe_for(g, trace);
     if (trace == 2)
       k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
     else
@@ -2398,6 +2569,7 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;
   P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
+  P.probe = probe_for(g, 0);
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);

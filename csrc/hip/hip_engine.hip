@@ -80,6 +80,7 @@ struct HipBiBfs::Impl {
     const char* e = std::getenv("BIBFS_AUTO_MAX_DEG");
     return e ? std::strtoull(e, nullptr, 10) : 64ull;
   }();
+  uint32_t probe_edges = launch::lds_probe_budget();  // LDS meet probe (HipBiBfs::set_lds_probe_edges)
   bool auto_on = [] {
     const char* e = std::getenv("BIBFS_AUTO_HANDOFF");
     return !(e && e[0] == '0');
@@ -278,7 +279,7 @@ struct HipBiBfs::Impl {
   vid_t step_src = 0, step_dst = 0;
 
   launch::GraphView view() const {
-    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj, max_deg, d_padj8};
+    return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj, max_deg, d_padj8, probe_edges};
   }
 
   bool server_usable() const { return d_row_off32 != nullptr && n > 0 && n <= 0x7fffffffu; }
@@ -1222,6 +1223,12 @@ int HipBiBfs::auto_levels() const { return p_->auto_levels; }
 void HipBiBfs::set_auto_max_degree(uint64_t deg) { p_->auto_max_deg = deg; }
 uint64_t HipBiBfs::auto_max_degree() const { return p_->auto_max_deg; }
 bool HipBiBfs::auto_handoff() const { return p_->auto_on; }
+void HipBiBfs::set_lds_probe_edges(uint32_t edges) {
+  if (edges == p_->probe_edges) return;
+  p_->probe_edges = edges;
+  p_->stop_server();  // a running LDS server holds the old budget: relaunched by the next search
+}
+uint32_t HipBiBfs::lds_probe_edges() const { return p_->probe_edges; }
 uint64_t HipBiBfs::tiny_overflows() const { return p_->tiny_overflows; }
 void HipBiBfs::set_host_stamps(bool on) {
   p_->host_stamps_on = on;
@@ -1286,6 +1293,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   bool grid = opt.force_grid;
   double lds_ms = 0.0;
   int stats_handoff_levels = -1;  // levels the LDS phase ran before a hand-off
+  uint32_t lds_probe = 0;         // HostResult::probe of the LDS phase
   bool use_auto = false, auto_final = false;  // device hand-off (grid_auto) behind a resident search
   uint32_t pub_auto = 0, auto_ls = 0, auto_tag = 0;
   grid = grid || I.n > 0x7fffffffu;
@@ -1330,6 +1338,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
       // every resident search answers through h_res (a hand-off too); the
       // auto level behind it publishes into its own record, h_gres
       lds_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;
+      lds_probe = I.h_res->probe;
       if (I.h_res->status == kHandoff) {
         grid = true;
         stats.handoff = true;
@@ -1368,6 +1377,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         I.wait_seq(seq);
       }
       lds_ms = (double)(I.h_res->rt_end - I.h_res->rt_begin) * 1e-5;  // 100 MHz
+      lds_probe = I.h_res->probe;
       if (I.h_res->status == kHandoff) {
         grid = true;
         stats.handoff = true;
@@ -1414,6 +1424,10 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   // on the query path); a search that never ran in LDS is timed with events
   const bool timed_by_events = grid && !stats.handoff;
   if (timed_by_events) HIP_CHECK(hipEventRecord(I.ev1, I.stream));
+  if (!timed_by_events) {  // the LDS engine ran: its meet probe's record
+    stats.probe_edges = lds_probe & 0x7fffffffu;
+    stats.probe_hit = (lds_probe >> 31) != 0;
+  }
   SearchResult r = I.collect(grid ? *I.gres : *I.h_res, opt, std::move(stats));
   r.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   r.search_ms = lds_ms;

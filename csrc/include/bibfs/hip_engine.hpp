@@ -116,6 +116,13 @@ class HipBiBfs {
   // (default 64: hub graphs keep host-planned levels; env BIBFS_AUTO_MAX_DEG).
   void set_auto_max_degree(uint64_t deg);
   uint64_t auto_max_degree() const;
+  // Meet probe of the LDS engine (hub graphs, largest degree > 64): before a
+  // level that does not fit LDS is handed to the grid engine, up to this many
+  // of its frontier edges are tested against the other side's visited set;
+  // any hit ends the search with the shortest length (default 16384; env
+  // BIBFS_LDS_PROBE_EDGES; 0 = off).
+  void set_lds_probe_edges(uint32_t edges);
+  uint32_t lds_probe_edges() const;
 
   // --- step-wise API (parity with the reference's per-level C API,
   //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)

@@ -49,6 +49,8 @@ struct SearchStats {
   double lds_ms = 0.0;         // GPU: device time of the one-workgroup (LDS / tiny) phase
   int lds_levels = 0;          // GPU: levels that phase ran (before a hand-off)
   double walk_ms = 0.0;        // GPU: the grid publish's path walk + result record (hand-off searches)
+  uint64_t probe_edges = 0;    // GPU: frontier edges the LDS engine's meet probe read before a hand-off
+  bool probe_hit = false;      // GPU: ... and it found the meet (no hand-off)
   std::vector<LevelTrace> trace;
 };
 

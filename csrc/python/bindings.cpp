@@ -45,6 +45,8 @@ py::dict stats_dict(const SearchStats& s) {
   d["lds_ms"] = s.lds_ms;
   d["lds_levels"] = s.lds_levels;
   d["walk_ms"] = s.walk_ms;
+  d["probe_edges"] = s.probe_edges;
+  d["probe_hit"] = s.probe_hit;
   py::list tr;
   for (const auto& t : s.trace) {
     py::dict x;
@@ -340,6 +342,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("auto_gate_misses", &HipBiBfs::auto_gate_misses)
       .def_property("auto_levels", &HipBiBfs::auto_levels, &HipBiBfs::set_auto_levels)
       .def_property("auto_max_degree", &HipBiBfs::auto_max_degree, &HipBiBfs::set_auto_max_degree)
+      .def_property("lds_probe_edges", &HipBiBfs::lds_probe_edges, &HipBiBfs::set_lds_probe_edges)
       .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
       .def_property_readonly("last_batch_fallbacks", &HipBiBfs::last_batch_fallbacks)
       .def("set_batch_tuning", &HipBiBfs::set_batch_tuning, py::arg("lds_first") = -1, py::arg("threads") = 0)

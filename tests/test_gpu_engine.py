@@ -291,6 +291,8 @@ def test_resident_back_to_back_handoffs(gpu_engine):
     (engine stream) still reads and clears the global visited words."""
     g = kronecker(22, 16, 5)
     gpu_engine.load(g)
+    probe0 = gpu_engine.lds_probe_edges
+    gpu_engine.lds_probe_edges = 0  # every search leaves LDS (no meet probe)
     rnd = random.Random(3)
     pairs = []
     while len(pairs) < 8:
@@ -307,6 +309,7 @@ def test_resident_back_to_back_handoffs(gpu_engine):
             if i % 100 == 0:
                 check_result(g.csr, s, d, r.hops, r.path, h)
     finally:
+        gpu_engine.lds_probe_edges = probe0
         gpu_engine.set_resident(False)
 
 
@@ -323,6 +326,8 @@ def test_resident_auto_handoff_vs_oracle(gpu_engine, spec):
     pairs = pairs_for(g.n, 40, 5)
     truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
     gpu_engine.set_resident(True)
+    probe0 = gpu_engine.lds_probe_edges
+    gpu_engine.lds_probe_edges = 0  # hub graphs: searches must leave LDS
     try:
         for on in (True, False, True):
             gpu_engine.auto_handoff = on
@@ -341,6 +346,7 @@ def test_resident_auto_handoff_vs_oracle(gpu_engine, spec):
             check_result(g.csr, s, d, hops, path, h)
     finally:
         gpu_engine.auto_handoff = True
+        gpu_engine.lds_probe_edges = probe0
         gpu_engine.set_resident(False)
 
 
@@ -358,7 +364,8 @@ def test_resident_auto_levels_chain_vs_oracle(gpu_engine, spec):
     pairs = pairs_for(g.n, 32, 9)
     truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
     gpu_engine.set_resident(True)
-    md0, lv0 = gpu_engine.auto_max_degree, gpu_engine.auto_levels
+    md0, lv0, probe0 = gpu_engine.auto_max_degree, gpu_engine.auto_levels, gpu_engine.lds_probe_edges
+    gpu_engine.lds_probe_edges = 0  # hub graphs: searches must reach the grid levels
     try:
         gpu_engine.auto_max_degree = 1 << 40
         for lv in (1, 2, 3, 8, 2):
@@ -375,6 +382,48 @@ def test_resident_auto_levels_chain_vs_oracle(gpu_engine, spec):
     finally:
         gpu_engine.auto_max_degree = md0
         gpu_engine.auto_levels = lv0
+        gpu_engine.lds_probe_edges = probe0
+        gpu_engine.set_resident(False)
+
+
+@pytest.mark.parametrize("spec", ["kron:20:16:2", "rmat:262144:4194304:4", "rmat:65536:1048576:3"])
+def test_lds_meet_probe_vs_oracle(gpu_engine, spec):
+    """LDS meet probe (hub graphs): before a level that does not fit LDS goes
+    to the grid engine, up to lds_probe_edges of its frontier edges are tested
+    against the other side's visited set, and a hit ends the search.  Default
+    budget, one pass (4096 edges) and off; resident and one-shot searches
+    (hash-set and bitmap LDS modes); every answer against the oracle with its
+    path validated; hits and hand-offs both seen, the budget never exceeded."""
+    g = bb.from_spec(spec)
+    gpu_engine.load(g)
+    pairs = pairs_for(g.n, 40, 21)
+    truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
+    b0 = gpu_engine.lds_probe_edges
+    assert b0 > 0
+    hits = handed = handed0 = 0
+    try:
+        for budget in (b0, 4096, 0):
+            gpu_engine.lds_probe_edges = budget
+            assert gpu_engine.lds_probe_edges == budget
+            for resident in (True, False):
+                gpu_engine.set_resident(resident)
+                for (s, d), h in zip(pairs, truth):
+                    r = gpu_engine.search(s, d)
+                    check_result(g.csr, s, d, r.hops, r.path, h)
+                    st = r.stats
+                    assert st["probe_edges"] <= budget, (s, d, st["probe_edges"], budget)
+                    if st["probe_hit"]:
+                        assert not r.handoff
+                        hits += 1
+                    handed += bool(r.handoff)
+                    if budget == 0:
+                        assert not st["probe_hit"]
+                        handed0 += bool(r.handoff)
+                gpu_engine.set_resident(False)
+        if spec.startswith("kron"):  # Kronecker searches leave LDS, and the probe ends many of them
+            assert handed0 > 0 and hits > 0 and handed > handed0, (handed0, hits, handed)
+    finally:
+        gpu_engine.lds_probe_edges = b0
         gpu_engine.set_resident(False)
 
 
