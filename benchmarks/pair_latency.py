@@ -39,11 +39,13 @@ def main():
             tot.append(r.total_ms)
             lds.append(r.stats["lds_ms"])
             walk.append(r.stats["walk_ms"])
+            probe = (r.stats["probe_edges"], r.stats["probe_hit"])
         rec = {"src": s, "dst": d, "hops": h, "search_us": round(statistics.median(dev) * 1e3, 2),
                "query_us": round(statistics.median(tot) * 1e3, 2), "levels": r.levels,
                "edges": r.edges_inspected, "visited": r.visited, "handoff": r.handoff,
                "grid_levels": r.stats["grid_levels"], "lds_us": round(statistics.median(lds) * 1e3, 2),
-               "lds_levels": r.stats["lds_levels"], "walk_us": round(statistics.median(walk) * 1e3, 2)}
+               "lds_levels": r.stats["lds_levels"], "walk_us": round(statistics.median(walk) * 1e3, 2),
+               "probe_edges": probe[0], "probe_hit": probe[1]}
         agg.append(rec)
         if a.summary is None:
             print(json.dumps(rec), flush=True)
@@ -61,7 +63,13 @@ def main():
                           "handoff_search_us_mean": round(statistics.mean(
                               [x["search_us"] for x in agg if x["handoff"]] or [0.0]), 2),
                           "handoff_walk_us_mean": round(statistics.mean(
-                              [x["walk_us"] for x in agg if x["handoff"]] or [0.0]), 2)}),
+                              [x["walk_us"] for x in agg if x["handoff"]] or [0.0]), 2),
+                          "probe_hit_fraction": round(statistics.mean(float(x["probe_hit"]) for x in agg), 3),
+                          "probe_edges_mean": round(statistics.mean(x["probe_edges"] for x in agg), 1),
+                          "probe_hit_search_us_mean": round(statistics.mean(
+                              [x["search_us"] for x in agg if x["probe_hit"]] or [0.0]), 2),
+                          "probe_hit_lds_us_mean": round(statistics.mean(
+                              [x["lds_us"] for x in agg if x["probe_hit"]] or [0.0]), 2)}),
               flush=True)
     eng.set_resident(False)
 

@@ -1139,7 +1139,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
           meet = v;
           md0 = pq ? dob : dq + 1;
           md1 = pq ? dq + 1 : dob;
-          ++levels;  // the probed level ended the search
+          record_trace(pq, sel(pq, s0, s1), walked, 1u, 9u);  // mode 9: a level the probe ended
+          ++levels;
           einsp += walked;
           status = kFound;
           probe_hit = true;
@@ -2522,9 +2523,7 @@ uint32_t lds_probe_budget() {
 // hub graphs only: on a graph without hubs (G(n, p)) the other side holds a
 // vanishing share of the vertices when a level leaves LDS, so a probe of a
 // few thousand edges almost never hits
-static uint32_t probe_for(const GraphView& g, int trace) {
-  return (trace == 0 && g.max_deg > 64) ? g.probe_edges : 0u;
-}
+static uint32_t probe_for(const GraphView& g) { return g.max_deg > 64 ? g.probe_edges : 0u; }
 
 size_t lds_bytes(bool wide) {
   return 2 * kHashSize * 4 + 4 * (wide ? LdsRec<uint64_t>::cap * 16 : LdsRec<uint32_t>::cap * 8) + 128;
@@ -2539,7 +2538,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
     LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
-    P.probe = probe_for(g, trace);
+    P.probe = probe_for(g);
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
       if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -2551,7 +2550,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   } else {
     LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
-    P.probe = probe_for(g, trace);
+    P.probe = probe_for(g);
     if (trace == 2)
       k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
     else
@@ -2569,7 +2568,7 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;
   P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
-  P.probe = probe_for(g, 0);
+  P.probe = probe_for(g);
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);

@@ -36,7 +36,8 @@ struct LevelTrace {
   uint64_t frontier = 0;    // vertices expanded
   uint64_t edges = 0;       // edges inspected
   uint64_t discovered = 0;  // newly claimed vertices
-  int mode = 0;  // 0 CPU, 1 LDS lockstep round, 2 LDS single wave, 3 LDS all waves, 4 grid top-down, 5 grid bottom-up
+  int mode = 0;  // 0 CPU, 1 LDS lockstep round, 2 LDS single wave, 3 LDS all waves, 4 grid top-down,
+                 // 5 grid bottom-up, 9 LDS meet probe (a level ended at its first meet, edges = edges read)
 };
 
 struct SearchStats {

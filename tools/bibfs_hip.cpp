@@ -19,6 +19,7 @@ static const char* bibfs_mode_name(int m) {
     case 6: return "lds-lean";
     case 7: return "reg-lockstep";
     case 8: return "wave-lockstep";
+    case 9: return "lds-probe";
     default: return "cpu";
   }
 }
