@@ -449,9 +449,29 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   uint32_t ticket_old = 0;
   if (tid == 0 && !elected) ticket_old = atomicMax(P.ticket, P.seq);
 
-  // Lane writes its vertex's dl edge records Rn[eb .. eb+dl) (exec-masked loop).
+  // Each lane's vertex gets its dl edge records Rn[eb .. eb+dl).  Short runs
+  // are written by their own lane (exec-masked loop); a run longer than
+  // kCoopRun -- a hub's neighbour on a power-law graph, thousands of records
+  // -- by the whole wave, 64 records per store, one run after another: one
+  // lane writing 2k records serially held a Kronecker 22 lockstep round for
+  // ~18k cycles (profiles/r5_kron22_probe_stamps.txt).  Every lane of the
+  // wave calls it (ballot inside).
   auto append_records = [&](Rec* Rn, uint32_t dl, uint32_t eb, uint32_t v, OffT base) {
-    for (uint32_t j = 0; j < dl; ++j) rec_set(Rn[eb + j], v, base + j);
+    constexpr uint32_t kCoopRun = 32;
+    const bool coop = dl > kCoopRun;
+    for (uint32_t j = 0; j < (coop ? 0u : dl); ++j) rec_set(Rn[eb + j], v, base + j);
+    for (unsigned long long m = __ballot(coop); m; m &= m - 1) {
+      const int l = __ffsll((long long)m) - 1;
+      const uint32_t d = __builtin_amdgcn_readlane(dl, l), e = __builtin_amdgcn_readlane(eb, l);
+      const uint32_t vl = __builtin_amdgcn_readlane(v, l);
+      OffT bl;
+      if constexpr (sizeof(OffT) == 8)
+        bl = (OffT)__builtin_amdgcn_readlane((uint32_t)base, l) |
+             ((OffT)__builtin_amdgcn_readlane((uint32_t)((uint64_t)base >> 32), l) << 32);
+      else
+        bl = (OffT)__builtin_amdgcn_readlane((uint32_t)base, l);
+      for (uint32_t j = lane; j < d; j += kWave) rec_set(Rn[e + j], vl, bl + j);
+    }
   };
   // Edge k -> (neighbour v, its row [ob, oe)): one packed load, or col[k] then
   // the row offsets (a second dependent load) when no packed adjacency exists.
