@@ -2540,10 +2540,14 @@ uint32_t lds_probe_budget() {
   return b;
 }
 
-// hub graphs only: on a graph without hubs (G(n, p)) the other side holds a
-// vanishing share of the vertices when a level leaves LDS, so a probe of a
-// few thousand edges almost never hits
-static uint32_t probe_for(const GraphView& g) { return g.max_deg > 64 ? g.probe_edges : 0u; }
+// graphs whose largest degree is above BIBFS_LDS_PROBE_MIN_DEG (default 64)
+static uint32_t probe_for(const GraphView& g) {
+  static const uint64_t min_deg = [] {
+    const char* e = std::getenv("BIBFS_LDS_PROBE_MIN_DEG");
+    return e ? std::strtoull(e, nullptr, 10) : 64ull;
+  }();
+  return g.max_deg > min_deg ? g.probe_edges : 0u;
+}
 
 size_t lds_bytes(bool wide) {
   return 2 * kHashSize * 4 + 4 * (wide ? LdsRec<uint64_t>::cap * 16 : LdsRec<uint32_t>::cap * 8) + 128;
