@@ -292,6 +292,7 @@ struct LevelPlan {
   uint32_t status;
   uint32_t E[2], cur[2], off[2], nxt[2], qbase[2], depth[2];
   uint32_t pside, pfb, pcnt;  // kProbing: the side that does not fit, its frontier in the global queue
+  uint32_t prec;              // ... its level's records in LDS (R[cur[side]][off[side] ..]), or 0
 };
 
 // Internal plan status: probe the level that does not fit LDS for a meet
@@ -308,15 +309,18 @@ constexpr uint32_t kProbeU = 4;  // frontier edges per thread per probe pass
 // the same, shortest, length dq + 1 + do.  The CPU engine stops at the first
 // one, after a few thousand edges on hub graphs; the grid level reads them
 // all.  So before handing off, the frontier's edges are read in passes of
-// kLdsThreads * kProbeU (queue order, edge-parallel over a chunk of 1024
-// frontier vertices: block scan of their degrees, binary search per edge)
-// and tested against the other side's LDS visited set -- no claims, no
-// state written -- until an edge hits or `budget` edges were read.
+// kLdsThreads * kProbeU and tested against the other side's LDS visited set
+// -- no claims, no state written -- until an edge hits or `budget` edges
+// were read.  The edges come from the level's records when they are in LDS
+// (`recs`: a level that leaves LDS because a visited set is full -- one
+// dependent load per pass), else from the queue (a level whose records did
+// not fit: chunks of 1024 frontier vertices, block scan of their degrees,
+// binary search per edge -- three dependent loads per chunk).
 // Returns (u << 32) | v of a hit (u in q's frontier, v visited by the other
 // side), or ~0; *walked = edges read.  Every wave calls it (barriers inside).
-template <typename OffT, bool kBm>
+template <typename OffT, bool kBm, typename Rec>
 __device__ unsigned long long lds_meet_probe(const LdsParams<OffT>& P, int q, uint32_t fb, uint32_t F,
-                                             uint32_t budget, const uint32_t* Ho,
+                                             const Rec* recs, uint32_t nrec, uint32_t budget, const uint32_t* Ho,
                                              const unsigned long long* Wo, void* scratch, uint32_t* walked_out) {
   __shared__ unsigned long long pr_hit;
   __shared__ uint32_t pr_wsum[kLdsThreads / kWave], pr_total;
@@ -327,8 +331,53 @@ __device__ unsigned long long lds_meet_probe(const LdsParams<OffT>& P, int q, ui
   uint32_t* sEb = reinterpret_cast<uint32_t*>(sbp + kLdsThreads);  // exclusive prefix of the (clamped) degrees
   const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
   if (tid == 0) pr_hit = ~0ull;
+  __syncthreads();
   uint32_t walked = 0;
   bool stop = false;
+  // one pass's test: the other side's visited set, the smallest hit kept; true
+  // (uniform) once any wave hit
+  auto test_pass = [&](const uint32_t (&uu)[kProbeU], const uint32_t (&v)[kProbeU], const bool (&ok)[kProbeU]) {
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (uint32_t j = 0; j < kProbeU; ++j) {
+      bool hit;
+      if constexpr (kBm) hit = ok[j] && bm_state(Wo, v[j]) != 0u;
+      else hit = ok[j] && hash_find(Ho, v[j]) != kEmpty;
+      const unsigned long long key = ((unsigned long long)uu[j] << 32) | v[j];
+      if (hit && key < best) best = key;
+    }
+    if (__ballot(best != ~0ull)) {
+      unsigned long long m = best;
+      for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long y = __shfl_xor(m, off);
+        m = y < m ? y : m;
+      }
+      if (lane == 0) atomicMin(&pr_hit, m);
+    }
+    __syncthreads();
+    return uni((uint32_t)(pr_hit >> 32)) != 0xffffffffu;
+  };
+  if (recs) {
+    for (uint32_t base = 0; base < nrec; base += kLdsThreads * kProbeU) {
+      const uint32_t pass = min(kLdsThreads * kProbeU, nrec - base);
+      if (walked + pass > budget) break;  // (uniform)
+      walked += pass;
+      uint32_t v[kProbeU], uu[kProbeU];
+      bool ok[kProbeU];
+#pragma unroll
+      for (uint32_t j = 0; j < kProbeU; ++j) {
+        const uint32_t i = base + j * kLdsThreads + (uint32_t)tid;
+        ok[j] = i < nrec;
+        const Rec r = recs[ok[j] ? i : 0u];
+        uu[j] = r.x;
+        const OffT k = min((OffT)rec_k(r), P.nnz_m1);
+        v[j] = 0u;
+        if (ok[j]) v[j] = P.padj8 ? launch::pack8_v(P.padj8[k]) : P.padj ? P.padj[k].x : P.col[k];
+      }
+      if (test_pass(uu, v, ok)) break;
+    }
+    F = 0;  // (no queue chunks)
+  }
   for (uint32_t c0 = 0; c0 < F && !stop; c0 += kLdsThreads) {
     const uint32_t i = c0 + (uint32_t)tid;
     uint32_t u = 0, d = 0;
@@ -378,25 +427,7 @@ __device__ unsigned long long lds_meet_probe(const LdsParams<OffT>& P, int q, ui
         uu[j] = su[lo];
         v[j] = ok[j] ? P.col[sbp[lo] + (OffT)(e - sEb[lo])] : 0u;  // every pass's loads in flight together
       }
-      unsigned long long best = ~0ull;
-#pragma unroll
-      for (uint32_t j = 0; j < kProbeU; ++j) {
-        bool hit;
-        if constexpr (kBm) hit = ok[j] && bm_state(Wo, v[j]) != 0u;
-        else hit = ok[j] && hash_find(Ho, v[j]) != kEmpty;
-        const unsigned long long key = ((unsigned long long)uu[j] << 32) | v[j];
-        if (hit && key < best) best = key;
-      }
-      if (__ballot(best != ~0ull)) {
-        unsigned long long m = best;
-        for (int off = 32; off >= 1; off >>= 1) {
-          const unsigned long long y = __shfl_xor(m, off);
-          m = y < m ? y : m;
-        }
-        if (lane == 0) atomicMin(&pr_hit, m);
-      }
-      __syncthreads();
-      if (uni((uint32_t)(pr_hit >> 32)) != 0xffffffffu) {
+      if (test_pass(uu, v, ok)) {
         stop = true;
         break;
       }
@@ -1135,6 +1166,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         p.pside = (uint32_t)q;
         p.pfb = q ? s1.fbeg : s0.fbeg;
         p.pcnt = q ? s1.cnt : s0.cnt;
+        p.prec = (q ? s1.ovf : s0.ovf) ? 0u : (uint32_t)(q ? s1.fed : s0.fed);  // records in LDS: their count
         plan = p;
       }
     }
@@ -1145,9 +1177,13 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     if (fstatus == kProbing) {
       const int pq = (int)uni(plan.pside);
       uint32_t walked = 0;
+      const uint32_t nrec = uni(plan.prec);
+      const Rec* recs = nrec ? &R[uni(plan.cur[pq])][uni(plan.off[pq])] : nullptr;
+      // the chunk path's scratch: a record buffer the level's records are not in
+      const uint32_t sbuf = (uint32_t)__builtin_ctz(~(1u << uni(plan.cur[pq])) & 0xfu);
       const unsigned long long hit =
-          lds_meet_probe<OffT, kBm>(P, pq, uni(plan.pfb), uni(plan.pcnt), P.probe, pq ? H[0] : H[1],
-                                    W(pq ^ 1), &R[0][0], &walked);
+          lds_meet_probe<OffT, kBm, Rec>(P, pq, uni(plan.pfb), uni(plan.pcnt), recs, nrec, P.probe,
+                                         pq ? H[0] : H[1], W(pq ^ 1), &R[sbuf][0], &walked);
       probed = true;
       probe_walked = walked;
       if (wid == 0) {
