@@ -417,8 +417,15 @@ def main(argv=None) -> int:
         t0 = time.perf_counter()
         for i in range(steps):
             query(warmup + i)  # answer checked in query()
-        stream_barrier()
-        dt = max_over_ranks(time.perf_counter() - t0)
+        # closing bracket: this rank's streams synchronized, its clock read,
+        # then the barrier -- the max over ranks is the slowest rank's K steps
+        # from the common start, without the closing barrier's own latency
+        # (~50-500 us with gloo / RCCL: several steps of a ~15 us query)
+        eng.synchronize()
+        dt_local = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        dt = max_over_ranks(dt_local)
         # queries of the timed loop the tiny server handed to the general engine
         timed_overflows = int(max_over_ranks(float(eng.tiny_overflows - ov0)))
         # statistics, untimed: the same queries again, reading the per-query
