@@ -1083,6 +1083,53 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     }
   };
 
+  // Wave 0: side q's level records were lost -- a lockstep round puts side
+  // 1's records after side 0's in one buffer, so a big side 0 overflowed a
+  // small side 1 with it -- but the level itself is small: rebuild them from
+  // the global queue into a free buffer (queue entry -> row, one wave-wide
+  // degree scan, cooperative appends), so the search stays in LDS instead of
+  // handing a level of a few dozen edges to the grid.  At most kRebuildMax
+  // frontier vertices (their loads all in flight at once).  true = rebuilt.
+  auto rebuild = [&](int q) -> bool {
+    constexpr uint32_t kRebuildMax = 4 * kWave;
+    SideState x = sel(q, s0, s1);
+    if (!x.ovf || x.cnt > kRebuildMax || x.fed > CAP || !(kBm || x.hcnt + x.fed <= kHashLimit)) return false;
+    const uint32_t buf = free_buf();
+    const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
+    uint32_t u[4], d[4];
+    OffT b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = (uint32_t)j * kWave + lane;
+      u[j] = i < x.cnt ? load_agent(&qu[x.fbeg + i]) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = (uint32_t)j * kWave + lane;
+      b[j] = 0;
+      d[j] = 0;
+      if (i < x.cnt) {
+        b[j] = P.row_off[u[j]];
+        d[j] = (uint32_t)min((OffT)(P.row_off[u[j] + 1] - b[j]), (OffT)CAP + 1);
+      }
+    }
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t incl = wave_incl_scan(d[j]);
+      const uint32_t eb = run + incl - d[j];
+      append_records(R[buf], eb + d[j] <= CAP ? d[j] : 0u, eb, u[j], b[j]);
+      run += __builtin_amdgcn_readlane(incl, 63);
+    }
+    if (uni(run) != (uint32_t)x.fed) return false;  // (never: fed is this frontier's degree sum)
+    x.cur = buf;
+    x.off = 0;
+    x.ovf = 0;
+    s0 = sel(q, x, s0);
+    s1 = sel(q, s1, x);
+    return true;
+  };
+
   unsigned long long clk0 = 0;
   const unsigned long long rt0 = tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
   if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
@@ -1105,6 +1152,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         const bool fq = q ? f1 : f0;
         const unsigned long long eq = q ? s1.fed : s0.fed;
         if (!dual && (!fq || eq > kSmallEdges)) {
+          if (!fq && rebuild(q)) continue;  // a small level whose records were lost: rebuilt, stays in LDS
           // a level that does not fit: probe it for a meet first (hub graphs)
           if (!fq) status = (P.probe && !P.batch && !probed) ? kProbing : kHandoff;
           break;  // big level (all waves), probe or hand-off
