@@ -2671,7 +2671,15 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
                 dev::ServerBox* box, uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
                 unsigned long long idle_ticks, hipStream_t s) {
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
-  BIBFS_REQUIRE(g.row_off32 != nullptr, "resident server: 32-bit row offsets required");
+  if (!g.row_off32) {  // nnz >= 2^32 (Kronecker 27+): 64-bit offsets, hash-set mode
+    LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
+                          (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
+    P.b_alt = b_alt;
+    P.probe = probe_for(g);
+    k_lds_server<uint64_t, false><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;

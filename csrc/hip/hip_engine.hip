@@ -282,7 +282,9 @@ struct HipBiBfs::Impl {
     return launch::GraphView{n, nnz, d_row_off, d_row_off32, d_col, d_padj, max_deg, d_padj8, probe_edges};
   }
 
-  bool server_usable() const { return d_row_off32 != nullptr && n > 0 && n <= 0x7fffffffu; }
+  bool server_usable() const { return d_row_off32 != nullptr && n > 0 && n <= 0x7fffffffu; }  // batch kernel
+  // the resident LDS server runs with 32- or 64-bit row offsets
+  bool lds_server_usable() const { return n > 0 && n <= 0x7fffffffu; }
 
   static bool dbg() {
     static const bool on = std::getenv("BIBFS_DEBUG") != nullptr;
@@ -579,7 +581,10 @@ struct HipBiBfs::Impl {
   }
 
   void finish_graph(double ms) {
-    if (nnz < 0xFFFFFFFFULL) {
+    // BIBFS_WIDE_OFFSETS=1 (tests): no 32-bit copy of the row offsets, so a
+    // small graph takes the 64-bit-offset kernels of an nnz >= 2^32 graph
+    const char* wide = std::getenv("BIBFS_WIDE_OFFSETS");
+    if (nnz < 0xFFFFFFFFULL && !(wide && wide[0] == '1')) {
       HIP_CHECK(hipMalloc(&d_row_off32, ((size_t)n + 1) * 4));
       launch::make_row_off32(d_row_off, n, d_row_off32, stream);
     }
@@ -1307,7 +1312,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
     static const bool stamp_srv = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
     // with the tiny server resident for this graph, the queries it cannot take
     // (non-default options, overflow) run one-shot beside it
-    if (I.resident && !I.tiny_ok && (!opt.trace || stamp_srv) && I.server_usable()) {
+    if (I.resident && !I.tiny_ok && (!opt.trace || stamp_srv) && I.lds_server_usable()) {
       I.flip_state_set();  // the server (own stream) must not share state with a running cleanup
       use_auto = I.auto_usable(opt);
       I.gres = use_auto ? I.h_gres : I.h_res;

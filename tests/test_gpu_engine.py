@@ -427,6 +427,35 @@ def test_lds_meet_probe_vs_oracle(gpu_engine, spec):
         gpu_engine.set_resident(False)
 
 
+@pytest.mark.parametrize("spec", ["kron:18:16:2", "gnp:1000000::2"])
+def test_wide_offsets_resident_server_vs_oracle(gpu_engine, spec, monkeypatch):
+    """64-bit row offsets (what a graph with nnz >= 2^32 gets, forced here on a
+    small one): the resident LDS server, its hand-offs and the meet probe run
+    the OffT = uint64 kernels; one-shot and resident answers against the
+    oracle."""
+    g = bb.from_spec(spec)
+    pairs = pairs_for(g.n, 40, 33)
+    truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
+    monkeypatch.setenv("BIBFS_WIDE_OFFSETS", "1")
+    gpu_engine.load(g)
+    try:
+        handed = 0
+        for resident in (True, False):
+            gpu_engine.set_resident(resident)
+            for (s, d), h in zip(pairs, truth):
+                r = gpu_engine.search(s, d)
+                check_result(g.csr, s, d, r.hops, r.path, h)
+                handed += bool(r.handoff)
+            for (s, d), h in zip(pairs[:8], truth[:8]):
+                hops, path = gpu_engine.query(s, d)
+                check_result(g.csr, s, d, hops, path, h)
+        assert handed > 0 or spec.startswith("kron"), "expected hand-offs on the G(n, p) graph"
+    finally:
+        gpu_engine.set_resident(False)
+        monkeypatch.delenv("BIBFS_WIDE_OFFSETS")
+        gpu_engine.load(g)  # 32-bit offsets again for the tests after this one
+
+
 def test_auto_handoff_gate_timeout_falls_back_to_host(gpu_engine):
     """The gated first grid level gives up when its search has not left LDS in
     time (forced here: a zero wait).  Such a search still hands off later; the
