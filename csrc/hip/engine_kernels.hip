@@ -102,6 +102,14 @@ static_assert(kWaveB == 1 || kWaveB == 2 || kWaveB == 4, "batches per wave: 1, 2
 #endif
 constexpr bool kWaveHashG = BIBFS_KNOB_WAVE_HASH_G;
 constexpr uint64_t kWaveHashMaxDeg = 255;
+// (host) the gate, overridable for A/B runs: BIBFS_WAVE_HASH_MAX_DEG
+static uint64_t wave_hash_max_deg() {
+  static const uint64_t d = [] {
+    const char* e = std::getenv("BIBFS_WAVE_HASH_MAX_DEG");
+    return e ? std::strtoull(e, nullptr, 10) : kWaveHashMaxDeg;
+  }();
+  return d;
+}
 // Resident server: the mailbox diagnostics (stage / seen / poll latency) are
 // system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
 // issued them, its first global load of the search would wait for their PCIe
@@ -2645,7 +2653,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   if (g.row_off32) {
     LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
-    P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
+    P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
     P.probe = probe_for(g);
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
@@ -2683,7 +2691,7 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;
-  P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
+  P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
   P.probe = probe_for(g);
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
