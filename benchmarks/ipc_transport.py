@@ -40,18 +40,20 @@ def main():
     ap.add_argument("--spec", default="gnp:1000000::2")
     ap.add_argument("--ranks", default="2,4")
     ap.add_argument("--queries", type=int, default=16)
+    ap.add_argument("--torch", default="0,1", help="BIBFS_PROC_TORCH values: 0 no torch, 1 imported, 2 + device context")
     a = ap.parse_args()
     _, n, _, _ = parse_spec(a.spec)
     rnd = random.Random(3)
     qs = [(0, n - 1)] + [(rnd.randrange(n), rnd.randrange(n)) for _ in range(a.queries - 1)]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     for P in [int(x) for x in a.ranks.split(",")]:
-        for torch_first in ("0", "1"):
+        for torch_first in a.torch.split(","):
             env = {"BIBFS_PROC_TORCH": torch_first, "BIBFS_IPC_STATS": "1"}
             rcs, outs, el = dist_proc_launch(P, a.spec, qs, [({}, {}), ({}, {})], env=env, timeout=300)
             run = outs[0]["runs"][-1] if "runs" in outs[0] else {}
             ms = run.get("query_ms", [])
-            rec = {"setup": "python workers, torch runtime" if torch_first == "1" else "python workers, /opt/rocm runtime",
+            rec = {"setup": {"0": "python workers, /opt/rocm runtime", "1": "python workers, torch runtime",
+                             "2": "python workers, torch runtime + torch device context"}[torch_first],
                    "ranks": P, "spec": a.spec, "rcs": rcs,
                    "median_query_ms": round(statistics.median(ms), 4) if ms else None,
                    "mean_rounds": round(statistics.mean(st.get("rounds", 0) for st in run.get("last_stats", [{}])), 2)

@@ -30,6 +30,10 @@ def main(job_path: str, rank: int) -> int:
         if os.environ.get("BIBFS_PROC_TORCH", "1") != "0":
             import torch  # noqa: F401  (binds the HIP runtime first, as every GPU test does)
 
+            if os.environ.get("BIBFS_PROC_TORCH", "1") == "2":  # also a torch device context (as bench.py)
+                torch.cuda.set_device(int(job["device"]))
+                torch.cuda.synchronize()
+
         from .. import native
         from ..ops import make_options
         from . import make_tuning
