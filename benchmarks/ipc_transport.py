@@ -59,6 +59,9 @@ def main():
                    "mean_rounds": round(statistics.mean(st.get("rounds", 0) for st in run.get("last_stats", [{}])), 2)
                    if run.get("last_stats") else None}
             rec.update(stats_of("".join(o.get("log", "") for o in outs)))
+            errs = [o.get("error") for o in outs if o.get("error")]
+            if errs:
+                rec["errors"] = errs[:2]
             print(json.dumps(rec), flush=True)
         cmd = [MPIEXEC, "-n", str(P), os.path.join(root, "build", "bin", "mpi_bibfs"), a.spec, "0", str(n - 1),
                "--comm", "ipc", "--repeat", "20", "--json"]
