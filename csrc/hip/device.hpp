@@ -118,6 +118,8 @@ struct alignas(16) TinyPkt {
 };
 enum : uint32_t { kTinyFound = 1, kTinyNoPath = 2, kTinyOverflow = 3 };
 constexpr uint32_t kTinyQ = 4096;  // LDS queue capacity per side (12-bit queue indices)
+// next-round records past the LDS buffer (all-wave rounds): global, per buffer and side
+constexpr uint32_t kTinySpill = 2048;
 constexpr uint32_t kTinyPktCap = 2 + (2 * kTinyQ + 2) / 3 + 1;
 
 // Result of one query of the batched global-visited kernel (batch_global.hip).
@@ -252,6 +254,7 @@ struct TinyArgs {
   uint32_t* ticket;
   unsigned long long idle_ticks;
   unsigned long long* stamps;       // device, 16 words (stamp build only)
+  unsigned long long* spill;        // device, [2 buffers][2 sides][kTinySpill] records
 };
 bool tiny_supported(uint32_t n, uint64_t nnz, uint64_t max_deg);
 void build_tiny_adj(const uint64_t* row_off, const uint32_t* col, uint32_t n, uint64_t nnz,

@@ -253,6 +253,7 @@ struct HipBiBfs::Impl {
   // small-graph server (tiny_engine.hip): packed adjacency + self-tagged result packets
   unsigned long long* d_tadj = nullptr;
   unsigned long long* d_tinfo = nullptr;
+  unsigned long long* d_tspill = nullptr;  // tiny server: records past its LDS buffers
   unsigned long long* d_stamps = nullptr;
   TinyPkt* h_pkts = nullptr;
   bool tiny_ok = false;
@@ -306,7 +307,7 @@ struct HipBiBfs::Impl {
     __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
     if (kind == kSrvTiny) {
       launch::TinyArgs a{d_tadj, d_tinfo, n, h_box, h_box, h_pkts,
-                         srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, d_stamps};
+                         srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, d_stamps, d_tspill};
       launch::tiny_server(a, tiny_stamp(), sstream);
     } else {
       launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
@@ -478,7 +479,8 @@ struct HipBiBfs::Impl {
     if (d_padj8) HIP_CHECK(hipFree(d_padj8));
     if (d_tadj) HIP_CHECK(hipFree(d_tadj));
     if (d_tinfo) HIP_CHECK(hipFree(d_tinfo));
-    d_tadj = d_tinfo = nullptr;
+    if (d_tspill) HIP_CHECK(hipFree(d_tspill));
+    d_tadj = d_tinfo = d_tspill = nullptr;
     tiny_ok = false;
     if (d_uv) HIP_CHECK(hipFree(d_uv));
     if (state_block) HIP_CHECK(hipFree(state_block));
@@ -616,6 +618,7 @@ struct HipBiBfs::Impl {
     if (!tiny_disabled() && launch::tiny_supported(n, nnz, max_deg)) {
       HIP_CHECK(hipMalloc(&d_tadj, (std::max<uint64_t>(nnz, 1) + 4) * 8));  // +4: 16-byte first-edge loads
       HIP_CHECK(hipMalloc(&d_tinfo, (size_t)n * 8));
+      HIP_CHECK(hipMalloc(&d_tspill, (size_t)4 * kTinySpill * 8));
       launch::build_tiny_adj(d_row_off, d_col, n, nnz, d_tadj, d_tinfo, stream);
       tiny_ok = true;
     }

@@ -23,9 +23,12 @@
 //   * the path is walked in LDS (one LDS load per hop, both chains at once);
 //   * the answer goes to pinned host memory as self-tagged 16-byte packets
 //     (TinyPkt): no release fence, no flag store behind the payload.
-// Queries that do not fit (a round above 2048 frontier edges, a queue above
-// kTinyQ) answer kTinyOverflow and the host re-runs them on the general
-// engine (engine_kernels.hip), which has the grid hand-off.
+// Records that do not fit the LDS buffers spill to global memory (all-wave
+// rounds, L2-resident; a round of up to ~4k items runs in two passes), so a
+// long-path query's big last level still ends here.  Queries that still do
+// not fit (a round above 4095 items, a queue above kTinyQ without a meet)
+// answer kTinyOverflow and the host re-runs them on the general engine
+// (engine_kernels.hip), which has the grid hand-off.
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -105,6 +108,12 @@ static_assert(kTinyUnroll == 4, "two 16-byte loads per neighbour");
 #define BIBFS_TINY_LAZY2 0
 #endif
 constexpr bool kLazy2 = BIBFS_TINY_LAZY2;
+// 1 = all-wave rounds spill next-round records past the LDS buffers to global
+// memory (TinyArgs::spill) instead of answering kTinyOverflow
+#ifndef BIBFS_TINY_SPILL
+#define BIBFS_TINY_SPILL 1
+#endif
+constexpr bool kSpillOn = BIBFS_TINY_SPILL;
 __device__ __forceinline__ void load_first4(unsigned long long (&w)[kTinyUnroll],
                                             const unsigned long long* __restrict__ p, uint32_t deg) {
   if (deg) {  // (exec-masked per lane)
@@ -120,9 +129,10 @@ static_assert(kTinyQ == 1u << kQBits, "queue index width");
 
 // Per-round counter (three slots, rotated): new records of side 0 [19:0] and
 // side 1 [39:20], new queue entries of side 0 [51:40] and side 1 [63:52].
-// Field bounds: a round has at most kCapR = 2048 new vertices per side
-// (< 2^12 with the queue capped at kTinyQ = 4096 -- a larger sum is an overflow
-// anyway) and 2048 x kTinyMaxDeg < 2^20 new records.
+// Field bounds: a round has at most kMaxRound = 4095 items, so at most 4095
+// new vertices per side (< 2^12); the record fields take 20 bits, so each
+// wave's record count is clamped to kTRC + kTinySpill + 1 when it is added
+// (past that the records overflow anyway, caught per lane).
 struct TinyCtl {
   unsigned long long cnt[3];
   unsigned long long meet;   // min over candidates of len << 32 | side << 31 | queue index; 0 = overflow
@@ -193,6 +203,10 @@ struct RoundCtx {
   const unsigned long long* rb0;     // side 0's current records
   const unsigned long long* rb1x;    // side 1's current records, minus x0 (indexed by the item)
   unsigned long long* nb[2];         // next-round record buffers
+  // records past the LDS buffers (slot >= kTRC) live in global memory: the
+  // current round's per side, and the next round's
+  const unsigned long long* sp[2];
+  unsigned long long* ns[2];
   uint32_t par[2];                   // depth parity bit of this round's claims per side
   uint32_t dep[2];                   // frontier depth per side before the round
   bool exp[2];                       // the side expands this round
@@ -223,7 +237,13 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
     W.act[b] = i < R.tot;
     W.s1[b] = i >= R.x0;
     W.rec[b] = 1ull;  // an idle lane: vertex 0, base 0, degree 1
-    if (b < nb && W.act[b]) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
+    const uint32_t li = W.s1[b] ? i - R.x0 : i;  // the record's slot in its side's buffer
+    if (b < nb && W.act[b]) {
+      if (li < kTRC) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
+      else  // a spilled record (written by another wave last round: L2, past this CU's L1)
+        W.rec[b] = __hip_atomic_load(R.sp[W.s1[b] ? 1 : 0] + (li - kTRC), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (kSpec) {
 #pragma unroll
@@ -342,7 +362,7 @@ __device__ __forceinline__ void round_count(Counts<NB>& K, const Work<NB>& W) {
 // would (fatal only if the round finds no meet: records feed the NEXT round).
 // A lane with nothing to store writes its own junk slot (no branch).
 constexpr uint32_t kOvfQueue = 1, kOvfRec = 2;
-template <int NB, bool kSpec>
+template <int NB, bool kSpec, bool kSpill>
 __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K, const RoundCtx& R, int nb,
                                                 uint32_t q0b, uint32_t q1b, uint32_t e0b, uint32_t e1b, uint32_t lane,
                                                 const unsigned long long* __restrict__ tadj, uint32_t (*QU)[kTinyQ],
@@ -362,7 +382,7 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
     if (s1) e1 += deg;
     else e0 += deg;
     const bool qok = nw && q < kTinyQ;
-    const bool rok = qok && e + deg <= kTRC;
+    const bool rok = qok && e + deg <= (kSpill ? kTRC + kTinySpill : kTRC);
     if (nw && !qok) ovf |= kOvfQueue;
     if (qok && !rok) ovf |= kOvfRec;
     *(qok ? &QU[s1 ? 1 : 0][q] : JQ + lane) = v << kQBits | tw_pq(W.rec[b]);
@@ -370,12 +390,22 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
     unsigned long long* junk = JR + lane;
     const uint32_t dd = rok ? deg : 0u;
     const unsigned long long tag = (unsigned long long)q << 52;
-    // past the degree (or with nothing to store) a store goes to the lane's junk slot
+    if (!kSpill || !__ballot(rok && e + deg > kTRC)) {
+      // past the degree (or with nothing to store) a store goes to the lane's junk slot
 #pragma unroll
-    for (uint32_t j = 0; j < kTinyUnroll; ++j) *(j < dd ? out + j : junk) = W.nbw[b][j] | tag;
-    if (__ballot(rok && deg > kTinyUnroll)) {  // rare: a vertex of degree > 4
+      for (uint32_t j = 0; j < kTinyUnroll; ++j) *(j < dd ? out + j : junk) = W.nbw[b][j] | tag;
+      if (__ballot(rok && deg > kTinyUnroll)) {  // rare: a vertex of degree > 4
+        const uint32_t base = tw_base(W.rec[b]);
+        for (uint32_t j = kTinyUnroll; rok && j < deg; ++j) out[j] = tadj[base + j] | tag;
+      }
+    } else {  // rare: some of the wave's records go past the LDS buffer (global spill)
+      unsigned long long* sp = R.ns[s1 ? 1 : 0];
       const uint32_t base = tw_base(W.rec[b]);
-      for (uint32_t j = kTinyUnroll; rok && j < deg; ++j) out[j] = tadj[base + j] | tag;
+      for (uint32_t j = 0; j < dd; ++j) {
+        const unsigned long long w = (j < kTinyUnroll ? W.nbw[b][j] : tadj[base + j]) | tag;
+        if (e + j < kTRC) out[j] = w;
+        else sp[e + j - kTRC] = w;
+      }
     }
     const uint32_t bt = v & 31;
     const uint32_t ost = (uint32_t)((W.oth[b] >> bt) & 1ull) | (uint32_t)((W.oth[b] >> (bt + 32)) & 1ull) << 1;
@@ -394,7 +424,12 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
 template <bool kStamp>
 __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
   static_assert(kTinyB == 2, "two items per lane");
-  constexpr uint32_t kCapR = (uint32_t)kTT * kTinyB;  // frontier edges one all-wave round expands
+  constexpr uint32_t kCapR = (uint32_t)kTT * kTinyB;  // frontier edges one all-wave pass expands
+  // A single-side round may take two passes (the queue-count fields are 12
+  // bits): a long-path query's last level is often just above one pass, and
+  // it usually holds the meet -- run on instead of falling back to the
+  // general engine (a host round trip and a launch).
+  constexpr uint32_t kMaxRound = 2 * kCapR - 1;
   constexpr uint32_t kCapW = 64u * kSwNB;              // ... one single-wave round
   __shared__ unsigned long long VIS[2][kTW];
   __shared__ uint32_t QU[2][kTinyQ];
@@ -436,6 +471,10 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     X.rb1x = &R[cb1][1][0] - x0;
     X.nb[0] = &R[cb0 ^ 1][0][0];
     X.nb[1] = &R[cb1 ^ 1][1][0];
+    X.sp[0] = P.spill + (size_t)(cb0 * 2 + 0) * kTinySpill;  // [buffer][side][kTinySpill]
+    X.sp[1] = P.spill + (size_t)(cb1 * 2 + 1) * kTinySpill;
+    X.ns[0] = P.spill + (size_t)((cb0 ^ 1) * 2 + 0) * kTinySpill;
+    X.ns[1] = P.spill + (size_t)((cb1 ^ 1) * 2 + 1) * kTinySpill;
     X.par[0] = (d0 + 1) & 1;
     X.par[1] = (d1 + 1) & 1;
     X.dep[0] = d0;
@@ -520,7 +559,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           Counts<NB> K;
           round_count<NB>(K, W);
           const uint32_t ovf =
-              round_place<NB, true>(W, K, X, NB, T.ql0, T.ql1, 0u, 0u, lane, P.tadj, QU, JQ, JR, &C.meet);
+              round_place<NB, true, false>(W, K, X, NB, T.ql0, T.ql1, 0u, 0u, lane, P.tadj, QU, JQ, JR, &C.meet);
           const bool qovf = __ballot(ovf & kOvfQueue) != 0, rovf = __ballot(ovf & kOvfRec) != 0;
           T.x0 = x0;
           T.x1 = x1;
@@ -585,7 +624,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       if (x0 + x1 > kCapR || x0 + x1 > kLockMax) {  // the side with fewer edges alone
         if (x0 <= x1) x1 = 0;
         else x0 = 0;
-        if (x0 + x1 > kCapR) {
+        if (x0 + x1 > kMaxRound) {
           status = kTinyOverflow;
           break;
         }
@@ -598,37 +637,52 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       // one item per lane when the round has at most kTT edges (every round
       // under the lockstep cap), two otherwise: as in the single-wave phase
       // the one-item body carries none of the second item's instructions
-      auto aw_round = [&](auto nbc) {
+      // c0: first item of this pass (a two-pass round: 0, then kCapR)
+      auto aw_round = [&](auto nbc, uint32_t c0) {
         constexpr int NB = decltype(nbc)::value;
-        const int nb = (NB == 2 && wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
+        const int nb = (NB == 2 && c0 + wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
         Work<NB> W;
-        round_issue<NB, kSpecAll>(W, X, tid, kTT, nb, P.tadj, VIS);
+        round_issue<NB, kSpecAll>(W, X, c0 + tid, kTT, nb, P.tadj, VIS);
         if (!kSpecAll) round_fetch<NB>(W, nb, P.tadj);
         Counts<NB> K;
         round_count<NB>(K, W);
         TINY_PH(3)
         if (K.qt[0] | K.qt[1]) {  // uniform
-          // ONE ds_add_rtn_u64 on the packed round counter (TinyCtl layout)
+          // ONE ds_add_rtn_u64 on the packed round counter (TinyCtl layout).
+          // A wave's record count is clamped to kTRC + kTinySpill + 1: past
+          // that its lanes overflow anyway (kOvfRec), and the clamp keeps 32
+          // wave passes below 2^20, so a field never carries into the next.
           unsigned long long base = 0;
           if (lane == 0)
-            base = atomicAdd(&C.cnt[slot], (unsigned long long)K.et[0] |
-                                               (unsigned long long)K.et[1] << 20 |
+            base = atomicAdd(&C.cnt[slot], (unsigned long long)min(K.et[0], kTRC + kTinySpill + 1) |
+                                               (unsigned long long)min(K.et[1], kTRC + kTinySpill + 1) << 20 |
                                                (unsigned long long)K.qt[0] << 40 | (unsigned long long)K.qt[1] << 52);
           const uint32_t blo = lane0((uint32_t)base), bhi = lane0((uint32_t)(base >> 32));
           TINY_PH(4)
-          const uint32_t ovf = round_place<NB, kSpecAll>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20),
+          const uint32_t ovf = round_place<NB, kSpecAll, kSpillOn>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20),
                                                blo & 0xFFFFFu, ((blo >> 20) | (bhi << 12)) & 0xFFFFFu, lane, P.tadj,
                                                QU, JQ, JR, &C.meet);
-          if (ovf & kOvfQueue) atomicMin(&C.meet, 0ull);  // key 0 = overflow (a meet has length >= 1)
+          // a full queue: fatal in a lockstep round (a dropped candidate may be
+          // the shorter one -- key 0 = overflow, a meet has length >= 1); in a
+          // single-side round every candidate has the same length, so like a
+          // record overflow it is fatal only if the round finds no meet
+          if (ovf & kOvfQueue) {
+            if (X.x0 != 0 && X.x0 != X.tot) atomicMin(&C.meet, 0ull);
+            else C.rovf = 1u;
+          }
           if (ovf & kOvfRec) C.rovf = 1u;
         }
       };
-      if (wid * 64 < X.tot) {
-        if (kAwSplit && X.tot <= (uint32_t)kTT) aw_round(std::integral_constant<int, 1>{});
-        else aw_round(std::integral_constant<int, 2>{});
+      for (uint32_t c0 = 0; c0 < X.tot; c0 += kCapR) {  // one pass, two for a big single-side round
+        if (c0 + wid * 64 < X.tot) {
+          if (kAwSplit && X.tot - c0 <= (uint32_t)kTT) aw_round(std::integral_constant<int, 1>{}, c0);
+          else aw_round(std::integral_constant<int, 2>{}, c0);
+        }
       }
       TINY_PH(5)
-      lds_barrier();
+      // LDS barrier, plus the round's spilled records (global stores, rare;
+      // nothing else is in vmcnt here) drained for the next round's readers
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       TINY_PH(6)
       einsp += X.tot;
       levels += (x0 != 0) + (x1 != 0);

@@ -538,6 +538,29 @@ def test_tiny_server_overflow_falls_back(gpu_engine):
         gpu_engine.set_resident(False)
 
 
+@pytest.mark.parametrize("deg", [3.2, 5.0])
+def test_tiny_server_spilled_records_vs_oracle(gpu_engine, deg):
+    """Frontiers whose next-round records pass the LDS buffers: the records
+    spill to global memory and big single-side rounds run in two passes, so
+    long-path queries stay on the tiny server -- every answer against the
+    oracle, paths validated, and fewer fallbacks than queries."""
+    n = 110000
+    g = gnp(n, deg / n, 17)
+    gpu_engine.load(g)
+    assert gpu_engine.tiny_engine
+    gpu_engine.set_resident(True)
+    ovf0 = gpu_engine.tiny_overflows
+    rnd = random.Random(int(deg * 10))
+    pairs = [(0, n - 1)] + [(rnd.randrange(n), rnd.randrange(n)) for _ in range(120)]
+    try:
+        for s, d in pairs:
+            h, path = gpu_engine.query(s, d)
+            check_result(g.csr, s, d, h, path, native.bfs_oracle(g.csr, s, d).hops)
+        assert gpu_engine.tiny_overflows - ovf0 < len(pairs) // 4
+    finally:
+        gpu_engine.set_resident(False)
+
+
 def test_tiny_server_not_used_for_hubs(gpu_engine):
     """A degree above the packed-word limit keeps the graph on the general server."""
     star = Graph.from_edges(5001, [[0, i] for i in range(1, 5001)])
