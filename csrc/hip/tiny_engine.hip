@@ -207,6 +207,7 @@ struct RoundCtx {
   // current round's per side, and the next round's
   const unsigned long long* sp[2];
   unsigned long long* ns[2];
+  bool spilled;                      // a side's current records pass kTRC (uniform)
   uint32_t par[2];                   // depth parity bit of this round's claims per side
   uint32_t dep[2];                   // frontier depth per side before the round
   bool exp[2];                       // the side expands this round
@@ -226,7 +227,7 @@ struct Work {
 // neighbour's first edges (the NEXT round's records, fetched speculatively
 // so their latency overlaps the claim) and the claims.  Branch-free: an idle
 // lane reads a harmless word and claims with an empty mask.
-template <int NB, bool kSpec>
+template <int NB, bool kSpec, bool kSpill>
 __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint32_t i0, uint32_t stride, int nb,
                                             const unsigned long long* __restrict__ tadj,
                                             unsigned long long (*VIS)[kTW]) {
@@ -237,9 +238,9 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
     W.act[b] = i < R.tot;
     W.s1[b] = i >= R.x0;
     W.rec[b] = 1ull;  // an idle lane: vertex 0, base 0, degree 1
-    const uint32_t li = W.s1[b] ? i - R.x0 : i;  // the record's slot in its side's buffer
     if (b < nb && W.act[b]) {
-      if (li < kTRC) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
+      const uint32_t li = W.s1[b] ? i - R.x0 : i;  // the record's slot in its side's buffer
+      if (!kSpill || !R.spilled || li < kTRC) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
       else  // a spilled record (written by another wave last round: L2, past this CU's L1)
         W.rec[b] = __hip_atomic_load(R.sp[W.s1[b] ? 1 : 0] + (li - kTRC), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
@@ -364,7 +365,7 @@ __device__ __forceinline__ void round_count(Counts<NB>& K, const Work<NB>& W) {
 constexpr uint32_t kOvfQueue = 1, kOvfRec = 2;
 template <int NB, bool kSpec, bool kSpill>
 __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K, const RoundCtx& R, int nb,
-                                                uint32_t q0b, uint32_t q1b, uint32_t e0b, uint32_t e1b, uint32_t lane,
+                                                uint32_t q0b, uint32_t q1b, uint32_t e0b, uint32_t e1b, bool wspill, uint32_t lane,
                                                 const unsigned long long* __restrict__ tadj, uint32_t (*QU)[kTinyQ],
                                                 uint32_t* JQ, unsigned long long* JR, unsigned long long* meet) {
   uint32_t ovf = 0;
@@ -390,7 +391,7 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
     unsigned long long* junk = JR + lane;
     const uint32_t dd = rok ? deg : 0u;
     const unsigned long long tag = (unsigned long long)q << 52;
-    if (!kSpill || !__ballot(rok && e + deg > kTRC)) {
+    if (!kSpill || !wspill) {
       // past the degree (or with nothing to store) a store goes to the lane's junk slot
 #pragma unroll
       for (uint32_t j = 0; j < kTinyUnroll; ++j) *(j < dd ? out + j : junk) = W.nbw[b][j] | tag;
@@ -481,6 +482,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     X.dep[1] = d1;
     X.exp[0] = x0 != 0;
     X.exp[1] = x1 != 0;
+    X.spilled = x0 > kTRC || x1 > kTRC;
     return X;
   };
 
@@ -555,11 +557,11 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           const uint32_t x0 = T.E0, x1 = T.E1;
           const RoundCtx X = make_ctx(x0, x1, T.cb0, T.cb1, T.d0, T.d1);
           Work<NB> W;
-          round_issue<NB, true>(W, X, lane, 64, NB, P.tadj, VIS);
+          round_issue<NB, true, false>(W, X, lane, 64, NB, P.tadj, VIS);
           Counts<NB> K;
           round_count<NB>(K, W);
           const uint32_t ovf =
-              round_place<NB, true, false>(W, K, X, NB, T.ql0, T.ql1, 0u, 0u, lane, P.tadj, QU, JQ, JR, &C.meet);
+              round_place<NB, true, false>(W, K, X, NB, T.ql0, T.ql1, 0u, 0u, false, lane, P.tadj, QU, JQ, JR, &C.meet);
           const bool qovf = __ballot(ovf & kOvfQueue) != 0, rovf = __ballot(ovf & kOvfRec) != 0;
           T.x0 = x0;
           T.x1 = x1;
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         constexpr int NB = decltype(nbc)::value;
         const int nb = (NB == 2 && c0 + wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
         Work<NB> W;
-        round_issue<NB, kSpecAll>(W, X, c0 + tid, kTT, nb, P.tadj, VIS);
+        round_issue<NB, kSpecAll, kSpillOn>(W, X, c0 + tid, kTT, nb, P.tadj, VIS);
         if (!kSpecAll) round_fetch<NB>(W, nb, P.tadj);
         Counts<NB> K;
         round_count<NB>(K, W);
@@ -659,9 +661,12 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
                                                (unsigned long long)K.qt[0] << 40 | (unsigned long long)K.qt[1] << 52);
           const uint32_t blo = lane0((uint32_t)base), bhi = lane0((uint32_t)(base >> 32));
           TINY_PH(4)
-          const uint32_t ovf = round_place<NB, kSpecAll, kSpillOn>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu), ql1 + (bhi >> 20),
-                                               blo & 0xFFFFFu, ((blo >> 20) | (bhi << 12)) & 0xFFFFFu, lane, P.tadj,
-                                               QU, JQ, JR, &C.meet);
+          const uint32_t e0b = blo & 0xFFFFFu, e1b = ((blo >> 20) | (bhi << 12)) & 0xFFFFFu;
+          // (uniform) does any of this wave's records land past the LDS buffer?
+          const bool wspill = e0b + K.et[0] > kTRC || e1b + K.et[1] > kTRC;
+          const uint32_t ovf = round_place<NB, kSpecAll, kSpillOn>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu),
+                                                                   ql1 + (bhi >> 20), e0b, e1b, wspill, lane, P.tadj,
+                                                                   QU, JQ, JR, &C.meet);
           // a full queue: fatal in a lockstep round (a dropped candidate may be
           // the shorter one -- key 0 = overflow, a meet has length >= 1); in a
           // single-side round every candidate has the same length, so like a
