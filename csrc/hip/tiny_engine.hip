@@ -639,6 +639,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       // one item per lane when the round has at most kTT edges (every round
       // under the lockstep cap), two otherwise: as in the single-wave phase
       // the one-item body carries none of the second item's instructions
+      bool wsp = false;  // (uniform) this wave stored spilled records this round
       // c0: first item of this pass (a two-pass round: 0, then kCapR)
       auto aw_round = [&](auto nbc, uint32_t c0) {
         constexpr int NB = decltype(nbc)::value;
@@ -664,6 +665,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           const uint32_t e0b = blo & 0xFFFFFu, e1b = ((blo >> 20) | (bhi << 12)) & 0xFFFFFu;
           // (uniform) does any of this wave's records land past the LDS buffer?
           const bool wspill = e0b + K.et[0] > kTRC || e1b + K.et[1] > kTRC;
+          wsp = wsp || wspill;
           const uint32_t ovf = round_place<NB, kSpecAll, kSpillOn>(W, K, X, nb, ql0 + ((bhi >> 8) & 0xFFFu),
                                                                    ql1 + (bhi >> 20), e0b, e1b, wspill, lane, P.tadj,
                                                                    QU, JQ, JR, &C.meet);
@@ -685,9 +687,11 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         }
       }
       TINY_PH(5)
-      // LDS barrier, plus the round's spilled records (global stores, rare;
-      // nothing else is in vmcnt here) drained for the next round's readers
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // LDS barrier; a wave that spilled records (global stores, rare) drains
+      // them first for the next round's readers -- the others leave their
+      // unused speculative loads in flight
+      if (kSpillOn && wsp) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();
       TINY_PH(6)
       einsp += X.tot;
       levels += (x0 != 0) + (x1 != 0);
