@@ -16,7 +16,7 @@
 #   suite    reference suite table (C21): scripts/make_graphs + scripts/benchmark_test.sh
 #            over 1k/10k/50k/100k x v1, v2 (np 4), v3 (--resident), v4 (np 4: ranks share the GPU over IPC)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench
-#   pmc      one SQ counter pass (rocprofv3 --pmc) over the resident 100k workload
+#   pmc      one SQ counter pass (rocprofv3 --pmc) over the resident 100k workload (PMCGRAPH=spec: another graph)
 #   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
 #            (SPECS / RANKS / OVERLAP / QUERIES override benchmarks/dist_rounds.py's defaults)
@@ -28,6 +28,7 @@
 #   trace    rocprofv3 --kernel-trace of pair_latency over GRAPHS (per-query kernel timelines)
 #   kron     benchmarks/kron_scale.py over SCALES (default 20,22,24,26,27,28), resident server
 #   stress   benchmarks/stress_resident.py
+#   dstress  benchmarks/stress_dist_local.py --procs (partitioned engine as processes, answers vs the CPU)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
@@ -59,7 +60,10 @@ run_task() {
     pmc)
       timeout -s KILL 120 rocprofv3 --output-format csv --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
         SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES -d $O/${TAG}_pmc_sq -- \
-        python3 benchmarks/pmc_100k.py --mode resident > $O/${TAG}_pmc_sq.log 2>&1 ;;
+        python3 benchmarks/pmc_100k.py --mode resident ${PMCGRAPH:+--graph $PMCGRAPH} > $O/${TAG}_pmc_sq.log 2>&1 ;;
+    dstress)
+      $T 900 python3 -u benchmarks/stress_dist_local.py --procs ${RANKS:+--ranks $RANKS} ${QUERIES:+--queries $QUERIES} \
+        > $O/${TAG}_dstress.jsonl 2> $O/${TAG}_dstress.err ;;
     distab)
       $T 900 python3 benchmarks/dist_rounds.py ${SPECS:+--specs $SPECS} ${RANKS:+--ranks $RANKS} \
         ${OVERLAP:+--overlap $OVERLAP} ${QUERIES:+--queries $QUERIES} \
