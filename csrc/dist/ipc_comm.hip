@@ -255,10 +255,31 @@ class IpcComm final : public Comm {
     // whose IPC handle some runtimes (torch's bundled HIP 7.0) refuse to open
     size_t cap = 2u << 20;
     while (cap < bytes) cap <<= 1;
-    HIP_CHECK(hipMalloc(&stage_[slot], cap));
-    IpcGroup::Blob& me = group_.mine(slot);
+    // A block the runtime will not export (seen with 8 ranks on one device:
+    // hipIpcGetMemHandle "invalid argument" on a fresh 2 MiB hipMalloc) is
+    // held while a larger one is tried -- so the allocator cannot hand the
+    // same block back -- and freed once one exports.
+    std::vector<void*> refused;
     hipIpcMemHandle_t h;
-    HIP_CHECK(hipIpcGetMemHandle(&h, stage_[slot]));
+    for (int attempt = 0;; ++attempt) {
+      HIP_CHECK(hipMalloc(&stage_[slot], cap));
+      const hipError_t e = hipIpcGetMemHandle(&h, stage_[slot]);
+      if (e == hipSuccess) break;
+      (void)hipGetLastError();
+      if (std::getenv("BIBFS_IPC_DEBUG"))
+        std::fprintf(stderr, "[ipc rank %d] hipIpcGetMemHandle(%p, %zu bytes): %s; retrying larger\n", rank_,
+                     stage_[slot], cap, hipGetErrorString(e));
+      refused.push_back(stage_[slot]);
+      stage_[slot] = nullptr;
+      if (attempt == 5) {
+        for (void* p : refused) (void)hipFree(p);
+        throw Error(std::string("ipc comm: rank ") + std::to_string(rank_) +
+                    " cannot export a staging buffer: hipIpcGetMemHandle: " + hipGetErrorString(e));
+      }
+      cap <<= 1;
+    }
+    for (void* p : refused) HIP_CHECK(hipFree(p));
+    IpcGroup::Blob& me = group_.mine(slot);
     std::memcpy(me.handle, &h, sizeof(h));
     me.cap = cap;
     me.gen = ++gen_;

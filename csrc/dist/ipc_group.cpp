@@ -55,6 +55,7 @@ struct IpcGroup::Shm {
   std::atomic<int32_t> attached;
   std::atomic<int32_t> aborted;   // 0, or 1 + the rank that aborted first
   std::atomic<int32_t> detached;  // ranks through the teardown rendezvous
+  std::atomic<int32_t> why_ready; // `why` is written (after the abort CAS)
   char why[240];
   IpcRankSlot r[kIpcMax];
 };
@@ -156,6 +157,10 @@ bool IpcGroup::aborted() const { return aborted_ || (shm_ && shm_->aborted.load(
 
 std::string IpcGroup::abort_message() const {
   const int who = shm_ ? shm_->aborted.load(std::memory_order_acquire) : 0;
+  if (who) {  // the first aborter writes its reason right after its CAS
+    const auto until = clock::now() + std::chrono::milliseconds(2);
+    while (!shm_->why_ready.load(std::memory_order_acquire) && clock::now() < until) std::this_thread::yield();
+  }
   const std::string why = shm_ && who ? std::string(shm_->why, strnlen(shm_->why, sizeof(shm_->why))) : "";
   return "ipc group aborted" + (who ? " (first by rank " + std::to_string(who - 1) + ": " + why + ")" : std::string());
 }
@@ -166,7 +171,7 @@ void IpcGroup::abort(const std::string& why) {
   int expect = 0;
   if (shm_->aborted.compare_exchange_strong(expect, rank_ + 1, std::memory_order_acq_rel)) {
     std::snprintf(shm_->why, sizeof(shm_->why), "%s", why.c_str());
-    std::atomic_thread_fence(std::memory_order_release);
+    shm_->why_ready.store(1, std::memory_order_release);
   }
 }
 
