@@ -505,12 +505,15 @@ def main(argv=None) -> int:
         """ONE partitioned engine (one communicator) for every config: its
         bootstrap -- the first RCCL communicator of the process pays ~3.5 s of
         library / kernel loading -- is reported once (partitioned_comm_init_ms),
-        not inside the first config; release() frees a config's graph."""
+        not inside the first config; release() frees a config's graph.  At
+        world size 1 the engine's collectives are copies to itself (an
+        in-process group of one: no RCCL bootstrap, no unique id needed)."""
         if "eng" not in dstate:
             barrier()
             t0 = time.perf_counter()
             if world == 1:
-                dstate["eng"] = DistEngine(0, 1, local, DistEngine.unique_id(comm), comm)
+                uid = DistEngine.unique_id(comm) if os.environ.get("BIBFS_WORLD1_COMM") == comm else b""
+                dstate["eng"] = DistEngine(0, 1, local, uid, comm)
             else:
                 dstate["eng"] = DistEngine.from_torch_distributed(local, backend=comm)
             dstate["init_ms"] = max_over_ranks((time.perf_counter() - t0) * 1e3)

@@ -3527,7 +3527,12 @@ void DistBiBfs::Impl::walk_path_per_hop(uint64_t key, uint32_t it, SearchResult&
 DistBiBfs::DistBiBfs(int rank, int size, int device, const std::vector<uint8_t>& uid, const std::string& backend)
     : p_(new Impl) {
   HIP_CHECK(hipSetDevice(device));
-  if (backend == "ipc")
+  const char* w1 = std::getenv("BIBFS_WORLD1_COMM");  // "rccl" / "ipc": keep that backend at one rank (tests)
+  if (size == 1 && (backend == "ipc" || backend == "rccl") && !(w1 && backend == w1))
+    // one rank: every collective is a copy to itself -- the in-process group
+    // of one does that without RCCL's ~3.4 s communicator bootstrap
+    p_->comm = dist::make_local_comm(dist::make_local_group(1, p_->tune.timeout_s), 0);
+  else if (backend == "ipc")
     p_->comm = dist::make_ipc_comm(rank, size, uid, p_->tune.timeout_s);
   else if (backend == "rccl")
     p_->comm = dist::make_rccl_comm(rank, size, uid);

@@ -1,5 +1,6 @@
-"""Multi-GPU engine (world size 1 on the single-GPU box: RCCL communicator of
-one rank), the GPU CLI tools and the bench.py contract."""
+"""Multi-GPU engine (world size 1 on the single-GPU box: the in-process group
+of one rank, and an RCCL communicator of one rank), the GPU CLI tools and the
+bench.py contract."""
 import json
 import os
 import random
@@ -17,12 +18,19 @@ from bidirectional_bfs_amd.utils.oracle import check_result
 pytestmark = pytest.mark.gpu
 
 
-def test_dist_engine_world1():
+@pytest.mark.parametrize("world1_comm", ["", "rccl"])
+def test_dist_engine_world1(world1_comm, monkeypatch):
+    """World size 1: by default the engine's collectives go to an in-process
+    group of one (no RCCL bootstrap); BIBFS_WORLD1_COMM=rccl keeps a one-rank
+    RCCL communicator, so the RCCL backend stays exercised on one GPU."""
     import torch  # noqa: F401
 
     from bidirectional_bfs_amd.parallel import DistEngine
 
+    if world1_comm:
+        monkeypatch.setenv("BIBFS_WORLD1_COMM", world1_comm)
     eng = DistEngine(0, 1, 0, DistEngine.unique_id())
+    assert eng.backend == (world1_comm or "local")
     for spec in ["gnp:100000::6", "rmat:65536:1048576:3"]:
         g = bb.from_spec(spec)
         eng.load(g)
