@@ -339,6 +339,9 @@ __device__ unsigned long long lds_meet_probe(const LdsParams<OffT>& P, int q, ui
   uint32_t* sEb = reinterpret_cast<uint32_t*>(sbp + kLdsThreads);  // exclusive prefix of the (clamped) degrees
   const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
   if (tid == 0) pr_hit = ~0ull;
+  // every wave's queue stores complete before any wave reads the queue with
+  // L2 loads (__syncthreads() alone waits for no store on gfx950)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   uint32_t walked = 0;
   bool stop = false;
@@ -1059,7 +1062,11 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       }
       if (!kLq) {
         // global queue and parents all along: nothing to materialise, the path
-        // is walked along the global parent arrays
+        // is walked along the global parent arrays.  The wave-0 schedule may
+        // read queue entries other waves wrote (rebuild, meet probe: L2
+        // loads), so every wave's stores complete before it goes on alone --
+        // __syncthreads() alone waits for no store on gfx950.
+        if (status == kRunning && rounds_done) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       } else if (status != kRunning) {
         lq_done = true;  // the path is walked in LDS
       } else {
@@ -1081,7 +1088,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
             R[a1][o1 + i - E0].x = LQ[1][R[a1][o1 + i - E0].x];
           }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        // (the queue / parent stores complete too: see the !kLq case)
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
       }
       if (rounds_done == 0) return;
       s0.cur = a0, s0.off = o0, s0.fed = E0, s0.depth = (int)d0, s0.fbeg = qe0 - c0, s0.qend = qe0;
@@ -1104,6 +1112,9 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     if (!x.ovf || x.cnt > kRebuildMax || x.fed > CAP || !(kBm || x.hcnt + x.fed <= kHashLimit)) return false;
     const uint32_t buf = free_buf();
     const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
+    // wave 0's own queue stores complete (other waves drained theirs before
+    // the barrier that left wave 0 alone)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t u[4], d[4];
     OffT b[4];
 #pragma unroll
@@ -1357,7 +1368,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
         if (base + (uint32_t)wid * kWave < ET) batch(std::integral_constant<int, kBatch>{}, base);
     }
     if (kStamp && tid == 0) ts1 = stamp();
-    __syncthreads();  // B2: every claim of the big level is in LDS
+    // B2: every claim of the big level is in LDS, and its queue / parent
+    // stores are complete (wave 0 may read queue entries next: rebuild, probe)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
     if (kStamp && tid == 0) ts2 = stamp();
     if (wid == 0) {
       const unsigned long long p0 = ctr[slot][0], p1 = ctr[slot][1];
