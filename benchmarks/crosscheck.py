@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--graph", default="kron:27:16:1")
     ap.add_argument("--pairs", type=int, default=400)
     ap.add_argument("--seed", type=int, default=5)
+    ap.add_argument("--resident", type=int, default=1)
+    ap.add_argument("--probe", type=int, default=-1, help="lds_probe_edges (-1: the default)")
     a = ap.parse_args()
     import torch  # noqa: F401
     import bench
@@ -29,23 +31,26 @@ def main():
     eng = bench.generate(HipEngine(0), a.graph)
     rnd = random.Random(a.seed)
     pairs = [(rnd.randrange(n), rnd.randrange(n)) for _ in range(a.pairs)]
-    eng.set_resident(True)
-    res = []
+    if a.probe >= 0:
+        eng.lds_probe_edges = a.probe
+    eng.set_resident(bool(a.resident))
+    res, info = [], []
     hits = hand = 0
     for s, d in pairs:
         r = eng.search(s, d)
         res.append(r.hops)
+        info.append((bool(r.stats["probe_hit"]), bool(r.handoff), r.stats["lds_levels"], r.stats["grid_levels"]))
         hits += bool(r.stats["probe_hit"])
         hand += bool(r.handoff)
         assert r.hops < 0 or (len(r.path) == r.hops + 1 and r.path[0] == s and r.path[-1] == d)
     eng.set_resident(False)
     grid = make_options(force_grid=True)
     wrong = []
-    for (s, d), h in zip(pairs, res):
+    for (s, d), h, inf in zip(pairs, res, info):
         g = eng.search(s, d, grid).hops
         if g != h:
-            wrong.append((s, d, h, g))
-    print(json.dumps({"graph": a.graph, "pairs": len(pairs), "probe_hits": hits, "handoffs": hand,
+            wrong.append((s, d, h, g) + inf)
+    print(json.dumps({"graph": a.graph, "resident": a.resident, "probe": eng.lds_probe_edges, "pairs": len(pairs), "probe_hits": hits, "handoffs": hand,
                       "wrong": len(wrong), "examples": wrong[:5]}), flush=True)
     return 1 if wrong else 0
 
