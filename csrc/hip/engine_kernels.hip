@@ -199,6 +199,7 @@ struct LdsParams {
   // meet probe before a hand-off: frontier edges it may read (0 = off; see
   // lds_meet_probe)
   uint32_t probe = 0;
+  int rebuild = 1;  // lost small-level records rebuilt from the queue (BIBFS_LDS_REBUILD=0: off)
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -1109,7 +1110,8 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   auto rebuild = [&](int q) -> bool {
     constexpr uint32_t kRebuildMax = 4 * kWave;
     SideState x = sel(q, s0, s1);
-    if (!x.ovf || x.cnt > kRebuildMax || x.fed > CAP || !(kBm || x.hcnt + x.fed <= kHashLimit)) return false;
+    if (!P.rebuild || !x.ovf || x.cnt > kRebuildMax || x.fed > CAP || !(kBm || x.hcnt + x.fed <= kHashLimit))
+      return false;
     const uint32_t buf = free_buf();
     const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
     // wave 0's own queue stores complete (other waves drained theirs before
@@ -2647,6 +2649,14 @@ uint32_t lds_probe_budget() {
 }
 
 // graphs whose largest degree is above BIBFS_LDS_PROBE_MIN_DEG (default 64)
+static int rebuild_on() {
+  static const int on = [] {
+    const char* e = std::getenv("BIBFS_LDS_REBUILD");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on;
+}
+
 static uint32_t probe_for(const GraphView& g) {
   static const uint64_t min_deg = [] {
     const char* e = std::getenv("BIBFS_LDS_PROBE_MIN_DEG");
@@ -2669,6 +2679,8 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
     P.probe = probe_for(g);
+  P.rebuild = rebuild_on();
+    P.rebuild = rebuild_on();
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
       if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -2681,6 +2693,8 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
     LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.probe = probe_for(g);
+  P.rebuild = rebuild_on();
+    P.rebuild = rebuild_on();
     if (trace == 2)
       k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
     else
@@ -2698,6 +2712,8 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
                           (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.b_alt = b_alt;
     P.probe = probe_for(g);
+  P.rebuild = rebuild_on();
+    P.rebuild = rebuild_on();
     k_lds_server<uint64_t, false><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
     HIP_CHECK(hipGetLastError());
     return;
@@ -2707,6 +2723,7 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
   P.b_alt = b_alt;
   P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
   P.probe = probe_for(g);
+  P.rebuild = rebuild_on();
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
