@@ -4,7 +4,7 @@ import torch  # noqa
 import bench
 from bidirectional_bfs_amd.ops import HipEngine, make_options
 spec = sys.argv[1] if len(sys.argv) > 1 else "kron:27:16:1"
-pairs = [(26740478, 130093872)]
+pairs = [tuple(int(x) for x in a.split(":")) for a in sys.argv[2:]] or [(26740478, 130093872)]
 eng = bench.generate(HipEngine(0), spec)
 for s, d in pairs:
     for resident in (False, True):
@@ -19,5 +19,6 @@ for s, d in pairs:
         eng.set_resident(False)
     r = eng.search(s, d, make_options(force_grid=True))
     print(json.dumps({"force_grid": True, "hops": r.hops, "path": list(r.path)}), flush=True)
-    r = eng.search(s, d, make_options(trace=True))
-    print(json.dumps({"trace": True, "hops": r.hops, "levels": [(t["side"], t["depth"], t["frontier"], t["edges"], t["discovered"], t["mode"]) for t in r.stats["trace"]]}), flush=True)
+    for fg in (False, True):
+        r = eng.search(s, d, make_options(trace=True, force_grid=fg))
+        print(json.dumps({"trace": True, "force_grid": fg, "hops": r.hops, "levels": [(t["side"], t["depth"], t["frontier"], t["edges"], t["discovered"], t["mode"]) for t in r.stats["trace"]]}), flush=True)
