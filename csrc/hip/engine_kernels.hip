@@ -508,12 +508,14 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       const int l = __ffsll((long long)m) - 1;
       const uint32_t d = __builtin_amdgcn_readlane(dl, l), e = __builtin_amdgcn_readlane(eb, l);
       const uint32_t vl = __builtin_amdgcn_readlane(v, l);
+      // (readlane returns int: widen through uint32_t, or a row base at or
+      // above 2^31 -- Kronecker 27 -- is sign-extended into garbage)
       OffT bl;
       if constexpr (sizeof(OffT) == 8)
-        bl = (OffT)__builtin_amdgcn_readlane((uint32_t)base, l) |
-             ((OffT)__builtin_amdgcn_readlane((uint32_t)((uint64_t)base >> 32), l) << 32);
+        bl = (OffT)(uint32_t)__builtin_amdgcn_readlane((uint32_t)base, l) |
+             ((OffT)(uint32_t)__builtin_amdgcn_readlane((uint32_t)((uint64_t)base >> 32), l) << 32);
       else
-        bl = (OffT)__builtin_amdgcn_readlane((uint32_t)base, l);
+        bl = (OffT)(uint32_t)__builtin_amdgcn_readlane((uint32_t)base, l);
       for (uint32_t j = lane; j < d; j += kWave) rec_set(Rn[e + j], vl, bl + j);
     }
   };
@@ -1954,8 +1956,8 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
       bool seen = false;
       for (;;) {
         g = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        g = ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
-            __builtin_amdgcn_readfirstlane((uint32_t)g);
+        g = ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(g >> 32)) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)g);
         const uint32_t gs = (uint32_t)(g >> 32);
         if (gs == P.gate_seq) {
           seen = true;
