@@ -199,8 +199,6 @@ struct LdsParams {
   // meet probe before a hand-off: frontier edges it may read (0 = off; see
   // lds_meet_probe)
   uint32_t probe = 0;
-  int rebuild = 1;  // lost small-level records rebuilt from the queue (BIBFS_LDS_REBUILD=0: off)
-  int coop = 1;     // long record runs appended by the whole wave (BIBFS_LDS_COOP=0: off, diagnosis)
 };
 
 __device__ __forceinline__ uint32_t xcc_id() {
@@ -502,7 +500,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   // wave calls it (ballot inside).
   auto append_records = [&](Rec* Rn, uint32_t dl, uint32_t eb, uint32_t v, OffT base) {
     constexpr uint32_t kCoopRun = 32;
-    const bool coop = P.coop && dl > kCoopRun;
+    const bool coop = dl > kCoopRun;
     for (uint32_t j = 0; j < (coop ? 0u : dl); ++j) rec_set(Rn[eb + j], v, base + j);
     for (unsigned long long m = __ballot(coop); m; m &= m - 1) {
       const int l = __ffsll((long long)m) - 1;
@@ -1113,8 +1111,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   auto rebuild = [&](int q) -> bool {
     constexpr uint32_t kRebuildMax = 4 * kWave;
     SideState x = sel(q, s0, s1);
-    if (!P.rebuild || !x.ovf || x.cnt > kRebuildMax || x.fed > CAP || !(kBm || x.hcnt + x.fed <= kHashLimit))
-      return false;
+    if (!x.ovf || x.cnt > kRebuildMax || x.fed > CAP || !(kBm || x.hcnt + x.fed <= kHashLimit)) return false;
     const uint32_t buf = free_buf();
     const uint32_t* qu = q ? P.b.queue[1] : P.b.queue[0];
     // wave 0's own queue stores complete (other waves drained theirs before
@@ -2652,22 +2649,6 @@ uint32_t lds_probe_budget() {
 }
 
 // graphs whose largest degree is above BIBFS_LDS_PROBE_MIN_DEG (default 64)
-static int coop_on() {
-  static const int on = [] {
-    const char* e = std::getenv("BIBFS_LDS_COOP");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return on;
-}
-
-static int rebuild_on() {
-  static const int on = [] {
-    const char* e = std::getenv("BIBFS_LDS_REBUILD");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  return on;
-}
-
 static uint32_t probe_for(const GraphView& g) {
   static const uint64_t min_deg = [] {
     const char* e = std::getenv("BIBFS_LDS_PROBE_MIN_DEG");
@@ -2690,11 +2671,6 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
     P.probe = probe_for(g);
-  P.rebuild = rebuild_on();
-  P.coop = coop_on();
-    P.rebuild = rebuild_on();
-  P.coop = coop_on();
-    P.coop = coop_on();
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
       if (bm) k_lds_bibfs<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P);
@@ -2707,11 +2683,6 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
     LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.probe = probe_for(g);
-  P.rebuild = rebuild_on();
-  P.coop = coop_on();
-    P.rebuild = rebuild_on();
-  P.coop = coop_on();
-    P.coop = coop_on();
     if (trace == 2)
       k_lds_bibfs<uint64_t, true, false><<<blocks, kLdsThreads, 0, s>>>(P);
     else
@@ -2729,11 +2700,6 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
                           (uint64_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
     P.b_alt = b_alt;
     P.probe = probe_for(g);
-  P.rebuild = rebuild_on();
-  P.coop = coop_on();
-    P.rebuild = rebuild_on();
-  P.coop = coop_on();
-    P.coop = coop_on();
     k_lds_server<uint64_t, false><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
     HIP_CHECK(hipGetLastError());
     return;
@@ -2743,8 +2709,6 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
   P.b_alt = b_alt;
   P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
   P.probe = probe_for(g);
-  P.rebuild = rebuild_on();
-  P.coop = coop_on();
   static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
   if (g.n <= kBmMaxN && stamp)
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
