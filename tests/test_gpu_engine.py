@@ -456,6 +456,33 @@ def test_wide_offsets_resident_server_vs_oracle(gpu_engine, spec, monkeypatch):
         gpu_engine.load(g)  # 32-bit offsets again for the tests after this one
 
 
+def test_row_bases_above_2_31_vs_grid_engine(gpu_engine):
+    """A graph whose CSR row bases pass 2^31 (Kronecker 26, edge factor 20:
+    2.7B directed edges, generated on the device): resident LDS searches --
+    meet probe, cooperative hub appends, lost-record rebuild, hand-offs --
+    against the grid-only engine on 300 random pairs.  (A 64-bit row base
+    sign-extended through a 32-bit lane read once sent a whole hub's records
+    to one edge and returned too-long paths on Kronecker 27.)"""
+    gpu_engine.generate_rmat(1 << 26, 20 << 26, 1)
+    assert gpu_engine.nnz > (1 << 31)
+    n = 1 << 26
+    rnd = random.Random(27)
+    pairs = [(rnd.randrange(n), rnd.randrange(n)) for _ in range(300)]
+    gpu_engine.set_resident(True)
+    try:
+        got = []
+        for s, d in pairs:
+            r = gpu_engine.search(s, d)
+            assert r.hops < 0 or (len(r.path) == r.hops + 1 and r.path[0] == s and r.path[-1] == d)
+            got.append(r.hops)
+    finally:
+        gpu_engine.set_resident(False)
+    grid = make_options(force_grid=True)
+    wrong = [(s, d, h, gpu_engine.search(s, d, grid).hops) for (s, d), h in zip(pairs, got)
+             if gpu_engine.search(s, d, grid).hops != h]
+    assert not wrong, wrong[:5]
+
+
 def test_auto_handoff_gate_timeout_falls_back_to_host(gpu_engine):
     """The gated first grid level gives up when its search has not left LDS in
     time (forced here: a zero wait).  Such a search still hands off later; the
