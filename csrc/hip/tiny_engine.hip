@@ -203,10 +203,11 @@ struct RoundCtx {
   const unsigned long long* rb0;     // side 0's current records
   const unsigned long long* rb1x;    // side 1's current records, minus x0 (indexed by the item)
   unsigned long long* nb[2];         // next-round record buffers
-  // records past the LDS buffers (slot >= kTRC) live in global memory: the
-  // current round's per side, and the next round's
-  const unsigned long long* sp[2];
-  unsigned long long* ns[2];
+  // records past the LDS buffers (slot >= kTRC) live in global memory
+  // (TinyArgs::spill, [buffer][side][kTinySpill]); the slices are computed
+  // only on the rare paths that touch them, to keep this context small
+  unsigned long long* spill;
+  uint32_t cb;                       // current record buffer per side: bit 0 side 0, bit 1 side 1
   bool spilled;                      // a side's current records pass kTRC (uniform)
   uint32_t par[2];                   // depth parity bit of this round's claims per side
   uint32_t dep[2];                   // frontier depth per side before the round
@@ -242,7 +243,8 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
       const uint32_t li = W.s1[b] ? i - R.x0 : i;  // the record's slot in its side's buffer
       if (!kSpill || !R.spilled || li < kTRC) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
       else  // a spilled record (written by another wave last round: L2, past this CU's L1)
-        W.rec[b] = __hip_atomic_load(R.sp[W.s1[b] ? 1 : 0] + (li - kTRC), __ATOMIC_RELAXED,
+        W.rec[b] = __hip_atomic_load(R.spill + (size_t)(((R.cb >> (W.s1[b] ? 1 : 0)) & 1u) * 2 + (W.s1[b] ? 1 : 0)) *
+                                                  kTinySpill + (li - kTRC), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -400,7 +402,8 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
         for (uint32_t j = kTinyUnroll; rok && j < deg; ++j) out[j] = tadj[base + j] | tag;
       }
     } else {  // rare: some of the wave's records go past the LDS buffer (global spill)
-      unsigned long long* sp = R.ns[s1 ? 1 : 0];
+      const uint32_t side = s1 ? 1u : 0u;
+      unsigned long long* sp = R.spill + (size_t)((((R.cb >> side) & 1u) ^ 1u) * 2 + side) * kTinySpill;
       const uint32_t base = tw_base(W.rec[b]);
       for (uint32_t j = 0; j < dd; ++j) {
         const unsigned long long w = (j < kTinyUnroll ? W.nbw[b][j] : tadj[base + j]) | tag;
@@ -472,10 +475,8 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
     X.rb1x = &R[cb1][1][0] - x0;
     X.nb[0] = &R[cb0 ^ 1][0][0];
     X.nb[1] = &R[cb1 ^ 1][1][0];
-    X.sp[0] = P.spill + (size_t)(cb0 * 2 + 0) * kTinySpill;  // [buffer][side][kTinySpill]
-    X.sp[1] = P.spill + (size_t)(cb1 * 2 + 1) * kTinySpill;
-    X.ns[0] = P.spill + (size_t)((cb0 ^ 1) * 2 + 0) * kTinySpill;
-    X.ns[1] = P.spill + (size_t)((cb1 ^ 1) * 2 + 1) * kTinySpill;
+    X.spill = P.spill;
+    X.cb = cb0 | cb1 << 1;
     X.par[0] = (d0 + 1) & 1;
     X.par[1] = (d1 + 1) & 1;
     X.dep[0] = d0;
