@@ -241,7 +241,7 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
     W.rec[b] = 1ull;  // an idle lane: vertex 0, base 0, degree 1
     if (b < nb && W.act[b]) {
       const uint32_t li = W.s1[b] ? i - R.x0 : i;  // the record's slot in its side's buffer
-      if (!kSpill || li < kTRC) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
+      if (!kSpill || !R.spilled || li < kTRC) W.rec[b] = (W.s1[b] ? R.rb1x : R.rb0)[i];
       else  // a spilled record (written by another wave last round: L2, past this CU's L1)
         W.rec[b] = __hip_atomic_load(R.spill + (size_t)(((R.cb >> (W.s1[b] ? 1 : 0)) & 1u) * 2 + (W.s1[b] ? 1 : 0)) *
                                                   kTinySpill + (li - kTRC), __ATOMIC_RELAXED,
@@ -642,14 +642,11 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       // the one-item body carries none of the second item's instructions
       bool wsp = false;  // (uniform) this wave stored spilled records this round
       // c0: first item of this pass (a two-pass round: 0, then kCapR)
-      // rd: this round reads spilled records (compiled apart: the common
-      // round carries none of the spill reads)
-      auto aw_round = [&](auto nbc, auto rdc, uint32_t c0) {
+      auto aw_round = [&](auto nbc, uint32_t c0) {
         constexpr int NB = decltype(nbc)::value;
-        constexpr bool kRd = decltype(rdc)::value;
         const int nb = (NB == 2 && c0 + wid * 64 + kTT < X.tot) ? 2 : 1;  // uniform
         Work<NB> W;
-        round_issue<NB, kSpecAll, kRd>(W, X, c0 + tid, kTT, nb, P.tadj, VIS);
+        round_issue<NB, kSpecAll, kSpillOn>(W, X, c0 + tid, kTT, nb, P.tadj, VIS);
         if (!kSpecAll) round_fetch<NB>(W, nb, P.tadj);
         Counts<NB> K;
         round_count<NB>(K, W);
@@ -686,12 +683,8 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
       };
       for (uint32_t c0 = 0; c0 < X.tot; c0 += kCapR) {  // one pass, two for a big single-side round
         if (c0 + wid * 64 < X.tot) {
-          if (kSpillOn && X.spilled)  // rare: a round past kTRC records (two passes, spilled reads)
-            aw_round(std::integral_constant<int, 2>{}, std::true_type{}, c0);
-          else if (kAwSplit && X.tot - c0 <= (uint32_t)kTT)
-            aw_round(std::integral_constant<int, 1>{}, std::false_type{}, c0);
-          else
-            aw_round(std::integral_constant<int, 2>{}, std::false_type{}, c0);
+          if (kAwSplit && X.tot - c0 <= (uint32_t)kTT) aw_round(std::integral_constant<int, 1>{}, c0);
+          else aw_round(std::integral_constant<int, 2>{}, c0);
         }
       }
       TINY_PH(5)
