@@ -205,7 +205,13 @@ struct SearchBuffers {
   // for the kernels behind it.
   uint32_t* aux;
   uint32_t* hdump;      // raw LDS hash tables of a hash-set search's hand-off (handoff_dump_bytes())
+  // stamped traces (BIBFS_STAMP): per grid level (levels % kGridStampLevels)
+  // kGridStampWords s_memrealtime stamps of a top-down level -- block 0's
+  // entry / chunk staged / chunk edges done / leaving, the finisher's start /
+  // end -- so a level's time splits into its dependent phases
+  unsigned long long* gstamp;
 };
+constexpr uint32_t kGridStampLevels = 64, kGridStampWords = 8;
 
 struct HostSide {
   dev::HostResult* res;  // pinned, device-visible

@@ -2043,6 +2043,12 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
   const int s = P.side;
   DevState* st = P.b.st;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // stamped trace (BIBFS_STAMP): block 0's phases, kGridStampWords per level
+  unsigned long long* gst = nullptr;
+  if (!kAuto && P.trace == 2 && blockIdx.x == 0 && tid == 0 && P.b.gstamp) {
+    gst = P.b.gstamp + (size_t)(st->levels % launch::kGridStampLevels) * launch::kGridStampWords;
+    gst[0] = __builtin_amdgcn_s_memrealtime();
+  }
   const uint32_t fbase = kAuto ? P.fbase : st->fbeg[s];
   const uint32_t F = kAuto ? P.fcount : st->fend[s] - fbase;
   const uint32_t parts = P.nparts ? P.nparts : gridDim.x;
@@ -2101,6 +2107,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     __syncthreads();
     sEb[tid] = x - deg + wsum[wid];
     __syncthreads();
+    if (gst && round == 0) gst[1] = __builtin_amdgcn_s_memrealtime();  // first chunk staged
     const uint32_t Ec = stotal;
     for (uint32_t base = 0, it = 0; base < Ec; base += kGridThreads, ++it) {
       // a meet ends the level (single-side level: every meet has the same
@@ -2134,8 +2141,12 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
       }
       grid_claim(P, valid, uu, v, vdeg);
     }
+    if (gst && round == 0) {  // first chunk's claims and appends issued ...
+      gst[2] = __builtin_amdgcn_s_memrealtime();
+    }
     __syncthreads();
   }
+  if (gst) gst[3] = __builtin_amdgcn_s_memrealtime();  // block 0 leaves its chunks
   if (P.mirror) fused_finish(P, 1, false);
 }
 
@@ -2452,6 +2463,11 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   __syncthreads();
   if (!__builtin_amdgcn_readfirstlane(slast)) return;
   uint32_t* w = reinterpret_cast<uint32_t*>(b.st);
+  unsigned long long* gst = nullptr;  // stamped trace: the finisher's start / end
+  if (P.trace == 2 && tid == 0 && b.gstamp) {
+    gst = b.gstamp + (size_t)(b.st->levels % launch::kGridStampLevels) * launch::kGridStampWords;
+    gst[4] = __builtin_amdgcn_s_memrealtime();
+  }
   if (tid < kWords) reinterpret_cast<uint32_t*>(&sv)[tid] = atomicAdd(&w[tid], 0u);
   __syncthreads();
   const bool defer = !hub_pass && sv.hub_count != 0;  // the hub pass finishes this level
@@ -2483,6 +2499,7 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
     next = snext != 0;
   }
   if (P.mirror && !next && tid < 64) publish_state(sv, P.mirror, P.seq, tid);
+  if (gst) gst[5] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Seed a search for the grid engine / step-wise API.

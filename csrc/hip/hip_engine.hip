@@ -555,6 +555,7 @@ struct HipBiBfs::Impl {
     size_t o_flag = take(64);
     size_t o_aux = take(64);
     size_t o_hdump = take(launch::handoff_dump_bytes());
+    size_t o_gst = take((size_t)launch::kGridStampLevels * launch::kGridStampWords * 8);
     state_bytes = off;
     HIP_CHECK(hipMalloc(&state_block, state_bytes));
     char* base = static_cast<char*>(state_block);
@@ -573,6 +574,7 @@ struct HipBiBfs::Impl {
     buf.words = (uint32_t)words;
     d_flag = reinterpret_cast<uint32_t*>(base + o_flag);
     buf.aux = reinterpret_cast<uint32_t*>(base + o_aux);
+    buf.gstamp = reinterpret_cast<unsigned long long*>(base + o_gst);
     buf.hdump = reinterpret_cast<uint32_t*>(base + o_hdump);
     // visited bitmaps must start (and stay) all-zero
     for (int s = 0; s < 2; ++s) HIP_CHECK(hipMemsetAsync(buf.vis[s], 0, words * 4, stream));
@@ -812,6 +814,25 @@ struct HipBiBfs::Impl {
     HIP_CHECK(hipStreamSynchronize(stream));
     std::fprintf(stderr, "[stamp] publish: hand-off state %u result puts %u bitmaps issued %u drained %u fence %llu\n",
                  w.side, w.depth, w.frontier, w.mode, (unsigned long long)w.edges);
+  }
+
+  // Stamped grid levels (BIBFS_STAMP + trace): block 0's phases and the
+  // finisher's, in us from block 0's entry (s_memrealtime, 100 MHz).
+  void fetch_grid_stamps(const SearchResult& r) {
+    std::vector<unsigned long long> g((size_t)launch::kGridStampLevels * launch::kGridStampWords);
+    HIP_CHECK(hipMemcpyAsync(g.data(), buf.gstamp, g.size() * 8, hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    for (size_t l = 0; l < r.stats.trace.size() && l < launch::kGridStampLevels; ++l) {
+      if (r.stats.trace[l].mode != 4) continue;  // grid top-down levels
+      const unsigned long long* t = &g[l * launch::kGridStampWords];
+      if (!t[0] || t[5] < t[0]) continue;
+      auto us = [&](int k) { return t[k] >= t[0] ? (double)(t[k] - t[0]) * 0.01 : -1.0; };
+      std::fprintf(stderr,
+                   "[grid stamp] level %zu (frontier %llu, edges %llu): block 0 staged %.2f us, claims issued %.2f, "
+                   "left %.2f; finisher start %.2f, end %.2f\n",
+                   l, (unsigned long long)r.stats.trace[l].frontier, (unsigned long long)r.stats.trace[l].edges, us(1),
+                   us(2), us(3), us(4), us(5));
+    }
   }
 
   void fetch_trace(SearchResult& r) {
@@ -1456,7 +1477,10 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
     r.search_ms += ms;
   }
   if (opt.trace) I.fetch_trace(r);
-  if (opt.trace && std::getenv("BIBFS_STAMP")) I.fetch_clock(r);
+  if (opt.trace && std::getenv("BIBFS_STAMP")) {
+    I.fetch_clock(r);
+    I.fetch_grid_stamps(r);
+  }
   return r;
 }
 
