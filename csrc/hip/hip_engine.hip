@@ -763,7 +763,8 @@ struct HipBiBfs::Impl {
     dir[0] = dir[1] = 1;
     fbits_valid[0] = fbits_valid[1] = false;
     int turn = 0;
-    const int trace = opt.trace ? 1 : 0;
+    // 2 = stamped (BIBFS_STAMP): the level kernels also write their phase stamps
+    const int trace = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
     for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
       if (guard == 0 && !mirror_valid) sync_state();  // state left by the seed
       if (h_state->status != kRunning || h_state->meet != kEmpty) break;
