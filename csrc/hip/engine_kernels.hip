@@ -1751,9 +1751,18 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
 constexpr int kGridThreads = 256;
 constexpr uint32_t kHubDegree = 4096;  // deferred to k_grid_hubs
 #ifndef BIBFS_KNOB_GRID_CHUNK_MIN
-#define BIBFS_KNOB_GRID_CHUNK_MIN 64
+#define BIBFS_KNOB_GRID_CHUNK_MIN 32
 #endif
 constexpr uint64_t kGridChunkMin = BIBFS_KNOB_GRID_CHUNK_MIN;  // smallest chunk (vertices) of k_grid_topdown
+// A chunk holds this percentage of one 256-edge batch at the frontier's mean
+// degree.  At 100 about half the chunks of a G(n, p) level went just past
+// 256 edges and walked a second serial batch, and the level waits for its
+// slowest block (stamped 10M levels: block claims at ~4.5 or ~9 us,
+// profiles/r5_grid_stamps_10m.txt).
+#ifndef BIBFS_KNOB_GRID_CHUNK_FILL
+#define BIBFS_KNOB_GRID_CHUNK_FILL 75
+#endif
+constexpr uint64_t kGridChunkFill = BIBFS_KNOB_GRID_CHUNK_FILL;
 constexpr int kHubTile = 1024;  // k_grid_hubs: hubs staged in LDS per pass
 // a hub-free level of at most one hub tile runs as one edge-parallel pass when
 // its top-down pass would walk more than this many 256-edge batches per block
@@ -1856,7 +1865,8 @@ __device__ __forceinline__ AutoPlan plan_auto_level(const GridParams<OffT>& P, u
   if (P.max_deg > kHubDegree && fe > kHubDegree) a.hub = kHubDegree;
   if (a.F <= 4096 && fe > 16384 && P.max_deg > 64) a.hub = 64;
   if ((a.F + kGridThreads - 1) / kGridThreads < P.cus * 4u && fe > 0)
-    a.cv = (uint32_t)min<uint64_t>(kGridThreads, max<uint64_t>(kGridChunkMin, kGridThreads * (uint64_t)a.F / fe));
+    a.cv = (uint32_t)min<uint64_t>(kGridThreads,
+                                   max<uint64_t>(kGridChunkMin, kGridThreads * kGridChunkFill * (uint64_t)a.F / (100 * fe)));
   // grid_topdown's rule: a hub level of at most one hub tile is one
   // edge-parallel pass (P.hub_direct: allowed on this chain)
   {
@@ -2785,7 +2795,8 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   // 256-vertex chunks (fewer ticket atomics).
   uint64_t cv = kGridThreads;
   if ((frontier + kGridThreads - 1) / kGridThreads < (uint64_t)cus * 4 && frontier_edges > 0)
-    cv = std::min<uint64_t>(kGridThreads, std::max<uint64_t>(kGridChunkMin, kGridThreads * frontier / frontier_edges));
+    cv = std::min<uint64_t>(kGridThreads, std::max<uint64_t>(kGridChunkMin, kGridThreads * kGridChunkFill * frontier /
+                                                                               (100 * frontier_edges)));
   const uint64_t chunks = (frontier + cv - 1) / cv;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, chunks));
   unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
