@@ -17,6 +17,8 @@
 #            over 1k/10k/50k/100k x v1, v2 (np 4), v3 (--resident), v4 (np 4: ranks share the GPU over IPC)
 #   prof     rocprofv3 --kernel-trace --stats of a short bench
 #   pmc      one SQ counter pass (rocprofv3 --pmc) over the resident 100k workload (PMCGRAPH=spec: another graph)
+#   benchab  driver-style headline bench (no extras) A/B over ABENV=<var> ABVALS="<v1> <v2>"
+#            [ROUNDS=3 STEPS=20 WARMUP=5], one JSON line per run
 #   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
 #            (SPECS / RANKS / OVERLAP / QUERIES override benchmarks/dist_rounds.py's defaults)
@@ -54,6 +56,13 @@ run_task() {
       $T 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${TAG}_prof -o prof -- \
         python3 bench.py --steps 20 --warmup 5 --extra-steps 50 --batch 0 --no-cpu-ref \
         > $O/${TAG}_prof_bench.json 2> $O/${TAG}_prof_bench.err ;;
+    benchab)  # headline bench (no extras), interleaved over ABENV=ABVALS, ROUNDS times
+      for r in $(seq 1 ${ROUNDS:-3}); do for v in $ABVALS; do
+        env $ABENV=$v $T 300 python3 bench.py --gpus 1 --steps ${STEPS:-20} --warmup ${WARMUP:-5} \
+          --extra-graph '' --dist-graphs '' --batch 0 --no-cpu-ref 2>> $O/${TAG}_benchab.err |
+          python3 -c "import json,sys; d=json.loads(sys.stdin.read()); x=d['detail']; print(json.dumps({'$ABENV': '$v', 'round': $r, 'query_ms': x['query_ms'], 'device_ms': x['device_ms_per_query'], 'value': d['value'], 'tiny_overflows': x['tiny_overflows']}))" \
+          >> $O/${TAG}_benchab.jsonl || exit 1
+      done; done ;;
     stamp)
       BIBFS_TINY_STAMP=1 $T 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999 --verify --resident --repeat 8 \
         > $O/${TAG}_stamp_100k.txt 2>&1 ;;
