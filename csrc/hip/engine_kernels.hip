@@ -1891,20 +1891,36 @@ __device__ __forceinline__ void write_auto_plan(uint32_t* aux, const AutoPlan& a
   aux[6] = a.fb;
 }
 
+// The per-level values a grid kernel reads: the host's (GridParams) for a
+// host-planned level, the plan in aux for an auto level.  Kept apart from
+// GridParams so that no kernel writes its kernel-argument struct: the auto
+// kernels did, which put a copy of it in scratch (320 B per thread), and every
+// pointer read through the copy became a scratch load plus a flat access
+// (flat operations also count in lgkmcnt, so each LDS wait waited for them).
+struct GridLv {
+  int side, precheck, hub_direct;
+  uint32_t hub_deg, chunk_v, fbase, fcount, nparts;
+  bool packed;  // the level may read the packed adjacency (an auto big level: 4-byte column loads)
+};
 template <typename OffT>
-__device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass);
+__device__ __forceinline__ GridLv grid_lv(const GridParams<OffT>& P) {
+  return GridLv{P.side, P.precheck, P.hub_direct, P.hub_deg, P.chunk_v, P.fbase, P.fcount, P.nparts, true};
+}
+
+template <typename OffT>
+__device__ void fused_finish(const GridParams<OffT>& P, const GridLv& L, int mode, bool hub_pass);
 
 // Claim v for side s from parent u; wave-uniform call (every lane calls it,
 // `valid` masks lanes with no edge).  Appends claimed vertices to the queue
 // with one atomic per wave and checks the other side's bitmap (fused meet).
 template <typename OffT>
-__device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, bool valid, uint32_t u, uint32_t v,
-                                           uint32_t vdeg = ~0u) {
-  const int s = P.side, o = s ^ 1;
+__device__ __forceinline__ void grid_claim(const GridParams<OffT>& P, const GridLv& L, bool valid, uint32_t u,
+                                           uint32_t v, uint32_t vdeg = ~0u) {
+  const int s = L.side, o = s ^ 1;
   DevState* st = P.b.st;
   const uint32_t w = v >> 5, bit = 1u << (v & 31);
   bool mine = false;
-  if (valid && (!P.precheck || !(P.b.vis[s][w] & bit))) mine = !(atomicOr(&P.b.vis[s][w], bit) & bit);
+  if (valid && (!L.precheck || !(P.b.vis[s][w] & bit))) mine = !(atomicOr(&P.b.vis[s][w], bit) & bit);
   const unsigned long long mask = __ballot(mine);
   if (!mask) return;
   const int lane = __lane_id();
@@ -2025,32 +2041,33 @@ __global__ __launch_bounds__(kGridThreads) void k_handoff(GridParams<OffT> P, in
 // beyond the level's chunk count (the host's launch size) -- it leaves before
 // any ticket or done-counter atomic.
 template <typename OffT>
-__device__ bool auto_plan(GridParams<OffT>& P) {
+__device__ bool auto_plan(const GridParams<OffT>& P, GridLv& L) {
   const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
   if (!(xp & kAuxActive) || (xp & kAuxDirect)) return false;  // direct: the hub pass runs the level
-  P.side = (int)((xp >> 1) & 1u);
-  P.precheck = (xp & kAuxPrecheck) ? 1 : 0;
-  if (P.precheck) P.padj = nullptr, P.padj8 = nullptr;  // big level: 4-byte column loads
-  P.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
-  P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
-  P.chunk_v = __builtin_amdgcn_readfirstlane(P.b.aux[5]);
-  P.fbase = __builtin_amdgcn_readfirstlane(P.b.aux[6]);
-  const uint32_t chunks = (P.fcount + P.chunk_v - 1) / P.chunk_v;
-  P.nparts = max(1u, min(gridDim.x, chunks));
-  return blockIdx.x < P.nparts;
+  L.side = (int)((xp >> 1) & 1u);
+  L.precheck = (xp & kAuxPrecheck) ? 1 : 0;
+  L.packed = !L.precheck;  // big level: 4-byte column loads
+  L.fcount = __builtin_amdgcn_readfirstlane(P.b.aux[3]);
+  L.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
+  L.chunk_v = __builtin_amdgcn_readfirstlane(P.b.aux[5]);
+  L.fbase = __builtin_amdgcn_readfirstlane(P.b.aux[6]);
+  const uint32_t chunks = (L.fcount + L.chunk_v - 1) / L.chunk_v;
+  L.nparts = max(1u, min(gridDim.x, chunks));
+  return blockIdx.x < L.nparts;
 }
 
 template <typename OffT, bool kAuto = false>
 __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> P) {
+  GridLv L = grid_lv(P);
   if constexpr (kAuto) {
-    if (!auto_plan(P)) return;
+    if (!auto_plan(P, L)) return;
   }
   __shared__ uint32_t sv[kGridThreads];
   __shared__ OffT sb[kGridThreads];
   __shared__ uint32_t sEb[kGridThreads];
   __shared__ uint32_t wsum[kGridThreads / kWave];
   __shared__ uint32_t schunk, stotal;
-  const int s = P.side;
+  const int s = L.side;
   DevState* st = P.b.st;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   // stamped trace (BIBFS_STAMP): block 0's phases, kGridStampWords per level
@@ -2059,9 +2076,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     gst = P.b.gstamp + (size_t)(st->levels % launch::kGridStampLevels) * launch::kGridStampWords;
     gst[0] = __builtin_amdgcn_s_memrealtime();
   }
-  const uint32_t fbase = kAuto ? P.fbase : st->fbeg[s];
-  const uint32_t F = kAuto ? P.fcount : st->fend[s] - fbase;
-  const uint32_t parts = P.nparts ? P.nparts : gridDim.x;
+  const uint32_t fbase = kAuto ? L.fbase : st->fbeg[s];
+  const uint32_t F = kAuto ? L.fcount : st->fend[s] - fbase;
+  const uint32_t parts = L.nparts ? L.nparts : gridDim.x;
+  const unsigned long long* const padj8 = L.packed ? P.padj8 : nullptr;
+  const uint4* const padj = L.packed ? P.padj : nullptr;
   for (uint32_t round = 0;; ++round) {
     if (kGridFast) {
       // chunk b first (no ticket); then tickets, numbered after the blocks'
@@ -2069,7 +2088,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
       if (tid == 0) {
         if (round == 0) {
           schunk = blockIdx.x;
-        } else if ((uint64_t)parts * P.chunk_v >= F) {
+        } else if ((uint64_t)parts * L.chunk_v >= F) {
           schunk = kEmpty;  // every chunk went to a block of its own: no ticket to take
         } else {
           const uint32_t t = atomicAdd(&st->chunk, 1u);
@@ -2081,7 +2100,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     }
     __syncthreads();
     const uint32_t c = schunk;
-    const uint32_t cv = P.chunk_v;
+    const uint32_t cv = L.chunk_v;
     if (c == kEmpty || (uint64_t)c * cv >= F) break;
     const uint32_t i = c * cv + tid;
     uint32_t deg = 0, u = 0;
@@ -2090,7 +2109,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
       u = P.b.queue[s][fbase + i];
       b = P.row_off[u];
       deg = (uint32_t)(P.row_off[u + 1] - b);
-      if (deg > P.hub_deg) {
+      if (deg > L.hub_deg) {
         P.b.hub_list[atomicAdd(&st->hub_count, 1u)] = u;
         deg = 0;
       }
@@ -2137,19 +2156,19 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
         }
         uu = sv[lo];
         const OffT k = sb[lo] + (OffT)(e - sEb[lo]);
-        if (P.padj8) {  // small level: the neighbour's degree with its id
-          const unsigned long long w = P.padj8[k];
+        if (padj8) {  // small level: the neighbour's degree with its id
+          const unsigned long long w = padj8[k];
           v = launch::pack8_v(w);
           vdeg = launch::pack8_deg(w);
-        } else if (P.padj) {
-          const uint4 q = P.padj[k];
+        } else if (padj) {
+          const uint4 q = padj[k];
           v = q.x;
           vdeg = q.y;
         } else {
           v = P.col[k];
         }
       }
-      grid_claim(P, valid, uu, v, vdeg);
+      grid_claim(P, L, valid, uu, v, vdeg);
     }
     if (gst && round == 0) {  // first chunk's claims and appends issued ...
       gst[2] = __builtin_amdgcn_s_memrealtime();
@@ -2157,7 +2176,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
     __syncthreads();
   }
   if (gst) gst[3] = __builtin_amdgcn_s_memrealtime();  // block 0 leaves its chunks
-  if (P.mirror) fused_finish(P, 1, false);
+  if (P.mirror) fused_finish(P, L, 1, false);
 }
 
 // Hub vertices (degree > hub_deg) deferred by k_grid_topdown, expanded
@@ -2175,22 +2194,23 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
   __shared__ unsigned long long hp[kHubTile + 1];
   __shared__ unsigned long long wsum[kGridThreads / kWave];
   DevState* st = P.b.st;
+  GridLv L = grid_lv(P);
   if constexpr (kAuto) {  // behind an auto level: its plan (written by the kernel before)
     const uint32_t xp = __builtin_amdgcn_readfirstlane(P.b.aux[2]);
     if (!(xp & kAuxActive)) return;
-    P.side = (int)((xp >> 1) & 1u);
-    P.hub_direct = (xp & kAuxDirect) ? 1 : 0;
-    P.precheck = (xp & kAuxPrecheck) ? 1 : 0;
-    P.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
+    L.side = (int)((xp >> 1) & 1u);
+    L.hub_direct = (xp & kAuxDirect) ? 1 : 0;
+    L.precheck = (xp & kAuxPrecheck) ? 1 : 0;
+    L.hub_deg = __builtin_amdgcn_readfirstlane(P.b.aux[4]);
     // the host's hub launch size: 4 workgroups per frontier vertex
-    P.nparts = max(1u, min(gridDim.x, 4u * __builtin_amdgcn_readfirstlane(P.b.aux[3])));
-    if (blockIdx.x >= P.nparts) return;
+    L.nparts = max(1u, min(gridDim.x, 4u * __builtin_amdgcn_readfirstlane(P.b.aux[3])));
+    if (blockIdx.x >= L.nparts) return;
   }
   // the hub list: the vertices k_grid_topdown deferred, or (hub_direct) the
   // whole frontier -- a small frontier of heavy vertices skips the top-down
   // pass, which ran it on a handful of workgroups
-  const uint32_t* const hl = P.hub_direct ? P.b.queue[P.side] + st->fbeg[P.side] : P.b.hub_list;
-  const uint32_t H = P.hub_direct ? st->fend[P.side] - st->fbeg[P.side] : st->hub_count;
+  const uint32_t* const hl = L.hub_direct ? P.b.queue[L.side] + st->fbeg[L.side] : P.b.hub_list;
+  const uint32_t H = L.hub_direct ? st->fend[L.side] - st->fbeg[L.side] : st->hub_count;
   if (H == 0) return;  // grid-uniform: the top-down finisher completed the level
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   for (uint32_t t0 = 0; t0 < H; t0 += kHubTile) {
@@ -2233,7 +2253,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
     __syncthreads();
     uint32_t it = 0;
     for (unsigned long long base = (unsigned long long)blockIdx.x * kGridThreads; base < tot;
-         base += (unsigned long long)(P.nparts ? P.nparts : gridDim.x) * kGridThreads, ++it) {
+         base += (unsigned long long)(L.nparts ? L.nparts : gridDim.x) * kGridThreads, ++it) {
       if (it > 0 && (it & kMeetCheckMask) == kMeetCheckMask &&
           __builtin_amdgcn_readfirstlane(load_agent(&st->meet)) != kEmpty)
         break;
@@ -2250,11 +2270,11 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
         uu = hu[a];
         v = P.col[hb[a] + (OffT)(e - hp[a])];
       }
-      grid_claim(P, valid, uu, v);
+      grid_claim(P, L, valid, uu, v);
     }
     __syncthreads();
   }
-  fused_finish(P, 1, true);
+  fused_finish(P, L, 1, true);
 }
 
 // Bottom-up level for side s: every unvisited vertex looks for a parent in the
@@ -2459,7 +2479,7 @@ __device__ void finish_state(DevState& sref, const launch::SearchBuffers& b, int
 // were stored write-through) and publishes the result.  A top-down level that
 // deferred hubs leaves the finish to k_grid_hubs (hub_pass), which runs next.
 template <typename OffT>
-__device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass) {
+__device__ void fused_finish(const GridParams<OffT>& P, const GridLv& L, int mode, bool hub_pass) {
   __shared__ DevState sv;
   __shared__ uint32_t slast;
   constexpr uint32_t kWords = (uint32_t)(sizeof(DevState) / sizeof(uint32_t));
@@ -2468,7 +2488,7 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   const uint32_t tid = threadIdx.x;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's atomics and sc1 stores have completed
   __syncthreads();
-  const uint32_t parts = P.nparts ? P.nparts : gridDim.x;
+  const uint32_t parts = L.nparts ? L.nparts : gridDim.x;
   if (tid == 0) slast = atomicAdd(&b.st->pad[1], 1u) == parts - 1;
   __syncthreads();
   if (!__builtin_amdgcn_readfirstlane(slast)) return;
@@ -2483,7 +2503,7 @@ __device__ void fused_finish(const GridParams<OffT>& P, int mode, bool hub_pass)
   const bool defer = !hub_pass && sv.hub_count != 0;  // the hub pass finishes this level
   if (tid == 0) {
     sv.pad[1] = 0;  // done counter, for the next kernel
-    if (!defer) finish_state(sv, b, P.side, mode, P.trace);
+    if (!defer) finish_state(sv, b, L.side, mode, P.trace);
   }
   __syncthreads();
   if (defer) {

@@ -418,7 +418,7 @@ struct HipBiBfs::Impl {
     }
     if (host_stamps_on) hs_t3 = std::chrono::steady_clock::now();
     if (tiny_stamp()) {
-      unsigned long long s[16];
+      unsigned long long s[22];
       HIP_CHECK(hipMemcpy(s, d_stamps, sizeof s, hipMemcpyDeviceToHost));
       std::fprintf(stderr,
                    "[tiny] cycles: seed %llu single-wave %llu all-wave %llu (%llu rounds, %.0f/round) meet-scan %llu "
@@ -430,6 +430,11 @@ struct HipBiBfs::Impl {
                    "[tiny] per all-wave round (wave 0): plan %.0f claim %.0f scan+atomic %.0f place %.0f barrier %.0f "
                    "book %.0f\n",
                    s[8] / r, s[11] / r, s[12] / r, s[13] / r, s[14] / r, s[15] / r);
+      const double w = s[16] ? (double)s[16] : 1.0;
+      std::fprintf(stderr,
+                   "[tiny] per single-wave round (%llu rounds, %.1f edges each): issue+claim %.0f count %.0f "
+                   "place %.0f meet-read %.0f\n",
+                   s[16], s[21] / w, s[17] / w, s[18] / w, s[19] / w, s[20] / w);
     }
     return a.status;
   }

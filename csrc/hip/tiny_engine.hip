@@ -269,23 +269,25 @@ __device__ __forceinline__ void round_issue(Work<NB>& W, const RoundCtx& R, uint
   // which the C++ model would let the compiler reorder (a store-buffer /
   // Dekker pattern), so a compiler-only fence pins the order (no instruction:
   // the hardware order then comes from in-order DS issue).
-  unsigned long long* own[NB];
+  // (word indices, not pointers: a pointer select here lost the LDS address
+  // space, and the other-side read became a flat load -- whose lgkmcnt wait
+  // then also waited for the speculative global loads issued just above)
+  uint32_t wi[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     old[b] = W.oth[b] = 0ull;
+    wi[b] = (W.s1[b] ? kTW : 0u) + (tw_v(W.rec[b]) >> 5);  // own word in the flat [2][kTW] set
     if (b >= nb) continue;
     const uint32_t v = tw_v(W.rec[b]);
     const uint32_t par = W.s1[b] ? R.par[1] : R.par[0];
     const unsigned long long m = W.act[b] ? 1ull << ((v & 31) + (par << 5)) : 0ull;
-    own[b] = &VIS[W.s1[b] ? 1 : 0][v >> 5];
-    old[b] = __hip_atomic_fetch_or(own[b], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    old[b] = __hip_atomic_fetch_or(&VIS[0][0] + wi[b], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b >= nb) continue;
-    W.oth[b] = __hip_atomic_load(W.s1[b] ? own[b] - kTW : own[b] + kTW, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+    W.oth[b] = __hip_atomic_load(&VIS[0][0] + (wi[b] ^ kTW), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
@@ -454,6 +456,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
   if (!uni(C.won)) return;
   if (tid == 0) __hip_atomic_store(&P.box->alive, P.launch_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 
+
   auto zero_state = [&]() {
     unsigned long long* V = &VIS[0][0];
 #pragma unroll 4
@@ -491,6 +494,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
   for (;;) {
     unsigned long long rt0 = 0;
     unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long sw[6] = {0, 0, 0, 0, 0, 0};  // stamp build: single-wave rounds, issue, count, place, meet read, edges
     uint32_t seq = 0;
     // ======== wave 0 alone: poll, seed, and the rounds small enough for one
     // wave -- no barrier, the round state in SGPRs, the counters from the
@@ -558,12 +562,27 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           const uint32_t x0 = T.E0, x1 = T.E1;
           const RoundCtx X = make_ctx(x0, x1, T.cb0, T.cb1, T.d0, T.d1);
           Work<NB> W;
+          unsigned long long t_ = kStamp ? stamp() : 0;
+          auto mark = [&](int k) {
+            if (kStamp) {
+              const unsigned long long u_ = stamp();
+              sw[k] += u_ - t_;
+              t_ = u_;
+            }
+          };
           round_issue<NB, true, false>(W, X, lane, 64, NB, P.tadj, VIS);
+          mark(1);
           Counts<NB> K;
           round_count<NB>(K, W);
+          mark(2);
           const uint32_t ovf =
               round_place<NB, true, false>(W, K, X, NB, T.ql0, T.ql1, 0u, 0u, false, lane, P.tadj, QU, JQ, JR, &C.meet);
           const bool qovf = __ballot(ovf & kOvfQueue) != 0, rovf = __ballot(ovf & kOvfRec) != 0;
+          mark(3);
+          if (kStamp) {
+            ++sw[0];
+            sw[5] += x0 + x1;
+          }
           T.x0 = x0;
           T.x1 = x1;
           T.einsp += x0 + x1;
@@ -576,6 +595,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
           }
           // the wave's own ds_min_u64 precede this read (one wave's LDS ops are in order)
           const unsigned long long m = uni64(__hip_atomic_load(&C.meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          mark(4);
           if (m != ~0ull) {
             T.meet = m;
             T.status = kTinyFound;
@@ -786,6 +806,7 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
         st[7] = rnd;
         for (int k = 0; k < 8; ++k) P.stamps[k] = st[k];
         for (int k = 0; k < 8; ++k) P.stamps[8 + k] = ph[k];
+        for (int k = 0; k < 6; ++k) P.stamps[16 + k] = sw[k];
       }
     }
     zero_state();
