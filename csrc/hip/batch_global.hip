@@ -76,15 +76,21 @@ __global__ __launch_bounds__(kBgThreads) void k_batch_global(BgArgs A) {
   const uint32_t n = A.n;
   const uint32_t src = A.src[q], dst = A.dst[q];
   uint32_t* base = A.slots + (size_t)q * 4 * n;
-  uint32_t* parent[2] = {base, base + n};
-  uint32_t* queue[2] = {base + 2 * (size_t)n, base + 3 * (size_t)n};
-  uint32_t* bits[2] = {A.bits + (size_t)q * 2 * A.words, A.bits + (size_t)q * 2 * A.words + A.words};
+  // per-side pointers as selects, not arrays indexed by the side: a
+  // dynamically indexed local array of pointers loses the global address
+  // space, and every access through it became a flat operation
+  uint32_t* const par0 = base;
+  uint32_t* const par1 = base + n;
+  uint32_t* const que0 = base + 2 * (size_t)n;
+  uint32_t* const que1 = base + 3 * (size_t)n;
+  uint32_t* const bit0 = A.bits + (size_t)q * 2 * A.words;
+  uint32_t* const bit1 = bit0 + A.words;
 
   if (tid < 2) {
     const uint32_t r = tid ? dst : src;
-    atomicOr(&bits[tid][r >> 5], 1u << (r & 31));
-    parent[tid][r] = r;
-    queue[tid][0] = r;
+    atomicOr(&(tid ? bit1 : bit0)[r >> 5], 1u << (r & 31));
+    (tid ? par1 : par0)[r] = r;
+    (tid ? que1 : que0)[0] = r;
   }
   if (tid == 0) meet = kEmpty;
   // every lane holds the same copy of the (small) search state
@@ -108,10 +114,10 @@ __global__ __launch_bounds__(kBgThreads) void k_batch_global(BgArgs A) {
       break;
     }
     const uint32_t t = s ^ 1u;
-    uint32_t* __restrict__ bs = bits[s];
-    const uint32_t* __restrict__ bt = bits[t];
-    uint32_t* __restrict__ ps = parent[s];
-    uint32_t* __restrict__ qs = queue[s];
+    uint32_t* __restrict__ bs = s ? bit1 : bit0;
+    const uint32_t* __restrict__ bt = t ? bit1 : bit0;
+    uint32_t* __restrict__ ps = s ? par1 : par0;
+    uint32_t* __restrict__ qs = s ? que1 : que0;
     if (tid == 0) {
       qtail = fend[s];
       nedges = 0;
@@ -207,12 +213,12 @@ __global__ __launch_bounds__(kBgThreads) void k_batch_global(BgArgs A) {
         uint32_t x = m;
         for (int k = d0; k >= 0; --k) {
           P[k] = x;
-          x = parent[0][x];
+          x = par0[x];
         }
         x = m;
         for (int k = d0; k <= d0 + d1; ++k) {
           P[k] = x;
-          x = parent[1][x];
+          x = par1[x];
         }
       } else {
         o.status = kHandoff;  // path longer than the slot: the host re-runs it
@@ -220,8 +226,8 @@ __global__ __launch_bounds__(kBgThreads) void k_batch_global(BgArgs A) {
     }
   }
   // leave the bitmaps all-zero: clear the word of every queued vertex
-  for (int k = 0; k < 2; ++k)
-    for (uint32_t i = tid; i < fend[k]; i += kBgThreads) bits[k][queue[k][i] >> 5] = 0u;
+  for (uint32_t i = tid; i < fend[0]; i += kBgThreads) bit0[que0[i] >> 5] = 0u;
+  for (uint32_t i = tid; i < fend[1]; i += kBgThreads) bit1[que1[i] >> 5] = 0u;
   // vertices claimed in a level interrupted by nothing: fend already covers
   // every append (levels always run to completion before the loop exits)
 }
