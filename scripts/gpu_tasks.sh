@@ -66,9 +66,10 @@ run_task() {
     stamp)
       BIBFS_TINY_STAMP=1 $T 120 ./build/bin/bibfs_hip gnp:100000::6 0 99999 --verify --resident --repeat 8 \
         > $O/${TAG}_stamp_100k.txt 2>&1 ;;
-    pmc)
-      timeout -s KILL 120 rocprofv3 --output-format csv --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS \
-        SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES -d $O/${TAG}_pmc_sq -- \
+    pmc)  # PMCCTRS: another counter set (<= 8 SQ); PMCLIB: a build/var/<dir> library build
+      local ctrs=${PMCCTRS:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES"}
+      env ${PMCLIB:+LD_LIBRARY_PATH=build/var/$PMCLIB} timeout -s KILL 120 rocprofv3 --output-format csv --pmc $ctrs \
+        -d $O/${TAG}_pmc_sq -- \
         python3 benchmarks/pmc_100k.py --mode resident ${PMCGRAPH:+--graph $PMCGRAPH} > $O/${TAG}_pmc_sq.log 2>&1 ;;
     dstress)
       $T 900 python3 -u benchmarks/stress_dist_local.py --procs ${RANKS:+--ranks $RANKS} ${QUERIES:+--queries $QUERIES} \
