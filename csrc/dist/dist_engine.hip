@@ -2313,15 +2313,17 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
                                                uint32_t capT, uint32_t slotsS, uint32_t slotsT, uint32_t meet,
                                                uint32_t hops, uint32_t* out) {
   extern __shared__ uint32_t lds[];
-  uint32_t* keys[2] = {lds, lds + 2 * slotsS};
-  const uint32_t nslot[2] = {slotsS, slotsT};
+  // per-side table base and size as selects, not local arrays indexed by the
+  // side (those went to scratch, and the table accesses became flat)
+  auto keys = [&](int s) { return s ? lds + 2 * slotsS : lds; };
+  auto nslot = [&](int s) { return s ? slotsT : slotsS; };
   // multiply-shift range reduction: any table size, so a ~0.77 load factor
   // fits ~15k (vertex, parent) pairs in 160 KB of LDS
-  auto home = [&](int s, uint32_t v) { return (uint32_t)(((uint64_t)(v * 2654435761u) * nslot[s]) >> 32); };
-  auto next = [&](int s, uint32_t h) { return h + 1 == nslot[s] ? 0u : h + 1; };
+  auto home = [&](int s, uint32_t v) { return (uint32_t)(((uint64_t)(v * 2654435761u) * nslot(s)) >> 32); };
+  auto next = [&](int s, uint32_t h) { return h + 1 == nslot(s) ? 0u : h + 1; };
   for (uint32_t i = threadIdx.x; i < slotsS + slotsT; i += blockDim.x) {
     const uint32_t s = i < slotsS ? 0 : 1, k = s ? i - slotsS : i;
-    keys[s][2 * k] = kEmpty;
+    keys(s)[2 * k] = kEmpty;
   }
   __syncthreads();
   const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
@@ -2334,11 +2336,11 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
       const uint2 x = pr[s ? capS + (i - c0) : i];
       uint32_t h = home(s, x.x);
       while (true) {
-        const uint32_t prev = atomicCAS(&keys[s][2 * h], kEmpty, x.x);
+        const uint32_t prev = atomicCAS(&keys(s)[2 * h], kEmpty, x.x);
         if (prev == kEmpty || prev == x.x) break;
         h = next(s, h);
       }
-      keys[s][2 * h + 1] = x.y;
+      keys(s)[2 * h + 1] = x.y;
     }
   }
   __syncthreads();
@@ -2348,9 +2350,9 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
   const int s = (int)threadIdx.x;
   auto parent_of = [&](uint32_t v, bool& ok) -> uint32_t {
     uint32_t h = home(s, v);
-    for (uint32_t probe = 0; probe < nslot[s]; ++probe) {
-      const uint32_t k = keys[s][2 * h];
-      if (k == v) return keys[s][2 * h + 1];
+    for (uint32_t probe = 0; probe < nslot(s); ++probe) {
+      const uint32_t k = keys(s)[2 * h];
+      if (k == v) return keys(s)[2 * h + 1];
       if (k == kEmpty) break;
       h = next(s, h);
     }

@@ -88,3 +88,9 @@ def test_batch_global_uses_no_flat(tmp_path):
     for k in _matching(priv, r"k_batch_global"):
         assert priv[k] == 0, (k, priv[k])
         assert sum(ops[k].values()) == 0, (k, dict(ops[k]))
+
+
+def test_dist_kernels_use_no_scratch_or_flat_ops(tmp_path):
+    ops, priv = _kernels(os.path.join(ROOT, "build/obj/dist/dist_engine.o"), tmp_path)
+    for k in _matching(priv, r"k_walk|k_spec_"):
+        assert sum(ops[k].values()) == 0, (k, dict(ops[k]))
