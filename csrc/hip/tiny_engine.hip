@@ -366,7 +366,8 @@ __device__ __forceinline__ void round_count(Counts<NB>& K, const Work<NB>& W) {
 // (fatal: the path walk needs every entry) and kOvfRec when a record buffer
 // would (fatal only if the round finds no meet: records feed the NEXT round).
 // A lane with nothing to store writes its own junk slot (no branch).
-constexpr uint32_t kOvfQueue = 1, kOvfRec = 2;
+// kCand (every lane, wave-uniform): the wave stored a meet candidate this round
+constexpr uint32_t kOvfQueue = 1, kOvfRec = 2, kCand = 4;
 template <int NB, bool kSpec, bool kSpill>
 __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K, const RoundCtx& R, int nb,
                                                 uint32_t q0b, uint32_t q1b, uint32_t e0b, uint32_t e1b, bool wspill, uint32_t lane,
@@ -416,7 +417,9 @@ __device__ __forceinline__ uint32_t round_place(Work<NB>& W, const Counts<NB>& K
     const uint32_t bt = v & 31;
     const uint32_t ost = (uint32_t)((W.oth[b] >> bt) & 1ull) | (uint32_t)((W.oth[b] >> (bt + 32)) & 1ull) << 1;
     const bool cand = qok && ost;
-    if (__ballot(cand) && cand) {  // a meet: the other side holds v at depth bo, or bo + 1 if it claimed v now
+    const bool anyc = __ballot(cand) != 0;
+    if (anyc) ovf |= kCand;
+    if (anyc && cand) {  // a meet: the other side holds v at depth bo, or bo + 1 if it claimed v now
       const uint32_t bo = s1 ? R.dep[0] : R.dep[1];
       const bool oexp = s1 ? R.exp[0] : R.exp[1];
       const uint32_t dov = (oexp && ost == (1u << ((bo + 1) & 1))) ? bo + 1 : bo;
@@ -593,8 +596,12 @@ __global__ __launch_bounds__(kTT, 1) void k_tiny_server(launch::TinyArgs P) {
             T.status = kTinyOverflow;
             return;
           }
-          // the wave's own ds_min_u64 precede this read (one wave's LDS ops are in order)
-          const unsigned long long m = uni64(__hip_atomic_load(&C.meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          // the wave's own ds_min_u64 precede this read (one wave's LDS ops are
+          // in order); read only when this round stored a candidate (C.meet is
+          // otherwise still ~0: a meet ends the search in the round that finds it)
+          const unsigned long long m =
+              (uni(ovf) & kCand) ? uni64(__hip_atomic_load(&C.meet, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+                                 : ~0ull;
           mark(4);
           if (m != ~0ull) {
             T.meet = m;
