@@ -196,6 +196,26 @@ def pick_pairs(eng, n: int, count: int, seed: int):
     return pairs
 
 
+PARTITIONED_HEADLINE = "gnp:1000000::2"  # BASELINE config 3: 1M-vertex G(n, 2.2/n), vertex-partitioned
+
+
+def partitioned_top(partitioned: dict) -> dict:
+    """Top-level fields beside the replicated headline: the partitioned
+    engine's BASELINE config-3 numbers (one query = one collective search over
+    every rank), so a scaling curve over N shows the v4 capability and not only
+    N independent servers.  None where that config did not run or failed."""
+    p = partitioned.get(PARTITIONED_HEADLINE)
+    ok = isinstance(p, dict) and "error" not in p and p.get("ms_per_query") is not None
+    return {
+        "partitioned_config": PARTITIONED_HEADLINE,
+        "partitioned_ms_per_query": p["ms_per_query"] if ok else None,
+        "partitioned_speedup_vs_single_gpu": p.get("speedup_vs_single_gpu") if ok else None,
+        "partitioned_gteps": round(p["gteps"], 4) if ok and p.get("gteps") is not None else None,
+        "partitioned_collectives_per_round": p.get("collectives_per_round") if ok else None,
+        "partitioned_verified": p.get("verified") if ok else None,
+    }
+
+
 def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks=None,
            comm_init_ms=None) -> dict:
     """The one JSON line rank 0 prints (driver contract)."""
@@ -219,6 +239,7 @@ def report(a, world: int, head: dict, extra: dict, partitioned: dict, rccl_ranks
             "seq_len": head["n"],
             "parallelism": (f"vertex-partition{world}" if part else f"dp{world}"),
         },
+        **partitioned_top(partitioned),
         "detail": {
             "query_ms": round(head["ms_per_step"], 6),
             "device_ms_per_query": round(head["device_ms_per_query"], 6),

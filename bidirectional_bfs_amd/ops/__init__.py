@@ -212,14 +212,23 @@ class HipEngine:
     def lds_probe_edges(self) -> int:
         """Meet probe of the LDS engine on hub graphs: frontier edges of a level
         that does not fit LDS tested against the other side's visited set
-        before the level is handed to the grid engine (default 16384, env
-        BIBFS_LDS_PROBE_EDGES; 0 = off).  ``stats["probe_edges"]`` /
+        before the level is handed to the grid engine (default 16384; 0 = off).  ``stats["probe_edges"]`` /
         ``stats["probe_hit"]`` report it per search."""
         return self._e.lds_probe_edges
 
     @lds_probe_edges.setter
     def lds_probe_edges(self, edges: int) -> None:
         self._e.lds_probe_edges = int(edges)
+
+    def set_build_flags(self, wide_offsets: bool = False, stream_gen: bool = False,
+                        tiny: bool = True) -> "HipEngine":
+        """Applied by the next load / generate: ``wide_offsets`` keeps no 32-bit
+        row-offset copy (a small graph then runs the kernels of an nnz >= 2^32
+        graph), ``stream_gen`` generates even small graphs straight into the
+        CSR (the large-graph path), ``tiny=False`` keeps the tiny server off
+        (the general resident server answers every graph)."""
+        self._e.set_build_flags(bool(wide_offsets), bool(stream_gen), bool(tiny))
+        return self
 
     # step-wise API (reference v4/comp.h parity)
     def begin(self, src: int, dst: int) -> None:

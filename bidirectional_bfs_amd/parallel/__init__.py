@@ -29,6 +29,7 @@ from __future__ import annotations
 import json
 import os
 import shutil
+import socket
 import subprocess
 import sys
 import tempfile
@@ -116,6 +117,14 @@ class DistEngine:
         import torch.distributed as dist
 
         rank, world = dist.get_rank(), dist.get_world_size()
+        if backend == "ipc":
+            # The IPC control plane is node-local shared memory with peer
+            # liveness checked by local pid: every rank must share one host.
+            hosts = [None] * world
+            dist.all_gather_object(hosts, socket.gethostname())
+            if len(set(hosts)) != 1:
+                raise RuntimeError(f"backend 'ipc' needs all {world} ranks on one node, got hosts "
+                                   f"{sorted(set(hosts))}; use backend 'rccl' (one rank per GPU)")
         obj = [native.dist_unique_id(backend) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         if device is None:

@@ -2477,15 +2477,6 @@ __global__ void k_cleanup(DView V, uint64_t sent_words) {
   for (uint64_t i = sent_words / 4 * 4 + tid; i < sent_words; i += nth) V.sent[0][i] = 0u;
 }
 
-// A/B: BIBFS_SOLO_SELFCLEAN=0 leaves a solo-ended search's reset to k_cleanup.
-bool solo_selfclean() {
-  static const bool on = [] {
-    const char* e = std::getenv("BIBFS_SOLO_SELFCLEAN");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
 unsigned blocks_for(uint64_t work, int cus) {
   uint64_t b = (work + kThreads - 1) / kThreads;
   b = std::min<uint64_t>(b, (uint64_t)cus * 8);
@@ -2573,10 +2564,13 @@ struct DistBiBfs::Impl {
   std::unique_ptr<HipBiBfs> single;
   void ensure_single() {
     if (single || !d_row_off) return;
-    single = std::make_unique<HipBiBfs>(device);
-    single->adopt_device_csr(n, nnz, m_input, d_row_off, d_col);
-    single->set_resident(true);
-    check_single_cap();
+    auto eng = std::make_unique<HipBiBfs>(device);
+    eng->adopt_device_csr(n, nnz, m_input, d_row_off, d_col);
+    // the cap is checked before the resident server starts and before the
+    // engine is kept: a caller that catches the error holds no engine over it
+    check_single_cap(*eng);
+    eng->set_resident(true);
+    single = std::move(eng);
   }
   int fault_at = 0, fault_mode = 0;
 
@@ -2613,7 +2607,7 @@ struct DistBiBfs::Impl {
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
     comm->set_timeout(tune.timeout_s);
-    if (const char* t = std::getenv("BIBFS_DIST_STAMP")) solo_stamp = std::atoi(t) != 0;
+    solo_stamp = env::stamps();  // BIBFS_STAMP: the solo workgroup's phase cycles
     HIP_CHECK(hipMalloc(&d_stamps, 16 * sizeof(unsigned long long)));
   }
 
@@ -2771,8 +2765,7 @@ struct DistBiBfs::Impl {
     if (padj_tried) return;
     padj_tried = true;
     if (!(size == 1 && lo == 0 && nnz)) return;
-    const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
-    const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
+    const uint64_t budget = env::padj_budget_bytes();
     if (nnz * 16 > budget) return;
     devmem::Scope scope(&mem);
     devmem::alloc(&d_padj, nnz * 16);
@@ -2803,9 +2796,9 @@ struct DistBiBfs::Impl {
   // The adopted single-GPU engine allocates outside devmem (its own arrays;
   // the CSR is this rank's): hold DistTuning::hbm_cap_bytes against
   // everything this rank holds once it exists.
-  void check_single_cap() {
-    if (!single || !mem.cap) return;
-    const size_t all = single->device_bytes(), csr = row_off_bytes() + col_bytes();
+  void check_single_cap(const HipBiBfs& eng) const {
+    if (!mem.cap) return;
+    const size_t all = eng.device_bytes(), csr = row_off_bytes() + col_bytes();
     const size_t held = mem.cur + (all > csr ? all - csr : 0);
     if (held > mem.cap)
       throw Error("dist: HBM cap exceeded: this rank would hold " + std::to_string(held) + " bytes with the " +
@@ -3170,11 +3163,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   // they carry the previous epoch.
   std::memset(h_plan, 0, kPlanRing * 8);
   std::atomic_thread_fence(std::memory_order_seq_cst);
-  static const bool no_solo = [] {  // A/B: BIBFS_DIST_SOLO=0 turns the solo workgroup off
-    const char* e = std::getenv("BIBFS_DIST_SOLO");
-    return e && e[0] == '0';
-  }();
-  const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0 && !no_solo;
+  const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
   if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
   if (P > 1) {
     comm->allgather(&V.red[1], V.redg[1], sizeof(Reduced), cs);
@@ -3198,7 +3187,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     const uint32_t tag = next_tag();
     const uint32_t emax = std::min<uint32_t>(std::max<uint32_t>(tune.solo_edges, 1), kSoloE);
     // bit 0: the workgroup seeds the search; bit 1: no self-cleanup (k_cleanup after the search instead)
-    const int sflags = 1 | (solo_selfclean() ? 0 : 2);
+    const int sflags = 1;  // the search that ends in the solo workgroup resets its own state
     if (solo_stamp) k_spec_solo<true><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, sflags, src, dst, h_fin, tag, d_stamps);
     else k_spec_solo<false><<<1, kSoloT, 0, cs>>>(V, it, pol, emax, sflags, src, dst, h_fin, tag, nullptr);
     HIP_CHECK(hipGetLastError());
@@ -3214,7 +3203,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
     }
     have_ctl = true;
     stats.solo_rounds = (int)(h_ctl->rounds);
-    solo_cleaned = solo_selfclean() && (h_ctl->state == kDead ||
+    solo_cleaned = (h_ctl->state == kDead ||
                    (h_ctl->state == kDone && !(pol.want_path && 4 + (h_ctl->key >> 32) + 1 > pol.walk_cap)));
     it = h_ctl->next_it;
     const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);

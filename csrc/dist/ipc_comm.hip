@@ -119,6 +119,10 @@ class IpcComm final : public Comm {
   }
 
   ~IpcComm() override {
+    // A pull kernel of the last collective may still read the peers' mapped
+    // buffers (after an abort ~DistBiBfs skips its stream sync): wait for it
+    // before unmapping.  Pull kernels never wait on peers, so this is bounded.
+    if (done_) (void)hipEventSynchronize(done_);
     for (int r = 0; r < size_; ++r)
       for (int s = 0; s < 2; ++s)
         if (peer_[r][s].ptr) (void)hipIpcCloseMemHandle(peer_[r][s].ptr);
@@ -266,9 +270,6 @@ class IpcComm final : public Comm {
       const hipError_t e = hipIpcGetMemHandle(&h, stage_[slot]);
       if (e == hipSuccess) break;
       (void)hipGetLastError();
-      if (std::getenv("BIBFS_IPC_DEBUG"))
-        std::fprintf(stderr, "[ipc rank %d] hipIpcGetMemHandle(%p, %zu bytes): %s; retrying larger\n", rank_,
-                     stage_[slot], cap, hipGetErrorString(e));
       refused.push_back(stage_[slot]);
       stage_[slot] = nullptr;
       if (attempt == 5) {

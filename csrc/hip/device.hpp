@@ -5,11 +5,41 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 
 #include "bibfs/common.hpp"
 
 namespace bibfs {
+// Environment switches of the engines -- diagnostics and one memory budget.
+// Every other setting is an API property (HipBiBfs setters, DistTuning).
+namespace env {
+// BIBFS_STAMP: cycle stamps (traced LDS / grid searches, the partitioned
+// engine's solo workgroup); BIBFS_STAMP_SERVER: the resident LDS server's
+// stamped build; BIBFS_TINY_STAMP: the tiny server's stamped build.
+inline bool stamps() {
+  static const bool on = std::getenv("BIBFS_STAMP") != nullptr;
+  return on;
+}
+inline bool server_stamps() {
+  static const bool on = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
+  return on;
+}
+inline bool tiny_stamps() {
+  static const bool on = std::getenv("BIBFS_TINY_STAMP") != nullptr;
+  return on;
+}
+// BIBFS_PADJ_MAX_MB: HBM budget of the packed adjacency (16 or 8 B per
+// directed edge beside the CSR; default 4096 MiB, 0 = none).
+inline uint64_t padj_budget_bytes() {
+  static const uint64_t b = [] {
+    const char* e = std::getenv("BIBFS_PADJ_MAX_MB");
+    return (e ? std::strtoull(e, nullptr, 10) : 4096ull) << 20;
+  }();
+  return b;
+}
+}  // namespace env
+
 namespace dev {
 
 #define HIP_CHECK(expr)                                                                   \
@@ -276,7 +306,7 @@ uint32_t lds_probe_budget();  // BIBFS_LDS_PROBE_EDGES (default 16384; 0 = no me
 size_t lds_bytes(bool wide);
 void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers& b_alt, const HostSide& h,
                 dev::ServerBox* box, uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
-                unsigned long long idle_ticks, hipStream_t s);
+                unsigned long long idle_ticks, bool stamp_server, hipStream_t s);
 void lds_batch(const GraphView& g, const SearchBuffers& b, uint32_t* h_src, uint32_t* h_dst,
                uint32_t k, uint32_t* d_slots, dev::HostResult* h_res, uint32_t* h_path, uint32_t path_cap,
                uint32_t seq, hipStream_t s);

@@ -65,28 +65,19 @@ using namespace dev;
 // answer is the minimum candidate of that round.  Two concurrent claims of the
 // same vertex are always seen by at least one side: each side completes its
 // own insert (LDS CAS) before reading the other set.
-// Tuning knobs (compile-time; scripts/build_variants.sh builds A/B libraries).
+// Tuning constants (each was A/B-measured; the files are named beside it).
 // Variants measured slower and removed from the code (results and the A/B
 // files: docs/DESIGN.md §8): a readfirstlane'd wave id, ballot-driven record
 // appends, hash-set all-wave rounds with an LDS queue (profiles/r2_wave_hash_ab.txt)
 // and 4-slot hash buckets (profiles/r4_lds_hash_bucket_ab.jsonl).
 // 1 = lockstep rounds of up to kLdsThreads frontier edges run on EVERY wave
 // with one LDS-only barrier per round (wave_rounds); 0 = the wave-0 rounds.
-#ifndef BIBFS_KNOB_WAVE_ROUNDS
-#define BIBFS_KNOB_WAVE_ROUNDS 1
-#endif
-constexpr bool kWaveRounds = BIBFS_KNOB_WAVE_ROUNDS;
+constexpr bool kWaveRounds = true;
 // 1 = an all-wave round that cannot carry both frontiers expands the smaller
 // side alone (while it fits) instead of leaving the all-wave rounds.
-#ifndef BIBFS_KNOB_WAVE_SINGLE
-#define BIBFS_KNOB_WAVE_SINGLE 1
-#endif
-constexpr bool kWaveSingle = BIBFS_KNOB_WAVE_SINGLE;
+constexpr bool kWaveSingle = true;
 // batches of 64 edges per wave in those rounds (1: frontiers up to 1024 edges, 2: 2048)
-#ifndef BIBFS_KNOB_WAVE_B
-#define BIBFS_KNOB_WAVE_B 2
-#endif
-constexpr uint32_t kWaveB = BIBFS_KNOB_WAVE_B;
+constexpr uint32_t kWaveB = 2;
 static_assert(kWaveB == 1 || kWaveB == 2 || kWaveB == 4, "batches per wave: 1, 2 or 4");
 // 1 = the all-wave rounds also run with LDS hash visited sets, claiming into
 // the GLOBAL queue and parent arrays (records carry parent ids, as in the
@@ -97,49 +88,28 @@ static_assert(kWaveB == 1 || kWaveB == 2 || kWaveB == 4, "batches per wave: 1, 2
 // (profiles/r4_lds_wave_hash_global_ab.jsonl, mean search): 10M G(n, p)
 // 67.5 -> 63.5-64.0 us, 3M 38.3 -> 34.2, 1M 30.2 -> 26.0; ungated it cost
 // Kronecker 22 +4 us (profiles/r4_lds_wave_hash_global_ungated.jsonl).
-#ifndef BIBFS_KNOB_WAVE_HASH_G
-#define BIBFS_KNOB_WAVE_HASH_G 1
-#endif
-constexpr bool kWaveHashG = BIBFS_KNOB_WAVE_HASH_G;
+constexpr bool kWaveHashG = true;
+// (lifting the gate once cooperative appends existed changed nothing:
+// profiles/r5_wave_hash_gate_ab.jsonl)
 constexpr uint64_t kWaveHashMaxDeg = 255;
-// (host) the gate, overridable for A/B runs: BIBFS_WAVE_HASH_MAX_DEG
-static uint64_t wave_hash_max_deg() {
-  static const uint64_t d = [] {
-    const char* e = std::getenv("BIBFS_WAVE_HASH_MAX_DEG");
-    return e ? std::strtoull(e, nullptr, 10) : kWaveHashMaxDeg;
-  }();
-  return d;
-}
 // Resident server: the mailbox diagnostics (stage / seen / poll latency) are
 // system-scope stores to host memory.  vmcnt counts stores too, so if wave 0
 // issued them, its first global load of the search would wait for their PCIe
 // acks.  1 = the last wave issues them (it is parked during small rounds).
-#ifndef BIBFS_KNOB_DIAG_WAVE
-#define BIBFS_KNOB_DIAG_WAVE 1
-#endif
-constexpr bool kDiagOffWave0 = BIBFS_KNOB_DIAG_WAVE;
+constexpr bool kDiagOffWave0 = true;
 
 // Workgroup size of the LDS engine.  1024 threads = 4 waves per SIMD caps a
 // wave at 128 VGPRs (the kernel sits at that limit; 2-4 spills); 512 threads
 // lift the cap to 256 but halve the lanes of the all-wave levels.  A/B on
 // 100k / 1M G(n,p) (profiles/r2_lds_ab.txt): 1024 is 0.5-0.9 us faster.
-#ifndef BIBFS_KNOB_LDS_THREADS
-#define BIBFS_KNOB_LDS_THREADS 1024
-#endif
-constexpr int kLdsThreads = BIBFS_KNOB_LDS_THREADS;
+constexpr int kLdsThreads = 1024;
 constexpr int kHashBits = 13;
 constexpr uint32_t kHashSize = 1u << kHashBits;  // slots per side
 constexpr uint32_t kHashMask = kHashSize - 1;
 constexpr uint32_t kHashLimit = kHashSize * 3 / 4;  // max visited per side in LDS
 constexpr int kBatch = 4;                           // edges per thread per round (big levels)
-#ifndef BIBFS_KNOB_SMALL_EDGES
-#define BIBFS_KNOB_SMALL_EDGES 128
-#endif
-#ifndef BIBFS_KNOB_DUAL_EDGES
-#define BIBFS_KNOB_DUAL_EDGES 256
-#endif
-constexpr uint32_t kSmallEdges = BIBFS_KNOB_SMALL_EDGES;  // a level this small runs on one wave
-constexpr uint32_t kDualEdges = BIBFS_KNOB_DUAL_EDGES;    // both sides together this small: one lockstep round
+constexpr uint32_t kSmallEdges = 128;  // a level this small runs on one wave
+constexpr uint32_t kDualEdges = 256;    // both sides together this small: one lockstep round
 constexpr uint32_t kDualBigEdges = 4096;                  // balanced sides up to this many edges: lockstep big level
 constexpr uint32_t kDegClamp = 65535;               // per-lane edge contribution to the packed counter
 // Bitmap mode with the all-wave rounds: smaller record buffers make room for
@@ -1750,54 +1720,36 @@ __global__ __launch_bounds__(kLdsThreads, 1) void k_lds_server(LdsParams<OffT> P
 // ============================================================================
 constexpr int kGridThreads = 256;
 constexpr uint32_t kHubDegree = 4096;  // deferred to k_grid_hubs
-#ifndef BIBFS_KNOB_GRID_CHUNK_MIN
-#define BIBFS_KNOB_GRID_CHUNK_MIN 32
-#endif
-constexpr uint64_t kGridChunkMin = BIBFS_KNOB_GRID_CHUNK_MIN;  // smallest chunk (vertices) of k_grid_topdown
+constexpr uint64_t kGridChunkMin = 32;  // smallest chunk (vertices) of k_grid_topdown
 // A chunk holds this percentage of one 256-edge batch at the frontier's mean
 // degree.  At 100 about half the chunks of a G(n, p) level went just past
 // 256 edges and walked a second serial batch, and the level waits for its
 // slowest block (stamped 10M levels: block claims at ~4.5 or ~9 us,
 // profiles/r5_grid_stamps_10m.txt).
-#ifndef BIBFS_KNOB_GRID_CHUNK_FILL
-#define BIBFS_KNOB_GRID_CHUNK_FILL 75
-#endif
-constexpr uint64_t kGridChunkFill = BIBFS_KNOB_GRID_CHUNK_FILL;
+constexpr uint64_t kGridChunkFill = 75;
 constexpr int kHubTile = 1024;  // k_grid_hubs: hubs staged in LDS per pass
 // a hub-free level of at most one hub tile runs as one edge-parallel pass when
 // its top-down pass would walk more than this many 256-edge batches per block
 // (1 vs 2: Kronecker 25 44.1-45.1 -> 43.4-43.8 us, Kronecker 22 37.5-37.9 ->
 // 36.9-37.3 us mean search, 10M unchanged; profiles/r4_grid_direct_batches_ab.jsonl)
-#ifndef BIBFS_KNOB_GRID_DIRECT_BATCHES
-#define BIBFS_KNOB_GRID_DIRECT_BATCHES 1
-#endif
-constexpr uint64_t kGridDirectBatches = BIBFS_KNOB_GRID_DIRECT_BATCHES;
+constexpr uint64_t kGridDirectBatches = 1;
 // Single-side grid levels stop at their first meet (every meet of such a level
 // has the same length).  The edge loops of k_grid_topdown / k_grid_hubs read
 // the meet word every (mask + 1) batches of 256 edges per workgroup: a
 // Kronecker hub level spans only a few grid-stride iterations, so a sparse
 // check never fires before the level has walked every hub edge.
-#ifndef BIBFS_KNOB_MEET_CHECK_MASK
-#define BIBFS_KNOB_MEET_CHECK_MASK 0
-#endif
-constexpr uint32_t kMeetCheckMask = BIBFS_KNOB_MEET_CHECK_MASK;
+constexpr uint32_t kMeetCheckMask = 0;
 // 1 = k_grid_topdown's dependent round trips trimmed: each workgroup's first
 // chunk is its block index (no ticket), the ticket and the meet word are read
 // side by side, and a claim reads its visited word before the atomicOr only
 // on levels of more than kGridPrecheckEdges frontier edges (small levels
 // claim mostly unvisited vertices: the read only adds a round trip).
-#ifndef BIBFS_KNOB_GRID_FAST
-#define BIBFS_KNOB_GRID_FAST 1
-#endif
-constexpr bool kGridFast = BIBFS_KNOB_GRID_FAST;
+constexpr bool kGridFast = true;
 constexpr uint64_t kGridPrecheckEdges = 1ull << 16;
 // 1 = small top-down levels read the packed adjacency (GridParams::padj):
 // 10M 61.9-62.2 -> 61.3-61.6 us, Kronecker 22 37.5-38.2 -> 36.5-37.8 us mean
 // search (profiles/r4_grid_padj_ab.jsonl)
-#ifndef BIBFS_KNOB_GRID_PADJ
-#define BIBFS_KNOB_GRID_PADJ 1
-#endif
-constexpr bool kGridPadj = BIBFS_KNOB_GRID_PADJ;
+constexpr bool kGridPadj = true;
 
 template <typename OffT>
 struct GridParams {
@@ -2685,24 +2637,15 @@ namespace launch {
 
 int lds_threads() { return kLdsThreads; }
 
-uint32_t lds_probe_budget() {
-  // BIBFS_LDS_PROBE_EDGES: frontier edges the meet probe may read before a
-  // hand-off (0 = off)
-  static const uint32_t b = [] {
-    const char* e = std::getenv("BIBFS_LDS_PROBE_EDGES");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 16384u;
-  }();
-  return b;
-}
+// frontier edges the meet probe may read before a hand-off (default of
+// HipBiBfs::set_lds_probe_edges; 0 = off)
+uint32_t lds_probe_budget() { return 16384u; }
 
-// graphs whose largest degree is above BIBFS_LDS_PROBE_MIN_DEG (default 64)
-static uint32_t probe_for(const GraphView& g) {
-  static const uint64_t min_deg = [] {
-    const char* e = std::getenv("BIBFS_LDS_PROBE_MIN_DEG");
-    return e ? std::strtoull(e, nullptr, 10) : 64ull;
-  }();
-  return g.max_deg > min_deg ? g.probe_edges : 0u;
-}
+// The probe runs on graphs whose largest degree is above 64 (hub graphs): on
+// G(n, p) it hit a quarter of the 10M hand-offs but a miss costs ~9 us on a
+// near-full hash set, a wash (profiles/r5_lds_coop_append_probe_ab.jsonl).
+constexpr uint64_t kProbeMinDeg = 64;
+static uint32_t probe_for(const GraphView& g) { return g.max_deg > kProbeMinDeg ? g.probe_edges : 0u; }
 
 size_t lds_bytes(bool wide) {
   return 2 * kHashSize * 4 + 4 * (wide ? LdsRec<uint64_t>::cap * 16 : LdsRec<uint32_t>::cap * 8) + 128;
@@ -2716,7 +2659,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
   if (g.row_off32) {
     LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, src, dst, seq, side_policy, trace, pin_xcc, ticket,
                            lockstep, (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
-    P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
+    P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
     P.probe = probe_for(g);
     const bool bm = g.n <= kBmMaxN;  // whole visited sets fit LDS as bitmaps
     if (trace == 2) {
@@ -2740,7 +2683,7 @@ void lds_search(const GraphView& g, const SearchBuffers& b, const HostSide& h, u
 
 void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers& b_alt, const HostSide& h,
                 dev::ServerBox* box, uint32_t launch_seq, uint32_t last_seq, int pin_xcc, uint32_t* ticket,
-                unsigned long long idle_ticks, hipStream_t s) {
+                unsigned long long idle_ticks, bool stamp_server, hipStream_t s) {
   const unsigned blocks = pin_xcc >= 0 ? 16 : 1;
   if (!g.row_off32) {  // nnz >= 2^32 (Kronecker 27+): 64-bit offsets, hash-set mode
     LdsParams<uint64_t> P{g.row_off, g.col, g.padj, nullptr, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
@@ -2754,10 +2697,9 @@ void lds_server(const GraphView& g, const SearchBuffers& b, const SearchBuffers&
   LdsParams<uint32_t> P{g.row_off32, g.col, g.padj, g.padj8, g.n, 0, 0, launch_seq, 0, 0, pin_xcc, ticket, 1,
                          (uint32_t)(g.nnz ? g.nnz - 1 : 0), 0, b, h};
   P.b_alt = b_alt;
-  P.wave_hash = g.max_deg <= wave_hash_max_deg() ? 1 : 0;
+  P.wave_hash = g.max_deg <= kWaveHashMaxDeg ? 1 : 0;
   P.probe = probe_for(g);
-  static const bool stamp = std::getenv("BIBFS_STAMP_SERVER") != nullptr;  // cycle stamps, warm L2
-  if (g.n <= kBmMaxN && stamp)
+  if (g.n <= kBmMaxN && stamp_server)  // cycle stamps of the server's phases
     k_lds_server<uint32_t, true, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
   else if (g.n <= kBmMaxN)
     k_lds_server<uint32_t, true><<<blocks, kLdsThreads, 0, s>>>(P, box, last_seq, idle_ticks);
@@ -2791,15 +2733,6 @@ void seed_state(const GraphView& g, const SearchBuffers& b, uint32_t src, uint32
 
 uint32_t grid_hub_degree() { return kHubDegree; }
 
-// BIBFS_GRID_HUB_DIRECT: 0 off, 1 on (the hub pass's grid), 2 on with one
-// workgroup per 256 frontier edges (up to 4 per CU; host-planned levels only)
-static int grid_hub_direct_mode() {
-  static const int mode = [] {
-    const char* e = std::getenv("BIBFS_GRID_HUB_DIRECT");
-    return e ? std::atoi(e) : 1;
-  }();
-  return mode;
-}
 
 void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus, uint64_t frontier,
                   uint64_t frontier_edges, dev::DevState* mirror, uint32_t seq, int trace, const HostSide& h, uint32_t res_seq,
@@ -2819,7 +2752,7 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
                                                                                (100 * frontier_edges)));
   const uint64_t chunks = (frontier + cv - 1) / cv;
   const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, chunks));
-  unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
+  const unsigned hblocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)cus * 4, frontier * 4));
   // A hub level whose whole frontier fits one hub tile runs as ONE edge-parallel
   // pass over every frontier edge (k_grid_hubs, hub_direct): the top-down pass
   // would walk its light vertices on frontier/cv workgroups (one, for a
@@ -2830,15 +2763,11 @@ void grid_topdown(const GraphView& g, const SearchBuffers& b, int side, int cus,
   // With the hub-free small heavy levels too (profiles/r4_grid_direct_levels_ab.jsonl):
   // Kronecker 22 46.9-48.1 -> 38.0-38.3 us, Kronecker 25 56.2-57.9 -> 44.0-44.2
   // us against no direct levels; 10M G(n, p) unchanged.
-  const int direct_mode = grid_hub_direct_mode();
   // (also a level without hubs whose top-down pass would walk more than
   // kGridDirectBatches 256-edge batches per workgroup: a few heavy-ish
   // vertices on one block)
-  const bool direct = direct_mode && frontier <= (uint64_t)kHubTile &&
+  const bool direct = frontier <= (uint64_t)kHubTile &&
                       (hub_deg != ~0u || frontier_edges > kGridDirectBatches * kGridThreads * blocks);
-  if (direct && direct_mode == 2)
-    hblocks = (unsigned)std::max<uint64_t>(
-        1, std::min<uint64_t>((uint64_t)cus * 4, (frontier_edges + kGridThreads - 1) / kGridThreads));
   auto launch_one = [&](auto P) {
     using OffT = std::remove_const_t<std::remove_pointer_t<decltype(P.row_off)>>;
     P.mirror = mirror, P.seq = seq, P.trace = trace, P.h = h, P.res_seq = res_seq;
@@ -2885,7 +2814,7 @@ void grid_auto(const GraphView& g, const SearchBuffers& b, int cus, uint64_t max
     P.alpha = (float)alpha;
     P.chain = 0;
     // the planners may choose direct hub levels (only with the hub pass enqueued)
-    P.hub_direct = grid_hub_direct_mode() == 1 && max_deg > 64 ? 1 : 0;
+    P.hub_direct = max_deg > 64 ? 1 : 0;
     k_handoff<OffT><<<kHandoffBlocks, kGridThreads, 0, s>>>(P, 1, scatter);
     for (int l = 0; l < std::max(1, levels); ++l) {
       P.chain = l + 1 < levels ? 1 : 0;

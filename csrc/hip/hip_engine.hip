@@ -44,7 +44,9 @@ struct HipBiBfs::Impl {
   // graphs above this many undirected edges are generated straight into the
   // CSR (two passes over the counter-based generator, no edge list in HBM)
   static constexpr uint64_t kKeepEdges = 1ull << 26;
-  static bool force_stream_gen() { return std::getenv("BIBFS_STREAM_GEN") != nullptr; }  // tests
+  bool force_stream_gen = false;  // (tests) stream-generate small graphs too: HipBiBfs::set_build_flags
+  bool wide_offsets = false;      // (tests) no 32-bit row-offset copy: the nnz >= 2^32 kernels
+  bool tiny_enabled = true;       // the tiny server for graphs it supports
   double build_ms = 0.0;
 
   // search state
@@ -65,38 +67,28 @@ struct HipBiBfs::Impl {
 
   // Device hand-off (grid_auto): on by default for resident searches of
   // graphs the general server takes, with the default level policy, when no
-  // vertex has more than auto_max_deg edges; BIBFS_AUTO_HANDOFF=0 turns it off
+  // vertex has more than auto_max_deg edges; HipBiBfs::set_auto_handoff(false) turns it off
   // (A/B).  Hub graphs keep the host-planned first level: on Kronecker 22 the
   // auto level lost in three A/Bs (0.058-0.060 vs 0.054-0.057 ms) while
   // 10M G(n, p) gains ~1% (profiles/r3_auto_handoff_ab2.jsonl).
-  // (BIBFS_AUTO_MAX_DEG overrides the bound, for A/B on hub graphs: with the
+  // (set_auto_max_degree overrides the bound, for A/B on hub graphs: with the
   // hub pass sized like the host's it still lost on Kronecker 22, 71.6-72.2 vs
   // 47.2-49.8 us mean search, profiles/r4_auto_chain_ab.jsonl; with direct hub
   // levels planned on the device too, 50.8-52.6 vs 44.5-44.7 and Kronecker 25
   // 60.6 vs 51.0, profiles/r4_auto_hub_direct_ab.jsonl -- a gated chain of
   // k_handoff + top-down + 1024-block hub launches behind EVERY query costs
   // ~30 us of stream time, which the next query's hand-off queues behind)
-  uint64_t auto_max_deg = [] {
-    const char* e = std::getenv("BIBFS_AUTO_MAX_DEG");
-    return e ? std::strtoull(e, nullptr, 10) : 64ull;
-  }();
+  uint64_t auto_max_deg = 64;
   uint32_t probe_edges = launch::lds_probe_budget();  // LDS meet probe (HipBiBfs::set_lds_probe_edges)
-  bool auto_on = [] {
-    const char* e = std::getenv("BIBFS_AUTO_HANDOFF");
-    return !(e && e[0] == '0');
-  }();
+  bool auto_on = true;
   // Device-planned grid levels chained behind the hand-off (the first one
   // planned by k_handoff, each further one by the finisher of the level before):
-  // BIBFS_AUTO_LEVELS, default 1.  Chains of 2 / 3 measured slower on 10M
+  // set_auto_levels, default 1.  Chains of 2 / 3 measured slower on 10M
   // G(n, p): 69.3-70.1 / 71.4 vs 67.1-67.2 us mean search -- the LDS phase
   // itself slows by ~2 us per chained level (the extra launches behind every
   // query) and the second level saves less than that
   // (profiles/r4_auto_chain_ab.jsonl).
-  int auto_levels = [] {
-    const char* e = std::getenv("BIBFS_AUTO_LEVELS");
-    const int v = e ? std::atoi(e) : 1;
-    return v < 1 ? 1 : (v > 8 ? 8 : v);
-  }();
+  int auto_levels = 1;
   // (A lazy chain -- the host enqueuing the planned next level only after the
   // search handed off -- measured slower too: 10M 61.3 -> 64.0 us mean search,
   // profiles/r4_auto_lazy_ab.jsonl; removed.)
@@ -117,9 +109,6 @@ struct HipBiBfs::Impl {
   enum AutoOutcome { kAutoFinal, kAutoMirror, kAutoMissed };
   AutoOutcome wait_auto(uint32_t pub, uint32_t ls) {
     for (uint64_t it = 1;; ++it) {
-      if (dbg() && (it & ((1ull << 26) - 1)) == 0)
-        std::fprintf(stderr, "[auto] waiting: pub %u ls %u gres.seq %u mirror.seq %u levels %u status %u\n", pub, ls,
-                     h_gres->seq, h_state->pad[0], h_state->levels, h_state->status);
       if (__atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub) return kAutoFinal;
       if (__atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) == ls) {
         return __atomic_load_n(&h_gres->seq, __ATOMIC_ACQUIRE) == pub ? kAutoFinal : kAutoMirror;
@@ -261,14 +250,7 @@ struct HipBiBfs::Impl {
   uint64_t tiny_overflows = 0;  // queries the tiny server handed back (re-run on the general engine)
   double last_ms = 0.0;
   uint64_t last_einsp = 0;
-  static bool tiny_stamp() {
-    static const bool on = std::getenv("BIBFS_TINY_STAMP") != nullptr;
-    return on;
-  }
-  static bool tiny_disabled() {
-    static const bool off = std::getenv("BIBFS_NO_TINY") != nullptr;
-    return off;
-  }
+  static bool tiny_stamp() { return env::tiny_stamps(); }
   bool tiny_usable(const SearchOptions& opt) const {
     return tiny_ok && resident && !opt.trace && !opt.force_grid && opt.lockstep &&
            opt.direction == Direction::kAuto && opt.side == SidePolicy::kSmallerEdges;
@@ -287,11 +269,6 @@ struct HipBiBfs::Impl {
   // the resident LDS server runs with 32- or 64-bit row offsets
   bool lds_server_usable() const { return n > 0 && n <= 0x7fffffffu; }
 
-  static bool dbg() {
-    static const bool on = std::getenv("BIBFS_DEBUG") != nullptr;
-    return on;
-  }
-
   // one aligned 16-byte store: the server reads the request with one load
   void post(uint32_t s, uint32_t src, uint32_t dst, uint32_t flags) {
     const __m128i v = _mm_set_epi32((int)req_tag(s, flags), (int)dst, (int)src, (int)s);
@@ -302,7 +279,6 @@ struct HipBiBfs::Impl {
   // Launch a server kernel of `kind`; it serves requests whose seq != last.
   void launch_kind(int kind, int pin, uint32_t last) {
     srv_launch_seq = ++seq == 0 ? ++seq : seq;
-    if (dbg()) std::fprintf(stderr, "[server] launch kind %d seq %u pin %d\n", kind, srv_launch_seq, pin);
     HIP_CHECK(hipSetDevice(device));
     __atomic_store_n(&h_box->alive, 0u, __ATOMIC_RELEASE);
     if (kind == kSrvTiny) {
@@ -311,7 +287,7 @@ struct HipBiBfs::Impl {
       launch::tiny_server(a, tiny_stamp(), sstream);
     } else {
       launch::lds_server(view(), bufs[0], bufs[1], launch::HostSide{h_res, h_path, h_path_cap, h_state}, h_box,
-                         srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, sstream);
+                         srv_launch_seq, last, pin, d_flag + 4, srv_idle_ticks, env::server_stamps(), sstream);
     }
     srv_kind = kind;
     srv_running = true;
@@ -443,9 +419,7 @@ struct HipBiBfs::Impl {
     if (!srv_running) return;
     const uint32_t s = ++seq == 0 ? ++seq : seq;
     post(s, 0, 0, kReqStop);
-    if (dbg()) std::fprintf(stderr, "[server] stop (stage %u alive %u)\n", h_box->stage, h_box->alive);
     HIP_CHECK(hipStreamSynchronize(sstream));
-    if (dbg()) std::fprintf(stderr, "[server] stopped\n");
     srv_running = false;
   }
 
@@ -454,18 +428,9 @@ struct HipBiBfs::Impl {
   void server_post(uint32_t src, uint32_t dst, const SearchOptions& opt, uint32_t qseq) {
     ensure_server(kSrvLds);
     post(qseq, src, dst, (opt.lockstep ? kReqLockstep : 0u) | ((uint32_t)opt.side & 3u) << 2 | (cur ? kReqAltBuf : 0u));
-    if (dbg()) std::fprintf(stderr, "[server] post %u (stage %u alive %u)\n", qseq, h_box->stage, h_box->alive);
   }
   void server_wait(uint32_t qseq) {
-    const auto t0 = std::chrono::steady_clock::now();
     wait_server(kSrvLds, qseq, [&] { return __atomic_load_n(&h_res->seq, __ATOMIC_ACQUIRE) == qseq; });
-    if (dbg()) {
-      const double host_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-      const double dev_us = (double)(h_res->rt_end - h_res->rt_pickup) * 0.01;
-      const double srch_us = (double)(h_res->rt_end - h_res->rt_begin) * 0.01;
-      std::fprintf(stderr, "[server] host round trip %.2f us, device pickup->result %.2f us (search %.2f)\n", host_us,
-                   dev_us, srch_us);
-    }
   }
 
   bool borrowed_csr = false;  // d_row_off / d_col belong to the caller (adopt_device_csr)
@@ -590,10 +555,10 @@ struct HipBiBfs::Impl {
   }
 
   void finish_graph(double ms) {
-    // BIBFS_WIDE_OFFSETS=1 (tests): no 32-bit copy of the row offsets, so a
-    // small graph takes the 64-bit-offset kernels of an nnz >= 2^32 graph
-    const char* wide = std::getenv("BIBFS_WIDE_OFFSETS");
-    if (nnz < 0xFFFFFFFFULL && !(wide && wide[0] == '1')) {
+    // wide_offsets (tests, set_build_flags): no 32-bit copy of the row
+    // offsets, so a small graph takes the 64-bit-offset kernels of an
+    // nnz >= 2^32 graph
+    if (nnz < 0xFFFFFFFFULL && !wide_offsets) {
       HIP_CHECK(hipMalloc(&d_row_off32, ((size_t)n + 1) * 4));
       launch::make_row_off32(d_row_off, n, d_row_off32, stream);
     }
@@ -601,19 +566,14 @@ struct HipBiBfs::Impl {
     // Budget BIBFS_PADJ_MAX_MB (default 4096 MiB; 0 disables) -- a 10M-vertex
     // G(n, 2.2/n) needs 352 MB, a scale-27 Kronecker graph would need ~69 GB,
     // where the plain CSR path is used instead.
-    const char* env = std::getenv("BIBFS_PADJ_MAX_MB");
-    const uint64_t budget = (env ? std::strtoull(env, nullptr, 10) : 4096ull) << 20;
+    const uint64_t budget = env::padj_budget_bytes();
     max_deg = launch::max_degree(d_row_off, n, stream);
     // 8 B per edge (launch::pack8) where ids, bases and degrees fit: half the
     // bytes (10M G(n, p): 176 instead of 352 MB).  The hope was a MALL-resident
     // adjacency and shorter dependent loads; measured the same search times
     // (10M 62.8-63.1 vs 62.8-63.2 us, profiles/r4_padj8_ab.jsonl), so what it
-    // buys is the memory.  BIBFS_PADJ8=0: the 16-byte form.
-    static const bool p8_on = [] {
-      const char* e = std::getenv("BIBFS_PADJ8");
-      return !(e && e[0] == '0');
-    }();
-    if (p8_on && nnz && n < launch::kPack8MaxN && nnz < launch::kPack8MaxNnz && max_deg <= launch::kPack8MaxDeg &&
+    // buys is the memory.
+    if (nnz && n < launch::kPack8MaxN && nnz < launch::kPack8MaxNnz && max_deg <= launch::kPack8MaxDeg &&
         nnz * 8 <= budget) {
       HIP_CHECK(hipMalloc(&d_padj8, nnz * 8));
       launch::build_padj8(d_row_off, d_col, nnz, d_padj8, stream);
@@ -622,7 +582,7 @@ struct HipBiBfs::Impl {
       launch::build_padj(d_row_off, d_col, nnz, d_padj, stream);
     }
     // small graphs: the packed 8-byte adjacency of the tiny server (8 (nnz + n) B)
-    if (!tiny_disabled() && launch::tiny_supported(n, nnz, max_deg)) {
+    if (tiny_enabled && launch::tiny_supported(n, nnz, max_deg)) {
       HIP_CHECK(hipMalloc(&d_tadj, (std::max<uint64_t>(nnz, 1) + 4) * 8));  // +4: 16-byte first-edge loads
       HIP_CHECK(hipMalloc(&d_tinfo, (size_t)n * 8));
       HIP_CHECK(hipMalloc(&d_tspill, (size_t)4 * kTinySpill * 8));
@@ -681,8 +641,6 @@ struct HipBiBfs::Impl {
   // wait for the pinned DevState mirror of the last finished level
   void wait_level() {
     for (uint64_t it = 1; __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != level_seq; ++it) {
-      if (dbg() && (it & ((1ull << 26) - 1)) == 0)
-        std::fprintf(stderr, "[grid] waiting for level seq %u: mirror.seq %u\n", level_seq, h_state->pad[0]);
       if ((it & 8191) == 0) {
         const hipError_t e = hipStreamQuery(stream);
         if (e == hipSuccess && __atomic_load_n(&h_state->pad[0], __ATOMIC_ACQUIRE) != level_seq)
@@ -769,7 +727,7 @@ struct HipBiBfs::Impl {
     fbits_valid[0] = fbits_valid[1] = false;
     int turn = 0;
     // 2 = stamped (BIBFS_STAMP): the level kernels also write their phase stamps
-    const int trace = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
+    const int trace = opt.trace ? (env::stamps() ? 2 : 1) : 0;
     for (uint32_t guard = 0; guard <= 2 * (uint64_t)n + 2; ++guard) {
       if (guard == 0 && !mirror_valid) sync_state();  // state left by the seed
       if (h_state->status != kRunning || h_state->meet != kEmpty) break;
@@ -985,7 +943,7 @@ void HipBiBfs::generate_gnp(uint32_t n, double p, uint64_t seed) {
   HIP_CHECK(hipEventRecord(I.ev0, I.stream));
   HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)n + 1) * 8));
   const double expect_m = p * 0.5 * (double)n * (double)(n - 1);
-  if (expect_m > (double)Impl::kKeepEdges || Impl::force_stream_gen()) {
+  if (expect_m > (double)Impl::kKeepEdges || p_->force_stream_gen) {
     // large graph: CSR straight from the generator, no edge list in HBM
     uint64_t m = 0;
     I.nnz = launch::gen_rows_gnp(n, p, seed, 0, n, I.d_row_off, &I.d_col, &m, I.stream);
@@ -1015,7 +973,7 @@ void HipBiBfs::generate_rmat(uint32_t n, uint64_t m, uint64_t seed, double a, do
   I.m_input = m;
   HIP_CHECK(hipEventRecord(I.ev0, I.stream));
   HIP_CHECK(hipMalloc(&I.d_row_off, ((size_t)n + 1) * 8));
-  if (m > Impl::kKeepEdges || Impl::force_stream_gen()) {
+  if (m > Impl::kKeepEdges || p_->force_stream_gen) {
     // large graph: CSR straight from the generator, no edge list in HBM
     I.nnz = launch::gen_rows_rmat(n, m, seed, a, b, c, 0, n, I.d_row_off, &I.d_col, I.stream);
   } else {
@@ -1247,6 +1205,11 @@ double HipBiBfs::last_search_ms() const { return p_->last_ms; }
 uint64_t HipBiBfs::last_edges_inspected() const { return p_->last_einsp; }
 bool HipBiBfs::tiny_engine() const { return p_->tiny_ok; }
 void HipBiBfs::set_auto_handoff(bool on) { p_->auto_on = on; }
+void HipBiBfs::set_build_flags(bool wide_offsets, bool stream_gen, bool tiny) {
+  p_->wide_offsets = wide_offsets;
+  p_->force_stream_gen = stream_gen;
+  p_->tiny_enabled = tiny;
+}
 void HipBiBfs::set_auto_gate_timeout_us(double us) { p_->auto_gate_us = us; }
 double HipBiBfs::auto_gate_timeout_us() const { return p_->auto_gate_us; }
 uint64_t HipBiBfs::auto_gate_misses() const { return p_->auto_gate_misses; }
@@ -1336,10 +1299,10 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
   // around grid levels, where their ~µs cost is noise
   if (grid) HIP_CHECK(hipEventRecord(I.ev0, I.stream));  // LDS hash keys carry a parity bit: ids < 2^31
   if (!grid) {
-    const int tr = opt.trace ? (std::getenv("BIBFS_STAMP") ? 2 : 1) : 0;
+    const int tr = opt.trace ? (env::stamps() ? 2 : 1) : 0;
     const int lock = (opt.lockstep && I.n <= 0x7fffffffu) ? 1 : 0;
     // BIBFS_STAMP_SERVER: the server's profiling build answers traced queries too
-    static const bool stamp_srv = std::getenv("BIBFS_STAMP_SERVER") != nullptr;
+    const bool stamp_srv = env::server_stamps();
     // with the tiny server resident for this graph, the queries it cannot take
     // (non-default options, overflow) run one-shot beside it
     if (I.resident && !I.tiny_ok && (!opt.trace || stamp_srv) && I.lds_server_usable()) {
@@ -1361,10 +1324,6 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         launch::cleanup(I.buf, I.n, I.d_flag + 8, I.h_clean, auto_tag, 2, I.stream);
       }
       I.server_wait(seq);
-      if (I.dbg())
-        std::fprintf(stderr, "[server] answer seq %u status %u hops %d levels %u stage %u poll_rt %.2f us polls %u\n",
-                     I.h_res->seq, I.h_res->status, I.h_res->hops, I.h_res->levels, I.h_box->stage,
-                     I.h_box->pad[0] * 0.01, I.h_box->pad[1]);
     } else {
       launch::lds_search(g, I.buf, hs, src, dst, seq, (int)opt.side, tr, I.pin_xcc, I.d_flag + 4, lock,
                          I.stream);
@@ -1380,9 +1339,6 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
         const uint32_t lv1 = I.h_res->levels;
         stats_handoff_levels = (int)lv1;
         const auto outcome = I.wait_auto(pub_auto, auto_ls);
-        if (I.dbg())
-          std::fprintf(stderr, "[auto] outcome %d lds levels %u gres levels %u mirror levels %u\n", (int)outcome, lv1,
-                       I.h_gres->levels, I.h_state->levels);
         auto_final = outcome == Impl::kAutoFinal;
         if (auto_final) {
           stats.grid_levels = (int)(I.gres->levels - lv1);
@@ -1483,7 +1439,7 @@ SearchResult HipBiBfs::search_general(vid_t src, vid_t dst, const SearchOptions&
     r.search_ms += ms;
   }
   if (opt.trace) I.fetch_trace(r);
-  if (opt.trace && std::getenv("BIBFS_STAMP")) {
+  if (opt.trace && env::stamps()) {
     I.fetch_clock(r);
     I.fetch_grid_stamps(r);
   }

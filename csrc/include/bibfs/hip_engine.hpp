@@ -107,22 +107,27 @@ class HipBiBfs {
   void set_auto_gate_timeout_us(double us);
   double auto_gate_timeout_us() const;
   uint64_t auto_gate_misses() const;
-  // Device-planned grid levels chained behind the hand-off (1-8, default 1;
-  // env BIBFS_AUTO_LEVELS): each level's finisher plans the next one, so a
+  // Device-planned grid levels chained behind the hand-off (1-8, default 1):
+  // each level's finisher plans the next one, so a
   // search that needs that many grid levels never waits for the host.
   void set_auto_levels(int levels);
   int auto_levels() const;
   // The device hand-off runs on graphs whose largest degree is at most this
-  // (default 64: hub graphs keep host-planned levels; env BIBFS_AUTO_MAX_DEG).
+  // (default 64: hub graphs keep host-planned levels).
   void set_auto_max_degree(uint64_t deg);
   uint64_t auto_max_degree() const;
   // Meet probe of the LDS engine (hub graphs, largest degree > 64): before a
   // level that does not fit LDS is handed to the grid engine, up to this many
   // of its frontier edges are tested against the other side's visited set;
-  // any hit ends the search with the shortest length (default 16384; env
-  // BIBFS_LDS_PROBE_EDGES; 0 = off).
+  // any hit ends the search with the shortest length (default 16384; 0 = off).
   void set_lds_probe_edges(uint32_t edges);
   uint32_t lds_probe_edges() const;
+  // Build-time flags, applied by the next load / generate: wide_offsets keeps
+  // no 32-bit row-offset copy (a small graph then runs the nnz >= 2^32
+  // kernels; tests), stream_gen generates even small graphs straight into the
+  // CSR (the large-graph path; tests), tiny = false keeps the tiny server off
+  // (the general resident server answers every graph; benchmarks).
+  void set_build_flags(bool wide_offsets, bool stream_gen, bool tiny = true);
 
   // --- step-wise API (parity with the reference's per-level C API,
   //     v4/comp.h:8-36: init frontiers, expand one side, check intersection)

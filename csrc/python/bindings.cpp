@@ -343,6 +343,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property("auto_levels", &HipBiBfs::auto_levels, &HipBiBfs::set_auto_levels)
       .def_property("auto_max_degree", &HipBiBfs::auto_max_degree, &HipBiBfs::set_auto_max_degree)
       .def_property("lds_probe_edges", &HipBiBfs::lds_probe_edges, &HipBiBfs::set_lds_probe_edges)
+      .def("set_build_flags", &HipBiBfs::set_build_flags, py::arg("wide_offsets") = false,
+           py::arg("stream_gen") = false, py::arg("tiny") = true)
       .def_property("batch_edge_cap", &HipBiBfs::batch_edge_cap, &HipBiBfs::set_batch_edge_cap)
       .def_property_readonly("last_batch_fallbacks", &HipBiBfs::last_batch_fallbacks)
       .def("set_batch_tuning", &HipBiBfs::set_batch_tuning, py::arg("lds_first") = -1, py::arg("threads") = 0)

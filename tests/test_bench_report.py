@@ -150,3 +150,51 @@ def test_cpu_serial_reference_on_small_graph():
             pairs.append((s, d, int(r.hops)))
     med, mean, e2e, ok, first = bench.cpu_serial_ms(spec, pairs, reps=2, oracle_pairs=2)
     assert med > 0 and mean > 0 and e2e > 0 and first > 0 and ok == min(2, len(pairs))
+
+
+def test_partitioned_headline_fields_beside_the_replicated_value():
+    """Round-6: the partitioned BASELINE config-3 numbers (1M G(n, p), one
+    collective search per query) sit at the top level next to the replicated
+    headline, so a scaling run over N reports the v4 engine too."""
+    part = {"gnp:1000000::2": {"verified": True, "ms_per_query": 0.41, "speedup_vs_single_gpu": 0.09,
+                               "gteps": 2.68, "collectives_per_round": 1.1}}
+    out = bench.report(_args(), 4, _head(gteps=36.0), {}, part)
+    assert out["value"] == 36.0 and out["scaling"] == "weak"
+    assert out["partitioned_config"] == "gnp:1000000::2"
+    assert out["partitioned_ms_per_query"] == 0.41 and out["partitioned_speedup_vs_single_gpu"] == 0.09
+    assert out["partitioned_collectives_per_round"] == 1.1 and out["partitioned_verified"] is True
+    failed = bench.report(_args(), 4, _head(), {}, {"gnp:1000000::2": {"error": "x"}})
+    assert failed["partitioned_ms_per_query"] is None
+    assert bench.report(_args(), 1, _head(), {}, {})["partitioned_ms_per_query"] is None
+
+
+def _rehearsals():
+    import glob
+    import os
+
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return sorted(glob.glob(os.path.join(here, "profiles", "r6_bench_[24]rank_1gpu_ipc*.json")))
+
+
+def test_ipc_rehearsal_lines_carry_partitioned_fields():
+    """The 2- and 4-rank IPC rehearsals (bench.py --gpus 2/4 on one GPU,
+    measured on the GPU box and committed under profiles/) carry the
+    top-level partitioned fields, verified, with every rank counted."""
+    import pytest
+
+    files = _rehearsals()
+    if not files:
+        pytest.skip("no round-6 rehearsal profiles committed")
+    seen = set()
+    for f in files:
+        with open(f) as fh:
+            line = [ln for ln in fh.read().splitlines() if ln.strip().startswith("{")][-1]
+        d = json.loads(line)
+        assert d["n_gpus"] in (2, 4), f
+        seen.add(d["n_gpus"])
+        assert d["partitioned_config"] == "gnp:1000000::2"
+        assert d["partitioned_ms_per_query"] > 0 and d["partitioned_verified"] is True, f
+        assert d["partitioned_speedup_vs_single_gpu"] is not None
+        p = d["detail"]["partitioned"]["gnp:1000000::2"]
+        assert p["ranks"] == d["n_gpus"] and p["ms_per_query"] == d["partitioned_ms_per_query"]
+    assert seen == {2, 4}, seen

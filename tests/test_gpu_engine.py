@@ -436,7 +436,7 @@ def test_wide_offsets_resident_server_vs_oracle(gpu_engine, spec, monkeypatch):
     g = bb.from_spec(spec)
     pairs = pairs_for(g.n, 40, 33)
     truth = [native.bfs_oracle(g.csr, s, d).hops for s, d in pairs]
-    monkeypatch.setenv("BIBFS_WIDE_OFFSETS", "1")
+    gpu_engine.set_build_flags(wide_offsets=True)
     gpu_engine.load(g)
     try:
         handed = 0
@@ -452,7 +452,7 @@ def test_wide_offsets_resident_server_vs_oracle(gpu_engine, spec, monkeypatch):
         assert handed > 0 or spec.startswith("kron"), "expected hand-offs on the G(n, p) graph"
     finally:
         gpu_engine.set_resident(False)
-        monkeypatch.delenv("BIBFS_WIDE_OFFSETS")
+        gpu_engine.set_build_flags()
         gpu_engine.load(g)  # 32-bit offsets again for the tests after this one
 
 
@@ -631,12 +631,14 @@ def test_streamed_generation_equals_edge_list_csr(gpu_engine, spec, monkeypatch)
     kind, n, arg, seed = spec.split(":")[0], int(spec.split(":")[1]), float(spec.split(":")[2]), int(spec.split(":")[3])
     el = native.gen_gnp(n, arg, seed) if kind == "gnp" else native.gen_rmat(n, int(arg), seed)
     h = native.build_csr(el)
-    monkeypatch.setenv("BIBFS_STREAM_GEN", "1")
-    if kind == "gnp":
-        gpu_engine.generate_gnp(n, arg, seed)
-    else:
-        gpu_engine.generate_rmat(n, int(arg), seed)
-    monkeypatch.delenv("BIBFS_STREAM_GEN")
+    gpu_engine.set_build_flags(stream_gen=True)
+    try:
+        if kind == "gnp":
+            gpu_engine.generate_gnp(n, arg, seed)
+        else:
+            gpu_engine.generate_rmat(n, int(arg), seed)
+    finally:
+        gpu_engine.set_build_flags()
     d = gpu_engine.download_csr()
     assert gpu_engine.m == el.m
     assert np.array_equal(d.row_off, h.row_off)

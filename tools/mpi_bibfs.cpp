@@ -47,13 +47,26 @@ int main(int argc, char** argv) {
   }
   int rc = 0;
   try {
-    int local_rank = 0, local_size = 1, max_local = 1;
+    int local_rank = 0, local_size = 1, max_local = 1, min_local = 1;
     node_rank(&local_rank, &local_size);
     MPI_Allreduce(&local_size, &max_local, 1, MPI_INT, MPI_MAX, MPI_COMM_WORLD);
+    MPI_Allreduce(&local_size, &min_local, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+    // The IPC control plane is node-local shared memory and checks peer
+    // liveness by local pid, so it needs every rank on one node.
+    const bool one_node = min_local == size;
     const int ndev = bibfs::gpu_count();
     std::string comm = a.has("comm") ? a.get("comm") : "auto";
-    if (comm == "auto") comm = max_local > ndev ? "ipc" : "rccl";
+    if (comm == "auto") comm = (max_local > ndev && one_node) ? "ipc" : "rccl";
     if (comm != "rccl" && comm != "ipc") throw bibfs::Error("--comm must be auto, rccl or ipc");
+    if (comm == "ipc" && !one_node) {
+      if (rank == 0)
+        std::fprintf(stderr,
+                     "--comm ipc needs all %d ranks on one node (this job spans several nodes: %d to %d ranks per "
+                     "node); use --comm rccl with at most one rank per GPU\n",
+                     size, min_local, max_local);
+      MPI_Finalize();
+      return 1;
+    }
     // RCCL: one rank per GPU (a rank owns a GPU's HBM and its RCCL endpoint).
     // IPC: ranks share the node's GPUs round-robin.  Every rank checks its
     // device and the verdict is agreed on before any rank touches a
