@@ -102,6 +102,9 @@ class DistEngine:
 
     def __init__(self, rank: int, world: int, device: int, unique_id: bytes, backend: str = "rccl"):
         self._e = native.DistBiBfs(int(rank), int(world), int(device), unique_id, backend)
+        # the serving call goes straight to the native method (no Python frame
+        # per query, as HipEngine.query); `query` below documents it
+        self.query = self._e.query
 
     @staticmethod
     def unique_id(backend: str = "rccl") -> bytes:
@@ -135,8 +138,10 @@ class DistEngine:
 
     def query(self, src: int, dst: int):
         """Lean serving call: ``(hops, path)``, hops = -1 when unreachable
-        (the stats stay in ``last_stats``, read outside any timed loop)."""
-        return self._e.query(int(src), int(dst))
+        (the stats stay in ``last_stats``, read outside any timed loop).  At
+        world size 1 it is the single-GPU engine's own query (resident tiny /
+        LDS server, GIL kept)."""
+        return self._e.query(src, dst)
 
     def load(self, graph: Graph) -> "DistEngine":
         self._e.load_edges(graph.edges)

@@ -3657,6 +3657,27 @@ SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   }
 }
 
+bool DistBiBfs::query_is_local() const {
+  const auto& I = *p_;
+  return I.size == 1 && I.tune.world1_single && I.single != nullptr;
+}
+
+int64_t DistBiBfs::query(vid_t src, vid_t dst, std::vector<vid_t>* path) {
+  auto& I = *p_;
+  if (query_is_local()) {
+    // world size 1: the rank's shard is the whole graph and the adopted
+    // single-GPU engine answers through its resident server (tiny / LDS),
+    // exactly as HipBiBfs::query -- the partitioned wrapper adds nothing
+    if (I.comm->aborted()) throw Error("dist: the communicator was aborted by an earlier failure");
+    I.stats = DistLevelStats{};
+    I.stats.single_engine = 1;
+    return I.single->query(src, dst, path);
+  }
+  SearchResult r = search(src, dst);
+  if (path) *path = std::move(r.path);
+  return r.found ? (int64_t)r.hops : -1;
+}
+
 void DistBiBfs::barrier() {
   auto& I = *p_;
   HIP_CHECK(hipSetDevice(I.device));

@@ -443,7 +443,13 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   __shared__ uint32_t won;
   __shared__ __attribute__((aligned(16))) uint32_t pub_img[64];  // hand-off DevState [0, 32) / HostResult [32, 64) images
 
-  const int tid = threadIdx.x;
+  // The thread index goes through an opaque copy: in the resident server this
+  // body sits inside the query loop, and without it the compiler hoists every
+  // tid-derived LDS address out of that loop and keeps them live across it --
+  // at the 128-VGPR cap of a 1024-thread workgroup, as scratch spills reloaded
+  // on every query.
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
   const int wid = tid >> 6;
   const uint32_t lane = __lane_id();
   // XCD affinity: the search is latency-bound on dependent CSR loads, so it
@@ -1122,7 +1128,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
   };
 
   unsigned long long clk0 = 0;
-  const unsigned long long rt0 = tid == 0 ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  // the search's start stamp waits in LDS for the publish (held in registers
+  // across the search it was the kernel's one VGPR spill)
+  __shared__ unsigned long long rt0_lds;
+  if (tid == 0) rt0_lds = __builtin_amdgcn_s_memrealtime();
   if (kStamp && tid == 0) clk0 = __builtin_amdgcn_s_memtime();
   wave_rounds();  // every wave; the replicated state continues below
   uint32_t fstatus = kRunning;
@@ -1350,7 +1359,11 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       const unsigned long long mk = meetk[slot];
       // the other slot is used by the next big level (wave 0 read it one big
       // level ago)
-      if (lane < 2) ctr[slot ^ 1][lane] = 0;
+      // (the lane index re-read: an address derived from `lane` was kept live
+      // across the search, a spill in the 64-bit-offset kernel)
+      uint32_t l = __lane_id();
+      asm volatile("" : "+v"(l));
+      if (l < 2) ctr[slot ^ 1][l] = 0;
       if (lane == 0) meetk[slot ^ 1] = ~0ull;
       const uint32_t mk_hi = uni((uint32_t)(mk >> 32)), mk_lo = uni((uint32_t)mk);
       if (mk != ~0ull && (meet == kEmpty || mk_hi < md0 + md1)) {
@@ -1382,7 +1395,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     LevelTraceDev& t = P.b.trace[P.b.trace_cap - 1];
     e3 = __builtin_amdgcn_s_memtime();
     t.edges = e3 - clk0;
-    t.discovered = __builtin_amdgcn_s_memrealtime() - rt0;
+    t.discovered = __builtin_amdgcn_s_memrealtime() - rt0_lds;
   }
 
   // search state is valid in wave 0; fstatus (from the final plan) in every wave
@@ -1411,8 +1424,9 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
     uint32_t* pbuf = reinterpret_cast<uint32_t*>(&R[0][0]);
     constexpr uint32_t kPbufCap = sizeof(R) / sizeof(uint32_t);
     const bool staged = !path_dev && !path_skip && path_len <= kPbufCap;
-    if (status == kFound && !path_skip && tid < 2) {
-      uint32_t* const out = staged ? pbuf : (path_dev ? P.b.dpath : P.h.path);
+    // (staged and unstaged walks are separate calls: one pointer selected
+    // between LDS and global memory would make every path store a flat store)
+    auto walk = [&](uint32_t* out) {
       if (kLq && lq_done) {
         // LDS walk: lane 0 from the meet back to the source (positions md0 .. 0),
         // lane 1 on to the target (md0 .. md0 + md1), one LDS load per hop
@@ -1428,6 +1442,10 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       } else {
         walk_side(tid ? P.b.parent[1] : P.b.parent[0], P.n, meet, tid, (int)md0, (int)md1, out);
       }
+    };
+    if (status == kFound && !path_skip && tid < 2) {
+      if (staged) walk(pbuf);
+      else walk(path_dev ? P.b.dpath : P.h.path);
     }
     if (staged) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1473,7 +1491,7 @@ __device__ __forceinline__ void lds_search_body(const LdsParams<OffT>& P, bool e
       rv.path_len = path_len;
       rv.path_on_device = path_dev ? 1u : path_skip ? 2u : 0u;
       rv.probe = min(probe_walked, 0x7fffffffu) | (probe_hit ? 0x80000000u : 0u);
-      rv.rt_begin = rt0;
+      rv.rt_begin = rt0_lds;
       rv.rt_end = __builtin_amdgcn_s_memrealtime();
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // same wave: lane 0's LDS writes precede the reads

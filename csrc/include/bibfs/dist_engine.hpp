@@ -134,6 +134,14 @@ class DistBiBfs {
   // Collective: every rank calls it with the same arguments; every rank gets
   // the full result (hops + path).
   SearchResult search(vid_t src, vid_t dst, const SearchOptions& opt = {});
+  // Lean serving call (collective like search): the hop count (-1 = no path)
+  // and the path.  At world size 1 with world1_single it is the single-GPU
+  // engine's own query() -- no SearchResult, no stats, no device switch -- so
+  // a one-rank job serves at the single engine's latency.
+  int64_t query(vid_t src, vid_t dst, std::vector<vid_t>* path);
+  // true when query() is answered by the single-GPU engine without a
+  // collective (bindings keep the GIL for it, like HipBiBfs.query)
+  bool query_is_local() const;
 
   // Collective checks that need no copy of the whole graph anywhere:
   // validate_path -- every edge (path[i], path[i+1]) is looked up in the row

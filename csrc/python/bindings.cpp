@@ -439,12 +439,16 @@ PYBIND11_MODULE(_native, m) {
       // lean serving call, the twin of HipBiBfs.query: (hops, path), hops -1 when unreachable
       .def("query",
            [](DistBiBfs& e, vid_t s, vid_t d) {
-             SearchResult r;
-             {
+             static thread_local std::vector<vid_t> p;  // reused: no allocation per query
+             p.clear();
+             int64_t h;
+             if (e.query_is_local()) {  // world size 1: the single engine's query, GIL kept (~10 us)
+               h = e.query(s, d, &p);
+             } else {  // a collective: other ranks' Python threads may need the GIL meanwhile
                py::gil_scoped_release rel;
-               r = e.search(s, d);
+               h = e.query(s, d, &p);
              }
-             return hops_path(r.found ? r.hops : -1, r.path);
+             return hops_path(h, p);
            })
       .def("barrier", &DistBiBfs::barrier, py::call_guard<py::gil_scoped_release>())
       .def("allreduce_max", &DistBiBfs::allreduce_max, py::call_guard<py::gil_scoped_release>())

@@ -94,3 +94,18 @@ def test_dist_kernels_use_no_scratch_or_flat_ops(tmp_path):
     ops, priv = _kernels(os.path.join(ROOT, "build/obj/dist/dist_engine.o"), tmp_path)
     for k in _matching(priv, r"k_walk|k_spec_"):
         assert sum(ops[k].values()) == 0, (k, dict(ops[k]))
+
+
+def test_lds_engine_kernels_use_no_scratch_or_flat(tmp_path):
+    """The LDS engine (one-shot k_lds_bibfs, resident k_lds_server, batched
+    k_lds_batch) runs at the 128-VGPR cap of a 1024-thread workgroup.  Round 6
+    removed its spills (tid-derived LDS addresses hoisted out of the server's
+    query loop, the start stamp held across the search) and the flat path
+    stores (one walk pointer selected between LDS and global memory).  The
+    stamped profiling builds (kStamp) are exempt."""
+    ops, priv = _kernels(os.path.join(ROOT, "build/obj/hip/engine_kernels.o"), tmp_path)
+    prod = _matching(priv, r"k_lds_bibfsI[jm]Lb0E|k_lds_serverI[jm]Lb[01]ELb0E|k_lds_batch")
+    assert len(prod) == 8, prod
+    for k in prod:
+        assert priv[k] == 0, (k, priv[k])
+        assert sum(ops[k].values()) == 0, (k, dict(ops[k]))
