@@ -659,6 +659,8 @@ def main(argv=None) -> int:
             "collectives_per_round": sum(s["collectives"] for s in st) / max(1, sum(s["rounds"] for s in st)),
             "speculative_rounds_per_query": sum(s["spec_rounds"] for s in st) / steps,
             "dense_levels_per_query": sum(s["dense_levels"] for s in st) / steps,
+            # pipelined searches that stalled and finished with exact plans
+            "pipe_drains_per_query": sum(s.get("pipe_drains", 0) for s in st) / steps,
             "verified": ok, "checked_queries": steps + warmup,
             "world1_engine": ("single-GPU engine over the rank's own device CSR (DistTuning.world1_single)"
                               if world == 1 and st and st[0].get("single_engine") else None),
@@ -704,9 +706,10 @@ def main(argv=None) -> int:
         # candidate exchange and the status allgather leave
         out.update(round_split(eng, query, warmup, min(steps, 8)))
         if world > 1:
-            # the same timed loop with DistTuning.overlap on (side 0's exchange
-            # overlapping side 1's expansion), side by side with the default
-            eng.set_tuning(overlap=True)
+            # the same timed loop with exact plans (DistTuning.pipeline off: a
+            # status allgather per round beside the candidate exchange), side by
+            # side with the default pipelined rounds (one collective per round)
+            eng.set_tuning(pipeline=False)
             for i in range(2):
                 lean(i)
             eng.barrier()
@@ -715,30 +718,30 @@ def main(argv=None) -> int:
             for i in range(steps):
                 lean(warmup + i)
             eng.barrier()
-            dto = max_over_ranks(time.perf_counter() - t1)
-            ov = {"ms_per_query": round(dto * 1e3 / steps, 5),
-                  "speedup_vs_overlap_off": round(dt / dto, 4)}
-            ov.update(round_split(eng, query, warmup, min(steps, 8), overlap=True))
-            out["overlap_on"] = ov
+            dte = max_over_ranks(time.perf_counter() - t1)
+            ex = {"ms_per_query": round(dte * 1e3 / steps, 5),
+                  "pipelined_speedup": round(dte / dt, 4)}
+            ex.update(round_split(eng, query, warmup, min(steps, 8), pipeline=False))
+            out["pipeline_off"] = ex
             eng.set_tuning()
             out["verified"] = all_ranks_ok(not wrong) and dist_ok
         else:
-            out["overlap_on"] = None  # one rank: nothing is exchanged, nothing to overlap
+            out["pipeline_off"] = None  # one rank: nothing is exchanged, every plan is exact
         if wrong:
             out["mismatch"] = wrong[:4]
         out["comm"] = eng.backend
         eng.release()
         return out, eng.world
 
-    def round_split(eng, query, first: int, count: int, overlap: bool = False) -> dict:
-        eng.set_tuning(stamps=True, overlap=overlap)
+    def round_split(eng, query, first: int, count: int, pipeline: bool = True) -> dict:
+        eng.set_tuning(stamps=True, pipeline=pipeline)
         acc = {"stamped_rounds": 0, "expand_us": 0.0, "claim_us": 0.0, "exchange_us": 0.0, "status_us": 0.0}
         for i in range(count):
             query(first + i)
             st = eng.last_stats
             for k in acc:
                 acc[k] += st[k]
-        eng.set_tuning(overlap=overlap)
+        eng.set_tuning(pipeline=pipeline)
         nr = acc["stamped_rounds"]
         if not nr:
             return {"stamped_rounds_per_query": 0.0}

@@ -13,13 +13,14 @@ claim launch (csrc/dist/dist_engine.hip, RoundStamp).  Per round:
                exchange (here device-to-device copies between the ranks'
                streams; RCCL send/recv on a node) plus the launch gap
   status_us    claim end -> next expansion start: the status allgather plus
-               the launch gap
+               the launch gap (pipelined rounds, the default with P > 1: the
+               launch gap alone -- the status travels with the next exchange)
 
 Rank 0's numbers, median over queries of the per-round means.  The ranks
 share the GPU's CUs, so kernel times are an upper bound for one rank per
 GPU; the exchange column is the local group's copies, not xGMI.
 
-    python benchmarks/dist_rounds.py --specs gnp:1000000::2,kron:22 --ranks 1,2,4 --overlap 0,1
+    python benchmarks/dist_rounds.py --specs gnp:1000000::2,kron:22 --ranks 1,2,4 --pipeline 1,0
 
 --procs runs the ranks as separate PROCESSES over the HIP-IPC transport
 (csrc/dist/ipc_comm.hip, parallel.dist_proc_matrix) instead of threads of one
@@ -48,7 +49,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--specs", default="gnp:1000000::2,kron:22")
     ap.add_argument("--ranks", default="1,2,4")
-    ap.add_argument("--overlap", default="0,1")
+    ap.add_argument("--pipeline", default="1,0", help="DistTuning.pipeline values to run (P > 1)")
     ap.add_argument("--queries", type=int, default=24)
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--solo", type=int, default=1, help="P = 1: 0 runs the multi-workgroup rounds (stampable)")
@@ -59,25 +60,32 @@ def main():
         rnd = random.Random(a.seed)
         qs = [(rnd.randrange(n), rnd.randrange(n)) for _ in range(a.queries)]
         for ranks in [int(x) for x in a.ranks.split(",")]:
-            for ov in [int(x) for x in a.overlap.split(",")]:
-                if ov and ranks == 1:
+            for pv in [int(x) for x in a.pipeline.split(",")]:
+                if not pv and ranks == 1:
                     continue
                 if a.procs:
-                    tk = {"stamps": True, "overlap": bool(ov), "solo": bool(a.solo)}
+                    tk = {"stamps": True, "pipeline": bool(pv), "solo": bool(a.solo)}
                     got, _ = dist_proc_matrix(ranks, spec, qs, [({}, tk)])
                     rs, st0, run = got[0]
                     t = {"query_ms": run["query_ms"], "stats": st0}
                 else:
-                    tun = make_tuning(stamps=True, overlap=bool(ov), solo=bool(a.solo))
+                    tun = make_tuning(stamps=True, pipeline=bool(pv), solo=bool(a.solo))
                     rs, t = dist_local_generate_run(ranks, spec, qs, tuning=tun)
                 keep = [(r, ms, st) for r, ms, st in zip(rs, t["query_ms"], t["stats"]) if r.found and r.hops > 0]
                 sts = [st for _, _, st in keep]
                 rec = {
-                    "spec": spec, "ranks": ranks, "overlap": bool(ov), "queries": len(keep),
+                    "spec": spec, "ranks": ranks, "pipeline": bool(pv) and ranks > 1, "queries": len(keep),
                     "transport": "ipc-processes" if a.procs else "local-threads",
                     "median_query_ms": round(statistics.median(ms for _, ms, _ in keep), 4) if keep else None,
                     "mean_rounds": round(statistics.mean(st["rounds"] for st in sts), 2) if sts else None,
                     "mean_stamped_rounds": round(statistics.mean(st["stamped_rounds"] for st in sts), 2) if sts else None,
+                    # collectives of the whole search (seed gather, rounds, path gather) per
+                    # accounted round, and per enqueued round (pipelined: +1 round at the end)
+                    "collectives_per_round": (round(sum(st["collectives"] for st in sts) /
+                                                    max(1, sum(st["rounds"] for st in sts)), 3) if sts else None),
+                    "collectives_per_query": round(statistics.mean(st["collectives"] for st in sts), 2) if sts else None,
+                    "spec_rounds_per_query": round(statistics.mean(st["spec_rounds"] for st in sts), 2) if sts else None,
+                    "pipe_drains": sum(st["pipe_drains"] for st in sts),
                     "expand_us_per_round": per_round(sts, "expand_us"),
                     "claim_us_per_round": per_round(sts, "claim_us"),
                     "exchange_us_per_round": per_round(sts, "exchange_us"),

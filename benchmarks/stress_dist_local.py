@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--specs", default="gnp:1000000::2,kron:20:16:1,rmat:262144:4194304:4")
     ap.add_argument("--ranks", default="2,3,4,8")
     ap.add_argument("--queries", type=int, default=256)
-    ap.add_argument("--overlap", type=int, default=0)
+    ap.add_argument("--pipeline", type=int, default=1)
     ap.add_argument("--procs", action="store_true", help="ranks as processes over the IPC transport")
     a = ap.parse_args()
     import torch  # noqa: F401
@@ -44,18 +44,18 @@ def main():
         for P in [int(x) for x in a.ranks.split(",")]:
             t0 = time.perf_counter()
             if a.procs:
-                got, _ = dist_proc_matrix(P, spec, qs, [({}, {"overlap": bool(a.overlap)})], verify=8)
+                got, _ = dist_proc_matrix(P, spec, qs, [({}, {"pipeline": bool(a.pipeline)})], verify=8)
                 rs, _, run = got[0]
                 t = {"path_valid": run["path_valid"], "uni_hops": run["uni_hops"]}
             else:
-                rs, t = dist_local_generate_run(P, spec, qs, tuning=make_tuning(overlap=bool(a.overlap)), verify=8)
+                rs, t = dist_local_generate_run(P, spec, qs, tuning=make_tuning(pipeline=bool(a.pipeline)), verify=8)
             dt = time.perf_counter() - t0
             wrong = sum(1 for r, h in zip(rs, truth) if (r.hops if r.found else -1) != h)
             bad_paths = sum(1 for ok in t.get("path_valid", []) if ok == 0)  # 1 valid, -1 no path
             uni = [(u, h) for u, h in zip(t.get("uni_hops", []), truth) if u != -2]  # -2: not re-run
             uni_bad = sum(1 for u, h in uni if u != h)
             rec = {"spec": spec, "ranks": P, "transport": "ipc-processes" if a.procs else "local-threads",
-                   "overlap": bool(a.overlap), "queries": len(qs), "wrong_hops": wrong, "bad_paths": bad_paths,
+                   "pipeline": bool(a.pipeline), "queries": len(qs), "wrong_hops": wrong, "bad_paths": bad_paths,
                    "uni_checked": len(uni), "uni_wrong": uni_bad, "wall_s": round(dt, 2)}
             print(json.dumps(rec), flush=True)
             if wrong or bad_paths or uni_bad:

@@ -52,7 +52,7 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                 nosync_bytes: Optional[int] = None, timeout_s: Optional[float] = None,
                 walk_max: Optional[int] = None, solo: Optional[bool] = None,
                 solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
-                overlap: Optional[bool] = None, spec_stall_edges: Optional[int] = None,
+                pipeline: Optional[bool] = None, spec_stall_edges: Optional[int] = None,
                 stamps: Optional[bool] = None, hbm_cap_bytes: Optional[int] = None,
                 world1_single: Optional[bool] = None, spill_cap: Optional[int] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
@@ -66,9 +66,12 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
     of a speculative round (0 = predicted per round from the last per-owner
     counts); candidates that do not fit are re-offered by a continuation round.
 
-    overlap (more than one rank): the two sides of a speculative round expand
-    as separate launches (side 1 on the compute stream) so side 0's exchange
-    overlaps side 1's expansion.
+    pipeline (more than one rank, default on): ONE collective per speculative
+    round -- each round's reduction travels in the header of the next round's
+    candidate exchange, and each plan accounts the round before the last one
+    (a finished search runs one extra round); the first stall (a spill, a big
+    or dense frontier) drains the pipeline and the search goes on with exact
+    plans.  Off: exact plans, a status allgather per round.
 
     stamps: per-round device stamps; ``last_stats`` then splits the
     speculative rounds into ``expand_us`` / ``claim_us`` (kernels) and
@@ -89,7 +92,7 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
     t = native.DistTuning()
     for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
-                 ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("overlap", overlap),
+                 ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("pipeline", pipeline),
                  ("spec_stall_edges", spec_stall_edges), ("stamps", stamps), ("hbm_cap_bytes", hbm_cap_bytes),
                  ("world1_single", world1_single), ("spill_cap", spill_cap)):
         if v is not None:

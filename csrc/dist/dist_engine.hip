@@ -102,11 +102,17 @@ constexpr int kSmallU = 4;                      // items per thread in flight pe
 // values only).  Double-buffered by round parity: round `it` reads
 // ctl[(it-1)&1] and writes ctl[it&1].
 enum : uint32_t { kRun = 0, kDone = 1, kDead = 2, kStall = 3 };
-enum : uint32_t { kStallNone = 0, kStallDense = 1, kStallCap = 2, kStallHost = 3 };
+enum : uint32_t { kStallNone = 0, kStallDense = 1, kStallCap = 2, kStallHost = 3, kStallPipe = 4 };
 constexpr uint32_t kSeedBit = 4;                       // Ctl::sides of the seeding pseudo-round
 // plan_round flags: account only / run the stalled plan speculatively / run it
 // as a host-planned round / plan, then stall for the host (host-only mode)
-enum : int { kPlanAccountOnly = 1, kPlanResume = 2, kPlanForce = 4, kPlanStall = 8 };
+// ... / a pipelined plan (accounts the pending round psides, stalls on any
+// spill) / a drain (account the pending round exactly, then leave the pipeline)
+enum : int { kPlanAccountOnly = 1, kPlanResume = 2, kPlanForce = 4, kPlanStall = 8, kPlanPipe = 16, kPlanDrain = 32 };
+// A pipelined plan stalls (and the search continues with exact plans) once a
+// rank's frontier share passes this many edges: the next round's frontier,
+// which it cannot see yet, must stay far below the spill lists.
+constexpr uint64_t kPipeMaxEdges = 1u << 14;
 
 struct Ctl {
   unsigned long long cnt[2];   // current frontier sizes (vertices)
@@ -132,6 +138,13 @@ struct Ctl {
   uint32_t cont_due;           // sides whose level is incomplete (spilled candidates wait to be offered)
   uint32_t cont_rounds;        // continuation rounds run
   uint32_t lost;               // a rank's spill list overflowed (candidates dropped): the search failed
+  // Pipelined rounds (DistTuning::pipeline): the plan of round it is made
+  // before round it-1's claims are reduced, so it accounts round it-2.  The
+  // round planned last time, not accounted yet, is psides / pcont; xdepth is
+  // the depth of the frontier THIS round expands (= depth when nothing is
+  // pending) -- every expansion / claim kernel takes its depths from xdepth.
+  uint32_t psides, pcont;
+  uint32_t xdepth[2];
 };
 
 struct Policy {
@@ -163,7 +176,16 @@ struct Reduced {
   uint32_t spillmax[2];
   unsigned long long spill[2]; // candidates of side s that did not fit their owner's block (sum)
   unsigned long long nocmax;   // ~(largest candidate count this rank addressed to one owner): min = ~max
+  // pipelined rounds: candidates of side s that did not fit their owner's
+  // block in the round whose exchange carried this record (max) -- the level
+  // that round expanded is incomplete, so the next plan stalls and drains
+  uint32_t nsp[2];
 };
+// Pipelined rounds: every owner-addressed exchange carries, in front of each
+// peer's candidate blocks, the sender's reduction of the round before (its
+// `red` with nsp of this round): the round's ONE collective is the exchange.
+constexpr uint32_t kHdrWords = 32;
+static_assert(sizeof(Reduced) <= kHdrWords * 4, "reduction header");
 
 // One accounted round (SearchOptions::trace): the frontiers it expanded and
 // what they discovered -- the same record on every rank.
@@ -178,9 +200,9 @@ struct RoundRec {
 // the entry of the round's expansion launch(es) and of its claim launch, and
 // when their last workgroup finishes -- so the host can split a round into
 // kernel time and the gaps the exchanges (and launch latencies) leave between
-// the kernels.  eb1/ee1: the side-1 launch of a split (overlap) round.
+// the kernels.
 struct RoundStamp {
-  unsigned long long eb, ee, cb, ce, eb1, ee1;
+  unsigned long long eb, ee, cb, ce;
   // small rounds (block 0): expansion planned, frontier staged + scanned,
   // edges done; claim: candidates claimed
   unsigned long long ep, es, ex, cx;
@@ -200,8 +222,7 @@ struct DState {
   uint32_t spill_n[2][2];               // [side][list] spilled candidates held (owner-addressed rounds)
   uint32_t spill_cur[2];                // [side] the list holding the candidates still to be offered
   uint32_t ocmax;                       // largest per-owner candidate count of this round (the header writer)
-  uint32_t done_side[2];                // last-block detection of a one-side expansion launch (overlap)
-  uint32_t pad2;
+  uint32_t pad2[3];
 };
 
 struct DView {
@@ -254,6 +275,13 @@ __device__ __forceinline__ T* pick(T* const (&a)[2], int s) {
 }
 
 __host__ __device__ inline uint64_t block_words(uint32_t cap) { return 2 + 2 * (uint64_t)cap; }
+// Owner-addressed exchange (speculative rounds with more than one rank): one
+// region per peer o -- the reduction header, then o's side-0 and side-1
+// blocks of `ocap` pairs -- so ONE alltoall moves both sides and the header.
+__host__ __device__ inline uint64_t peer_words(uint32_t ocap) { return kHdrWords + 2 * block_words(ocap); }
+__host__ __device__ inline uint64_t oblock(int s, uint32_t o, uint32_t ocap) {
+  return (uint64_t)o * peer_words(ocap) + kHdrWords + (uint64_t)s * block_words(ocap);
+}
 
 // Copy a small struct into LDS, one 32-bit word per thread (the block's
 // threads issue the loads together).
@@ -278,6 +306,7 @@ __device__ void reduce_gathered(const Reduced* g, int P, Reduced& out) {
       r.maxsend[s] = max(r.maxsend[s], x.maxsend[s]);
       r.md[s] = min(r.md[s], x.md[s]);
       r.spillmax[s] = max(r.spillmax[s], x.spillmax[s]);
+      r.nsp[s] = max(r.nsp[s], x.nsp[s]);
     }
   }
   out = r;
@@ -304,12 +333,26 @@ __device__ __forceinline__ void plan_round(const Ctl& p, const Reduced& rd, cons
 }
 
 
-__device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd, const Policy& pol,
+__device__ __forceinline__ void plan_round_regs(const Ctl& p0, const Reduced& rd, const Policy& pol,
                                                 uint64_t spec_cap, int flags, Ctl& c) {
+  // A pipelined plan (and the drain that leaves the pipeline) accounts the
+  // PENDING round -- planned last time, its reduction arrived with the round
+  // planned after it -- not the round planned last time.  Terminal plans
+  // (no-op rounds past the end) account nothing.
+  const bool pipe = (flags & kPlanPipe) != 0;
+  Ctl p = p0;
+  if ((pipe && p0.state == kRun) || (flags & kPlanDrain)) {
+    p.sides = p0.psides;
+    p.cont = p0.pcont;
+    if (flags & kPlanDrain) p.state = kRun;  // the pipelined stall this drain answers
+  }
   c = p;
   c.sides = 0;
   c.modes = 0;
   c.cont = 0;
+  // the round planned now becomes the pending one (pipelined), or nothing is pending
+  c.psides = pipe ? p0.sides : 0u;
+  c.pcont = pipe ? p0.cont : 0u;
   uint32_t want = 0, wm = 0;
   if (p.state == kStall) {
     if (!(flags & (kPlanResume | kPlanForce))) return;  // stays stalled until the host acts
@@ -361,6 +404,8 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
         return;
       }
       c.cont_due = (rd.spill[0] ? 1u : 0u) | (rd.spill[1] ? 2u : 0u);
+      // (pipelined: a spilling round stalls the plan after it before any
+      // round is accounted with cont_due, so it is never set here)
       if (!c.cont_due) {
         if (c.pkey != kNoKey) {
           c.state = kDone;
@@ -374,7 +419,18 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
           if (c.cnt[s] == 0) c.state = kDead;
       }
     }
+    c.xdepth[0] = c.depth[0];
+    c.xdepth[1] = c.depth[1];
     if (c.state != kRun || (flags & kPlanAccountOnly)) return;
+    // Pipelined: the round planned last time left candidates unsent (its
+    // level is incomplete) -- stall; the host drains the pipeline (accounts
+    // that round exactly) and the search goes on with exact plans, which run
+    // the continuation round.
+    if (pipe && (rd.nsp[0] | rd.nsp[1] | c.cont_due)) {
+      c.state = kStall;
+      c.stall = kStallPipe;
+      return;
+    }
     if (c.cont_due) {  // the continuation round: no expansion, the spilled candidates offered again
       c.cont = c.cont_due;
       c.cont_due = 0;
@@ -425,10 +481,11 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
   if (!(flags & kPlanForce)) {
     bool fits = wm == 0;
     for (int s = 0; s < 2; ++s)
-      if (((want >> s) & 1) && c.fmax[s] > spec_cap) fits = false;  // a rank's block holds its share
+      if (((want >> s) & 1) && (c.fmax[s] > spec_cap || (pipe && c.fmax[s] > kPipeMaxEdges)))
+        fits = false;  // a rank's block holds its share
     if (!fits || (flags & kPlanStall)) {
       c.state = kStall;
-      c.stall = (flags & kPlanStall) ? kStallHost : (wm ? kStallDense : kStallCap);
+      c.stall = pipe ? kStallPipe : (flags & kPlanStall) ? kStallHost : (wm ? kStallDense : kStallCap);
       return;
     }
   }
@@ -436,6 +493,8 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
   c.stall = kStallNone;
   c.sides = want;
   c.modes = wm;
+  if (pipe)  // the pending round's output is this round's frontier
+    for (int s = 0; s < 2; ++s) c.xdepth[s] = c.depth[s] + ((p0.sides >> s) & 1u);
   for (int s = 0; s < 2; ++s)
     if ((want >> s) & 1) {
       c.einsp += c.fed[s];
@@ -443,13 +502,18 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p, const Reduced& rd,
     }
 }
 
-// Publish round `p`'s plan; with tracing on, also record the round it accounted.
-__device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& rd, const Ctl& c) {
+// Publish round `p`'s plan; with tracing on, also record the round it
+// accounted (pipelined plans and drains: the pending round psides / pcont,
+// always top-down).
+__device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& rd, const Ctl& c, bool pend = false) {
   V.ctl[p] = c;
-  if (V.trace && prev.sides && !(prev.sides & kSeedBit) && c.rounds >= 1 && c.rounds <= V.trace_cap) {
+  const bool live = prev.state == kRun || prev.state == kStall;
+  const uint32_t asides = pend ? (live ? prev.psides : 0u) : prev.sides;
+  const uint32_t acont = pend ? (live ? prev.pcont : 0u) : prev.cont;
+  if (V.trace && asides && !(asides & kSeedBit) && c.rounds >= 1 && c.rounds <= V.trace_cap) {
     RoundRec& t = V.trace[c.rounds - 1];
-    t.sides = prev.sides;
-    t.modes = prev.modes;
+    t.sides = asides;
+    t.modes = pend ? 0u : prev.modes;
     for (int s = 0; s < 2; ++s) {
       t.depth[s] = prev.depth[s];
       t.cnt[s] = prev.cnt[s];
@@ -457,7 +521,7 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
     }
     for (int k = 0; k < 4; ++k) t.sums[k] = rd.sums[k];
     t.meetkey = rd.meetkey;
-  } else if (V.trace && prev.cont && c.rounds >= 1 && c.rounds <= V.trace_cap) {
+  } else if (V.trace && acont && c.rounds >= 1 && c.rounds <= V.trace_cap) {
     RoundRec& t = V.trace[c.rounds - 1];  // a continuation adds to its round's record
     for (int k = 0; k < 4; ++k) t.sums[k] += rd.sums[k];
     t.meetkey = min(t.meetkey, rd.meetkey);
@@ -562,7 +626,7 @@ __device__ __forceinline__ void emit_owned_pair(const DView& V, int s, uint32_t 
   const uint32_t o = v / V.chunk;
   const uint32_t pos = atomicAdd(&V.ocount[s * V.P + o], 1u);
   if (pos < oe.cap) {
-    reinterpret_cast<uint2*>(V.sendbuf + ((size_t)s * V.P + o) * oe.bw)[1 + pos] = make_uint2(v, u);
+    reinterpret_cast<uint2*>(V.sendbuf + oblock(s, o, oe.cap))[1 + pos] = make_uint2(v, u);
   } else {
     // (a rank's candidates of a level never exceed the list while its frontier
     // edges stay within round_edge_cap(); if they ever do, the count still
@@ -572,16 +636,48 @@ __device__ __forceinline__ void emit_owned_pair(const DView& V, int s, uint32_t 
   }
 }
 
+// Pipelined rounds: the reduction header in front of every peer's blocks --
+// this rank's `red` of round it - 1 (final since that round's claim kernel)
+// with nsp = the candidates of round `it` that went to the spill lists.
+__device__ void write_peer_headers(const DView& V, uint32_t cap, uint32_t it, uint32_t nsp0, uint32_t nsp1) {
+  constexpr uint32_t kRedW = sizeof(Reduced) / 4, kNspW = offsetof(Reduced, nsp) / 4;
+  const uint32_t* red = reinterpret_cast<const uint32_t*>(&V.red[(it - 1u) & 1u]);
+  for (uint32_t t = threadIdx.x; t < (uint32_t)V.P * kHdrWords; t += blockDim.x) {
+    const uint32_t o = t / kHdrWords, w = t % kHdrWords;
+    const uint32_t x = w == kNspW ? nsp0 : w == kNspW + 1 ? nsp1 : w < kRedW ? red[w] : 0u;
+    V.sendbuf[(uint64_t)o * peer_words(cap) + w] = x;
+  }
+}
+
 // The last workgroup of a round's emitting kernel: every owner block's count
 // into its header, the counters reset, the largest per-owner count kept for
-// the host's sizing of the next blocks.
-__device__ void write_owner_headers(const DView& V, uint32_t cap, int side0 = 0, int nsides = 2) {
-  const uint64_t bw = block_words(cap);
-  for (uint32_t t = threadIdx.x; t < (uint32_t)nsides * V.P; t += blockDim.x) {
-    const uint32_t ss = side0 + t / V.P, o = t % V.P, k = ss * V.P + o;
+// the host's sizing of the next blocks; pipelined rounds also write the
+// reduction headers.
+__device__ void write_owner_headers(const DView& V, uint32_t cap, uint32_t it, int pipe) {
+  for (uint32_t t = threadIdx.x; t < 2u * V.P; t += blockDim.x) {
+    const uint32_t ss = t / V.P, o = t % V.P, k = ss * V.P + o;
     const uint32_t cnt = atomicExch(&V.ocount[k], 0u);
-    V.sendbuf[k * bw] = min(cnt, cap);
+    V.sendbuf[oblock((int)ss, o, cap)] = min(cnt, cap);
     if (cnt) atomicMax(&V.st->ocmax, cnt);
+  }
+  if (pipe) {
+    // the other blocks' spills are atomics completed before they counted in
+    const DState* st = V.st;
+    const uint32_t n0 = __hip_atomic_load(&st->spill_n[0][st->spill_cur[0]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t n1 = __hip_atomic_load(&st->spill_n[1][st->spill_cur[1]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    write_peer_headers(V, cap, it, n0, n1);
+  }
+}
+
+// Pipelined rounds, claim kernel: every peer's header -- its reduction of
+// round it - 1 -- into the gathered slot of that round (what the round's
+// separate allgather delivers in exact mode), read by the plan of round it + 1.
+__device__ void scatter_peer_headers(const DView& V, uint32_t cap, uint32_t it) {
+  constexpr uint32_t kRedW = sizeof(Reduced) / 4;
+  uint32_t* g = reinterpret_cast<uint32_t*>(V.redg[(it - 1u) & 1u]);
+  for (uint32_t t = threadIdx.x; t < (uint32_t)V.P * kRedW; t += blockDim.x) {
+    const uint32_t r = t / kRedW, w = t % kRedW;
+    g[t] = V.recvbuf[(uint64_t)r * peer_words(cap) + w];
   }
 }
 
@@ -829,8 +925,8 @@ struct SmallStage {
 };
 __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S, uint32_t t, uint32_t nt);
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
-                             SmallStage& S, RoundStamp* rs, int only = -1);
-__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs);
+                             SmallStage& S, RoundStamp* rs, int pipe);
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs, int pipe);
 __device__ __forceinline__ bool small_expand_ok(const Ctl& c, int P) {
   if (c.cont || !c.sides || P > kStageRanks) return false;
   for (int s = 0; s < 2; ++s)
@@ -853,11 +949,16 @@ __device__ __forceinline__ RoundStamp* round_stamp(const DView& V, uint32_t it) 
 // pre phase of both sides (blockIdx.y = side) into blocks of `cap` pairs.
 // header = 0: k_td_hubs runs next (it writes the headers); finish: this
 // kernel ends the round's claims on this rank (one rank, no hub pass).
+// pipe: a pipelined round (more than one rank, DistTuning::pipeline) -- the
+// plan accounts the pending round from the reductions the last exchange
+// carried (gathered slot it & 1; round 0 plans exactly from the seed), and
+// the exchange of this round carries this rank's reduction of the last one.
 __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, Policy pol, uint32_t cap,
                                                           int flags, uint64_t hub_deg, int header, int finish,
-                                                          uint32_t ocap, int side0, int nsides, uint32_t plan_cap) {
+                                                          uint32_t ocap, uint32_t plan_cap, int pipe) {
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   const int p = it & 1;
+  const bool pplan = pipe && it > 0;  // a pipelined plan (round 0: the seed, exact)
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
   __shared__ uint32_t fr[4];  // frontier bounds: fbeg[2], fend[2]
@@ -865,8 +966,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // with one round of parallel loads (thread 0 alone would chain them
   // through plan_round's branches)
   stage_words(&prev, &V.ctl[p ^ 1], sizeof(Ctl));
+  const Reduced* const gsrc = V.redg[pplan ? p : p ^ 1];
   __shared__ Reduced gst[kStageRanks];
-  if (V.P <= kStageRanks) stage_words(gst, V.redg[p ^ 1], (size_t)V.P * sizeof(Reduced));
+  if (V.P <= kStageRanks) stage_words(gst, gsrc, (size_t)V.P * sizeof(Reduced));
   if (threadIdx.x >= kThreads - 4) {
     const uint32_t k = threadIdx.x - (kThreads - 4);
     fr[k] = k < 2 ? V.st->fbeg[k] : V.st->fend[k - 2];
@@ -879,11 +981,10 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
       // (two call sites, not one through a conditional pointer: that made every
       // load of the planner's inputs a flat load)
       if (V.P <= kStageRanks) reduce_gathered(gst, V.P, rd);
-      else reduce_gathered(V.redg[p ^ 1], V.P, rd);
-      plan_round(prev, rd, pol, plan_cap, flags, c);
+      else reduce_gathered(gsrc, V.P, rd);
+      plan_round(prev, rd, pol, plan_cap, flags | (pplan ? kPlanPipe : 0), c);
     }
-  } else if (threadIdx.x >= kWave && ocap && header && nsides == 2 && V.P <= kStageRanks && blockIdx.x == 0 &&
-             blockIdx.y == 0) {
+  } else if (threadIdx.x >= kWave && ocap && header && V.P <= kStageRanks && blockIdx.x == 0 && blockIdx.y == 0) {
     small_prefetch(V, fr, sm, threadIdx.x - kWave, kThreads - kWave);  // (a no-op unless the round is small)
   }
   __syncthreads();
@@ -892,9 +993,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // row, so the plan publication (its system-scope stores and fence, several
   // microseconds on one lane) never delays block (0, 0), which runs a small
   // round's whole expansion (small_expand).
-  const bool planner = blockIdx.x == 0 && blockIdx.y == (gridDim.y > 1 ? 1u : 0u) && side0 == 0;
+  const bool planner = blockIdx.x == 0 && blockIdx.y == (gridDim.y > 1 ? 1u : 0u);
   if (planner && threadIdx.x < kWave) {
-    if (threadIdx.x == 0) publish(V, p, prev, rd, c);
+    if (threadIdx.x == 0) publish(V, p, prev, rd, c, pplan);
     // the round that ends the search hands the host its accounted Ctl directly
     // (no k_final launch + wait after the batch); later no-op rounds repeat it
     const bool first_end = terminal && prev.state == kRun;
@@ -926,32 +1027,27 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // end (every block sees the same plan, so no block counts itself in)
   if (terminal) return;
   if (RoundStamp* rs = round_stamp(V, it); rs && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    if (side0 == 0) {
-      rs->eb = t_in;
-      rs->tag = plan_tag(pol.epoch, it);
-      rs->small = 0;
-      if (nsides == 2) rs->eb1 = rs->ee1 = 0;
-    } else {
-      rs->eb1 = t_in;
-    }
+    rs->eb = t_in;
+    rs->tag = plan_tag(pol.epoch, it);
+    rs->small = 0;
   }
-  // small round: one workgroup (an overlap round's one-side launch: one per side)
+  // small round: one workgroup
   if (ocap && header && small_expand_ok(c, V.P)) {
     if (blockIdx.x == 0 && blockIdx.y == 0) {
-      if (RoundStamp* rs = round_stamp(V, it); rs && threadIdx.x == 0 && side0 == 0) {
+      if (RoundStamp* rs = round_stamp(V, it); rs && threadIdx.x == 0) {
         rs->ep = __builtin_amdgcn_s_memrealtime();
         rs->sg = t_staged;
         rs->small = 1;
       }
-      small_expand(V, c, it, ocap, fr, sm, side0 == 0 ? round_stamp(V, it) : nullptr, nsides == 2 ? -1 : side0);
+      small_expand(V, c, it, ocap, fr, sm, round_stamp(V, it), pipe);
       if (RoundStamp* rs = round_stamp(V, it)) {
         __syncthreads();
-        if (threadIdx.x == 0) (side0 == 0 ? rs->ee : rs->ee1) = __builtin_amdgcn_s_memrealtime();
+        if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
       }
     }
     return;
   }
-  const int s = side0 + (int)blockIdx.y;
+  const int s = (int)blockIdx.y;
   OwnerEmit oe;
   if (ocap) {
     const uint32_t cur = V.st->spill_cur[s], tgt = ((c.cont >> s) & 1) ? cur ^ 1 : cur;
@@ -963,10 +1059,10 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   if ((c.sides >> s) & 1) {
     ClaimMeet cm;
     cm.meetkey = &V.red[p].meetkey;
-    cm.dclaim = c.depth[s ^ 1] + 1;  // (only a claim of the other side this round reads kEmpty)
+    cm.dclaim = c.xdepth[s ^ 1] + 1;  // (only a claim of the other side this round reads kEmpty)
     cm.single = c.sides != 3u;
     cm.precheck = c.fed[s] > kPrecheckEdges;
-    td_expand_side(V, s, c.depth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
+    td_expand_side(V, s, c.xdepth[s] + 1, reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1, cap,
                    blockIdx.x, gridDim.x, hub_deg, c.sides != 3u, cm, fr[s], fr[2 + s] - fr[s], oe);
   } else if (ocap && ((c.cont >> s) & 1)) {
     // a continuation: the candidates of this side's level that did not fit
@@ -981,10 +1077,10 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   }
   if (!header) return;  // k_td_hubs runs next and writes the headers
   if (finish) drain_atomics();
-  uint32_t* done = nsides == 2 ? &V.st->done_blocks[0] : &V.st->done_side[side0];
+  uint32_t* done = &V.st->done_blocks[0];
   if (last_block(done, gridDim.x * gridDim.y)) {
     if (ocap) {
-      write_owner_headers(V, ocap, side0, nsides);
+      write_owner_headers(V, ocap, it, pipe);
       if (threadIdx.x == 0) atomicExch(done, 0u);
     } else if (threadIdx.x < 2) {
       const int ss = threadIdx.x;
@@ -995,11 +1091,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     if (finish && threadIdx.x == kWave) spec_round_end(V, it, c.sides, c.cont);  // another wave: the header atomics are independent
     if (RoundStamp* rs = round_stamp(V, it)) {
       __syncthreads();
-      if (threadIdx.x == 0) {
-        const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-        if (side0 == 0) rs->ee = t;
-        else rs->ee1 = t;
-      }
+      if (threadIdx.x == 0) rs->ee = __builtin_amdgcn_s_memrealtime();
     }
   }
 }
@@ -1385,7 +1477,6 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
     st->new_edges[sd] = 0;
   }
   st->done_blocks[0] = st->done_blocks[1] = st->done_blocks[2] = 0;
-  st->done_side[0] = st->done_side[1] = 0;
   st->meet_found = 0;
   V.ctl[p ^ 1] = pc;  // round it - 1, executed, and its reduction
   V.red[p ^ 1] = rd;
@@ -1505,10 +1596,8 @@ __device__ void small_scan(uint32_t* X, uint32_t cnt) {
 // LDS.  Wave-cooperative (every lane calls it); the side is per lane, so one
 // call serves both sides of a lockstep round.  dcl[s]: the depth a claim of
 // the other side made in THIS round has (its depth store may not be visible).
-// kAgent: the claim's atomicOr at agent scope -- a one-side expansion of an
-// overlap round, while the other side's launch may claim in the same words
-// from another XCD; one workgroup alone keeps it at workgroup scope (its L2).
-template <bool kAgent = false>
+// One workgroup alone claims in these words during the launch: workgroup
+// scope (its L2) is enough, the kernel boundary publishes them.
 __device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const uint32_t* qbase, bool want, int s,
                                             uint32_t v, uint32_t u, const uint32_t* dn, const uint32_t* dcl,
                                             bool single) {
@@ -1520,9 +1609,7 @@ __device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const u
     const unsigned long long m = 1ull << ((li & 31) + 32 * s);
     // the row bounds are loaded beside the claim (independent of its result:
     // one dependent round trip fewer; a loser's load is wasted)
-    const unsigned long long old =
-        kAgent ? __hip_atomic_fetch_or(visw + (li >> 5), m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-               : wg_fetch_or(visw + (li >> 5), m);
+    const unsigned long long old = wg_fetch_or(visw + (li >> 5), m);
     rb = V.row_off[li];
     re = V.row_off[li + 1];
     mine = !(old & m);
@@ -1577,7 +1664,7 @@ __device__ __forceinline__ void small_emit(const DView& V, SmallCtr& K, const ui
   const uint32_t o = v / V.chunk;
   const uint32_t pos = atomicAdd(&K.oc[s][o], 1u);
   if (pos < ocap) {
-    reinterpret_cast<uint2*>(V.sendbuf + ((size_t)s * V.P + o) * block_words(ocap))[1 + pos] = make_uint2(v, u);
+    reinterpret_cast<uint2*>(V.sendbuf + oblock(s, o, ocap))[1 + pos] = make_uint2(v, u);
   } else {
     const uint32_t q = (s ? spbase[1] : spbase[0]) + atomicAdd(&K.sp[s], 1u);
     if (q < V.spill_cap) V.spill[s][s ? lst[1] : lst[0]][q] = make_uint2(v, u);  // past it: Ctl::lost (plan_round)
@@ -1618,10 +1705,9 @@ __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S
   }
 }
 
-// only >= 0: an overlap round's one-side launch -- that side alone (the other
-// side's launch runs beside it), claims at agent scope, only its headers.
+// pipe: the round's exchange also carries this rank's reduction header.
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
-                             SmallStage& S, RoundStamp* rs, int only) {
+                             SmallStage& S, RoundStamp* rs, int pipe) {
   __shared__ SmallCtr K;
   uint32_t* const su = S.su;
   unsigned long long* const sb = S.sb;
@@ -1629,8 +1715,8 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
   const uint32_t tid = threadIdx.x;
   const int p = it & 1;
   DState* st = V.st;
-  const uint32_t mine_sides = only < 0 ? c.sides : (c.sides & (1u << only));
-  if (only >= 0 || !S.valid) {  // (a big idle side, or one side of an overlap round): stage the expanding sides only
+  const uint32_t mine_sides = c.sides;
+  if (!S.valid) {  // (a big idle side): stage the expanding sides only
     const uint32_t F0 = (mine_sides & 1) ? fr[2] - fr[0] : 0u, F1 = (mine_sides & 2) ? fr[3] - fr[1] : 0u;
     if (tid == 0) {
       S.n0 = F0;
@@ -1676,8 +1762,8 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
   small_scan(se, nv);
   if (rs && tid == 0) rs->es = __builtin_amdgcn_s_memrealtime();
   const uint32_t E = se[nv];
-  const uint32_t dn[2] = {c.depth[0] + 1, c.depth[1] + 1};
-  const uint32_t dcl[2] = {c.depth[1] + 1, c.depth[0] + 1};  // (only this round's claims of the other side read kEmpty)
+  const uint32_t dn[2] = {c.xdepth[0] + 1, c.xdepth[1] + 1};
+  const uint32_t dcl[2] = {c.xdepth[1] + 1, c.xdepth[0] + 1};  // (only this round's claims of the other side read kEmpty)
   const bool single = c.sides != 3u;
   for (uint32_t base = 0; base < E; base += kThreads * kSmallU) {  // block-uniform trip count
     uint32_t vv[kSmallU], uu[kSmallU];
@@ -1704,25 +1790,23 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
 #pragma unroll
     for (int k = 0; k < kSmallU; ++k) {
       const bool own = ok[k] && vv[k] >= V.lo && vv[k] < V.hi;
-      if (only >= 0) small_claim<true>(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
-      else small_claim(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
+      small_claim(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
       small_emit(V, K, spbase, lst, ok[k] && !own, ss[k], vv[k], uu[k], ocap);
     }
   }
   __syncthreads();
   if (rs && tid == 0) rs->ex = __builtin_amdgcn_s_memrealtime();
-  // owner headers of its sides (count capped to the block), the round's state
-  const uint64_t bw = block_words(ocap);
+  // owner headers (count capped to the block), the reduction headers of a
+  // pipelined round, the round's state
   for (uint32_t t = tid; t < 2u * V.P; t += kThreads) {
     const uint32_t s = t / V.P, o = t % V.P;
-    if (only >= 0 && (int)s != only) continue;
     const uint32_t cnt = K.oc[s][o];
-    V.sendbuf[((uint64_t)s * V.P + o) * bw] = min(cnt, ocap);
+    V.sendbuf[oblock((int)s, o, ocap)] = min(cnt, ocap);
     if (cnt) atomicMax(&st->ocmax, cnt);
   }
+  if (pipe) write_peer_headers(V, ocap, it, spbase[0] + K.sp[0], spbase[1] + K.sp[1]);
   if (tid == 0) {
     for (int s = 0; s < 2; ++s) {
-      if (only >= 0 && s != only) continue;
       st->qtail[s] = qbase[s] + K.q[s];
       st->new_edges[s] += K.ne[s];
       st->spill_n[s][lst[s]] = spbase[s] + K.sp[s];
@@ -1735,7 +1819,7 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
 // The claims of a small round by block (0, 0) of k_spec_claim: every sender's
 // block of both sides, then the round's end (spec_round_end's bookkeeping,
 // from the LDS counters -- one thread, plain accesses).
-__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs) {
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs, int pipe) {
   __shared__ uint32_t cnt[2 * kStageRanks + 1];
   __shared__ SmallCtr K;
   __shared__ uint32_t qbase[2], fend0[2], spn[2], ocm;
@@ -1744,7 +1828,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
   const int p = it & 1;
   const int P = V.P;
   DState* st = V.st;
-  const uint64_t bw = block_words(cap);
+  if (pipe) scatter_peer_headers(V, cap, it);
   if (tid < 2) {
     qbase[tid] = st->qtail[tid];
     K.q[tid] = 0;
@@ -1764,7 +1848,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
   // item space: side 0's P blocks, then side 1's (a side that did not expand: 0)
   if (tid < 2u * P) {
     const uint32_t s = tid / P;
-    cnt[tid] = ((c.sides >> s) & 1) ? min(V.recvbuf[(uint64_t)tid * bw], cap) : 0u;
+    cnt[tid] = ((c.sides >> s) & 1) ? min(V.recvbuf[oblock((int)s, tid % P, cap)], cap) : 0u;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1778,9 +1862,9 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
   }
   __syncthreads();
   const uint32_t tot = cnt[2 * P];
-  const uint32_t dn[2] = {c.depth[0] + 1, c.depth[1] + 1};
-  const uint32_t dcl[2] = {((c.sides >> 1) & 1) ? c.depth[1] + 1 : c.depth[1],
-                           (c.sides & 1) ? c.depth[0] + 1 : c.depth[0]};
+  const uint32_t dn[2] = {c.xdepth[0] + 1, c.xdepth[1] + 1};
+  const uint32_t dcl[2] = {((c.sides >> 1) & 1) ? c.xdepth[1] + 1 : c.xdepth[1],
+                           (c.sides & 1) ? c.xdepth[0] + 1 : c.xdepth[0]};
   const bool single = c.sides != 3u;
   for (uint32_t base = 0; base < tot; base += kThreads * kSmallU) {
     uint2 x[kSmallU];
@@ -1800,7 +1884,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
           else z = mid;
         }
         ss[k] = (int)(a / P);
-        x[k] = reinterpret_cast<const uint2*>(V.recvbuf + (uint64_t)a * bw)[1 + (i - cnt[a])];
+        x[k] = reinterpret_cast<const uint2*>(V.recvbuf + oblock((int)(a / P), a % P, cap))[1 + (i - cnt[a])];
       }
     }
 #pragma unroll
@@ -1845,7 +1929,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
 // of hubs with their degree prefix in LDS and walks the tile's flattened edge
 // range with a grid stride, so each hub's edges spread over all CUs.
 __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int side, uint32_t dnew_fixed,
-                                                      uint32_t cap, int single, int finish, uint32_t ocap) {
+                                                      uint32_t cap, int single, int finish, uint32_t ocap, int pipe) {
   __shared__ uint32_t hu[kHubTile];
   __shared__ unsigned long long hb[kHubTile], hp[kHubTile + 1];
   __shared__ unsigned long long wsum[kThreads / kWave];
@@ -1855,7 +1939,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
     const Ctl& c = V.ctl[it & 1];
     if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
     sides = c.sides;
-    dnew = c.depth[s] + 1;
+    dnew = c.xdepth[s] + 1;
   }
   const uint32_t H = V.st->hub_count[s];
   uint2* pairs = reinterpret_cast<uint2*>(V.sendbuf + s * block_words(cap)) + 1;
@@ -1866,7 +1950,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   OwnerEmit oe;
   if (side < 0) {
     cm.meetkey = &V.red[it & 1].meetkey;
-    cm.dclaim = V.ctl[it & 1].depth[s ^ 1] + 1;
+    cm.dclaim = V.ctl[it & 1].xdepth[s ^ 1] + 1;
     if (ocap) {  // (a continuation round has no hubs: the expanding side's list)
       const uint32_t cur = V.st->spill_cur[s];
       oe.cap = ocap;
@@ -1949,7 +2033,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   if (finish) drain_atomics();
   if (last_block(&V.st->done_blocks[2], gridDim.x * gridDim.y)) {
     if (ocap) {
-      write_owner_headers(V, ocap);
+      write_owner_headers(V, ocap, it, pipe);
       if (threadIdx.x == 0) atomicExch(&V.st->done_blocks[2], 0u);
     } else if (threadIdx.x < 2) {
       const int ss = threadIdx.x;
@@ -1966,10 +2050,11 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
 }
 
 // Post phase of both sides: owners claim the candidates addressed to them
-// (rank r's side-s block is recvbuf[(2r + s) * block_words(cap)]).
+// (rank r's side-s block at recvbuf + oblock(s, r, cap)).
 // (more than one rank: this kernel ends the round's claims; its last
-// workgroup closes the round)
-__global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap) {
+// workgroup closes the round.  pipe: block (0, 0) also moves the reduction
+// headers the exchange carried into the gathered slot of round it - 1.)
+__global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap, int pipe) {
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   const Ctl& c = V.ctl[it & 1];
   if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
@@ -1978,7 +2063,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   if (small_claim_ok(c, V.P)) {  // small round: one workgroup claims and closes it
     if (blockIdx.x == 0 && blockIdx.y == 0) {
       if (rs && threadIdx.x == 0) rs->small |= 2u;
-      small_claim_round(V, c, it, cap, rs);
+      small_claim_round(V, c, it, cap, rs, pipe);
       if (rs) {
         __syncthreads();
         if (threadIdx.x == 0) rs->ce = __builtin_amdgcn_s_memrealtime();
@@ -1987,14 +2072,15 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
     return;
   }
   const int s = blockIdx.y;
+  if (pipe && blockIdx.x == 0 && s == 0) scatter_peer_headers(V, cap, it);
   // a continuation side claims at the depth its level already has
-  const uint32_t dnew = ((c.sides >> s) & 1) ? c.depth[s] + 1 : c.depth[s];
+  const uint32_t dnew = ((c.sides >> s) & 1) ? c.xdepth[s] + 1 : c.xdepth[s];
   ClaimMeet cm;
   cm.meetkey = &V.red[it & 1].meetkey;
-  cm.dclaim = ((c.sides >> (s ^ 1)) & 1) ? c.depth[s ^ 1] + 1 : c.depth[s ^ 1];
+  cm.dclaim = ((c.sides >> (s ^ 1)) & 1) ? c.xdepth[s ^ 1] + 1 : c.xdepth[s ^ 1];
   cm.single = c.sides != 3u;
   for (int r = 0; (((c.sides | c.cont) >> s) & 1) && r < V.P; ++r) {  // block-uniform
-    const uint32_t* b = V.recvbuf + ((uint64_t)s * V.P + r) * block_words(cap);
+    const uint32_t* b = V.recvbuf + oblock(s, (uint32_t)r, cap);
     const uint32_t cnt = min(b[0], cap);
     const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
     for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < cnt; base += (uint64_t)gridDim.x * kThreads) {
@@ -2077,10 +2163,13 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags, 
   const int p = it & 1;
   Ctl c;
   Reduced rd;
-  reduce_gathered(V.redg[p ^ 1], V.P, rd);
+  // (a drain: the pending round's reduction came with the stalled round's
+  // exchange, into the gathered slot of round it - 2)
+  const bool drain = (flags & kPlanDrain) != 0;
+  reduce_gathered(drain ? V.redg[p] : V.redg[p ^ 1], V.P, rd);
   plan_round(V.ctl[p ^ 1], rd, pol, 0, flags, c);
   c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
-  publish(V, p, V.ctl[p ^ 1], rd, c);
+  publish(V, p, V.ctl[p ^ 1], rd, c, drain);
   V.red[p ^ 1].meetkey = kNoKey;  // read; it is the buffer of the next round (it + 1)
   *host = c;
   __threadfence_system();
@@ -2238,6 +2327,8 @@ __global__ void k_seed(DView V, uint32_t src, uint32_t dst) {
     st->spill_cur[s] = 0;
     r.spill[s] = 0;
     r.spillmax[s] = 0;
+    r.nsp[s] = 0;
+    V.red[0].nsp[s] = 0;  // (only exchange headers carry nsp: a gathered copy of red must read 0)
     r.sums[2 * s] = r.sums[2 * s + 1] = 0;
     const uint32_t v = s ? dst : src;
     if (v >= V.lo && v < V.hi) {
@@ -2556,6 +2647,7 @@ struct DistBiBfs::Impl {
   DistLevelStats stats;
   DistTuning tune;
   bool source_only = false;  // the search in progress is search_unidirectional's
+  bool pipe_off = false;     // the search in progress runs exact plans (a pipelined attempt overflowed)
   // World size 1 (DistTuning::world1_single): the rank's shard is the whole
   // graph, so queries go to the single-GPU engine over the same device CSR
   // (adopted, not copied) with its resident server; the partitioned rounds
@@ -2687,7 +2779,8 @@ struct DistBiBfs::Impl {
       o_gb[s] = take(words * 4 * size);
     }
     // send: one block per side, or (owner-addressed rounds) one per side and owner
-    const size_t o_send = take(2 * block * 4 * size), o_recv = take(2 * block * 4 * size);
+    // (owner-addressed rounds: per peer a reduction header and two blocks)
+    const size_t o_send = take((kHdrWords + 2 * block) * 4 * size), o_recv = take((kHdrWords + 2 * block) * 4 * size);
     const size_t o_ocount = take(2 * (size_t)size * 4);
     size_t o_spill[2][2];
     for (int s = 0; s < 2; ++s)
@@ -2992,13 +3085,13 @@ struct DistBiBfs::Impl {
       const RoundStamp& x = ring[i % kTraceCap];
       if (x.tag != plan_tag(epoch, i) || !x.eb || !x.ee) continue;
       stats.stamped_rounds++;
-      const unsigned long long ee = std::max(x.ee, x.ee1);
-      stats.expand_us += us(x.eb, x.ee) + (x.eb1 ? us(x.eb1, x.ee1) : 0.0);
+      const unsigned long long ee = x.ee;
+      stats.expand_us += us(x.eb, x.ee);
       if (x.cb && x.ce && x.cb >= x.eb) {
         stats.claim_us += us(x.cb, x.ce);
         stats.exchange_us += us(ee, x.cb);
       }
-      if (prev && prev_it + 1 == i) stats.status_us += us(prev->ce ? prev->ce : std::max(prev->ee, prev->ee1), x.eb);
+      if (prev && prev_it + 1 == i) stats.status_us += us(prev->ce ? prev->ce : prev->ee, x.eb);
       if (x.small & 1) {
         stats.small_expand_rounds++;
         stats.sx_plan_us += us(x.eb, x.ep);
@@ -3051,7 +3144,7 @@ void DistBiBfs::Impl::host_round(uint32_t it, const Policy& pol, SearchResult& r
       k_td_expand<<<fblocks, kThreads, 0, ps>>>(V, s, dnew, hubs ? kHubDeg : kNoHubs, ns == 1);
       if (hubs)
         k_td_hubs<<<blocks_for(std::min<uint64_t>(h.fed[s], (uint64_t)cus * 8 * kThreads), cus), kThreads, 0, ps>>>(
-            V, it, s, dnew, capr, ns == 1, 0, 0);
+            V, it, s, dnew, capr, ns == 1, 0, 0, 0);
       k_send_header<<<1, 64, 0, ps>>>(V, s, it);
     } else {
       HIP_CHECK(hipMemsetAsync(V.obits[s], 0, (size_t)words * 4, ps));
@@ -3177,6 +3270,13 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   bool have_ctl = false;  // h_ctl describes the current device state
   const int K = std::min<int>(std::max(0, tune.spec_rounds), (int)kPlanRing - 1);
   const bool host_only = K == 0;  // A/B mode: every round planned on the host
+  // Pipelined rounds (DistTuning::pipeline, more than one rank): the round's
+  // reduction travels with the next round's candidate exchange -- ONE
+  // collective per round -- and each plan accounts the round before the last
+  // one.  The first stall (a spill, a big or dense frontier) drains the
+  // pipeline and the search continues with exact plans.
+  bool pipe = P > 1 && tune.pipeline && !host_only && !pipe_off;
+  bool pipe_used = pipe;
   const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
   if (host_only) {
     final_and_wait(it++, pol, kPlanStall, cs);
@@ -3255,8 +3355,10 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         const uint64_t f = w >> 32;
         uint64_t g = 2;  // growth per round; x2 until two plans are seen
         if (f_prev) g = std::min<uint64_t>(8, std::max<uint64_t>(1, (f + f_prev - 1) / f_prev));
+        // (a pipelined plan's frontier is one round older: one more round of growth)
+        const int lag = pipe ? 1 : 0;
         uint64_t pred = f;
-        for (int j = 0; j < K && pred < spec_max; ++j) pred *= g;
+        for (int j = 0; j < K + lag && pred < spec_max; ++j) pred *= g;
         cap_it = std::max<uint32_t>(cap_it, std::min<uint32_t>(spec_max, next_pow2(std::min<uint64_t>(pred + pred / 2, spec_max))));
         f_prev = f;
         // owner blocks: the largest per-owner count of round need - 1, grown
@@ -3264,7 +3366,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         // costs a continuation round, too big only bytes
         const uint64_t om = __atomic_load_n(&h_aux[need % kPlanRing], __ATOMIC_ACQUIRE);
         uint64_t op = om;
-        for (int j = 0; j <= K && op < cap_it; ++j) op *= g;
+        for (int j = 0; j <= K + lag && op < cap_it; ++j) op *= g;
         ocap = std::min<uint32_t>(cap_it, std::max<uint32_t>(kOwnerCapMin, next_pow2(op + op / 2 + 16)));
       }
       if (P == 1) ocap = 0;  // nothing is ever offered
@@ -3275,7 +3377,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       const unsigned bx = std::min<unsigned>((unsigned)cus * 2, cap_it / kThreads + 1);  // ~ this rank's edges
       const unsigned cx = std::min<unsigned>((unsigned)cus * 2,
                                              std::max<unsigned>(1, (uint32_t)P * ocap / kThreads / 4 + 1));
-      const uint64_t peer_bytes = block_words(ocap) * 4;  // one side's block for one owner
+      const uint64_t peer_bytes = peer_words(ocap) * 4;  // header + both sides' blocks for one owner
       // With blocks of at most kSpecHubCap pairs a frontier vertex has at most
       // that many edges: one workgroup walks them in <= 16 steps, no hub pass.
       const bool hubs = cap_it > kSpecHubCap && max_deg > kHubDeg;
@@ -3285,50 +3387,32 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       // claim time): the claim kernel with more than one rank, else the hub
       // pass or the expansion itself -- no separate meet / round-end kernel.
       const int end_in_expand = (P == 1 && !hubs) ? 1 : 0;
-      // Owner-addressed exchange, one alltoall per side (block (s, o) at
-      // sendbuf + (s P + o) * block_words): each rank receives only the
-      // blocks addressed to it.  With DistTuning::overlap the two sides
-      // expand as separate launches -- side 1 on the compute stream -- so
-      // side 0's exchange runs while side 1 is still expanding.
-      const uint64_t side_words = (uint64_t)P * block_words(ocap);
       // The plan stalls a round whose per-rank frontier edges exceed this:
       // with one rank nothing is exchanged, so nothing bounds a round; with
       // more, a rank's candidates (at most its frontier edges) must fit the
       // spill lists (owner blocks overflow into them).
       const uint32_t plan_cap = round_edge_cap();
-      const bool split = P > 1 && tune.overlap && !hubs;
-      if (split) {
-        HIP_CHECK(hipEventRecord(ev_round, cs));  // the previous round is complete on cs
-        HIP_CHECK(hipStreamWaitEvent(stream, ev_round, 0));
-        k_spec_expand<<<dim3(bx, 1), kThreads, 0, stream>>>(V, it, pol, cap_it, k == 0 ? flags : 0, kNoHubs, 1, 0,
-                                                            ocap, 1, 1, plan_cap);
-        HIP_CHECK(hipEventRecord(ev_pre[1], stream));
-        k_spec_expand<<<dim3(bx, 1), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0, kNoHubs, 1, 0,
-                                                        ocap, 0, 1, plan_cap);
+      const int pp = pipe ? 1 : 0;
+      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
+                                                      hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap,
+                                                      plan_cap, pp);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap, pp);
+      HIP_CHECK(hipGetLastError());
+      if (P > 1) {
+        // Owner-addressed exchange: ONE alltoall moves, per peer, the
+        // reduction header and both sides' candidate blocks (oblock); each
+        // rank receives only what is addressed to it.  Pipelined, the header
+        // is the round's status too: no second collective.
         comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
-        HIP_CHECK(hipStreamWaitEvent(cs, ev_pre[1], 0));
-        comm->alltoall(V.sendbuf + side_words, V.recvbuf + side_words, peer_bytes, cs);
-      } else {
-        k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
-                                                        hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap,
-                                                        0, 2, plan_cap);
-        if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap);
-        if (P > 1) {
-          comm->group_begin();
-          comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
-          comm->alltoall(V.sendbuf + side_words, V.recvbuf + side_words, peer_bytes, cs);
-          comm->group_end();
+        k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, ocap, pp);
+        HIP_CHECK(hipGetLastError());
+        stats.collectives++;
+        stats.exchanged_bytes += peer_bytes * (P - 1);
+        if (!pipe) {  // exact plans: the round's reduction, every rank's values gathered, reduced by the reader
+          comm->allgather(&V.red[it & 1], V.redg[it & 1], sizeof(Reduced), cs);
+          stats.collectives++;
+          stats.exchanged_bytes += sizeof(Reduced) * (P - 1);
         }
-      }
-      HIP_CHECK(hipGetLastError());
-      if (P > 1) {  // one rank owns every vertex: expand claimed them all, nothing to exchange
-        k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, ocap);
-      }
-      HIP_CHECK(hipGetLastError());
-      if (P > 1) {  // the round's reduction: every rank's values gathered, reduced by the reader
-        comm->allgather(&V.red[it & 1], V.redg[it & 1], sizeof(Reduced), cs);
-        stats.collectives += 2;  // the candidate exchange + this one
-        stats.exchanged_bytes += 2 * peer_bytes * (P - 1) + sizeof(Reduced) * (P - 1);
       }
       stats.spec_rounds++;
       ++it;
@@ -3344,13 +3428,39 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       ++it;
       break;
     }
-    final_and_wait(it++, pol, kPlanAccountOnly, cs);
+    if (pipe && seen_state == kStall) {
+      // drain: the stalled pipelined plan is replaced by the exact account of
+      // the round it left pending (its reduction arrived with the stalled
+      // round's exchange); from here on every plan is exact
+      final_and_wait(it++, pol, kPlanAccountOnly | kPlanDrain, cs);
+      pipe = false;
+      stats.pipe_drains++;
+    } else {
+      final_and_wait(it++, pol, kPlanAccountOnly, cs);
+    }
     if (h_ctl->state == kRun) {  // size the next batch for the frontier we have now
       const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
       spec_cap = std::min(spec_max, std::max<uint32_t>(spec_cap, next_pow2(4 * fm)));
     }
   }
   const Ctl h = *h_ctl;
+  if (h.lost && pipe_used) {
+    // a pipelined round ran on a frontier its plan could not see yet and
+    // overflowed the spill lists: every rank saw it (reduced values), so
+    // every rank answers the query again with exact plans
+    cleanup_enqueue(h);
+    pipe_off = true;
+    SearchResult again;
+    try {
+      again = search(src, dst, opt);
+    } catch (...) {
+      pipe_off = false;
+      throw;
+    }
+    pipe_off = false;
+    stats.pipe_retries++;
+    return again;
+  }
   if (h.lost) {
     // every rank decided `lost` from the same reduced values, so every rank
     // throws here, after the same collectives: the communicator stays usable

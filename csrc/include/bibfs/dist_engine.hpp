@@ -71,6 +71,8 @@ struct DistLevelStats {
   int path_collectives = 0;        // collectives spent reconstructing the path
   int solo_rounds = 0;             // rounds run by the one-workgroup solo kernel (one rank)
   int cont_rounds = 0;             // continuation rounds: candidates that overflowed an owner block re-offered
+  int pipe_drains = 0;             // pipelined searches that stalled and continued with exact plans
+  int pipe_retries = 0;            // pipelined searches answered again with exact plans (a spill list overflowed)
   int single_engine = 0;           // world size 1: answered by the single-GPU engine (DistTuning::world1_single)
   // DistTuning::stamps: the speculative rounds split by device stamps (sums
   // over the stamped rounds, microseconds): expansion kernel(s), claim kernel,
@@ -101,8 +103,10 @@ struct DistTuning {
   uint32_t owner_cap = 0;          // > 1 rank: pairs per owner-addressed block (0 = predicted per round)
   uint32_t spec_stall_edges = 0;   // a speculative round above this many per-rank frontier edges stalls for a
                                    // host-planned round (0 = only when the spill lists could overflow)
-  bool overlap = false;            // > 1 rank: lockstep rounds expand side 1 on the compute stream while side 0's
-                                   // candidates are exchanged (off until measured on a multi-GPU node)
+  bool pipeline = true;            // > 1 rank: ONE collective per speculative round -- each round's reduction
+                                   // travels with the next round's candidate exchange and every plan accounts
+                                   // the round before the last; false = exact plans, a status
+                                   // allgather per round
   size_t hbm_cap_bytes = 0;        // > 0: a build that would make this rank hold more device memory throws
                                    // (tests: rehearse "does not fit one GPU" at small scale)
   bool world1_single = true;       // one rank: answer queries with the single-GPU engine over this rank's device

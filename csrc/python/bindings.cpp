@@ -89,6 +89,8 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["path_collectives"] = s.path_collectives;
   d["solo_rounds"] = s.solo_rounds;
   d["cont_rounds"] = s.cont_rounds;
+  d["pipe_drains"] = s.pipe_drains;
+  d["pipe_retries"] = s.pipe_retries;
   d["exchanged_bytes"] = s.exchanged_bytes;
   d["comm_ms"] = s.comm_ms;
   d["device_ms"] = s.device_ms;
@@ -393,7 +395,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("solo", &DistTuning::solo)
       .def_readwrite("solo_edges", &DistTuning::solo_edges)
       .def_readwrite("owner_cap", &DistTuning::owner_cap)
-      .def_readwrite("overlap", &DistTuning::overlap)
+      .def_readwrite("pipeline", &DistTuning::pipeline)
       .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges)
       .def_readwrite("stamps", &DistTuning::stamps)
       .def_readwrite("spill_cap", &DistTuning::spill_cap)

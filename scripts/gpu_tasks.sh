@@ -21,7 +21,7 @@
 #            [ROUNDS=3 STEPS=20 WARMUP=5], one JSON line per run
 #   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
-#            (SPECS / RANKS / OVERLAP / QUERIES override benchmarks/dist_rounds.py's defaults)
+#            (SPECS / RANKS / PIPELINE / QUERIES / PROCS=1 override benchmarks/dist_rounds.py's defaults)
 #   procs    partitioned engine as separate processes on the one GPU (IPC transport):
 #            tests/test_gpu_dist_proc.py
 #   pairab   A/B of one environment knob over pair latencies: ABENV=<var> ABVALS="<v1> <v2>"
@@ -34,7 +34,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-TAG="${TAG:-r5}"
+TAG="${TAG:-r6}"
 T="timeout -k 10"
 PT="python -u -m pytest -x -v --timeout 120 --timeout-method thread"
 O=gpurun_out
@@ -76,7 +76,7 @@ run_task() {
         > $O/${TAG}_dstress.jsonl 2> $O/${TAG}_dstress.err ;;
     distab)
       $T 900 python3 benchmarks/dist_rounds.py ${SPECS:+--specs $SPECS} ${RANKS:+--ranks $RANKS} \
-        ${OVERLAP:+--overlap $OVERLAP} ${QUERIES:+--queries $QUERIES} \
+        ${PIPELINE:+--pipeline $PIPELINE} ${QUERIES:+--queries $QUERIES} ${PROCS:+--procs} \
         > $O/${TAG}_dist_rounds.jsonl 2> $O/${TAG}_dist_rounds.err ;;
     procs)
       $T 900 $PT -m gpu tests/test_gpu_dist_proc.py > $O/${TAG}_procs.log 2>&1 ;;

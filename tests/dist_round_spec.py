@@ -13,6 +13,12 @@ must produce exactly this trace:
 
 The native engine reports it with SearchOptions.trace (stats.trace) and the
 gloo model (tests/dist_protocol_model.py) in ``result.trace``.
+
+Pipelined rounds (DistTuning.pipeline, more than one rank): a round's plan is
+made before the previous round's claims are reduced, so round r's sides come
+from the frontier sizes round r - 1 started with (round 0: the roots); the
+meet and an exhausted side are still found in the round that has them, so
+the trace and the hop count follow the same level sets (``pipelined=True``).
 """
 import numpy as np
 
@@ -20,7 +26,7 @@ LOCKSTEP_EDGES = 1 << 16  # dist_engine.hip kLockstepEdges
 LOCKSTEP_MAX_EDGES = 1 << 20  # dist_engine.hip kLockstepMaxEdges
 
 
-def round_trace(csr, src: int, dst: int, side: str = "edges", lockstep: bool = True):
+def round_trace(csr, src: int, dst: int, side: str = "edges", lockstep: bool = True, pipelined: bool = False):
     row_off = np.asarray(csr.row_off, dtype=np.int64)
     col = np.asarray(csr.col, dtype=np.int64)
     deg = np.diff(row_off)
@@ -34,16 +40,19 @@ def round_trace(csr, src: int, dst: int, side: str = "edges", lockstep: bool = T
     front = [np.array([src], np.int64), np.array([dst], np.int64)]
     cnt, fed, depth, turn = [1, 1], [int(deg[src]), int(deg[dst])], [0, 0], 0
     trace = []
+    seen = []  # frontier sizes each round started with
     while True:
-        flo, fhi = min(fed), max(fed)
+        seen.append((list(cnt), list(fed)))
+        pc, pf = seen[max(len(seen) - 2, 0)] if pipelined else (cnt, fed)
+        flo, fhi = min(pf), max(pf)
         if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or (fhi <= 2 * flo and fhi <= LOCKSTEP_MAX_EDGES)):
             sides = [0, 1]
         elif side == "alternate":
             sides, turn = [turn], turn ^ 1
         elif side == "frontier":
-            sides = [0 if cnt[0] <= cnt[1] else 1]
+            sides = [0 if pc[0] <= pc[1] else 1]
         else:
-            sides = [0 if fed[0] <= fed[1] else 1]
+            sides = [0 if pf[0] <= pf[1] else 1]
         new = {}
         for s in sides:
             f = front[s]

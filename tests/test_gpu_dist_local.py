@@ -1,7 +1,7 @@
 """The native partitioned engine (csrc/dist/dist_engine.hip) with P > 1 ranks on
 ONE GPU: P threads, each a DistBiBfs over its own vertex block, exchanging
 through the in-process local group instead of RCCL.
-Covers lockstep rounds (exchange overlapped with the opposite expand),
+Covers lockstep rounds, pipelined rounds (one collective per round),
 single-side rounds, forced top-down / bottom-up, unreachable pairs and
 src == dst, against the CPU oracle."""
 import random
@@ -164,7 +164,10 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
     says and discovers what the BFS levels say (tests/dist_round_spec.py --
     the same spec the CPU model is held to in tests/test_dist_protocol.py),
     whether rounds are planned on the device or on the host, and through
-    tiny exchange blocks (count syncs, overflow to bottom-up)."""
+    tiny exchange blocks (count syncs, overflow to bottom-up).  Exact plans
+    follow the exact spec; pipelined plans (P > 1, the default) the spec's
+    lagged side choice -- unless the search drained to exact plans, where
+    the hop count is still checked."""
     import torch  # noqa: F401
     from dist_round_spec import round_trace
 
@@ -176,15 +179,20 @@ def test_native_rounds_follow_protocol_spec(ranks, spec_rounds):
         for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False},
                    {"direction": "bottomup"}):
             # (world1_single off: one rank runs the partitioned rounds too)
-            for tune in (make_tuning(spec_rounds=spec_rounds, world1_single=False),
+            for tune in (make_tuning(spec_rounds=spec_rounds, world1_single=False, pipeline=False),
                          make_tuning(spec_rounds=spec_rounds, cap=4, nosync_bytes=0, spec_stall_edges=64,
-                                     world1_single=False),
-                         make_tuning(spec_rounds=spec_rounds, owner_cap=2, world1_single=False),
-                         make_tuning(spec_rounds=spec_rounds, overlap=True, owner_cap=64, world1_single=False)):
-                rs = dist_local_run(ranks, g, qs, tuning=tune, trace=True, **kw)
-                for (s, d), r in zip(qs, rs):
+                                     world1_single=False, pipeline=False),
+                         make_tuning(spec_rounds=spec_rounds, owner_cap=2, world1_single=False, pipeline=False),
+                         make_tuning(spec_rounds=spec_rounds, world1_single=False),
+                         make_tuning(spec_rounds=spec_rounds, owner_cap=64, world1_single=False)):
+                rs, st = dist_local_run(ranks, g, qs, tuning=tune, trace=True, return_stats=True, **kw)
+                piped = tune.pipeline and ranks > 1 and spec_rounds > 0
+                for (s, d), r, x in zip(qs, rs, st):
                     want, hops = round_trace(g.csr, s, d, side=kw.get("side", "edges"),
-                                             lockstep=kw.get("lockstep", True))
+                                             lockstep=kw.get("lockstep", True), pipelined=piped)
+                    if piped and (x["pipe_drains"] or x["host_rounds"]):
+                        assert r.hops == hops, (spec, s, d, kw, r.hops, hops)  # pipelined, then exact plans
+                        continue
                     got = [(t["side"], t["depth"], t["frontier"], t["edges"], t["discovered"]) for t in r.stats["trace"]]
                     exp = [w[:5] for w in want]
                     # a single-side level stops at its first meet (every meet of such a
@@ -335,34 +343,62 @@ def test_owner_addressed_exchange_moves_only_addressed_bytes():
                 assert x["exchanged_bytes"] <= x["rounds"] * (ranks - 1) * 2 * (2 + 2 * 4096) * 4 + 65536, x
 
 
-@pytest.mark.parametrize("ranks", [1, 2, 3, 4])
-def test_overlap_knob_matches_oracle(ranks):
-    """DistTuning.overlap: each speculative round's sides expand as separate
-    launches on two streams, side 0's exchange beside side 1's expansion;
-    every answer still matches the oracle (and ranks agree)."""
+@pytest.mark.parametrize("ranks", [2, 3, 4])
+def test_pipeline_on_and_off_match_oracle_and_count_collectives(ranks):
+    """DistTuning.pipeline: with it (the default) a speculative round is ONE
+    collective -- the candidate exchange carries the previous round's
+    reduction -- and without it two (exchange + status allgather); answers
+    match the oracle either way.  Hub graphs and bottom-up drain the pipeline
+    (the first stall) and finish with exact plans."""
     import torch  # noqa: F401
     from bidirectional_bfs_amd.parallel import make_tuning
 
-    for spec in ("gnp:20000::6", "rmat:16384:262144:3"):
+    for spec in ("gnp:20000::6", "gnp:200000::3", "rmat:16384:262144:3"):
         g = bb.from_spec(spec)
         qs = _pairs(g.n, 10, 29)
         for kw in ({}, {"lockstep": False}, {"direction": "bottomup"}):
-            rs = dist_local_run(ranks, g, qs, tuning=make_tuning(overlap=True), **kw)
-            _check_all(g, qs, rs)
+            per = {}
+            for pipe in (True, False):
+                rs, st = dist_local_run(ranks, g, qs, tuning=make_tuning(pipeline=pipe), return_stats=True, **kw)
+                _check_all(g, qs, rs)
+                sr = sum(x["spec_rounds"] for x in st)
+                per[pipe] = (sum(x["collectives"] for x in st), sr, sum(x["pipe_drains"] + x["host_rounds"] for x in st))
+            if spec.startswith("gnp") and not kw:
+                coll, sr, drained = per[True]
+                assert drained == 0, (spec, per)
+                # one collective per enqueued round, plus the seed's gather and the path's
+                assert coll <= sr + 2 * len(qs), (spec, per)
+                assert per[False][0] >= 2 * per[False][1], (spec, per)
+
+
+def test_pipeline_drains_on_spills_to_continuation_rounds():
+    """2-pair owner blocks spill in the first pipelined round: the next plan
+    stalls, the host drains the pipeline (the pending round accounted
+    exactly) and continuation rounds complete the level -- hop counts and
+    paths still exact."""
+    import torch  # noqa: F401
+    from bidirectional_bfs_amd.parallel import make_tuning
+
+    g = bb.from_spec("gnp:50000::8")
+    qs = _pairs(g.n, 12, 77)
+    rs, st = dist_local_run(3, g, qs, tuning=make_tuning(owner_cap=2), return_stats=True)
+    _check_all(g, qs, rs)
+    assert sum(x["pipe_drains"] for x in st) > 0
+    assert sum(x["cont_rounds"] for x in st) > 0
 
 
 @pytest.mark.parametrize("ranks", [2, 4])
 def test_round_stamps_split_kernel_and_exchange(ranks):
     """DistTuning.stamps: the speculative rounds of a P > 1 search are stamped
     (expansion / claim kernels, and the gaps the exchanges leave between
-    them); answers unchanged, overlap on and off."""
+    them); answers unchanged, pipelined rounds and exact plans."""
     import torch  # noqa: F401
     from bidirectional_bfs_amd.parallel import make_tuning
 
     g = bb.from_spec("gnp:200000::5")
     qs = _pairs(g.n, 8, 41)
-    for ov in (False, True):
-        rs, st = dist_local_run(ranks, g, qs, tuning=make_tuning(stamps=True, overlap=ov), return_stats=True)
+    for pipe in (False, True):
+        rs, st = dist_local_run(ranks, g, qs, tuning=make_tuning(stamps=True, pipeline=pipe), return_stats=True)
         _check_all(g, qs, rs)
         stamped = [x for r, x in zip(rs, st) if r.found and r.hops > 2]
         assert stamped and all(x["stamped_rounds"] > 0 for x in stamped)

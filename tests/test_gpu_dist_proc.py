@@ -43,7 +43,8 @@ def test_processes_match_oracle_every_branch(ranks, spec):
     """Every option set and exchange branch over one group of processes that
     read their shards from one .bin: default, single-side, forced directions,
     alternate sides, host-planned rounds, tiny blocks (count syncs, overflow
-    to bottom-up), 2-pair owner blocks (continuation rounds) and overlap."""
+    to bottom-up), 2-pair owner blocks (continuation rounds) and exact plans
+    (pipeline off)."""
     g = bb.from_spec(spec)
     qs = _pairs(g.n, 10, ranks)
     runs = [({}, {}), ({"lockstep": False}, None), ({"direction": "topdown"}, None),
@@ -52,7 +53,7 @@ def test_processes_match_oracle_every_branch(ranks, spec):
             ({}, {"spec_rounds": 0}),
             ({}, {"cap": 4, "nosync_bytes": 0, "spec_cap_max": 1024, "spec_stall_edges": 1024}),
             ({}, {"owner_cap": 2}), ({"lockstep": False}, {"owner_cap": 2}),
-            ({}, {"overlap": True}), ({"direction": "bottomup"}, {"overlap": True})]
+            ({}, {"pipeline": False}), ({"direction": "bottomup"}, {"pipeline": False})]
     got, outs = dist_proc_matrix(ranks, g, qs, runs)
     assert all(o["backend"] == "ipc" for o in outs)
     assert len({o["pid"] for o in outs}) == ranks  # really separate processes
@@ -72,12 +73,19 @@ def test_processes_follow_protocol_spec():
     g = bb.from_spec("gnp:20000::6")
     qs = _pairs(g.n, 6, 13)
     kws = [{}, {"lockstep": False}, {"side": "alternate"}, {"direction": "bottomup"}]
-    tunes = [{}, {"owner_cap": 2}, {"overlap": True, "owner_cap": 64}]
+    tunes = [{}, {"owner_cap": 2}, {"pipeline": False, "owner_cap": 64}]
     runs = [(dict(kw, trace=True), t) for kw in kws for t in tunes]
     got, _ = dist_proc_matrix(3, g, qs, runs)
-    for (opts, _), (rs, _, _) in zip(runs, got):
-        for (s, d), r in zip(qs, rs):
-            want, hops = round_trace(g.csr, s, d, side=opts.get("side", "edges"), lockstep=opts.get("lockstep", True))
+    for (opts, tune), (rs, lst, _) in zip(runs, got):
+        for (s, d), r, x in zip(qs, rs, lst):
+            # pipelined rounds (the default with 3 ranks): the spec's lagged side
+            # choice, unless the search drained to exact plans (hops checked)
+            piped = tune.get("pipeline", True)
+            want, hops = round_trace(g.csr, s, d, side=opts.get("side", "edges"), lockstep=opts.get("lockstep", True),
+                                     pipelined=piped)
+            if piped and (x["pipe_drains"] or x["host_rounds"]):
+                assert r.hops == hops, (s, d, opts, tune)
+                continue
             tr = r.stats.get("trace", [])
             gotr = [(t["side"], t["depth"], t["frontier"], t["edges"], t["discovered"]) for t in tr]
             exp = [w[:5] for w in want]
