@@ -65,7 +65,7 @@ cpu: $(LIB)/libbibfs_core.so $(CPU_TOOLS)
 mpi: $(LIB)/libbibfs_mpi.so $(MPI_TOOLS)
 gpu: $(LIB)/libbibfs.so $(GPU_TOOLS) $(BIN)/bibfs_cuda_only
 python: $(NATIVE_PY)
-micro: $(BIN)/lat_probe $(BIN)/mailbox_rtt $(BIN)/place_probe
+micro: $(BIN)/lat_probe $(BIN)/mailbox_rtt $(BIN)/place_probe $(BIN)/grid_barrier
 
 # The LDS engine's counter atomics are already issued by one lane per wave:
 # the compiler's wave-reduction rewrite of them only adds instructions to the
@@ -75,6 +75,10 @@ $(OBJ)/hip/engine_kernels.o $(OBJ)/hip/tiny_engine.o: HIPFLAGS += -mllvm -amdgpu
 $(BIN)/mailbox_rtt: benchmarks/micro/mailbox_rtt.hip
 	@mkdir -p $(BIN)
 	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 $< -o $@ -L/opt/rocm/lib -lhsa-runtime64
+
+$(BIN)/grid_barrier: benchmarks/micro/grid_barrier.hip
+	@mkdir -p $(BIN)
+	$(HIPCC) -O3 -std=c++17 --offload-arch=$(ARCH) -mcode-object-version=5 $< -o $@
 
 $(BIN)/place_probe: benchmarks/micro/place_probe.hip
 	@mkdir -p $(BIN)
