@@ -29,6 +29,13 @@ frontier exchange, v2/main-v2.cpp:59-83):
   stops the search and its minimum key is the distance.
 * The path is walked with one ``all_reduce(MIN)`` per step: the owner of the
   current vertex contributes its parent, every other rank contributes ~0.
+* Pipelined rounds (``pipelined=True``; the native ``DistTuning::pipeline``):
+  a round's reduction reaches the planner one round late (natively it rides
+  the next round's candidate exchange), so round r is planned from the
+  rounds up to r - 2 and a meet or an exhausted side found in round r stops
+  the search when round r + 1 has already run; the answer is still round r's
+  minimum key and the path is unchanged (round r + 1 claims only vertices
+  neither chain goes through).
 """
 from __future__ import annotations
 
@@ -175,7 +182,7 @@ class TorchDistBiBfs:
         return np.array(sorted(new_local), dtype=np.int64)
 
     def search(self, src: int, dst: int, side: str = "edges", direction: str = "auto",
-               want_path: bool = True, lockstep: bool = True) -> DistSearchResult:
+               want_path: bool = True, lockstep: bool = True, pipelined: bool = False) -> DistSearchResult:
         ROp = self.dist.ReduceOp
         src, dst = int(src), int(dst)
         if src == dst:
@@ -201,7 +208,29 @@ class TorchDistBiBfs:
         res = DistSearchResult(False, -1, [], int(NONE))
         nnz_total = 2 * int(self._allreduce([self.m_input if self.rank == 0 else 0], ROp.SUM)[0])
         key = NO_KEY
+        # executed rounds whose reductions the planner has not seen yet:
+        # (sides, sums, key, trace rows); accounted one round late when pipelined
+        pending = []
+        act_cnt, act_fed = list(cnt), list(fed)  # the true frontier sizes (trace records)
+        stop = False
         while True:
+            while len(pending) > (1 if pipelined else 0):
+                psides, psums, pkey, rows = pending.pop(0)
+                res.trace += rows
+                if pkey != NO_KEY:
+                    key = pkey
+                    stop = True
+                    break
+                dead = False
+                for s in psides:
+                    cnt[s], fed[s] = int(psums[2 * s]), int(psums[2 * s + 1])
+                    ved[s] += fed[s]
+                    dead = dead or cnt[s] == 0  # that side's component is exhausted
+                if dead:
+                    stop = True
+                    break
+            if stop:
+                break
             # rounds: both sides in lockstep while their frontiers are comparable
             flo, fhi = min(fed), max(fed)
             if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or
@@ -236,20 +265,13 @@ class TorchDistBiBfs:
                 contrib += [0, 0] if arr is None else [arr.size, int(self.deg[arr - self.lo].sum()) if arr.size else 0]
             sums = self._allreduce(contrib, ROp.SUM)
             gkey = int(self._allreduce([best], ROp.MIN)[0])
+            rows = []
             for s in sides:
-                res.trace.append((s, depth[s], cnt[s], fed[s], int(sums[2 * s]), len(sides)))
+                rows.append((s, depth[s], act_cnt[s], act_fed[s], int(sums[2 * s]), len(sides)))
                 depth[s] += 1
                 front[s] = new[s]
-            if gkey != NO_KEY:
-                key = gkey
-                break
-            dead = False
-            for s in sides:
-                cnt[s], fed[s] = int(sums[2 * s]), int(sums[2 * s + 1])
-                ved[s] += fed[s]
-                dead = dead or cnt[s] == 0  # that side's component is exhausted
-            if dead:
-                break
+                act_cnt[s], act_fed[s] = int(sums[2 * s]), int(sums[2 * s + 1])
+            pending.append((sides, sums, gkey, rows))
         if key == NO_KEY:
             return res
         meet, hops = key & 0xFFFFFFFF, key >> 32

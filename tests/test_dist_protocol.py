@@ -74,6 +74,10 @@ def test_partitioned_protocol_matches_oracle(world):
         ("gnp:3000::3", 1 << 16, _pairs(3000, 3, 5), {"side": "alternate"}),
         ("gnp:3000::3", 1 << 16, _pairs(3000, 4, 6), {"lockstep": False}),
         ("rmat:4096:40000:2", 4, _pairs(4096, 3, 7), {"lockstep": False}),
+        # pipelined rounds (DistTuning.pipeline): lagged plans, one extra round
+        ("gnp:3000::3", 1 << 16, _pairs(3000, 8, 8), {"pipelined": True}),
+        ("rmat:4096:40000:2", 1 << 16, _pairs(4096, 6, 9), {"pipelined": True}),
+        ("gnp:3000::3", 1 << 16, _pairs(3000, 4, 10), {"pipelined": True, "lockstep": False}),
     ]
     out = _run(world, specs)
     graphs = {}
@@ -84,7 +88,8 @@ def test_partitioned_protocol_matches_oracle(world):
         g = graphs.setdefault(spec, bb.from_spec(spec))
         o = native.bfs_oracle(g.csr, s, d)
         assert found == o.found and hops == o.hops, (spec, s, d, hops, o.hops)
-        want, whops = round_trace(g.csr, s, d, side=kw.get("side", "edges"), lockstep=kw.get("lockstep", True))
+        want, whops = round_trace(g.csr, s, d, side=kw.get("side", "edges"), lockstep=kw.get("lockstep", True),
+                                  pipelined=kw.get("pipelined", False))
         assert trace == want and (whops if whops >= 0 else -1) == (hops if found else -1), (spec, s, d, kw)
         if found:
             ok, why = native.validate_path(g.csr, s, d, hops, path)
@@ -105,7 +110,8 @@ def test_round_spec_hops_match_oracle():
         g = bb.from_spec(spec)
         for s, d in _pairs(g.n, 12, 9) + [(5, 5)]:
             o = native.bfs_oracle(g.csr, s, d)
-            for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False}):
+            for kw in ({}, {"lockstep": False}, {"side": "alternate"}, {"side": "frontier", "lockstep": False},
+                       {"pipelined": True}, {"pipelined": True, "lockstep": False}):
                 trace, hops = round_trace(g.csr, s, d, **kw)
                 assert hops == (o.hops if o.found else -1), (spec, s, d, kw)
                 if s != d:
