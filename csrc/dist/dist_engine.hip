@@ -426,7 +426,7 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p0, const Reduced& rd
     // level is incomplete) -- stall; the host drains the pipeline (accounts
     // that round exactly) and the search goes on with exact plans, which run
     // the continuation round.
-    if (pipe && (rd.nsp[0] | rd.nsp[1] | c.cont_due)) {
+    if (pipe && ((((p0.sides & 3u) | p0.cont) && (rd.nsp[0] | rd.nsp[1])) || c.cont_due)) {
       c.state = kStall;
       c.stall = kStallPipe;
       return;
@@ -958,7 +958,9 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
                                                           uint32_t ocap, uint32_t plan_cap, int pipe) {
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   const int p = it & 1;
-  const bool pplan = pipe && it > 0;  // a pipelined plan (round 0: the seed, exact)
+  // a pipelined plan; round 0's accounts nothing (the seed is pending: its
+  // reduction rides round 0's exchange, no seed gather) and plans both roots
+  const bool pplan = pipe != 0;
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
   __shared__ uint32_t fr[4];  // frontier bounds: fbeg[2], fend[2]
@@ -966,7 +968,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // with one round of parallel loads (thread 0 alone would chain them
   // through plan_round's branches)
   stage_words(&prev, &V.ctl[p ^ 1], sizeof(Ctl));
-  const Reduced* const gsrc = V.redg[pplan ? p : p ^ 1];
+  const Reduced* const gsrc = V.redg[pplan ? p : p ^ 1];  // (round 0, pipelined: read, unused)
   __shared__ Reduced gst[kStageRanks];
   if (V.P <= kStageRanks) stage_words(gst, gsrc, (size_t)V.P * sizeof(Reduced));
   if (threadIdx.x >= kThreads - 4) {
@@ -3258,7 +3260,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   std::atomic_thread_fence(std::memory_order_seq_cst);
   const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
   if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
-  if (P > 1) {
+  const bool pipe_start = P > 1 && tune.pipeline && tune.spec_rounds > 0 && !pipe_off;
+  if (P > 1 && !pipe_start) {  // (pipelined: the seed's reduction rides round 0's exchange)
     comm->allgather(&V.red[1], V.redg[1], sizeof(Reduced), cs);
     stats.collectives++;
   }
@@ -3275,7 +3278,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   // collective per round -- and each plan accounts the round before the last
   // one.  The first stall (a spill, a big or dense frontier) drains the
   // pipeline and the search continues with exact plans.
-  bool pipe = P > 1 && tune.pipeline && !host_only && !pipe_off;
+  bool pipe = pipe_start;
   bool pipe_used = pipe;
   const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
   if (host_only) {

@@ -212,6 +212,10 @@ class TorchDistBiBfs:
         # (sides, sums, key, trace rows); accounted one round late when pipelined
         pending = []
         act_cnt, act_fed = list(cnt), list(fed)  # the true frontier sizes (trace records)
+        if pipelined:  # the seed's reduction rides round 0's exchange: round 0 is planned blind
+            pending.append(([0, 1], [cnt[0], fed[0], cnt[1], fed[1]], NO_KEY, []))
+            cnt, fed = [0, 0], [0, 0]
+            ved = [0, 0]
         stop = False
         while True:
             while len(pending) > (1 if pipelined else 0):

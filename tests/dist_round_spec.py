@@ -16,7 +16,8 @@ gloo model (tests/dist_protocol_model.py) in ``result.trace``.
 
 Pipelined rounds (DistTuning.pipeline, more than one rank): a round's plan is
 made before the previous round's claims are reduced, so round r's sides come
-from the frontier sizes round r - 1 started with (round 0: the roots); the
+from the frontier sizes round r - 1 started with (round 0: none -- both
+roots in lockstep, or side 0 when the policy picks one side); the
 meet and an exhausted side are still found in the round that has them, so
 the trace and the hop count follow the same level sets (``pipelined=True``).
 """
@@ -43,7 +44,10 @@ def round_trace(csr, src: int, dst: int, side: str = "edges", lockstep: bool = T
     seen = []  # frontier sizes each round started with
     while True:
         seen.append((list(cnt), list(fed)))
-        pc, pf = seen[max(len(seen) - 2, 0)] if pipelined else (cnt, fed)
+        if pipelined:  # round 0 sees nothing yet (the seed's reduction rides its exchange)
+            pc, pf = seen[-2] if len(seen) >= 2 else ([0, 0], [0, 0])
+        else:
+            pc, pf = cnt, fed
         flo, fhi = min(pf), max(pf)
         if lockstep and side != "alternate" and (fhi <= LOCKSTEP_EDGES or (fhi <= 2 * flo and fhi <= LOCKSTEP_MAX_EDGES)):
             sides = [0, 1]
