@@ -503,11 +503,12 @@ __device__ __forceinline__ void plan_round_regs(const Ctl& p0, const Reduced& rd
 }
 
 // Publish round `p`'s plan; with tracing on, also record the round it
-// accounted (pipelined plans and drains: the pending round psides / pcont,
-// always top-down).
-__device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& rd, const Ctl& c, bool pend = false) {
+// accounted (pend 1, pipelined plans: the pending round psides / pcont of a
+// running plan; pend 2, a drain: that of the stalled plan it answers; always
+// top-down).
+__device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& rd, const Ctl& c, int pend = 0) {
   V.ctl[p] = c;
-  const bool live = prev.state == kRun || prev.state == kStall;
+  const bool live = prev.state == kRun || (pend == 2 && prev.state == kStall);
   const uint32_t asides = pend ? (live ? prev.psides : 0u) : prev.sides;
   const uint32_t acont = pend ? (live ? prev.pcont : 0u) : prev.cont;
   if (V.trace && asides && !(asides & kSeedBit) && c.rounds >= 1 && c.rounds <= V.trace_cap) {
@@ -945,6 +946,42 @@ __device__ __forceinline__ RoundStamp* round_stamp(const DView& V, uint32_t it) 
   return V.rstamp ? V.rstamp + (it % kTraceCap) : nullptr;
 }
 
+// Publish the plan `c` of round `it` (one wave calls it; lane 0 stores): the
+// Ctl (and, tracing, the record of the round it accounted), the accounted
+// Ctl to the host when this plan ends the search (one rank: the path walked
+// into pinned memory first), the largest per-owner count of the round
+// before, then the plan word the host paces its enqueueing on.
+__device__ void publish_plan(const DView& V, uint32_t it, const Policy& pol, const Ctl& prev, const Reduced& rd,
+                             Ctl& c, int pend) {
+  const bool terminal = c.state == kDone || c.state == kDead;
+  if (threadIdx.x == 0) publish(V, it & 1, prev, rd, c, pend);
+  // the round that ends the search hands the host its accounted Ctl directly
+  // (no k_final launch + wait after the batch); later no-op rounds repeat it
+  const bool first_end = terminal && prev.state == kRun;
+  // one rank holds every parent: walk the path now, into pinned memory
+  if (first_end && V.P == 1 && c.state == kDone && pol.want_path) terminal_walk(V, c.key, pol);
+  if (threadIdx.x != 0) return;
+  if (first_end) {
+    c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(&c);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(V.host_ctl);
+    for (uint32_t k = 0; k < sizeof(Ctl) / 8; ++k)
+      __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __threadfence_system();
+  }
+  // the largest per-owner candidate count of the round before (sizes the
+  // host's owner blocks), then the plan word behind it
+  __hip_atomic_store(&V.plan_aux[it % kPlanRing], ~rd.nocmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __threadfence_system();
+  // one 8-byte write-through store per round: the host paces its enqueueing
+  // on the plan and sizes the rounds it enqueues from the frontier (larger
+  // side's edge count, clamped to 32 bits)
+  const unsigned long long fm = min(max(c.fmax[0], c.fmax[1]), 0xffffffffull);
+  __hip_atomic_store(&V.plan_ring[it % kPlanRing],
+                     (uint64_t)fm << 32 | ((uint64_t)plan_tag(pol.epoch, it) << 8) | (c.state << 2) | (c.sides & 3u),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Plan (every block computes the same plan; block 0 publishes it) + top-down
 // pre phase of both sides (blockIdx.y = side) into blocks of `cap` pairs.
 // header = 0: k_td_hubs runs next (it writes the headers); finish: this
@@ -959,18 +996,25 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   const int p = it & 1;
   // a pipelined plan; round 0's accounts nothing (the seed is pending: its
-  // reduction rides round 0's exchange, no seed gather) and plans both roots
+  // reduction rides round 0's exchange, no seed gather) and plans both roots.
+  // Every later pipelined round was planned by the previous round's claim
+  // kernel (pre): this kernel only loads the plan.
   const bool pplan = pipe != 0;
+  const bool pre = pipe && it > 0;
   __shared__ Ctl c, prev;
   __shared__ Reduced rd;
   __shared__ uint32_t fr[4];  // frontier bounds: fbeg[2], fend[2]
   // the previous plan and reduction (and the frontier bounds) staged into LDS
   // with one round of parallel loads (thread 0 alone would chain them
   // through plan_round's branches)
-  stage_words(&prev, &V.ctl[p ^ 1], sizeof(Ctl));
+  if (pre) {
+    stage_words(&c, &V.ctl[p], sizeof(Ctl));
+  } else {
+    stage_words(&prev, &V.ctl[p ^ 1], sizeof(Ctl));
+  }
   const Reduced* const gsrc = V.redg[pplan ? p : p ^ 1];  // (round 0, pipelined: read, unused)
   __shared__ Reduced gst[kStageRanks];
-  if (V.P <= kStageRanks) stage_words(gst, gsrc, (size_t)V.P * sizeof(Reduced));
+  if (!pre && V.P <= kStageRanks) stage_words(gst, gsrc, (size_t)V.P * sizeof(Reduced));
   if (threadIdx.x >= kThreads - 4) {
     const uint32_t k = threadIdx.x - (kThreads - 4);
     fr[k] = k < 2 ? V.st->fbeg[k] : V.st->fend[k - 2];
@@ -979,7 +1023,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
   __shared__ SmallStage sm;
   if (threadIdx.x < kWave) {  // wave 0 plans, on wave-uniform (scalar) registers
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && !pre) {
       // (two call sites, not one through a conditional pointer: that made every
       // load of the planner's inputs a flat load)
       if (V.P <= kStageRanks) reduce_gathered(gst, V.P, rd);
@@ -994,37 +1038,10 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
   // One block publishes the plan: block (0, 1) when the launch has a second
   // row, so the plan publication (its system-scope stores and fence, several
   // microseconds on one lane) never delays block (0, 0), which runs a small
-  // round's whole expansion (small_expand).
-  const bool planner = blockIdx.x == 0 && blockIdx.y == (gridDim.y > 1 ? 1u : 0u);
-  if (planner && threadIdx.x < kWave) {
-    if (threadIdx.x == 0) publish(V, p, prev, rd, c, pplan);
-    // the round that ends the search hands the host its accounted Ctl directly
-    // (no k_final launch + wait after the batch); later no-op rounds repeat it
-    const bool first_end = terminal && prev.state == kRun;
-    // one rank holds every parent: walk the path now, into pinned memory
-    if (first_end && V.P == 1 && c.state == kDone && pol.want_path) terminal_walk(V, c.key, pol);
-    if (first_end && threadIdx.x == 0) {
-      c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
-      const uint64_t* src = reinterpret_cast<const uint64_t*>(&c);
-      uint64_t* dst = reinterpret_cast<uint64_t*>(V.host_ctl);
-      for (uint32_t k = 0; k < sizeof(Ctl) / 8; ++k)
-        __hip_atomic_store(dst + k, src[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __threadfence_system();
-    }
-  }
-  if (planner && threadIdx.x == 0) {
-    // the largest per-owner candidate count of the round before (sizes the
-    // host's owner blocks), then the plan word behind it
-    __hip_atomic_store(&V.plan_aux[it % kPlanRing], ~rd.nocmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __threadfence_system();
-    // one 8-byte write-through store per round: the host paces its enqueueing
-    // on the plan and sizes the rounds it enqueues from the frontier (larger
-    // side's edge count, clamped to 32 bits)
-    const unsigned long long fm = min(max(c.fmax[0], c.fmax[1]), 0xffffffffull);
-    __hip_atomic_store(&V.plan_ring[it % kPlanRing],
-                       (uint64_t)fm << 32 | ((uint64_t)plan_tag(pol.epoch, it) << 8) | (c.state << 2) | (c.sides & 3u),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  // round's whole expansion (small_expand).  (A pipelined round after the
+  // first was planned and published by the previous round's claim kernel.)
+  const bool planner = !pre && blockIdx.x == 0 && blockIdx.y == (gridDim.y > 1 ? 1u : 0u);
+  if (planner && threadIdx.x < kWave) publish_plan(V, it, pol, prev, rd, c, pplan ? 1 : 0);
   // a round enqueued past the end of the search: nothing to expand, no round
   // end (every block sees the same plan, so no block counts itself in)
   if (terminal) return;
@@ -2051,13 +2068,41 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
   }
 }
 
+// Pipelined rounds: plan round it + 1 in the claim kernel of round it (one
+// block; see k_spec_claim) and publish it as k_spec_expand would.
+__device__ void plan_next_round(const DView& V, uint32_t it, uint32_t cap, const Policy& pol, uint32_t plan_cap) {
+  constexpr uint32_t kRedW = sizeof(Reduced) / 4;
+  __shared__ Ctl prev, c;
+  __shared__ Reduced rd;
+  __shared__ uint32_t gw[kStageRanks * kRedW];
+  stage_words(&prev, &V.ctl[it & 1], sizeof(Ctl));
+  for (uint32_t t = threadIdx.x; t < (uint32_t)V.P * kRedW; t += blockDim.x)
+    gw[t] = V.recvbuf[(uint64_t)(t / kRedW) * peer_words(cap) + t % kRedW];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    reduce_gathered(reinterpret_cast<const Reduced*>(gw), V.P, rd);
+    plan_round(prev, rd, pol, plan_cap, kPlanPipe, c);
+  }
+  __syncthreads();
+  if (threadIdx.x < kWave) publish_plan(V, it + 1, pol, prev, rd, c, 1);
+}
+
 // Post phase of both sides: owners claim the candidates addressed to them
 // (rank r's side-s block at recvbuf + oblock(s, r, cap)).
 // (more than one rank: this kernel ends the round's claims; its last
 // workgroup closes the round.  pipe: block (0, 0) also moves the reduction
 // headers the exchange carried into the gathered slot of round it - 1.)
-__global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap, int pipe) {
+__global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap, int pipe, Policy pol,
+                                                         uint32_t plan_cap) {
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
+  if (pipe && blockIdx.x == gridDim.x - 1) {
+    // Pipelined rounds: the extra block plans round it + 1 while the others
+    // claim round it -- its inputs (this round's plan, every rank's reduction
+    // of round it - 1 in the exchange's headers) are all here, and the claims
+    // do not change them -- so the next expansion starts with its plan ready.
+    if (blockIdx.y == 0) plan_next_round(V, it, cap, pol, plan_cap);
+    return;
+  }
   const Ctl& c = V.ctl[it & 1];
   if (c.state == kDone || c.state == kDead) return;  // past the end of the search (k_spec_expand)
   RoundStamp* rs = round_stamp(V, it);
@@ -2099,7 +2144,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
     }
   }
   drain_atomics();
-  if (last_block(&V.st->done_blocks[1], gridDim.x * gridDim.y) && threadIdx.x == 0) {
+  if (last_block(&V.st->done_blocks[1], (gridDim.x - (pipe ? 1u : 0u)) * gridDim.y) && threadIdx.x == 0) {
     spec_round_end(V, it, c.sides, c.cont);
     atomicExch(&V.st->done_blocks[1], 0u);
     if (rs) rs->ce = __builtin_amdgcn_s_memrealtime();
@@ -2171,7 +2216,7 @@ __global__ void k_final(DView V, uint32_t it, Policy pol, Ctl* host, int flags, 
   reduce_gathered(drain ? V.redg[p] : V.redg[p ^ 1], V.P, rd);
   plan_round(V.ctl[p ^ 1], rd, pol, 0, flags, c);
   c.ticks = __builtin_amdgcn_s_memrealtime() - V.st->t0;
-  publish(V, p, V.ctl[p ^ 1], rd, c, drain);
+  publish(V, p, V.ctl[p ^ 1], rd, c, drain ? 2 : 0);
   V.red[p ^ 1].meetkey = kNoKey;  // read; it is the buffer of the next round (it + 1)
   *host = c;
   __threadfence_system();
@@ -3260,7 +3305,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   std::atomic_thread_fence(std::memory_order_seq_cst);
   const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
   if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
-  const bool pipe_start = P > 1 && tune.pipeline && tune.spec_rounds > 0 && !pipe_off;
+  // (the pipelined planner reduces every rank's header in LDS: up to kStageRanks ranks)
+  const bool pipe_start = P > 1 && P <= kStageRanks && tune.pipeline && tune.spec_rounds > 0 && !pipe_off;
   if (P > 1 && !pipe_start) {  // (pipelined: the seed's reduction rides round 0's exchange)
     comm->allgather(&V.red[1], V.redg[1], sizeof(Reduced), cs);
     stats.collectives++;
@@ -3407,7 +3453,8 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         // rank receives only what is addressed to it.  Pipelined, the header
         // is the round's status too: no second collective.
         comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
-        k_spec_claim<<<dim3(cx, 2), kThreads, 0, cs>>>(V, it, ocap, pp);
+        // (pipelined: one extra block plans the next round beside the claims)
+        k_spec_claim<<<dim3(cx + (pipe ? 1u : 0u), 2), kThreads, 0, cs>>>(V, it, ocap, pp, pol, plan_cap);
         HIP_CHECK(hipGetLastError());
         stats.collectives++;
         stats.exchanged_bytes += peer_bytes * (P - 1);
