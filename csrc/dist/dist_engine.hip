@@ -113,6 +113,13 @@ enum : int { kPlanAccountOnly = 1, kPlanResume = 2, kPlanForce = 4, kPlanStall =
 // rank's frontier share passes this many edges: the next round's frontier,
 // which it cannot see yet, must stay far below the spill lists.
 constexpr uint64_t kPipeMaxEdges = 1u << 14;
+// ... and only on graphs without hubs: a round whose frontier the plan cannot
+// see yet is at most (its input's vertices) x (max degree) edges.  On a
+// Kronecker graph the roots' neighbourhoods hold hubs of degree 10^5: the
+// blind round expands them into tiny owner blocks, spills and drains on every
+// query (Kronecker 22, P = 2: 1.57 ms pipelined vs 0.63 ms exact,
+// profiles/r6_dist_rounds_local.jsonl).
+constexpr uint64_t kPipeMaxDeg = 64;
 
 struct Ctl {
   unsigned long long cnt[2];   // current frontier sizes (vertices)
@@ -1028,6 +1035,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
       // load of the planner's inputs a flat load)
       if (V.P <= kStageRanks) reduce_gathered(gst, V.P, rd);
       else reduce_gathered(gsrc, V.P, rd);
+      if (pplan) rd.nocmax = ~0ull;  // (round 0 planned blind: no owner counts yet, the host's sizing reads 0)
       plan_round(prev, rd, pol, plan_cap, flags | (pplan ? kPlanPipe : 0), c);
     }
   } else if (threadIdx.x >= kWave && ocap && header && V.P <= kStageRanks && blockIdx.x == 0 && blockIdx.y == 0) {
@@ -1050,8 +1058,11 @@ __global__ __launch_bounds__(kThreads) void k_spec_expand(DView V, uint32_t it, 
     rs->tag = plan_tag(pol.epoch, it);
     rs->small = 0;
   }
-  // small round: one workgroup
-  if (ocap && header && small_expand_ok(c, V.P)) {
+  // small round: one workgroup.  The frontiers it stages must fit its LDS
+  // arrays: checked on the frontier bounds every block read (a pipelined
+  // plan's sizes are a round old and only steer the choice).
+  const bool fits_stage = (!(c.sides & 1u) || fr[2] - fr[0] <= kSmallV) && (!(c.sides & 2u) || fr[3] - fr[1] <= kSmallV);
+  if (ocap && header && fits_stage && small_expand_ok(c, V.P)) {
     if (blockIdx.x == 0 && blockIdx.y == 0) {
       if (RoundStamp* rs = round_stamp(V, it); rs && threadIdx.x == 0) {
         rs->ep = __builtin_amdgcn_s_memrealtime();
@@ -2120,6 +2131,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   }
   const int s = blockIdx.y;
   if (pipe && blockIdx.x == 0 && s == 0) scatter_peer_headers(V, cap, it);
+  const uint32_t nbx = gridDim.x - (pipe ? 1u : 0u);  // the claiming blocks (pipelined: not the planner's column)
   // a continuation side claims at the depth its level already has
   const uint32_t dnew = ((c.sides >> s) & 1) ? c.xdepth[s] + 1 : c.xdepth[s];
   ClaimMeet cm;
@@ -2130,7 +2142,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
     const uint32_t* b = V.recvbuf + oblock(s, (uint32_t)r, cap);
     const uint32_t cnt = min(b[0], cap);
     const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
-    for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < cnt; base += (uint64_t)gridDim.x * kThreads) {
+    for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < cnt; base += (uint64_t)nbx * kThreads) {
       const uint64_t i = base + threadIdx.x;
       bool want = false;
       uint32_t v = 0, u = 0;
@@ -2144,7 +2156,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
     }
   }
   drain_atomics();
-  if (last_block(&V.st->done_blocks[1], (gridDim.x - (pipe ? 1u : 0u)) * gridDim.y) && threadIdx.x == 0) {
+  if (last_block(&V.st->done_blocks[1], nbx * gridDim.y) && threadIdx.x == 0) {
     spec_round_end(V, it, c.sides, c.cont);
     atomicExch(&V.st->done_blocks[1], 0u);
     if (rs) rs->ce = __builtin_amdgcn_s_memrealtime();
@@ -2425,8 +2437,11 @@ __global__ __launch_bounds__(kThreads) void k_path_edges(DView V, const uint32_t
 
 // Pack this rank's claimed (vertex, parent) pairs of both sides: one block of
 // {count_S, count_T, S pairs[capS], T pairs[capT]} (the queues hold exactly
-// the claimed owned vertices).
-__global__ void k_pack_parents(DView V, uint32_t capS, uint32_t capT) {
+// the claimed owned vertices).  Only vertices up to the accounted depths dS /
+// dT: a pipelined search ends one round before its last executed round, whose
+// claims the final plan has not counted (capS / capT); they sit at the queue's
+// end (queues are in level order) and go out as empty pairs the walk skips.
+__global__ void k_pack_parents(DView V, uint32_t capS, uint32_t capT, uint32_t dS, uint32_t dT) {
   uint32_t* out = V.sendbuf;
   const uint32_t qn0 = V.st->qtail[0], qn1 = V.st->qtail[1];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -2440,7 +2455,8 @@ __global__ void k_pack_parents(DView V, uint32_t capS, uint32_t capT) {
     const uint32_t k = s ? (uint32_t)(i - qn0) : (uint32_t)i;
     if (k >= (s ? capT : capS)) continue;
     const uint32_t v = pick(V.queue, s)[k];
-    pr[(s ? capS : 0) + k] = make_uint2(v, pick(V.parent, s)[v - V.lo]);
+    const bool acc = pick(V.depth, s)[v - V.lo] <= (s ? dT : dS);
+    pr[(s ? capS : 0) + k] = acc ? make_uint2(v, pick(V.parent, s)[v - V.lo]) : make_uint2(kEmpty, kEmpty);
   }
 }
 
@@ -2472,13 +2488,18 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
     for (uint32_t i = threadIdx.x; i < c0 + c1; i += blockDim.x) {
       const int s = i < c0 ? 0 : 1;
       const uint2 x = pr[s ? capS + (i - c0) : i];
+      if (x.x == kEmpty) continue;  // claimed after the accounted depth (k_pack_parents)
       uint32_t h = home(s, x.x);
-      while (true) {
+      bool placed = false;
+      for (uint32_t probe = 0; probe < nslot(s); ++probe) {  // (bounded: a full table ends the walk as not found)
         const uint32_t prev = atomicCAS(&keys(s)[2 * h], kEmpty, x.x);
-        if (prev == kEmpty || prev == x.x) break;
+        if (prev == kEmpty || prev == x.x) {
+          placed = true;
+          break;
+        }
         h = next(s, h);
       }
-      keys(s)[2 * h + 1] = x.y;
+      if (placed) keys(s)[2 * h + 1] = x.y;
     }
   }
   __syncthreads();
@@ -2623,8 +2644,8 @@ unsigned blocks_for(uint64_t work, int cus) {
 
 uint32_t next_pow2(uint64_t x) {
   uint64_t p = 1;
-  while (p < x) p <<= 1;
-  return (uint32_t)std::min<uint64_t>(p, 1ull << 31);
+  while (p < x && p < (1ull << 31)) p <<= 1;
+  return (uint32_t)p;
 }
 
 }  // namespace
@@ -3306,7 +3327,10 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   const bool solo = P == 1 && tune.solo && tune.spec_rounds > 0;
   if (!solo) k_seed<<<1, 64, 0, cs>>>(V, src, dst);  // (the solo workgroup seeds itself)
   // (the pipelined planner reduces every rank's header in LDS: up to kStageRanks ranks)
-  const bool pipe_start = P > 1 && P <= kStageRanks && tune.pipeline && tune.spec_rounds > 0 && !pipe_off;
+  // (a lookahead of one round only: the drain accounts the round the first
+  // stalled plan left pending, which deeper no-op tails would overwrite)
+  const bool pipe_start =
+      P > 1 && P <= kStageRanks && tune.pipeline && tune.spec_rounds == 1 && max_deg <= kPipeMaxDeg && !pipe_off;
   if (P > 1 && !pipe_start) {  // (pipelined: the seed's reduction rides round 0's exchange)
     comm->allgather(&V.red[1], V.redg[1], sizeof(Reduced), cs);
     stats.collectives++;
@@ -3326,6 +3350,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   // pipeline and the search continues with exact plans.
   bool pipe = pipe_start;
   bool pipe_used = pipe;
+  stats.pipelined = pipe ? 1 : 0;
   const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
   if (host_only) {
     final_and_wait(it++, pol, kPlanStall, cs);
@@ -3413,7 +3438,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         // owner blocks: the largest per-owner count of round need - 1, grown
         // over the K + 1 rounds since, with half again as slack; too small
         // costs a continuation round, too big only bytes
-        const uint64_t om = __atomic_load_n(&h_aux[need % kPlanRing], __ATOMIC_ACQUIRE);
+        const uint64_t om = std::min<uint64_t>(__atomic_load_n(&h_aux[need % kPlanRing], __ATOMIC_ACQUIRE), spec_max);
         uint64_t op = om;
         for (int j = 0; j <= K + lag && op < cap_it; ++j) op *= g;
         ocap = std::min<uint32_t>(cap_it, std::max<uint32_t>(kOwnerCapMin, next_pow2(op + op / 2 + 16)));
@@ -3613,7 +3638,7 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   // sized before the collective (every rank knows `hops`): a failing
   // allocation aborts the communicator before, not between, collectives
   ensure_path_dev((size_t)hops + 5);
-  k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(V, capS, capT);
+  k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(V, capS, capT, h.depth[0], h.depth[1]);
   const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
   comm->allgather(V.sendbuf, V.recvbuf, blk * 4, cs);
   stats.collectives++;

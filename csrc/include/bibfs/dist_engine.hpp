@@ -71,6 +71,7 @@ struct DistLevelStats {
   int path_collectives = 0;        // collectives spent reconstructing the path
   int solo_rounds = 0;             // rounds run by the one-workgroup solo kernel (one rank)
   int cont_rounds = 0;             // continuation rounds: candidates that overflowed an owner block re-offered
+  int pipelined = 0;               // 1: the search started with pipelined plans (DistTuning::pipeline, no hubs)
   int pipe_drains = 0;             // pipelined searches that stalled and continued with exact plans
   int pipe_retries = 0;            // pipelined searches answered again with exact plans (a spill list overflowed)
   int single_engine = 0;           // world size 1: answered by the single-GPU engine (DistTuning::world1_single)
@@ -105,8 +106,8 @@ struct DistTuning {
                                    // host-planned round (0 = only when the spill lists could overflow)
   bool pipeline = true;            // > 1 rank: ONE collective per speculative round -- each round's reduction
                                    // travels with the next round's candidate exchange and every plan accounts
-                                   // the round before the last; false = exact plans, a status
-                                   // allgather per round
+                                   // the round before the last (with spec_rounds == 1 only);
+                                   // false = exact plans, a status allgather per round
   size_t hbm_cap_bytes = 0;        // > 0: a build that would make this rank hold more device memory throws
                                    // (tests: rehearse "does not fit one GPU" at small scale)
   bool world1_single = true;       // one rank: answer queries with the single-GPU engine over this rank's device

@@ -89,6 +89,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["path_collectives"] = s.path_collectives;
   d["solo_rounds"] = s.solo_rounds;
   d["cont_rounds"] = s.cont_rounds;
+  d["pipelined"] = s.pipelined;
   d["pipe_drains"] = s.pipe_drains;
   d["pipe_retries"] = s.pipe_retries;
   d["exchanged_bytes"] = s.exchanged_bytes;

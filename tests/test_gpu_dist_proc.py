@@ -80,7 +80,8 @@ def test_processes_follow_protocol_spec():
         for (s, d), r, x in zip(qs, rs, lst):
             # pipelined rounds (the default with 3 ranks): the spec's lagged side
             # choice, unless the search drained to exact plans (hops checked)
-            piped = tune.get("pipeline", True)
+            piped = bool(x["pipelined"])
+            assert piped == tune.get("pipeline", True), (s, d, opts, tune)
             want, hops = round_trace(g.csr, s, d, side=opts.get("side", "edges"), lockstep=opts.get("lockstep", True),
                                      pipelined=piped)
             if piped and (x["pipe_drains"] or x["host_rounds"]):
