@@ -618,8 +618,12 @@ def main(argv=None) -> int:
             q0 = time.perf_counter()
             lean(warmup + i)
             qt.append(time.perf_counter() - q0)
+        # (the loop's end, as for the single-GPU loop above: every query is a
+        # collective search, so the ranks leave it together; the barrier after
+        # it -- an allreduce and the engine's streams drained -- is not a query)
+        t_end = time.perf_counter()
         eng.barrier()
-        dt = max_over_ranks(time.perf_counter() - t0)
+        dt = max_over_ranks(t_end - t0)
         # the same queries again, untimed, for the per-query statistics
         done = []
         for i in range(steps):

@@ -156,21 +156,37 @@ struct LocalGroup {
   int arrived = 0;
   uint64_t gen = 0;
   bool aborted = false;
+  std::atomic<uint64_t> gen_pub{0};  // gen / aborted, readable without the mutex (the spin)
+  std::atomic<bool> aborted_pub{false};
   std::vector<Slot> slot;
 
+  // Ranks arrive within microseconds of each other every round: a waiter
+  // spins on the generation for up to kSpinUs before it sleeps on the
+  // condition variable (a futex wake-up costs more than the round's kernels).
+  static constexpr double kSpinUs = 200.0;
   void barrier() {
     std::unique_lock<std::mutex> lk(mu);
     if (aborted) throw Error("local group aborted by another rank");
     const uint64_t g = gen;
     if (++arrived == P) {
       arrived = 0;
-      ++gen;
+      gen_pub.store(++gen, std::memory_order_release);
       cv.notify_all();
       return;
     }
+    lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t k = 0;; ++k) {
+      if (gen_pub.load(std::memory_order_acquire) != g || aborted_pub.load(std::memory_order_acquire)) break;
+      if ((k & 255) == 255 &&
+          std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > kSpinUs)
+        break;
+    }
+    lk.lock();
     const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
     if (!cv.wait_until(lk, deadline, [&] { return gen != g || aborted; })) {
       aborted = true;  // a peer never arrived: fail the whole group, not just this rank
+      aborted_pub.store(true, std::memory_order_release);
       cv.notify_all();
       throw Error("local group collective timed out after " + std::to_string(timeout_s) + " s");
     }
@@ -252,6 +268,43 @@ class LocalComm final : public Comm {
     exchange(send, recv, bytes, s, true);
   }
 
+  // In place: every rank's {send, ready} swapped as in exchange(), then the
+  // caller's kernels read the peers' blocks where they are; release records
+  // `done` behind them and orders this rank's next writes of its own send
+  // buffer after every peer's reads (the second half of exchange()).
+  void alltoall_view(const void* send, void* recv, size_t bytes, hipStream_t s, const void** peers) override {
+    LocalGroup& G = *g_;
+    if (G.P == 1) {
+      peers[0] = send;
+      return;
+    }
+    if (aborted_) throw Error("local group communicator was aborted after an earlier failure");
+    HIP_CHECK(hipEventRecord(ready_, s));
+    {
+      std::lock_guard<std::mutex> lk(G.mu);
+      G.slot[(size_t)rank_] = {send, ready_, done_};
+    }
+    G.barrier();
+    {
+      std::lock_guard<std::mutex> lk(G.mu);
+      view_peers_ = G.slot;
+    }
+    for (int r = 0; r < G.P; ++r) {
+      if (r != rank_) HIP_CHECK(hipStreamWaitEvent(s, view_peers_[(size_t)r].ready, 0));
+      peers[r] = static_cast<const char*>(view_peers_[(size_t)r].src) + (size_t)rank_ * bytes;
+    }
+    in_view_ = true;
+  }
+  void alltoall_release(hipStream_t s) override {
+    if (!in_view_) return;
+    in_view_ = false;
+    LocalGroup& G = *g_;
+    HIP_CHECK(hipEventRecord(done_, s));
+    G.barrier();  // every rank's reads enqueued and its `done` recorded
+    for (int r = 0; r < G.P; ++r)
+      if (r != rank_) HIP_CHECK(hipStreamWaitEvent(s, view_peers_[(size_t)r].done, 0));
+  }
+
   void abort() override {
     aborted_ = true;
     abort_local_group(*g_);
@@ -298,6 +351,8 @@ class LocalComm final : public Comm {
   void* scratch_ = nullptr;
   size_t scratch_bytes_ = 0;
   bool aborted_ = false;
+  std::vector<LocalGroup::Slot> view_peers_;  // alltoall_view -> alltoall_release
+  bool in_view_ = false;
 };
 
 }  // namespace
@@ -327,6 +382,7 @@ std::unique_ptr<Comm> make_local_comm(std::shared_ptr<LocalGroup> g, int rank) {
 void abort_local_group(LocalGroup& g) {
   std::lock_guard<std::mutex> lk(g.mu);
   g.aborted = true;
+  g.aborted_pub.store(true, std::memory_order_release);
   g.cv.notify_all();
 }
 

@@ -50,6 +50,17 @@ class Comm {
   // Owner-addressed exchange: send = P blocks of `bytes` (block r goes to rank
   // r), recv = P blocks (block r came from rank r); device memory.
   virtual void alltoall(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+  // The same exchange read in place where the transport can: `peers[r]` (P
+  // entries) is set to a device pointer to the block rank r addressed to this
+  // rank, readable by work enqueued on `s` until alltoall_release(s); the
+  // caller leaves `send` untouched until then.  Default: alltoall into `recv`
+  // and point into it.  The local group points straight into the peers' send
+  // buffers: no copy at all.
+  virtual void alltoall_view(const void* send, void* recv, size_t bytes, hipStream_t s, const void** peers) {
+    alltoall(send, recv, bytes, s);
+    for (int r = 0; r < size(); ++r) peers[r] = static_cast<const char*>(recv) + (size_t)r * bytes;
+  }
+  virtual void alltoall_release(hipStream_t s) {}
   // Throw if the communicator reported an asynchronous error (peer failure).
   virtual void check() {}
   // Abort every outstanding and future collective of this communicator

@@ -677,15 +677,29 @@ __device__ void write_owner_headers(const DView& V, uint32_t cap, uint32_t it, i
   }
 }
 
+// Where a claim kernel reads the exchange: rank r's block for this rank (its
+// header, then both sides' candidate blocks).  direct: the transport's
+// in-place view (Comm::alltoall_view -- the local group points into the
+// peers' send buffers, nothing is copied); else the copy in recvbuf.
+struct PeerTab {
+  const uint32_t* p[kStageRanks];
+  int direct;
+};
+__device__ __forceinline__ const uint32_t* peer_at(const DView& V, const PeerTab& pt, uint32_t r, uint32_t cap) {
+  return pt.direct ? pt.p[r] : V.recvbuf + (uint64_t)r * peer_words(cap);
+}
+// side s's candidate block inside a peer's block
+__device__ __forceinline__ uint64_t pblock(int s, uint32_t cap) { return kHdrWords + (uint64_t)s * block_words(cap); }
+
 // Pipelined rounds, claim kernel: every peer's header -- its reduction of
 // round it - 1 -- into the gathered slot of that round (what the round's
 // separate allgather delivers in exact mode), read by the plan of round it + 1.
-__device__ void scatter_peer_headers(const DView& V, uint32_t cap, uint32_t it) {
+__device__ void scatter_peer_headers(const DView& V, uint32_t cap, uint32_t it, const PeerTab& pt) {
   constexpr uint32_t kRedW = sizeof(Reduced) / 4;
   uint32_t* g = reinterpret_cast<uint32_t*>(V.redg[(it - 1u) & 1u]);
   for (uint32_t t = threadIdx.x; t < (uint32_t)V.P * kRedW; t += blockDim.x) {
     const uint32_t r = t / kRedW, w = t % kRedW;
-    g[t] = V.recvbuf[(uint64_t)r * peer_words(cap) + w];
+    g[t] = peer_at(V, pt, r, cap)[w];
   }
 }
 
@@ -934,7 +948,8 @@ struct SmallStage {
 __device__ void small_prefetch(const DView& V, const uint32_t* fr, SmallStage& S, uint32_t t, uint32_t nt);
 __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t ocap, const uint32_t* fr,
                              SmallStage& S, RoundStamp* rs, int pipe);
-__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs, int pipe);
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs, int pipe,
+                                  const PeerTab& pt);
 __device__ __forceinline__ bool small_expand_ok(const Ctl& c, int P) {
   if (c.cont || !c.sides || P > kStageRanks) return false;
   for (int s = 0; s < 2; ++s)
@@ -1849,7 +1864,8 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
 // The claims of a small round by block (0, 0) of k_spec_claim: every sender's
 // block of both sides, then the round's end (spec_round_end's bookkeeping,
 // from the LDS counters -- one thread, plain accesses).
-__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs, int pipe) {
+__device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uint32_t cap, RoundStamp* rs, int pipe,
+                                  const PeerTab& pt) {
   __shared__ uint32_t cnt[2 * kStageRanks + 1];
   __shared__ SmallCtr K;
   __shared__ uint32_t qbase[2], fend0[2], spn[2], ocm;
@@ -1858,7 +1874,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
   const int p = it & 1;
   const int P = V.P;
   DState* st = V.st;
-  if (pipe) scatter_peer_headers(V, cap, it);
+  if (pipe) scatter_peer_headers(V, cap, it, pt);
   if (tid < 2) {
     qbase[tid] = st->qtail[tid];
     K.q[tid] = 0;
@@ -1878,7 +1894,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
   // item space: side 0's P blocks, then side 1's (a side that did not expand: 0)
   if (tid < 2u * P) {
     const uint32_t s = tid / P;
-    cnt[tid] = ((c.sides >> s) & 1) ? min(V.recvbuf[oblock((int)s, tid % P, cap)], cap) : 0u;
+    cnt[tid] = ((c.sides >> s) & 1) ? min(peer_at(V, pt, tid % P, cap)[pblock((int)s, cap)], cap) : 0u;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1914,7 +1930,7 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
           else z = mid;
         }
         ss[k] = (int)(a / P);
-        x[k] = reinterpret_cast<const uint2*>(V.recvbuf + oblock((int)(a / P), a % P, cap))[1 + (i - cnt[a])];
+        x[k] = reinterpret_cast<const uint2*>(peer_at(V, pt, a % P, cap) + pblock((int)(a / P), cap))[1 + (i - cnt[a])];
       }
     }
 #pragma unroll
@@ -2081,14 +2097,15 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
 
 // Pipelined rounds: plan round it + 1 in the claim kernel of round it (one
 // block; see k_spec_claim) and publish it as k_spec_expand would.
-__device__ void plan_next_round(const DView& V, uint32_t it, uint32_t cap, const Policy& pol, uint32_t plan_cap) {
+__device__ void plan_next_round(const DView& V, uint32_t it, uint32_t cap, const Policy& pol, uint32_t plan_cap,
+                                const PeerTab& pt) {
   constexpr uint32_t kRedW = sizeof(Reduced) / 4;
   __shared__ Ctl prev, c;
   __shared__ Reduced rd;
   __shared__ uint32_t gw[kStageRanks * kRedW];
   stage_words(&prev, &V.ctl[it & 1], sizeof(Ctl));
   for (uint32_t t = threadIdx.x; t < (uint32_t)V.P * kRedW; t += blockDim.x)
-    gw[t] = V.recvbuf[(uint64_t)(t / kRedW) * peer_words(cap) + t % kRedW];
+    gw[t] = peer_at(V, pt, t / kRedW, cap)[t % kRedW];
   __syncthreads();
   if (threadIdx.x == 0) {
     reduce_gathered(reinterpret_cast<const Reduced*>(gw), V.P, rd);
@@ -2104,14 +2121,14 @@ __device__ void plan_next_round(const DView& V, uint32_t it, uint32_t cap, const
 // workgroup closes the round.  pipe: block (0, 0) also moves the reduction
 // headers the exchange carried into the gathered slot of round it - 1.)
 __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap, int pipe, Policy pol,
-                                                         uint32_t plan_cap) {
+                                                         uint32_t plan_cap, PeerTab pt) {
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   if (pipe && blockIdx.x == gridDim.x - 1) {
     // Pipelined rounds: the extra block plans round it + 1 while the others
     // claim round it -- its inputs (this round's plan, every rank's reduction
     // of round it - 1 in the exchange's headers) are all here, and the claims
     // do not change them -- so the next expansion starts with its plan ready.
-    if (blockIdx.y == 0) plan_next_round(V, it, cap, pol, plan_cap);
+    if (blockIdx.y == 0) plan_next_round(V, it, cap, pol, plan_cap, pt);
     return;
   }
   const Ctl& c = V.ctl[it & 1];
@@ -2121,7 +2138,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   if (small_claim_ok(c, V.P)) {  // small round: one workgroup claims and closes it
     if (blockIdx.x == 0 && blockIdx.y == 0) {
       if (rs && threadIdx.x == 0) rs->small |= 2u;
-      small_claim_round(V, c, it, cap, rs, pipe);
+      small_claim_round(V, c, it, cap, rs, pipe, pt);
       if (rs) {
         __syncthreads();
         if (threadIdx.x == 0) rs->ce = __builtin_amdgcn_s_memrealtime();
@@ -2130,7 +2147,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
     return;
   }
   const int s = blockIdx.y;
-  if (pipe && blockIdx.x == 0 && s == 0) scatter_peer_headers(V, cap, it);
+  if (pipe && blockIdx.x == 0 && s == 0) scatter_peer_headers(V, cap, it, pt);
   const uint32_t nbx = gridDim.x - (pipe ? 1u : 0u);  // the claiming blocks (pipelined: not the planner's column)
   // a continuation side claims at the depth its level already has
   const uint32_t dnew = ((c.sides >> s) & 1) ? c.xdepth[s] + 1 : c.xdepth[s];
@@ -2139,7 +2156,7 @@ __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, u
   cm.dclaim = ((c.sides >> (s ^ 1)) & 1) ? c.xdepth[s ^ 1] + 1 : c.xdepth[s ^ 1];
   cm.single = c.sides != 3u;
   for (int r = 0; (((c.sides | c.cont) >> s) & 1) && r < V.P; ++r) {  // block-uniform
-    const uint32_t* b = V.recvbuf + oblock(s, (uint32_t)r, cap);
+    const uint32_t* b = peer_at(V, pt, (uint32_t)r, cap) + pblock(s, cap);
     const uint32_t cnt = min(b[0], cap);
     const uint2* pr = reinterpret_cast<const uint2*>(b) + 1;
     for (uint64_t base = (uint64_t)blockIdx.x * kThreads; base < cnt; base += (uint64_t)nbx * kThreads) {
@@ -2481,25 +2498,39 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
   }
   __syncthreads();
   const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
+  // kU pairs per thread loaded before any is inserted: the loads of a pass
+  // are in flight together (one pair per iteration left every iteration a
+  // dependent global round trip: ~50 us for a G(1M) path at P = 2)
+  constexpr int kU = 8;
   for (int r = 0; r < P; ++r) {
     const uint32_t* b = recv + (uint64_t)r * blk;
     const uint32_t c0 = b[0], c1 = b[1];
     const uint2* pr = reinterpret_cast<const uint2*>(b + 2);
-    for (uint32_t i = threadIdx.x; i < c0 + c1; i += blockDim.x) {
-      const int s = i < c0 ? 0 : 1;
-      const uint2 x = pr[s ? capS + (i - c0) : i];
-      if (x.x == kEmpty) continue;  // claimed after the accounted depth (k_pack_parents)
-      uint32_t h = home(s, x.x);
-      bool placed = false;
-      for (uint32_t probe = 0; probe < nslot(s); ++probe) {  // (bounded: a full table ends the walk as not found)
-        const uint32_t prev = atomicCAS(&keys(s)[2 * h], kEmpty, x.x);
-        if (prev == kEmpty || prev == x.x) {
-          placed = true;
-          break;
-        }
-        h = next(s, h);
+    for (uint32_t base = 0; base < c0 + c1; base += kU * blockDim.x) {
+      uint2 xs[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const uint32_t i = base + k * blockDim.x + threadIdx.x;
+        xs[k] = i < c0 + c1 ? pr[i < c0 ? i : capS + (i - c0)] : make_uint2(kEmpty, kEmpty);
       }
-      if (placed) keys(s)[2 * h + 1] = x.y;
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const uint32_t i = base + k * blockDim.x + threadIdx.x;
+        const uint2 x = xs[k];
+        if (x.x == kEmpty) continue;  // past the count, or claimed after the accounted depth (k_pack_parents)
+        const int s = i < c0 ? 0 : 1;
+        uint32_t h = home(s, x.x);
+        bool placed = false;
+        for (uint32_t probe = 0; probe < nslot(s); ++probe) {  // (bounded: a full table ends the walk as not found)
+          const uint32_t prev = atomicCAS(&keys(s)[2 * h], kEmpty, x.x);
+          if (prev == kEmpty || prev == x.x) {
+            placed = true;
+            break;
+          }
+          h = next(s, h);
+        }
+        if (placed) keys(s)[2 * h + 1] = x.y;
+      }
     }
   }
   __syncthreads();
@@ -3477,10 +3508,20 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         // reduction header and both sides' candidate blocks (oblock); each
         // rank receives only what is addressed to it.  Pipelined, the header
         // is the round's status too: no second collective.
-        comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
+        // (read in place where the transport allows: no copy on the local group)
+        PeerTab pt{};
+        if (P <= kStageRanks) {
+          const void* pv[kStageRanks];
+          comm->alltoall_view(V.sendbuf, V.recvbuf, peer_bytes, cs, pv);
+          for (int r = 0; r < P; ++r) pt.p[r] = static_cast<const uint32_t*>(pv[r]);
+          pt.direct = 1;
+        } else {
+          comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
+        }
         // (pipelined: one extra block plans the next round beside the claims)
-        k_spec_claim<<<dim3(cx + (pipe ? 1u : 0u), 2), kThreads, 0, cs>>>(V, it, ocap, pp, pol, plan_cap);
+        k_spec_claim<<<dim3(cx + (pipe ? 1u : 0u), 2), kThreads, 0, cs>>>(V, it, ocap, pp, pol, plan_cap, pt);
         HIP_CHECK(hipGetLastError());
+        if (P <= kStageRanks) comm->alltoall_release(cs);
         stats.collectives++;
         stats.exchanged_bytes += peer_bytes * (P - 1);
         if (!pipe) {  // exact plans: the round's reduction, every rank's values gathered, reduced by the reader
