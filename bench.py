@@ -361,7 +361,17 @@ def main(argv=None) -> int:
         if a.dist_backend == "nccl":
             dist.init_process_group(backend="nccl", device_id=dev)
         else:
-            dist.init_process_group(backend="gloo")
+            # gloo prints its connection report on fd 1: keep it off the JSON
+            # line's stream (the rendezvous and first collective, on stderr)
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group(backend="gloo")
+                dist.barrier()
+            finally:
+                os.dup2(saved, 1)
+                os.close(saved)
 
     from bidirectional_bfs_amd.ops import HipEngine
     from bidirectional_bfs_amd.parallel import DistEngine
