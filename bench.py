@@ -44,6 +44,7 @@ import os
 import random
 import socket
 import subprocess
+import statistics
 import sys
 import threading
 import time
@@ -210,6 +211,7 @@ def partitioned_top(partitioned: dict) -> dict:
         "partitioned_config": PARTITIONED_HEADLINE,
         "partitioned_ms_per_query": p["ms_per_query"] if ok else None,
         "partitioned_speedup_vs_single_gpu": p.get("speedup_vs_single_gpu") if ok else None,
+        "partitioned_speedup_vs_single_gpu_median": p.get("speedup_vs_single_gpu_median") if ok else None,
         "partitioned_gteps": round(p["gteps"], 4) if ok and p.get("gteps") is not None else None,
         "partitioned_collectives_per_round": p.get("collectives_per_round") if ok else None,
         "partitioned_verified": p.get("verified") if ok else None,
@@ -561,7 +563,7 @@ def main(argv=None) -> int:
         _, n, _, seed = parse_spec(spec)
         hbm_total = torch.cuda.mem_get_info(dev)[1]
         fits = csr_bytes(spec) <= 0.6 * hbm_total
-        single_ms, single_reason, pairs = None, None, None
+        single_ms, single_med_ms, single_reason, pairs = None, None, None, None
         npairs = min(a.pairs, steps + warmup)
         if fits:
             ref = generate(HipEngine(local), spec)
@@ -573,10 +575,14 @@ def main(argv=None) -> int:
             for i in range(warmup):
                 ref.query(*pairs[i % len(pairs)][:2])
             ts = time.perf_counter()
+            sq = []
             for i in range(steps):
                 s_, d_, h_ = pairs[(warmup + i) % len(pairs)]
+                q0 = time.perf_counter()
                 assert ref.query(s_, d_)[0] == h_
+                sq.append(time.perf_counter() - q0)
             single_ms = max_over_ranks((time.perf_counter() - ts) * 1e3 / steps)
+            single_med_ms = max_over_ranks(statistics.median(sq) * 1e3)
             ref.set_resident(False)
             ref.release()
             del ref
@@ -661,6 +667,11 @@ def main(argv=None) -> int:
             "max_query_ms_rank0": round(max(qt) * 1e3, 5),
             "single_gpu_ms": round(single_ms, 5) if single_ms is not None else None,
             "speedup_vs_single_gpu": round(single_ms / (dt * 1e3 / steps), 4) if single_ms is not None else None,
+            # the same ratio on medians (max over ranks of each rank's median):
+            # one multi-millisecond outlier in 20 timed queries moves the means
+            "single_gpu_median_ms": round(single_med_ms, 5) if single_med_ms is not None else None,
+            "speedup_vs_single_gpu_median": (round(single_med_ms / max_over_ranks(statistics.median(qt) * 1e3), 4)
+                                             if single_med_ms is not None else None),
             "single_gpu_reason": single_reason,
             "gteps": m * steps / dt / 1e9,
             "device_ms_per_query": round(sum(r.search_ms for r, _ in done) / steps, 5),
