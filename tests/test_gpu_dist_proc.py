@@ -81,7 +81,8 @@ def test_processes_follow_protocol_spec():
             # pipelined rounds (the default with 3 ranks): the spec's lagged side
             # choice, unless the search drained to exact plans (hops checked)
             piped = bool(x["pipelined"])
-            assert piped == tune.get("pipeline", True), (s, d, opts, tune)
+            if s != d:  # (src == dst is answered without a round)
+                assert piped == tune.get("pipeline", True), (s, d, opts, tune)
             want, hops = round_trace(g.csr, s, d, side=opts.get("side", "edges"), lockstep=opts.get("lockstep", True),
                                      pipelined=piped)
             if piped and (x["pipe_drains"] or x["host_rounds"]):
