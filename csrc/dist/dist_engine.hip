@@ -547,6 +547,24 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
 // visible yet, so the depth is its frontier depth + 1.  single: a
 // single-side level, where every meet has the same length, so the first one
 // also raises DState::meet_found and the expansion loops stop early.
+// Last index a in [0, n) with pre[a] <= x, for ascending pre with pre[0] <= x:
+// binary lifting over a uniform trip count (`top`: the largest power of two
+// below n, computed once from a bound every lane shares).  The `while (z - a
+// > 1)` loops this replaces exit per lane, and the compiler drained every
+// outstanding global load (s_waitcnt vmcnt(0)) at that divergent exit -- once
+// per item of a pass, so a pass's loads and claim atomics ran one at a time.
+__device__ __forceinline__ uint32_t lift_top(uint32_t n) { return n > 1 ? 1u << (31 - __clz(n - 1)) : 0u; }
+template <typename T, typename X>
+__device__ __forceinline__ uint32_t lift_search(const T* pre, uint32_t n, X x, uint32_t top) {
+  uint32_t a = 0;
+  for (uint32_t step = top; step; step >>= 1) {
+    const uint32_t c = a + step;
+    const T pc = pre[c < n ? c : n - 1];
+    a = (c < n && pc <= x) ? c : a;
+  }
+  return a;
+}
+
 struct ClaimMeet {
   unsigned long long* meetkey = nullptr;
   uint32_t dclaim = 0;  // the depth the other side's claims of this round get (its kEmpty depth reads)
@@ -806,12 +824,7 @@ __device__ void td_expand_side(const DView& V, int s, uint32_t dnew, uint2* pair
       uint32_t uu = 0, v = 0;
       unsigned long long prb = 0, pre_ = 0;
       if (valid) {
-        uint32_t a = 0, z = kThreads;  // last slot whose edge range starts at or before e
-        while (z - a > 1) {
-          const uint32_t mid = (a + z) >> 1;
-          if (se[mid] <= e) a = mid;
-          else z = mid;
-        }
+        const uint32_t a = lift_search(se, kThreads, e, kThreads / 2);  // last slot whose edge range starts at or before e
         uu = su[a];
         const unsigned long long k = sb[a] + (e - se[a]);
         if (V.padj) {  // one rank: the neighbour's row comes with its id
@@ -1382,12 +1395,8 @@ __global__ __launch_bounds__(kSoloT, 1) void k_spec_solo(DView V, uint32_t it0, 
         const int sd = e >= E0;
         ss[j] = sd;
         const uint32_t k = ok[j] ? (sd ? e - E0 : e) : 0u, b = cb[sd];
-        uint32_t a = 0, z = ok[j] ? (sd ? F1 : F0) : 1u;  // last slot whose edge range starts at or before k
-        while (z - a > 1) {
-          const uint32_t mid = (a + z) >> 1;
-          if (FP[sd][mid] <= k) a = mid;
-          else z = mid;
-        }
+        // last slot whose edge range starts at or before k
+        const uint32_t a = lift_search(FP[sd], ok[j] ? (sd ? F1 : F0) : 1u, k, lift_top(max(F0, F1)));
         uu[j] = FV[b][sd][a];
         ad[j] = FB[b][sd][a] + (k - FP[sd][a]);
       }
@@ -1643,20 +1652,34 @@ __device__ void small_scan(uint32_t* X, uint32_t cnt) {
 // the other side made in THIS round has (its depth store may not be visible).
 // One workgroup alone claims in these words during the launch: workgroup
 // scope (its L2) is enough, the kernel boundary publishes them.
-__device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const uint32_t* qbase, bool want, int s,
-                                            uint32_t v, uint32_t u, const uint32_t* dn, const uint32_t* dcl,
-                                            bool single) {
+// Split in two so a pass's items overlap: small_claim_issue sends the claim
+// atomic and the row-bound loads of one item (nothing reads them), and the
+// caller issues every item's (and every offer's) atomics before the first
+// small_claim reads a result -- one round trip per pass, not one per item.
+// (the row bounds are loaded beside the claim, independent of its result; a
+// loser's load is wasted)
+struct ClaimIn {
+  unsigned long long old = 0, rb = 0, re = 0;
+};
+__device__ __forceinline__ void small_claim_issue(const DView& V, bool want, int s, uint32_t v, ClaimIn& in) {
+  if (!want) return;
   const uint32_t li = v - V.lo;
   unsigned long long* const visw = reinterpret_cast<unsigned long long*>(V.vis[0]);
+  in.old = wg_fetch_or(visw + (li >> 5), 1ull << ((li & 31) + 32 * s));
+  in.rb = V.row_off[li];
+  in.re = V.row_off[li + 1];
+}
+__device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const uint32_t* qbase, bool want, int s,
+                                            uint32_t v, uint32_t u, const uint32_t* dn, const uint32_t* dcl,
+                                            bool single, const ClaimIn& in) {
+  const uint32_t li = v - V.lo;
   bool mine = false;
   unsigned long long rb = 0, re = 0, best = kNoKey;
   if (want) {
     const unsigned long long m = 1ull << ((li & 31) + 32 * s);
-    // the row bounds are loaded beside the claim (independent of its result:
-    // one dependent round trip fewer; a loser's load is wasted)
-    const unsigned long long old = wg_fetch_or(visw + (li >> 5), m);
-    rb = V.row_off[li];
-    re = V.row_off[li + 1];
+    const unsigned long long old = in.old;
+    rb = in.rb;
+    re = in.re;
     mine = !(old & m);
     const bool other = (old >> ((li & 31) + 32 * (s ^ 1))) & 1ull;
     if (mine) {
@@ -1701,11 +1724,14 @@ __device__ __forceinline__ void small_claim(const DView& V, SmallCtr& K, const u
 
 // Offer remote vertex v (parent u) of side s to its owner: once per search
 // (the `sent` bit, workgroup scope), into the owner's block or the spill list.
+// (issued with the claims: small_emit_issue returns the old `sent` word)
+__device__ __forceinline__ uint32_t small_emit_issue(const DView& V, bool want, int s, uint32_t v) {
+  return want ? wg_fetch_or32(&pick(V.sent, s)[v >> 5], 1u << (v & 31)) : 0u;
+}
 __device__ __forceinline__ void small_emit(const DView& V, SmallCtr& K, const uint32_t* spbase, const uint32_t* lst,
-                                           bool want, int s, uint32_t v, uint32_t u, uint32_t ocap) {
+                                           bool want, int s, uint32_t v, uint32_t u, uint32_t ocap, uint32_t old) {
   if (!want) return;
-  const uint32_t bit = 1u << (v & 31);
-  if (wg_fetch_or32(&pick(V.sent, s)[v >> 5], bit) & bit) return;
+  if (old & (1u << (v & 31))) return;
   const uint32_t o = v / V.chunk;
   const uint32_t pos = atomicAdd(&K.oc[s][o], 1u);
   if (pos < ocap) {
@@ -1821,22 +1847,25 @@ __device__ void small_expand(const DView& V, const Ctl& c, uint32_t it, uint32_t
       vv[k] = uu[k] = 0;
       ss[k] = 0;
       if (ok[k]) {
-        uint32_t a = 0, z = nv;  // last vertex whose edge range starts at or before e
-        while (z - a > 1) {
-          const uint32_t mid = (a + z) >> 1;
-          if (se[mid] <= e) a = mid;
-          else z = mid;
-        }
+        const uint32_t a = lift_search(se, nv, e, lift_top(nv));  // last vertex whose edge range starts at or before e
         ss[k] = a >= F0;
         uu[k] = su[a];
         vv[k] = V.col[sb[a] + (e - se[a])];
       }
     }
+    bool own[kSmallU];
+    ClaimIn ci[kSmallU];
+    uint32_t so[kSmallU];
+#pragma unroll
+    for (int k = 0; k < kSmallU; ++k) {  // every item's claim / offer atomic in flight together
+      own[k] = ok[k] && vv[k] >= V.lo && vv[k] < V.hi;
+      small_claim_issue(V, own[k], ss[k], vv[k], ci[k]);
+      so[k] = small_emit_issue(V, ok[k] && !own[k], ss[k], vv[k]);
+    }
 #pragma unroll
     for (int k = 0; k < kSmallU; ++k) {
-      const bool own = ok[k] && vv[k] >= V.lo && vv[k] < V.hi;
-      small_claim(V, K, qbase, own, ss[k], vv[k], uu[k], dn, dcl, single);
-      small_emit(V, K, spbase, lst, ok[k] && !own, ss[k], vv[k], uu[k], ocap);
+      small_claim(V, K, qbase, own[k], ss[k], vv[k], uu[k], dn, dcl, single, ci[k]);
+      small_emit(V, K, spbase, lst, ok[k] && !own[k], ss[k], vv[k], uu[k], ocap, so[k]);
     }
   }
   __syncthreads();
@@ -1923,21 +1952,20 @@ __device__ void small_claim_round(const DView& V, const Ctl& c, uint32_t it, uin
       ss[k] = 0;
       x[k] = make_uint2(0, 0);
       if (ok[k]) {
-        uint32_t a = 0, z = 2 * P;  // the block holding item i
-        while (z - a > 1) {
-          const uint32_t mid = (a + z) >> 1;
-          if (cnt[mid] <= i) a = mid;
-          else z = mid;
-        }
+        const uint32_t a = lift_search(cnt, 2 * P, i, lift_top(2 * P));  // the block holding item i
         ss[k] = (int)(a / P);
         x[k] = reinterpret_cast<const uint2*>(peer_at(V, pt, a % P, cap) + pblock((int)(a / P), cap))[1 + (i - cnt[a])];
       }
     }
+    bool want[kSmallU];
+    ClaimIn ci[kSmallU];
 #pragma unroll
-    for (int k = 0; k < kSmallU; ++k) {
-      const bool want = ok[k] && x[k].x >= V.lo && x[k].x < V.hi;
-      small_claim(V, K, qbase, want, ss[k], x[k].x, x[k].y, dn, dcl, single);
+    for (int k = 0; k < kSmallU; ++k) {  // every item's claim atomic in flight together
+      want[k] = ok[k] && x[k].x >= V.lo && x[k].x < V.hi;
+      small_claim_issue(V, want[k], ss[k], x[k].x, ci[k]);
     }
+#pragma unroll
+    for (int k = 0; k < kSmallU; ++k) small_claim(V, K, qbase, want[k], ss[k], x[k].x, x[k].y, dn, dcl, single, ci[k]);
   }
   __syncthreads();
   if (rs && tid == 0) rs->cx = __builtin_amdgcn_s_memrealtime();
@@ -2059,12 +2087,7 @@ __global__ __launch_bounds__(kThreads) void k_td_hubs(DView V, uint32_t it, int 
         const bool valid = e < tot;
         uint32_t uu = 0, v = 0;
         if (valid) {
-          uint32_t a = 0, z = nt;  // last hub whose edge range starts at or before e
-          while (z - a > 1) {
-            const uint32_t mid = (a + z) >> 1;
-            if (hp[mid] <= e) a = mid;
-            else z = mid;
-          }
+          const uint32_t a = lift_search(hp, nt, e, lift_top(nt));  // last hub whose edge range starts at or before e
           uu = hu[a];
           v = V.col[hb[a] + (e - hp[a])];
         }
