@@ -547,24 +547,8 @@ __device__ void publish(const DView& V, int p, const Ctl& prev, const Reduced& r
 // visible yet, so the depth is its frontier depth + 1.  single: a
 // single-side level, where every meet has the same length, so the first one
 // also raises DState::meet_found and the expansion loops stop early.
-// Last index a in [0, n) with pre[a] <= x, for ascending pre with pre[0] <= x:
-// binary lifting over a uniform trip count (`top`: the largest power of two
-// below n, computed once from a bound every lane shares).  The `while (z - a
-// > 1)` loops this replaces exit per lane, and the compiler drained every
-// outstanding global load (s_waitcnt vmcnt(0)) at that divergent exit -- once
-// per item of a pass, so a pass's loads and claim atomics ran one at a time.
-__device__ __forceinline__ uint32_t lift_top(uint32_t n) { return n > 1 ? 1u << (31 - __clz(n - 1)) : 0u; }
-template <typename T, typename X>
-__device__ __forceinline__ uint32_t lift_search(const T* pre, uint32_t n, X x, uint32_t top) {
-  uint32_t a = 0;
-  for (uint32_t step = top; step; step >>= 1) {
-    const uint32_t c = a + step;
-    const T pc = pre[c < n ? c : n - 1];
-    a = (c < n && pc <= x) ? c : a;
-  }
-  return a;
-}
-
+// (edge searches: dev::lift_search, device.hpp -- uniform trip count, no
+// divergent loop exit for the compiler to drain outstanding loads at)
 struct ClaimMeet {
   unsigned long long* meetkey = nullptr;
   uint32_t dclaim = 0;  // the depth the other side's claims of this round get (its kEmpty depth reads)

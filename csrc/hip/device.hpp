@@ -53,6 +53,24 @@ namespace dev {
 constexpr int kWave = 64;
 constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
+// Last index a in [0, n) with pre[a] <= x, for ascending pre with pre[0] <= x,
+// by binary lifting over a uniform trip count (`top`: the largest power of
+// two below n, from a bound every lane shares).  A `while (hi - lo > 1)`
+// search exits per lane, and the compiler drains every outstanding global
+// load and store (s_waitcnt vmcnt(0)) at that divergent exit -- so loads
+// issued for several items of a pass ran one after another.
+__device__ __forceinline__ uint32_t lift_top(uint32_t n) { return n > 1 ? 1u << (31 - __clz(n - 1)) : 0u; }
+template <typename T, typename X>
+__device__ __forceinline__ uint32_t lift_search(const T* pre, uint32_t n, X x, uint32_t top) {
+  uint32_t a = 0;
+  for (uint32_t step = top; step; step >>= 1) {
+    const uint32_t c = a + step;
+    const T pc = pre[c < n ? c : n - 1];
+    a = (c < n && pc <= x) ? c : a;
+  }
+  return a;
+}
+
 // Search status codes (DevState::status / HostResult::status)
 enum : uint32_t { kRunning = 0, kFound = 1, kNoPath = 2, kHandoff = 3, kError = 4 };
 

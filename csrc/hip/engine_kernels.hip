@@ -399,12 +399,7 @@ __device__ unsigned long long lds_meet_probe(const LdsParams<OffT>& P, int q, ui
       for (uint32_t j = 0; j < kProbeU; ++j) {
         const uint32_t e = base + j * kLdsThreads + (uint32_t)tid;
         ok[j] = e < Ec;
-        uint32_t lo = 0, hi = kLdsThreads;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (sEb[mid] <= e) lo = mid;
-          else hi = mid;
-        }
+        const uint32_t lo = lift_search(sEb, kLdsThreads, e, kLdsThreads / 2);
         uu[j] = su[lo];
         v[j] = ok[j] ? P.col[sbp[lo] + (OffT)(e - sEb[lo])] : 0u;  // every pass's loads in flight together
       }
@@ -2118,12 +2113,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_topdown(GridParams<OffT> 
       const bool valid = e < Ec;
       uint32_t uu = 0, v = 0, vdeg = ~0u;
       if (valid) {
-        uint32_t lo = 0, hi = kGridThreads;
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (sEb[mid] <= e) lo = mid;
-          else hi = mid;
-        }
+        const uint32_t lo = lift_search(sEb, kGridThreads, e, kGridThreads / 2);
         uu = sv[lo];
         const OffT k = sb[lo] + (OffT)(e - sEb[lo]);
         if (padj8) {  // small level: the neighbour's degree with its id
@@ -2231,12 +2221,7 @@ __global__ __launch_bounds__(kGridThreads) void k_grid_hubs(GridParams<OffT> P) 
       const bool valid = e < tot;
       uint32_t uu = 0, v = 0;
       if (valid) {
-        uint32_t a = 0, z = nt;  // last hub whose edge range starts at or before e
-        while (z - a > 1) {
-          const uint32_t mid = (a + z) >> 1;
-          if (hp[mid] <= e) a = mid;
-          else z = mid;
-        }
+        const uint32_t a = lift_search(hp, nt, e, lift_top(nt));  // last hub whose edge range starts at or before e
         uu = hu[a];
         v = P.col[hb[a] + (OffT)(e - hp[a])];
       }
