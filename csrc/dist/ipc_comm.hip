@@ -3,7 +3,9 @@
 // P ranks are P processes.  They may share one GPU -- the reference's own v4
 // launch shape, 4 MPI ranks on one machine's GPU (single_machine_bench.sh:9,52;
 // v4/Makefile:64 uses 6) -- or sit on different GPUs of a node, where the very
-// same loads read peer HBM over xGMI.  RCCL refuses two ranks on one device
+// same loads read peer HBM over xGMI (UNVERIFIED: only the one-GPU shape has
+// run; test_mpi_bibfs_ipc_transport_across_gpus needs a multi-GPU box).
+// RCCL refuses two ranks on one device
 // ("Duplicate GPU detected"), so this transport is what runs the partitioned
 // engine as separate processes (separate HIP contexts and address spaces,
 // cross-process collective order, abort between processes) on a one-GPU box,
