@@ -202,6 +202,30 @@ class IpcComm final : public Comm {
     leave(s);
   }
 
+  // In place: the stage and the rendezvous as alltoall, then the caller's
+  // kernels read every peer's block straight out of its mapped staging slot
+  // (this rank's own block out of `send`) -- no pull kernel, no copy into
+  // recv.  alltoall_release records `done` behind those readers, which is
+  // what the next collective's stage (same stream) and the peers' rewrite of
+  // this slot two collectives later are ordered after.
+  void alltoall_view(const void* send, void* recv, size_t bytes, hipStream_t s, const void** peers) override {
+    live();
+    if (size_ == 1) {
+      peers[0] = send;
+      return;
+    }
+    const int slot = enter(send, bytes * (size_t)size_, s);
+    const IpcSrc src = sources(slot);
+    for (int r = 0; r < size_; ++r)
+      peers[r] = (r == rank_ ? static_cast<const unsigned char*>(send) : src.p[r]) + (size_t)rank_ * bytes;
+    in_view_ = true;
+  }
+  void alltoall_release(hipStream_t s) override {
+    if (!in_view_) return;
+    in_view_ = false;
+    leave(s);
+  }
+
   void check() override { group_.check(); }
   void abort() override { group_.abort("aborted by rank " + std::to_string(rank_)); }
   bool aborted() const override { return group_.aborted(); }
@@ -392,6 +416,7 @@ class IpcComm final : public Comm {
   uint64_t* h_tag_ = nullptr;  // pinned: the last stage tag the device wrote
   uint64_t tag_seq_ = 0;
   bool stats_on_ = false;      // BIBFS_IPC_STATS=1: per-collective host timings on teardown
+  bool in_view_ = false;       // alltoall_view -> alltoall_release
   uint64_t n_coll_ = 0, ns_stream_ = 0, ns_meet_ = 0, ns_total_ = 0;
   clock::time_point t_enter_{};
 };
