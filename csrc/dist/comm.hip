@@ -305,6 +305,15 @@ class LocalComm final : public Comm {
       if (r != rank_) HIP_CHECK(hipStreamWaitEvent(s, view_peers_[(size_t)r].done, 0));
   }
 
+  // (no dev_window: the ranks' streams share this process's hardware queues,
+  // and a claim kernel spinning at the head of one would block the very peer
+  // kernel it waits for -- only ranks with queues of their own, the IPC
+  // transport's processes, order their exchange on the device)
+
+  void check() override {
+    if (g_->aborted_pub.load(std::memory_order_acquire)) throw Error("local group aborted by another rank");
+  }
+
   void abort() override {
     aborted_ = true;
     abort_local_group(*g_);

@@ -61,6 +61,23 @@ class Comm {
     for (int r = 0; r < size(); ++r) peers[r] = static_cast<const char*>(recv) + (size_t)r * bytes;
   }
   virtual void alltoall_release(hipStream_t s) {}
+  // Device-synchronised exchange window (collective: every rank calls it with
+  // the same `bytes`).  Each rank gets `bytes` of device memory whose first
+  // kWinFlagBytes hold its epoch flag, and device pointers to every peer's
+  // window that its kernels may read in place; ranks then order their
+  // exchanges by polling the peers' flags on the device, with no host
+  // rendezvous.  Only where every rank's memory is mapped on the caller's
+  // device and every rank has hardware queues of its own (IPC ranks that
+  // share one GPU: one process each).  False: not supported (RCCL; the local
+  // group, whose ranks' streams share one process's queues), nothing was
+  // allocated.  The window lives as long as the communicator.
+  static constexpr int kWinMax = 16;
+  static constexpr size_t kWinFlagBytes = 256;
+  struct Window {
+    void* mine = nullptr;
+    const void* peer[kWinMax] = {};
+  };
+  virtual bool dev_window(size_t bytes, Window& w) { return false; }
   // Throw if the communicator reported an asynchronous error (peer failure).
   virtual void check() {}
   // Abort every outstanding and future collective of this communicator

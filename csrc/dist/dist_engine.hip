@@ -693,6 +693,63 @@ __device__ __forceinline__ const uint32_t* peer_at(const DView& V, const PeerTab
 // side s's candidate block inside a peer's block
 __device__ __forceinline__ uint64_t pblock(int s, uint32_t cap) { return kHdrWords + (uint64_t)s * block_words(cap); }
 
+// Device-ordered exchange (DistTuning::dev_sync over Comm::dev_window): the
+// round's expansion writes this rank's window half (epoch & 1) and the claim
+// kernel reads the peers' halves in place once every peer's flag reached the
+// round's epoch -- no host rendezvous and no cross-stream event between the
+// two kernels.  A rank's flag is raised by its claim kernel, so it also says
+// that rank's claims of the epoch before are complete: the half a rank
+// rewrites two epochs later is no longer read by anyone.  The data were
+// written by the peers' previous kernels (the kernel boundary writes the
+// XCD L2s back); the waiter polls with agent-scope loads and then acquires
+// (L1 invalidate) before any load of them.  epoch 0 = off.
+constexpr unsigned kDevSyncBlocks = 8;  // widest claim grid (per side) that waits on the device
+struct DevSync {
+  const unsigned long long* peer_flag[kStageRanks];
+  unsigned long long* flag;       // this rank's (its window's first word)
+  unsigned long long epoch;
+  unsigned long long limit;       // s_memrealtime ticks a wait may take (the host's timeout)
+  const uint32_t* h_abort;        // pinned: set when the host gave up on the search
+  int P;
+};
+
+// Thread 0 of a block: raise this rank's flag (block (0, 0) only), wait for
+// every peer's, acquire.  False: the wait ran out or the host aborted (the
+// block must leave without reading the exchange; the host throws).
+__device__ bool dev_sync_wait(const DevSync& ds) {
+  if (blockIdx.x == 0 && blockIdx.y == 0) __hip_atomic_store(ds.flag, ds.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  bool ok = true;
+  for (int r = 0; r < ds.P && ok; ++r) {
+    for (uint32_t k = 1; __hip_atomic_load(ds.peer_flag[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ds.epoch; ++k) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((k & 255) == 0 && (__builtin_amdgcn_s_memrealtime() - t0 > ds.limit ||
+                             __hip_atomic_load(ds.h_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)) {
+        ok = false;
+        break;
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return ok;
+}
+
+// Every block: the wait above on thread 0, shared through LDS.
+__device__ __forceinline__ bool dev_sync_block(const DevSync& ds) {
+  __shared__ int sok;
+  if (threadIdx.x == 0) sok = dev_sync_wait(ds) ? 1 : 0;
+  __syncthreads();
+  return sok != 0;
+}
+
+// The end of a search that exchanged through the window: after this kernel
+// every peer's claims of the search are complete (their windows may be
+// released or rewritten), one epoch of its own.
+__global__ void k_dev_barrier(DevSync ds) {
+  if (threadIdx.x == 0) (void)dev_sync_wait(ds);
+}
+
 // Pipelined rounds, claim kernel: every peer's header -- its reduction of
 // round it - 1 -- into the gathered slot of that round (what the round's
 // separate allgather delivers in exact mode), read by the plan of round it + 1.
@@ -2128,8 +2185,12 @@ __device__ void plan_next_round(const DView& V, uint32_t it, uint32_t cap, const
 // workgroup closes the round.  pipe: block (0, 0) also moves the reduction
 // headers the exchange carried into the gathered slot of round it - 1.)
 __global__ __launch_bounds__(kThreads) void k_spec_claim(DView V, uint32_t it, uint32_t cap, int pipe, Policy pol,
-                                                         uint32_t plan_cap, PeerTab pt) {
-  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
+                                                         uint32_t plan_cap, PeerTab pt, DevSync ds) {
+  unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
+  if (ds.epoch) {  // (the stamps count the wait as exchange)
+    if (!dev_sync_block(ds)) return;  // a wait that ran out: the host throws
+    t_in = __builtin_amdgcn_s_memrealtime();
+  }
   if (pipe && blockIdx.x == gridDim.x - 1) {
     // Pipelined rounds: the extra block plans round it + 1 while the others
     // claim round it -- its inputs (this round's plan, every rank's reduction
@@ -2741,6 +2802,28 @@ struct DistBiBfs::Impl {
   Reduced* h_red = nullptr;    // pinned
   Ctl* h_ctl = nullptr;        // pinned, written by k_final
   uint32_t* h_fin = nullptr;   // pinned, k_final's tag (written after h_ctl)
+  uint32_t* h_abort = nullptr; // pinned: 1 = the host gave up (DevSync waits leave)
+  // the device-ordered exchange (DistTuning::dev_sync): the window, the size
+  // of one half, and the epoch of the last round / barrier that used it
+  dist::Comm::Window win{};
+  bool win_ok = false;
+  size_t win_half = 0;
+  unsigned long long dev_epoch = 0;
+  DevSync dev_sync(unsigned long long e) const {
+    DevSync d{};
+    for (int r = 0; r < size; ++r)
+      d.peer_flag[r] = static_cast<const unsigned long long*>(win.peer[r]);
+    d.flag = static_cast<unsigned long long*>(win.mine);
+    d.epoch = e;
+    d.limit = (unsigned long long)(std::max(0.1, tune.timeout_s) * 1e8);  // (s_memrealtime: 100 MHz)
+    d.h_abort = h_abort;
+    d.P = size;
+    return d;
+  }
+  // a host wait that gives up releases the device waits too
+  void give_up() {
+    if (h_abort) __atomic_store_n(h_abort, 1u, __ATOMIC_RELEASE);
+  }
   uint32_t fin_seq = 0;
   uint64_t* h_plan = nullptr;  // pinned plan ring (k_spec_expand)
   uint64_t* h_aux = nullptr;   // pinned: per-round largest per-owner candidate count
@@ -2792,7 +2875,8 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red), sizeof(Reduced), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl), sizeof(Ctl), hipHostMallocDefault));
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_fin), 64, hipHostMallocDefault));
-    *h_fin = 0;
+    std::memset(h_fin, 0, 64);
+    h_abort = h_fin + 8;  // (the DevSync abort word shares h_fin's 64 bytes)
     HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_plan), kPlanRing * 8, hipHostMallocDefault));
     std::memset(h_plan, 0, kPlanRing * 8);
     V.plan_ring = h_plan;
@@ -2949,6 +3033,18 @@ struct DistBiBfs::Impl {
     HIP_CHECK(hipMemsetAsync(V.st, 0, sizeof(DState), stream));
     HIP_CHECK(hipMemsetAsync(d_scalar, 0, 64, stream));
     HIP_CHECK(hipStreamSynchronize(stream));
+    // the device-ordered exchange's window (collective: every rank decides
+    // alike): two halves of P owner blocks at the largest speculative block
+    if (!win_ok && size > 1 && size <= kStageRanks && tune.dev_sync) {
+      const uint32_t smax = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
+      const size_t half = (size_t)peer_words(smax) * 4 * (size_t)size;
+      dist::Comm::Window w;
+      if (comm->dev_window(dist::Comm::kWinFlagBytes + 2 * half, w)) {
+        win = w;
+        win_half = half;
+        win_ok = true;
+      }
+    }
   }
 
   // bytes of the owned CSR shard (row offsets + columns) and the generator's
@@ -3084,9 +3180,15 @@ struct DistBiBfs::Impl {
         if (e != hipSuccess && e != hipErrorNotReady) HIP_CHECK(e);
         if (e == hipSuccess && __atomic_load_n(h_fin, __ATOMIC_ACQUIRE) != tag)
           throw Error("dist: stream drained without its host tag");
-        comm->check();
+        try {
+          comm->check();
+        } catch (...) {
+          give_up();
+          throw;
+        }
         const auto now = std::chrono::steady_clock::now();
         if (now > deadline) {
+          give_up();
           comm->abort();
           throw Error("dist: rank " + std::to_string(rank) + " waited " + std::to_string(tune.timeout_s) +
                       " s for a round (peer failure or hang); communicator aborted");
@@ -3127,9 +3229,15 @@ struct DistBiBfs::Impl {
           throw Error("dist: stream drained before round " + std::to_string(need) + " was planned");
         }
         if (e != hipErrorNotReady) HIP_CHECK(e);
-        comm->check();
+        try {
+          comm->check();
+        } catch (...) {
+          give_up();
+          throw;
+        }
         const auto now = std::chrono::steady_clock::now();
         if (now > deadline) {
+          give_up();
           comm->abort();
           throw Error("dist: rank " + std::to_string(rank) + " waited " + std::to_string(tune.timeout_s) +
                       " s for round " + std::to_string(need) + " (peer failure or hang); communicator aborted");
@@ -3388,6 +3496,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
   // pipeline and the search continues with exact plans.
   bool pipe = pipe_start;
   bool pipe_used = pipe;
+  bool dsync_used = false;  // a round exchanged through the window (DevSync): a barrier closes the search
   stats.pipelined = pipe ? 1 : 0;
   const uint32_t spec_max = std::max<uint32_t>(kSpecCapMin, std::min<uint32_t>(tune.spec_cap_max, block_cap));
   if (host_only) {
@@ -3505,10 +3614,26 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       // spill lists (owner blocks overflow into them).
       const uint32_t plan_cap = round_edge_cap();
       const int pp = pipe ? 1 : 0;
-      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(V, it, pol, cap_it, k == 0 ? flags : 0,
+      // the device-ordered exchange: this round's candidates go to the
+      // window half of its epoch, which the peers' claim kernels read once
+      // this rank's flag says so (no host rendezvous; see DevSync)
+      // (small claim grids only: every waiting workgroup holds a CU slot, and
+      // the peers' expansions it waits for must still find room -- a wide claim
+      // grid per rank on one GPU starved them)
+      const bool dsync = P > 1 && win_ok && peer_bytes * (uint64_t)P <= win_half && cx + 1u <= kDevSyncBlocks;
+      DView VR = V;
+      unsigned long long ep = 0;
+      if (dsync) {
+        ep = ++dev_epoch;
+        VR.sendbuf = reinterpret_cast<uint32_t*>(static_cast<char*>(win.mine) + dist::Comm::kWinFlagBytes +
+                                                 (ep & 1) * win_half);
+        dsync_used = true;
+        stats.dev_sync_rounds++;
+      }
+      k_spec_expand<<<dim3(bx, 2), kThreads, 0, cs>>>(VR, it, pol, cap_it, k == 0 ? flags : 0,
                                                       hubs ? kHubDeg : kNoHubs, hubs ? 0 : 1, end_in_expand, ocap,
                                                       plan_cap, pp);
-      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(V, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap, pp);
+      if (hubs) k_td_hubs<<<dim3(hx, 2), kThreads, 0, cs>>>(VR, it, -1, 0, cap_it, 0, P == 1 ? 1 : 0, ocap, pp);
       HIP_CHECK(hipGetLastError());
       if (P > 1) {
         // Owner-addressed exchange: ONE alltoall moves, per peer, the
@@ -3517,7 +3642,14 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
         // is the round's status too: no second collective.
         // (read in place where the transport allows: no copy on the local group)
         PeerTab pt{};
-        if (P <= kStageRanks) {
+        DevSync ds{};
+        if (dsync) {
+          for (int r = 0; r < P; ++r)
+            pt.p[r] = reinterpret_cast<const uint32_t*>(static_cast<const char*>(win.peer[r]) + dist::Comm::kWinFlagBytes +
+                                                        (ep & 1) * win_half + (size_t)rank * peer_bytes);
+          pt.direct = 1;
+          ds = dev_sync(ep);
+        } else if (P <= kStageRanks) {
           const void* pv[kStageRanks];
           comm->alltoall_view(V.sendbuf, V.recvbuf, peer_bytes, cs, pv);
           for (int r = 0; r < P; ++r) pt.p[r] = static_cast<const uint32_t*>(pv[r]);
@@ -3526,9 +3658,9 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
           comm->alltoall(V.sendbuf, V.recvbuf, peer_bytes, cs);
         }
         // (pipelined: one extra block plans the next round beside the claims)
-        k_spec_claim<<<dim3(cx + (pipe ? 1u : 0u), 2), kThreads, 0, cs>>>(V, it, ocap, pp, pol, plan_cap, pt);
+        k_spec_claim<<<dim3(cx + (pipe ? 1u : 0u), 2), kThreads, 0, cs>>>(VR, it, ocap, pp, pol, plan_cap, pt, ds);
         HIP_CHECK(hipGetLastError());
-        if (P <= kStageRanks) comm->alltoall_release(cs);
+        if (!dsync && P <= kStageRanks) comm->alltoall_release(cs);
         stats.collectives++;
         stats.exchanged_bytes += peer_bytes * (P - 1);
         if (!pipe) {  // exact plans: the round's reduction, every rank's values gathered, reduced by the reader
@@ -3565,6 +3697,12 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       const uint64_t fm = std::max(h_ctl->fmax[0], h_ctl->fmax[1]);
       spec_cap = std::min(spec_max, std::max<uint32_t>(spec_cap, next_pow2(4 * fm)));
     }
+  }
+  if (dsync_used) {
+    // every peer's claims of this search complete before this rank's stream
+    // goes on (its window may be rewritten by the next search or released)
+    k_dev_barrier<<<1, 64, 0, cs>>>(dev_sync(++dev_epoch));
+    HIP_CHECK(hipGetLastError());
   }
   const Ctl h = *h_ctl;
   if (h.lost && pipe_used) {
@@ -3885,6 +4023,7 @@ SearchResult DistBiBfs::search(vid_t src, vid_t dst, const SearchOptions& opt) {
   } catch (...) {
     // A rank that fails mid-search would leave its peers blocked in a
     // collective forever: tear the communicator down so they return too.
+    I.give_up();
     I.comm->abort();
     throw;
   }

@@ -125,15 +125,18 @@ class IpcComm final : public Comm {
     // buffers (after an abort ~DistBiBfs skips its stream sync): wait for it
     // before unmapping.  Pull kernels never wait on peers, so this is bounded.
     if (done_) (void)hipEventSynchronize(done_);
-    for (int r = 0; r < size_; ++r)
+    for (int r = 0; r < size_; ++r) {
       for (int s = 0; s < 2; ++s)
         if (peer_[r][s].ptr) (void)hipIpcCloseMemHandle(peer_[r][s].ptr);
+      if (win_peer_[r]) (void)hipIpcCloseMemHandle(win_peer_[r]);
+    }
     // an exported buffer is freed only after every peer unmapped it (or the
     // group failed, or a bounded wait for peers that are gone ran out)
     group_.detach_wait(2.0);
     for (auto& x : retired_) (void)hipFree(x.ptr);
     for (int s = 0; s < 2; ++s)
       if (stage_[s]) (void)hipFree(stage_[s]);
+    if (win_) (void)hipFree(win_);
     if (done_) (void)hipEventDestroy(done_);
     if (h_tag_) (void)hipHostFree(h_tag_);
     if (stats_on_ && n_coll_)
@@ -224,6 +227,75 @@ class IpcComm final : public Comm {
     if (!in_view_) return;
     in_view_ = false;
     leave(s);
+  }
+
+  // Every rank exports a window; the handles (with each rank's PCI bus id)
+  // move in one allgather, and the peers' windows are mapped.  Only when every
+  // rank sits on the caller's GPU: the device-side flag protocol is measured
+  // there (cross-GPU windows over xGMI stay off).
+  bool dev_window(size_t bytes, Window& w) override {
+    live();
+    if (size_ > kWinMax) return false;
+    if (win_) {  // (one window per communicator: sized once, by the first caller)
+      if (bytes > win_bytes_) return false;
+      w.mine = win_;
+      for (int r = 0; r < size_; ++r) w.peer[r] = r == rank_ ? win_ : win_peer_[r];
+      return true;
+    }
+    struct Blob {
+      int32_t ok;
+      char pci[28];
+      unsigned char handle[64];
+    };
+    static_assert(sizeof(hipIpcMemHandle_t) <= 64, "IPC handle size");
+    Blob me{};
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    if (hipDeviceGetPCIBusId(me.pci, (int)sizeof me.pci, dev) != hipSuccess) {
+      (void)hipGetLastError();
+      me.pci[0] = 0;
+    }
+    size_t cap = 2u << 20;  // (>= 2 MiB: an exportable block, as grow_stage)
+    while (cap < bytes) cap <<= 1;
+    void* mine = nullptr;
+    hipIpcMemHandle_t h;
+    if (hipMalloc(&mine, cap) == hipSuccess && hipIpcGetMemHandle(&h, mine) == hipSuccess) {
+      HIP_CHECK(hipMemset(mine, 0, cap));
+      std::memcpy(me.handle, &h, sizeof h);
+      me.ok = me.pci[0] ? 1 : 0;
+    } else {
+      (void)hipGetLastError();
+      if (mine) (void)hipFree(mine);
+      mine = nullptr;
+    }
+    void* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, sizeof(Blob) * (size_t)(size_ + 1)));
+    std::vector<Blob> all((size_t)size_);
+    hipStream_t s = nullptr;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    HIP_CHECK(hipMemcpy(d, &me, sizeof me, hipMemcpyHostToDevice));
+    allgather(d, static_cast<Blob*>(d) + 1, sizeof(Blob), s);
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipMemcpy(all.data(), static_cast<Blob*>(d) + 1, sizeof(Blob) * (size_t)size_, hipMemcpyDeviceToHost));
+    HIP_CHECK(hipStreamDestroy(s));
+    HIP_CHECK(hipFree(d));
+    bool ok = true;
+    for (int r = 0; r < size_; ++r)
+      ok = ok && all[(size_t)r].ok && std::strncmp(all[(size_t)r].pci, me.pci, sizeof me.pci) == 0;
+    if (!ok) {  // every rank sees the same blobs: every rank declines
+      if (mine) (void)hipFree(mine);
+      return false;
+    }
+    win_ = mine;
+    win_bytes_ = cap;
+    for (int r = 0; r < size_; ++r) {
+      if (r == rank_) continue;
+      std::memcpy(&h, all[(size_t)r].handle, sizeof h);
+      HIP_CHECK(hipIpcOpenMemHandle(&win_peer_[r], h, hipIpcMemLazyEnablePeerAccess));
+    }
+    w.mine = win_;
+    for (int r = 0; r < size_; ++r) w.peer[r] = r == rank_ ? win_ : win_peer_[r];
+    return true;
   }
 
   void check() override { group_.check(); }
@@ -417,6 +489,9 @@ class IpcComm final : public Comm {
   uint64_t tag_seq_ = 0;
   bool stats_on_ = false;      // BIBFS_IPC_STATS=1: per-collective host timings on teardown
   bool in_view_ = false;       // alltoall_view -> alltoall_release
+  void* win_ = nullptr;        // dev_window: this rank's exported window and the peers' mapped ones
+  size_t win_bytes_ = 0;
+  void* win_peer_[kIpcMax] = {};
   uint64_t n_coll_ = 0, ns_stream_ = 0, ns_meet_ = 0, ns_total_ = 0;
   clock::time_point t_enter_{};
 };

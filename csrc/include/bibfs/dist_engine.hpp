@@ -74,6 +74,7 @@ struct DistLevelStats {
   int pipelined = 0;               // 1: the search started with pipelined plans (DistTuning::pipeline, no hubs)
   int pipe_drains = 0;             // pipelined searches that stalled and continued with exact plans
   int pipe_retries = 0;            // pipelined searches answered again with exact plans (a spill list overflowed)
+  int dev_sync_rounds = 0;         // speculative rounds whose exchange was ordered on the device (DistTuning::dev_sync)
   int single_engine = 0;           // world size 1: answered by the single-GPU engine (DistTuning::world1_single)
   // DistTuning::stamps: the speculative rounds split by device stamps (sums
   // over the stamped rounds, microseconds): expansion kernel(s), claim kernel,
@@ -108,6 +109,9 @@ struct DistTuning {
                                    // travels with the next round's candidate exchange and every plan accounts
                                    // the round before the last (with spec_rounds == 1 only);
                                    // false = exact plans, a status allgather per round
+  bool dev_sync = true;            // 2..16 IPC ranks (processes) sharing one GPU: a round's claim kernel waits on
+                                   // the peers' flags in a device window instead of a host rendezvous
+                                   // (other transports ignore it)
   size_t hbm_cap_bytes = 0;        // > 0: a build that would make this rank hold more device memory throws
                                    // (tests: rehearse "does not fit one GPU" at small scale)
   bool world1_single = true;       // one rank: answer queries with the single-GPU engine over this rank's device

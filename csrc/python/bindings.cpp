@@ -90,6 +90,7 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["solo_rounds"] = s.solo_rounds;
   d["cont_rounds"] = s.cont_rounds;
   d["pipelined"] = s.pipelined;
+  d["dev_sync_rounds"] = s.dev_sync_rounds;
   d["pipe_drains"] = s.pipe_drains;
   d["pipe_retries"] = s.pipe_retries;
   d["exchanged_bytes"] = s.exchanged_bytes;
@@ -397,6 +398,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("solo_edges", &DistTuning::solo_edges)
       .def_readwrite("owner_cap", &DistTuning::owner_cap)
       .def_readwrite("pipeline", &DistTuning::pipeline)
+      .def_readwrite("dev_sync", &DistTuning::dev_sync)
       .def_readwrite("spec_stall_edges", &DistTuning::spec_stall_edges)
       .def_readwrite("stamps", &DistTuning::stamps)
       .def_readwrite("spill_cap", &DistTuning::spill_cap)
