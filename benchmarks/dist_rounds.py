@@ -54,28 +54,31 @@ def main():
     ap.add_argument("--seed", type=int, default=7)
     ap.add_argument("--solo", type=int, default=1, help="P = 1: 0 runs the multi-workgroup rounds (stampable)")
     ap.add_argument("--procs", action="store_true", help="ranks as processes over the IPC transport")
+    ap.add_argument("--dev-sync", default="1", help="DistTuning.dev_sync values to run (IPC processes)")
     a = ap.parse_args()
     for spec in a.specs.split(","):
         _, n, _, _ = parse_spec(spec)
         rnd = random.Random(a.seed)
         qs = [(rnd.randrange(n), rnd.randrange(n)) for _ in range(a.queries)]
         for ranks in [int(x) for x in a.ranks.split(",")]:
-            for pv in [int(x) for x in a.pipeline.split(",")]:
+            for pv, dv in [(int(x), int(y)) for x in a.pipeline.split(",") for y in a.dev_sync.split(",")]:
                 if not pv and ranks == 1:
                     continue
                 if a.procs:
-                    tk = {"stamps": True, "pipeline": bool(pv), "solo": bool(a.solo)}
+                    tk = {"stamps": True, "pipeline": bool(pv), "solo": bool(a.solo), "dev_sync": bool(dv)}
                     got, _ = dist_proc_matrix(ranks, spec, qs, [({}, tk)])
                     rs, st0, run = got[0]
                     t = {"query_ms": run["query_ms"], "stats": st0}
                 else:
-                    tun = make_tuning(stamps=True, pipeline=bool(pv), solo=bool(a.solo))
+                    tun = make_tuning(stamps=True, pipeline=bool(pv), solo=bool(a.solo), dev_sync=bool(dv))
                     rs, t = dist_local_generate_run(ranks, spec, qs, tuning=tun)
                 keep = [(r, ms, st) for r, ms, st in zip(rs, t["query_ms"], t["stats"]) if r.found and r.hops > 0]
                 sts = [st for _, _, st in keep]
                 rec = {
                     "spec": spec, "ranks": ranks, "pipeline": bool(pv) and ranks > 1, "queries": len(keep),
-                    "transport": "ipc-processes" if a.procs else "local-threads",
+                    "transport": "ipc-processes" if a.procs else "local-threads", "dev_sync": bool(dv),
+                    "dev_sync_rounds_per_query": (round(statistics.mean(st["dev_sync_rounds"] for st in sts), 2)
+                                                  if sts else None),
                     "median_query_ms": round(statistics.median(ms for _, ms, _ in keep), 4) if keep else None,
                     "mean_rounds": round(statistics.mean(st["rounds"] for st in sts), 2) if sts else None,
                     "mean_stamped_rounds": round(statistics.mean(st["stamped_rounds"] for st in sts), 2) if sts else None,

@@ -54,7 +54,8 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
                 solo_edges: Optional[int] = None, owner_cap: Optional[int] = None,
                 pipeline: Optional[bool] = None, spec_stall_edges: Optional[int] = None,
                 stamps: Optional[bool] = None, hbm_cap_bytes: Optional[int] = None,
-                world1_single: Optional[bool] = None, spill_cap: Optional[int] = None) -> "native.DistTuning":
+                world1_single: Optional[bool] = None, spill_cap: Optional[int] = None,
+                dev_sync: Optional[bool] = None) -> "native.DistTuning":
     """Knobs of the partitioned engine; unset ones keep the production default.
 
     solo (one rank only): run the small rounds in one persistent workgroup
@@ -88,13 +89,17 @@ def make_tuning(spec_rounds: Optional[int] = None, spec_cap_max: Optional[int] =
 
     world1_single (default on): with ONE rank the shard is the whole graph,
     so queries are answered by the single-GPU engine over the same device CSR
-    (no copy); off = the partitioned rounds (solo workgroup) at world size 1."""
+    (no copy); off = the partitioned rounds (solo workgroup) at world size 1.
+
+    dev_sync (default on; IPC ranks that share one GPU): a round's claim
+    kernel waits for the peers' expansions on their flags in a device window
+    instead of a host rendezvous (no effect on other transports)."""
     t = native.DistTuning()
     for k, v in (("spec_rounds", spec_rounds), ("spec_cap_max", spec_cap_max), ("cap", cap),
                  ("nosync_bytes", nosync_bytes), ("timeout_s", timeout_s), ("walk_max", walk_max),
                  ("solo", solo), ("solo_edges", solo_edges), ("owner_cap", owner_cap), ("pipeline", pipeline),
                  ("spec_stall_edges", spec_stall_edges), ("stamps", stamps), ("hbm_cap_bytes", hbm_cap_bytes),
-                 ("world1_single", world1_single), ("spill_cap", spill_cap)):
+                 ("world1_single", world1_single), ("spill_cap", spill_cap), ("dev_sync", dev_sync)):
         if v is not None:
             setattr(t, k, v)
     return t

@@ -21,7 +21,7 @@
 #            [ROUNDS=3 STEPS=20 WARMUP=5], one JSON line per run
 #   stamp    cycle stamps of the 100k tiny resident server (BIBFS_TINY_STAMP: its stamped build)
 #   distab   partitioned engine: local-group P = 1/2/4 per-round kernel vs exchange stamps
-#            (SPECS / RANKS / PIPELINE / QUERIES / PROCS=1 override benchmarks/dist_rounds.py's defaults)
+#            (SPECS / RANKS / PIPELINE / QUERIES / PROCS=1 / DEVSYNC override benchmarks/dist_rounds.py's defaults)
 #   procs    partitioned engine as separate processes on the one GPU (IPC transport):
 #            tests/test_gpu_dist_proc.py
 #   pairab   A/B of one environment knob over pair latencies: ABENV=<var> ABVALS="<v1> <v2>"
@@ -76,7 +76,7 @@ run_task() {
         > $O/${TAG}_dstress.jsonl 2> $O/${TAG}_dstress.err ;;
     distab)
       $T 900 python3 benchmarks/dist_rounds.py ${SPECS:+--specs $SPECS} ${RANKS:+--ranks $RANKS} \
-        ${PIPELINE:+--pipeline $PIPELINE} ${QUERIES:+--queries $QUERIES} ${PROCS:+--procs} \
+        ${PIPELINE:+--pipeline $PIPELINE} ${QUERIES:+--queries $QUERIES} ${PROCS:+--procs} ${DEVSYNC:+--dev-sync $DEVSYNC} \
         > $O/${TAG}_dist_rounds.jsonl 2> $O/${TAG}_dist_rounds.err ;;
     procs)
       $T 900 $PT -m gpu tests/test_gpu_dist_proc.py > $O/${TAG}_procs.log 2>&1 ;;
