@@ -354,6 +354,11 @@ def main(argv=None) -> int:
     # several ranks on one GPU (a gloo / IPC rehearsal): decided alike on every
     # rank from the launcher's ranks-per-node, never from this rank's index
     shared_gpu = int(os.environ.get("LOCAL_WORLD_SIZE", world)) > ndev
+    if shared_gpu:
+        # ranks as processes on one GPU: one hardware queue each, set before
+        # this process's first HIP call (the GPU time-slices more queues;
+        # profiles/r6_hw_queues_procs.jsonl)
+        os.environ["GPU_MAX_HW_QUEUES"] = "1"
     if a.dist_backend == "auto":
         a.dist_backend = "gloo" if shared_gpu else "nccl"
     local = local % ndev

@@ -347,6 +347,12 @@ def dist_proc_launch(ranks: int, graph, queries: Sequence, runs: Sequence = ((No
             json.dump(job, f)
         e = dict(os.environ)
         e.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        if int(ranks) > 1:
+            # every rank on the one device: one hardware queue per process.  With
+            # HIP's 4 each, the GPU time-slices the processes' queues: G(1M) at
+            # 8 ranks 137-157 -> 1.4-2.2 ms per query, 4 ranks 0.54 -> 0.51 ms
+            # (profiles/r6_hw_queues_procs.jsonl)
+            e["GPU_MAX_HW_QUEUES"] = "1"
         if env:
             e.update(env)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

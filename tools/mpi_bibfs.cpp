@@ -20,6 +20,12 @@
 // fail instead of hanging.
 #include <mpi.h>
 
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
 #include "bibfs/dist_engine.hpp"
 #include "bibfs/hip_engine.hpp"
 #include "cli_common.hpp"
@@ -31,6 +37,29 @@ static void node_rank(int* local_rank, int* local_size) {
   MPI_Comm_rank(node, local_rank);
   MPI_Comm_size(node, local_size);
   MPI_Comm_free(&node);
+}
+
+// GPUs of this node without touching the HIP runtime: KFD topology nodes
+// with SIMDs (narrowed by ROCR_ / HIP_VISIBLE_DEVICES); 0 when unreadable.
+static int host_gpu_count() {
+  int n = 0;
+  for (int i = 0; i < 256; ++i) {
+    const std::string path = "/sys/class/kfd/kfd/topology/nodes/" + std::to_string(i) + "/properties";
+    std::FILE* f = std::fopen(path.c_str(), "r");
+    if (!f) break;
+    char key[64];
+    unsigned long long v = 0;
+    while (std::fscanf(f, "%63s %llu", key, &v) == 2)
+      if (std::strcmp(key, "simd_count") == 0 && v > 0) ++n;
+    std::fclose(f);
+  }
+  for (const char* var : {"ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"})
+    if (const char* e = std::getenv(var); e && *e) {
+      int listed = 1;
+      for (const char* c = e; *c; ++c) listed += *c == ',';
+      n = std::min(n, listed);
+    }
+  return n;
 }
 
 int main(int argc, char** argv) {
@@ -54,6 +83,15 @@ int main(int argc, char** argv) {
     // The IPC control plane is node-local shared memory and checks peer
     // liveness by local pid, so it needs every rank on one node.
     const bool one_node = min_local == size;
+    // Ranks sharing a GPU as processes (IPC): one hardware queue each, set
+    // before this process's first HIP call -- with HIP's 4 per process the GPU
+    // time-slices the ranks' queues (8 ranks on one GPU: ~140 -> ~2 ms per
+    // G(1M) query, profiles/r6_hw_queues_procs.jsonl).
+    {
+      const std::string want = a.has("comm") ? a.get("comm") : "auto";
+      const int hdev = host_gpu_count();
+      if (want != "rccl" && one_node && hdev > 0 && max_local > hdev) setenv("GPU_MAX_HW_QUEUES", "1", 1);
+    }
     const int ndev = bibfs::gpu_count();
     std::string comm = a.has("comm") ? a.get("comm") : "auto";
     if (comm == "auto") comm = (max_local > ndev && one_node) ? "ipc" : "rccl";
