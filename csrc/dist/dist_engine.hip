@@ -3620,7 +3620,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       // (small claim grids only: every waiting workgroup holds a CU slot, and
       // the peers' expansions it waits for must still find room -- a wide claim
       // grid per rank on one GPU starved them)
-      const bool dsync = P > 1 && win_ok && peer_bytes * (uint64_t)P <= win_half && cx + 1u <= kDevSyncBlocks;
+      const bool dsync = P > 1 && win_ok && tune.dev_sync && peer_bytes * (uint64_t)P <= win_half && cx + 1u <= kDevSyncBlocks;
       DView VR = V;
       unsigned long long ep = 0;
       if (dsync) {

@@ -65,6 +65,26 @@ def test_processes_match_oracle_every_branch(ranks, spec):
     assert cont > 0 and host > 0, (cont, host)
 
 
+@pytest.mark.parametrize("ranks", [2, 3])
+def test_processes_device_ordered_exchange(ranks):
+    """The processes order their small rounds' exchange on the device (epoch
+    flags in the exported windows, DevSync) by default; the same queries with
+    DistTuning.dev_sync off take the host rendezvous.  Both answer like the
+    oracle, and the counters show which path ran."""
+    g = bb.from_spec("gnp:20000::6")
+    qs = _pairs(g.n, 12, 40 + ranks)
+    runs = [({}, {}), ({}, {"dev_sync": False}), ({}, {"pipeline": False}),
+            ({}, {"pipeline": False, "dev_sync": False})]
+    got, _ = dist_proc_matrix(ranks, g, qs, runs)
+    for rs, _, _ in got:
+        _check(g, qs, rs)
+    dev = [sum(x.get("dev_sync_rounds", 0) for x in st) for _, st, _ in got]
+    assert dev[0] > 0 and dev[2] > 0, dev
+    assert dev[1] == 0 and dev[3] == 0, dev
+    for rs_on, rs_off in ((got[0][0], got[1][0]), (got[2][0], got[3][0])):
+        assert [r.hops for r in rs_on] == [r.hops for r in rs_off]
+
+
 def test_processes_follow_protocol_spec():
     """Round by round, the processes expand the sides the protocol spec says
     and discover what the BFS levels say (tests/dist_round_spec.py)."""
