@@ -97,6 +97,8 @@ def main():
                     "small_claim_rounds": sum(st["small_claim_rounds"] for st in sts),
                     "host_rounds": sum(st["host_rounds"] for st in sts),
                     "solo_rounds": sum(st["solo_rounds"] for st in sts),
+                    "walk_insert_us_per_query": round(statistics.mean(st.get("walk_insert_us", 0.0) for st in sts), 2) if sts else None,
+                    "walk_chain_us_per_query": round(statistics.mean(st.get("walk_chain_us", 0.0) for st in sts), 2) if sts else None,
                 }
                 for k, nk in (("sx_plan_us", "small_expand_rounds"), ("sx_staging_us", "small_expand_rounds"),
                               ("sx_stage_us", "small_expand_rounds"),

@@ -2552,6 +2552,7 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
                                                uint32_t capT, uint32_t slotsS, uint32_t slotsT, uint32_t meet,
                                                uint32_t hops, uint32_t* out) {
   extern __shared__ uint32_t lds[];
+  const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   // per-side table base and size as selects, not local arrays indexed by the
   // side (those went to scratch, and the table accesses became flat)
   auto keys = [&](int s) { return s ? lds + 2 * slotsS : lds; };
@@ -2602,16 +2603,22 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
     }
   }
   __syncthreads();
+  const unsigned long long t_built = __builtin_amdgcn_s_memrealtime();
   // lanes 0 and 1 of wave 0 walk one side each: the chain lengths, then (with
   // the meet's position known) each side's half of the path
   if (threadIdx.x >= 2) return;
+  // out[3]: the phases' 10 ns ticks (tables built | chains walked << 16), for stamped searches
+  auto stamp = [&] {
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    out[3] = (uint32_t)min(t_built - t_in, 0xffffull) | (uint32_t)min(t_end - t_built, 0xffffull) << 16;
+  };
   const int s = (int)threadIdx.x;
   auto parent_of = [&](uint32_t v, bool& ok) -> uint32_t {
     uint32_t h = home(s, v);
     for (uint32_t probe = 0; probe < nslot(s); ++probe) {
-      const uint32_t k = keys(s)[2 * h];
-      if (k == v) return keys(s)[2 * h + 1];
-      if (k == kEmpty) break;
+      const uint2 kv = reinterpret_cast<const uint2*>(keys(s))[h];  // key and parent in one LDS load
+      if (kv.x == v) return kv.y;
+      if (kv.x == kEmpty) break;
       h = next(s, h);
     }
     ok = false;
@@ -2627,6 +2634,7 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
       out[0] = 1;
       out[1] = d0;
       out[2] = d1;
+      stamp();
     }
     return;
   }
@@ -2640,6 +2648,7 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
     out[0] = 0;
     out[1] = d0;
     out[2] = d1;
+    stamp();
   } else {
     for (uint32_t i = d0; i <= hops; ++i) {
       path[i] = v;
@@ -3816,7 +3825,15 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   const uint64_t vS = h.vis[0], vT = h.vis[1];
   if (vS + vT > tune.walk_max) return false;
   const uint32_t capS = (uint32_t)std::max<uint64_t>(vS, 1), capT = (uint32_t)std::max<uint64_t>(vT, 1);
-  const uint32_t slotsS = capS + capS / 3 + 1, slotsT = capT + capT / 3 + 1;  // load factor <= 0.75
+  // Linear probing: as sparse as the LDS allows, down to a 0.75 load factor.
+  // At 0.75 the tables' clusters made the walk's inserts and lookups ~1,000
+  // cycles each (G(1M), ~3k pairs: 17 + 14 us of a 33 us walk kernel).
+  constexpr uint64_t kWalkSlots = 160 * 1024 / 8;
+  const uint64_t need = (uint64_t)capS + capS / 3 + 1 + capT + capT / 3 + 1;
+  if (need > kWalkSlots) return false;
+  const uint64_t f = std::min<uint64_t>(4, kWalkSlots / ((uint64_t)capS + capT + 2));  // slots per pair (1 = 0.75 fill)
+  const uint32_t slotsS = (uint32_t)(f > 1 ? f * capS + 1 : capS + capS / 3 + 1),
+                 slotsT = (uint32_t)(f > 1 ? f * capT + 1 : capT + capT / 3 + 1);
   const size_t lds = (size_t)(slotsS + slotsT) * 8;
   if (lds > 160 * 1024) return false;
   const uint32_t meet = (uint32_t)(key & 0xffffffffull), hops = (uint32_t)(key >> 32);
@@ -3844,6 +3861,10 @@ void DistBiBfs::Impl::finish_walk(SearchResult& r) {
                                     std::to_string(h_walk[1]) + " + " + std::to_string(h_walk[2]) +
                                     " != " + std::to_string(hops) + ")");
   r.path.assign(h_walk + 4, h_walk + 4 + hops + 1);
+  if (tune.stamps) {
+    stats.walk_insert_us += (h_walk[3] & 0xffffu) * 0.01;
+    stats.walk_chain_us += (h_walk[3] >> 16) * 0.01;
+  }
 }
 
 void DistBiBfs::Impl::cleanup_enqueue(const Ctl& h) {

@@ -82,6 +82,8 @@ struct DistLevelStats {
   // -> next expansion start (status allgather + launch gap)
   int stamped_rounds = 0;
   double expand_us = 0.0, claim_us = 0.0, exchange_us = 0.0, status_us = 0.0;
+  // the path gather's walk kernel (stamped searches): LDS tables built / both chains walked
+  double walk_insert_us = 0.0, walk_chain_us = 0.0;
   // ... of them, the rounds that took the one-workgroup small paths, by phase:
   // expansion = plan (entry -> planned) + stage (frontier staged, degree
   // prefix) + edges + end (headers, state); claim = claims + end

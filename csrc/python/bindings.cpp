@@ -102,6 +102,8 @@ static py::dict dist_stats_dict(const DistLevelStats& s) {
   d["claim_us"] = s.claim_us;
   d["exchange_us"] = s.exchange_us;
   d["status_us"] = s.status_us;
+  d["walk_insert_us"] = s.walk_insert_us;
+  d["walk_chain_us"] = s.walk_chain_us;
   d["small_expand_rounds"] = s.small_expand_rounds;
   d["small_claim_rounds"] = s.small_claim_rounds;
   d["sx_plan_us"] = s.sx_plan_us;
