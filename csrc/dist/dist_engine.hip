@@ -2547,10 +2547,12 @@ __global__ void k_pack_parents(DView V, uint32_t capS, uint32_t capT, uint32_t d
 
 // One workgroup: every rank's gathered pairs into two LDS hash tables
 // (vertex -> parent, one per side), then the two parent chains from the meet
-// vertex.  out = {status, dS, dT, pad, path[hops + 1]}; status 0 = ok.
+// vertex.  out (pinned host memory) = {status, dS, dT, stamps, path[hops + 1]};
+// status 0 = ok.  Then `tag` into fin, after a system-scope release: the host
+// reads the path where the kernel wrote it (no copy, no tag kernel behind).
 __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv, int P, uint32_t capS,
                                                uint32_t capT, uint32_t slotsS, uint32_t slotsT, uint32_t meet,
-                                               uint32_t hops, uint32_t* out) {
+                                               uint32_t hops, uint32_t* out, uint32_t* fin, uint32_t tag) {
   extern __shared__ uint32_t lds[];
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   // per-side table base and size as selects, not local arrays indexed by the
@@ -2607,10 +2609,16 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
   // lanes 0 and 1 of wave 0 walk one side each: the chain lengths, then (with
   // the meet's position known) each side's half of the path
   if (threadIdx.x >= 2) return;
-  // out[3]: the phases' 10 ns ticks (tables built | chains walked << 16), for stamped searches
+  // out[3]: the phases' 10 ns ticks (tables built | chains walked << 16), for
+  // stamped searches; then the release and the tag (lane 0, after both lanes'
+  // stores: the fence is the wave's)
   auto stamp = [&] {
     const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
     out[3] = (uint32_t)min(t_built - t_in, 0xffffull) | (uint32_t)min(t_end - t_built, 0xffffull) << 16;
+  };
+  auto release = [&] {
+    __threadfence_system();
+    if (threadIdx.x == 0) __hip_atomic_store(fin, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   };
   const int s = (int)threadIdx.x;
   auto parent_of = [&](uint32_t v, bool& ok) -> uint32_t {
@@ -2636,6 +2644,7 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
       out[2] = d1;
       stamp();
     }
+    release();
     return;
   }
   uint32_t* path = out + 4;  // src .. meet .. dst; both lanes write the meet at d0
@@ -2655,6 +2664,7 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
       v = parent_of(v, ok);
     }
   }
+  release();
 }
 
 // One rank owns every vertex: the two parent chains are walked straight from
@@ -2799,13 +2809,12 @@ struct DistBiBfs::Impl {
   size_t gen_hbm_peak_bytes = 0;  // hipMemGetInfo: free before the build - least free during it
   // path reconstruction buffers: O(path length), grown on demand (never O(n))
   uint32_t* d_pathbuf = nullptr;
-  size_t path_cap = 0;            // entries per path array (pathS, pathT; walk holds 4 + path)
+  size_t path_cap = 0;            // entries per path array (pathS, pathT, and a third behind them)
   uint32_t* sent_base = nullptr;  // both sides' sent bitmaps, contiguous (one memset)
   DView V{};
   uint32_t* d_cur = nullptr;
   uint32_t* d_pathS = nullptr;
   uint32_t* d_pathT = nullptr;
-  uint32_t* d_walk = nullptr;  // k_walk output
   RoundRec* d_trace = nullptr;
   RoundStamp* d_rstamp = nullptr;
   Reduced* h_red = nullptr;    // pinned
@@ -2943,10 +2952,11 @@ struct DistBiBfs::Impl {
       devmem::release(d_pathbuf, path_cap * 3 * 4 + 64);
     }
     path_cap = std::max<size_t>(entries, 1u << 14);
+    // three arrays: pathS, pathT, and room behind pathT (validate_path keeps
+    // its found flags after the indices there)
     devmem::alloc(&d_pathbuf, path_cap * 3 * 4 + 64);
     d_pathS = d_pathbuf;
     d_pathT = d_pathbuf + path_cap;
-    d_walk = d_pathbuf + 2 * path_cap;
   }
 
   // effective host-planned block capacity (tuning may shrink it for tests)
@@ -3332,7 +3342,7 @@ struct DistBiBfs::Impl {
       prev_it = i;
     }
   }
-  bool walk_path(uint64_t key, SearchResult& r);
+  bool walk_path(uint64_t key, SearchResult& r, uint32_t tag);
   void finish_walk(SearchResult& r);
   void cleanup_enqueue(const Ctl& h);
   void walk_path_per_hop(uint64_t key, uint32_t it, SearchResult& r);
@@ -3772,12 +3782,9 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       }
       path_pending = true;
     } else if (opt.want_path) {
-      if (!(path_pending = walk_path(key, r))) walk_path_per_hop(key, it, r);
-      if (path_pending) {
-        tag = next_tag();
-        k_host_tag<<<1, 64, 0, cs>>>(h_fin, tag);
-        HIP_CHECK(hipGetLastError());
-      }
+      const uint32_t wt = next_tag();  // k_walk releases the path with it
+      if ((path_pending = walk_path(key, r, wt))) tag = wt;
+      else walk_path_per_hop(key, it, r);
     }
   }
   if ((opt.trace || tune.stamps) && !tag) {  // trace records / stamps are plain device stores: drain the rounds first
@@ -3819,7 +3826,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
 // Path in O(1) collectives: every rank packs the (vertex, parent) pairs it
 // claimed, ONE allgather, and a one-workgroup kernel walks both parent chains
 // from LDS tables.  False when the visited sets are too large for that.
-bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
+bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r, uint32_t tag) {
   TraceRange range("dist:path_gather");
   const Ctl& h = *h_ctl;
   const uint64_t vS = h.vis[0], vT = h.vis[1];
@@ -3841,18 +3848,16 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r) {
   // sized before the collective (every rank knows `hops`): a failing
   // allocation aborts the communicator before, not between, collectives
   ensure_path_dev((size_t)hops + 5);
+  ensure_walk_buf(4 + (size_t)hops + 1);  // (k_walk writes the path there)
   k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(V, capS, capT, h.depth[0], h.depth[1]);
   const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
   comm->allgather(V.sendbuf, V.recvbuf, blk * 4, cs);
   stats.collectives++;
   stats.path_collectives++;
   stats.exchanged_bytes += blk * 4 * size;
-  k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, d_walk);
+  k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, h_walk, h_fin, tag);
   HIP_CHECK(hipGetLastError());
-  const size_t words = 4 + (size_t)hops + 1;
-  ensure_walk_buf(words);
-  HIP_CHECK(hipMemcpyAsync(h_walk, d_walk, words * 4, hipMemcpyDeviceToHost, cs));
-  return true;  // read by finish_walk after the search's last wait
+  return true;  // read by finish_walk after the search's last wait (its tag)
 }
 
 void DistBiBfs::Impl::finish_walk(SearchResult& r) {
