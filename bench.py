@@ -354,11 +354,11 @@ def main(argv=None) -> int:
     # several ranks on one GPU (a gloo / IPC rehearsal): decided alike on every
     # rank from the launcher's ranks-per-node, never from this rank's index
     shared_gpu = int(os.environ.get("LOCAL_WORLD_SIZE", world)) > ndev
-    if shared_gpu:
-        # ranks as processes on one GPU: one hardware queue each, set before
-        # this process's first HIP call (the GPU time-slices more queues;
-        # profiles/r6_hw_queues_procs.jsonl)
-        os.environ["GPU_MAX_HW_QUEUES"] = "1"
+    # (no GPU_MAX_HW_QUEUES=1 here, unlike the partitioned-only launchers: a
+    # rank's resident single-GPU server is a persistent kernel, and with one
+    # queue the hand-off levels queued behind it waited for its idle exit --
+    # 10M queries 0.09 -> 172 ms in the 2-rank rehearsal,
+    # profiles/r6_bench_2rank_1gpu_ipc_hwq1_end.json)
     if a.dist_backend == "auto":
         a.dist_backend = "gloo" if shared_gpu else "nccl"
     local = local % ndev
