@@ -2550,10 +2550,16 @@ __global__ void k_pack_parents(DView V, uint32_t capS, uint32_t capT, uint32_t d
 // vertex.  out (pinned host memory) = {status, dS, dT, stamps, path[hops + 1]};
 // status 0 = ok.  Then `tag` into fin, after a system-scope release: the host
 // reads the path where the kernel wrote it (no copy, no tag kernel behind).
-__global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv, int P, uint32_t capS,
-                                               uint32_t capT, uint32_t slotsS, uint32_t slotsT, uint32_t meet,
-                                               uint32_t hops, uint32_t* out, uint32_t* fin, uint32_t tag) {
+// k_walk's LDS tables: the CU's 160 KB less its static words (the DevSync flag word)
+constexpr uint64_t kWalkSlots = (160 * 1024 - 256) / 8;
+__global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv, PeerTab pt, DevSync ds, int P,
+                                               uint32_t capS, uint32_t capT, uint32_t slotsS, uint32_t slotsT,
+                                               uint32_t meet, uint32_t hops, uint32_t* out, uint32_t* fin,
+                                               uint32_t tag) {
   extern __shared__ uint32_t lds[];
+  // the device-ordered gather: every rank packed its pairs into its window
+  // half of the epoch; wait for the peers' flags, then read them in place
+  if (ds.epoch && !dev_sync_block(ds)) return;  // (a wait that ran out: the host throws)
   const unsigned long long t_in = __builtin_amdgcn_s_memrealtime();
   // per-side table base and size as selects, not local arrays indexed by the
   // side (those went to scratch, and the table accesses became flat)
@@ -2574,7 +2580,7 @@ __global__ __launch_bounds__(1024) void k_walk(const uint32_t* __restrict__ recv
   // dependent global round trip: ~50 us for a G(1M) path at P = 2)
   constexpr int kU = 8;
   for (int r = 0; r < P; ++r) {
-    const uint32_t* b = recv + (uint64_t)r * blk;
+    const uint32_t* b = pt.direct ? pt.p[r] : recv + (uint64_t)r * blk;
     const uint32_t c0 = b[0], c1 = b[1];
     const uint2* pr = reinterpret_cast<const uint2*>(b + 2);
     for (uint32_t base = 0; base < c0 + c1; base += kU * blockDim.x) {
@@ -2904,7 +2910,7 @@ struct DistBiBfs::Impl {
     V.host_ctl = h_ctl;
     ensure_walk_buf(1u << 14);
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&k_walk),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)(kWalkSlots * 8)));
     if (const char* t = std::getenv("BIBFS_DIST_TIMEOUT_S")) tune.timeout_s = std::max(0.1, std::atof(t));
     comm->set_timeout(tune.timeout_s);
     solo_stamp = env::stamps();  // BIBFS_STAMP: the solo workgroup's phase cycles
@@ -3343,6 +3349,7 @@ struct DistBiBfs::Impl {
     }
   }
   bool walk_path(uint64_t key, SearchResult& r, uint32_t tag);
+  bool path_dsync = false;  // the search's path gather went through the device window
   void finish_walk(SearchResult& r);
   void cleanup_enqueue(const Ctl& h);
   void walk_path_per_hop(uint64_t key, uint32_t it, SearchResult& r);
@@ -3717,13 +3724,18 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       spec_cap = std::min(spec_max, std::max<uint32_t>(spec_cap, next_pow2(4 * fm)));
     }
   }
-  if (dsync_used) {
-    // every peer's claims of this search complete before this rank's stream
-    // goes on (its window may be rewritten by the next search or released)
+  // every peer's reads of this rank's window during this search complete
+  // before this rank's stream goes on (the window may be released): one
+  // barrier epoch at the search's end -- after the path gather, or here on
+  // the paths that end the search now
+  auto window_barrier = [&] {
     k_dev_barrier<<<1, 64, 0, cs>>>(dev_sync(++dev_epoch));
     HIP_CHECK(hipGetLastError());
-  }
+    dsync_used = false;
+  };
+  path_dsync = false;
   const Ctl h = *h_ctl;
+  if (dsync_used && h.lost) window_barrier();
   if (h.lost && pipe_used) {
     // a pipelined round ran on a frontier its plan could not see yet and
     // overflowed the spill lists: every rank saw it (reduced values), so
@@ -3787,6 +3799,7 @@ SearchResult DistBiBfs::Impl::search(vid_t src, vid_t dst, const SearchOptions& 
       else walk_path_per_hop(key, it, r);
     }
   }
+  if (dsync_used || path_dsync) window_barrier();
   if ((opt.trace || tune.stamps) && !tag) {  // trace records / stamps are plain device stores: drain the rounds first
     tag = next_tag();
     k_host_tag<<<1, 64, 0, cs>>>(h_fin, tag);
@@ -3835,27 +3848,43 @@ bool DistBiBfs::Impl::walk_path(uint64_t key, SearchResult& r, uint32_t tag) {
   // Linear probing: as sparse as the LDS allows, down to a 0.75 load factor.
   // At 0.75 the tables' clusters made the walk's inserts and lookups ~1,000
   // cycles each (G(1M), ~3k pairs: 17 + 14 us of a 33 us walk kernel).
-  constexpr uint64_t kWalkSlots = 160 * 1024 / 8;
   const uint64_t need = (uint64_t)capS + capS / 3 + 1 + capT + capT / 3 + 1;
   if (need > kWalkSlots) return false;
   const uint64_t f = std::min<uint64_t>(4, kWalkSlots / ((uint64_t)capS + capT + 2));  // slots per pair (1 = 0.75 fill)
   const uint32_t slotsS = (uint32_t)(f > 1 ? f * capS + 1 : capS + capS / 3 + 1),
                  slotsT = (uint32_t)(f > 1 ? f * capT + 1 : capT + capT / 3 + 1);
   const size_t lds = (size_t)(slotsS + slotsT) * 8;
-  if (lds > 160 * 1024) return false;
+  if (lds > kWalkSlots * 8) return false;
   const uint32_t meet = (uint32_t)(key & 0xffffffffull), hops = (uint32_t)(key >> 32);
   hipStream_t cs = cstream;
   // sized before the collective (every rank knows `hops`): a failing
   // allocation aborts the communicator before, not between, collectives
   ensure_path_dev((size_t)hops + 5);
   ensure_walk_buf(4 + (size_t)hops + 1);  // (k_walk writes the path there)
-  k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(V, capS, capT, h.depth[0], h.depth[1]);
   const uint64_t blk = 2 + 2 * ((uint64_t)capS + capT);
-  comm->allgather(V.sendbuf, V.recvbuf, blk * 4, cs);
+  // the gather through the device window where the round exchange uses it
+  // (the same epoch protocol: pack into this epoch's half, raise, wait, read)
+  const bool dsync = win_ok && tune.dev_sync && size <= kStageRanks && blk * 4 <= win_half;
+  DView VR = V;
+  PeerTab pt{};
+  DevSync ds{};
+  if (dsync) {
+    const unsigned long long ep = ++dev_epoch;
+    VR.sendbuf = reinterpret_cast<uint32_t*>(static_cast<char*>(win.mine) + dist::Comm::kWinFlagBytes +
+                                             (ep & 1) * win_half);
+    for (int r = 0; r < size; ++r)
+      pt.p[r] = reinterpret_cast<const uint32_t*>(static_cast<const char*>(win.peer[r]) + dist::Comm::kWinFlagBytes +
+                                                  (ep & 1) * win_half);
+    pt.direct = 1;
+    ds = dev_sync(ep);
+    path_dsync = true;
+  }
+  k_pack_parents<<<blocks_for(vS + vT, cus), kThreads, 0, cs>>>(VR, capS, capT, h.depth[0], h.depth[1]);
+  if (!dsync) comm->allgather(V.sendbuf, V.recvbuf, blk * 4, cs);
   stats.collectives++;
   stats.path_collectives++;
   stats.exchanged_bytes += blk * 4 * size;
-  k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, size, capS, capT, slotsS, slotsT, meet, hops, h_walk, h_fin, tag);
+  k_walk<<<1, 1024, lds, cs>>>(V.recvbuf, pt, ds, size, capS, capT, slotsS, slotsT, meet, hops, h_walk, h_fin, tag);
   HIP_CHECK(hipGetLastError());
   return true;  // read by finish_walk after the search's last wait (its tag)
 }
